@@ -1,0 +1,573 @@
+// kbin_api.hip -- host side of the C-ABI declared in include/kbin.h.
+//
+// Owns device memory and the HIP stream of a context, plans the table size,
+// and sequences the kernels of kbin_kernels.hip:
+//   submit   : H2D (pinned staging) + pack, or adopt device-packed reads;
+//              per-read k-mer offsets (device scan)
+//   finalize : zero table -> scan_insert per batch -> [retry bigger on
+//              overflow] -> compact(prune) -> place -> sort
+//   export   : D2H of the CSR
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kbin.h"
+#include "kbin_internal.h"
+
+using namespace kb;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return fail(_e == hipErrorOutOfMemory ? KB_ENOMEM : KB_EDEVICE, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(_e), __FILE__, __LINE__);                \
+    } while (0)
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t n) {
+        if (n <= cap && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        uint64_t want = std::max<uint64_t>(n, 1);
+        hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Batch {
+    const uint64_t* words = nullptr;  // adopted or owned
+    const uint32_t* lens = nullptr;
+    uint64_t* own_words = nullptr;
+    uint32_t* own_lens = nullptr;
+    uint64_t* kmer_base = nullptr;  // owned, n_reads+1
+    int32_t* ids = nullptr;         // owned, n_reads
+    uint64_t n_reads = 0;
+    int RW = 0;
+    uint64_t ord_base = 0;
+    uint64_t occ_base = 0;
+    uint64_t n_occ = 0;
+};
+
+struct kb_ctx {
+    kb_params p{};
+    int KW = 1;
+    int dev = 0;
+    hipStream_t s = nullptr;
+    std::vector<Batch> batches;
+    uint64_t n_reads = 0, n_occ = 0;
+
+    // staging for host submissions
+    char* h_stage = nullptr;
+    uint64_t h_stage_cap = 0;
+    DevBuf<uint8_t> d_bases;
+    DevBuf<uint64_t> d_off;
+
+    // finalize working set
+    DevBuf<uint64_t> table;
+    uint64_t slots = 0, learned_slots = 0;
+    DevBuf<uint32_t> occ_slot;
+    DevBuf<int32_t> read_ids;
+    DevBuf<uint32_t> slot_entry;
+    DevBuf<uint32_t> e_mmer, e_cnt, cursor, lists;
+    DevBuf<uint64_t> e_hi, e_lo, e_off;
+    DevBuf<uint32_t> ids_ord, ids_tmp;
+    DevBuf<int32_t> ids_out;
+    DevBuf<uint64_t> scratch;
+    DevBuf<uint32_t> misc;    // [0] status [1] n_distinct [4..8) list counts
+    DevBuf<uint64_t> totals;  // [0] n_entries [1] n_ids
+    uint32_t* h_misc = nullptr;
+
+    // results
+    bool finalized = false;
+    uint64_t n_entries = 0, n_ids = 0, n_distinct = 0;
+    std::vector<uint32_t> h_mmer, h_cnt;
+    std::vector<uint64_t> h_hi, h_lo, h_off;
+    std::vector<int32_t> h_ids;
+    bool exported = false;
+
+    // timing
+    bool timing = false;
+    kb_timing tm{};
+    hipEvent_t ev[8] = {};
+};
+
+static int set_device(kb_ctx* c) {
+    HIPCHK(hipSetDevice(c->dev));
+    return KB_OK;
+}
+
+extern "C" int kb_abi_version(void) { return 1; }
+
+extern "C" const char* kb_last_error(void) { return g_err.c_str(); }
+
+extern "C" void* kb_stream(kb_ctx* ctx) { return ctx ? (void*)ctx->s : nullptr; }
+
+extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
+    if (!params || !out) return fail(KB_EINVAL, "null argument");
+    *out = nullptr;
+    const kb_params& p = *params;
+    if (p.M < 1 || p.M > 8)
+        return fail(KB_EINVAL, "M=%d outside [1,8] (power_val, binning.c:17)", p.M);
+    if (p.K < 2 * p.M)
+        return fail(KB_EINVAL,
+                    "K=%d < 2M=%d: the reference's incremental branch (binning.c:992-1021) is live; "
+                    "unsupported", p.K, 2 * p.M);
+    if (p.K > 63) return fail(KB_EINVAL, "K=%d > 63 unsupported", p.K);
+    if (p.cutoff < 0) return fail(KB_EINVAL, "cutoff < 0");
+    if (p.max_read_len < 1 || p.max_read_len > 65535)
+        return fail(KB_EINVAL, "max_read_len=%d outside [1,65535]", p.max_read_len);
+    if (p.table_slots && (p.table_slots & (p.table_slots - 1)))
+        return fail(KB_EINVAL, "table_slots must be a power of two");
+    kb_ctx* c = new kb_ctx();
+    c->p = p;
+    c->KW = p.K <= 31 ? 1 : 2;
+    c->dev = p.device;
+    int rc = set_device(c);
+    if (rc) { delete c; return rc; }
+    hipError_t e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; return fail(KB_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e)); }
+    for (auto& ev : c->ev) {
+        e = hipEventCreate(&ev);
+        if (e != hipSuccess) { kb_destroy(c); return fail(KB_EDEVICE, "hipEventCreate"); }
+    }
+    e = hipHostMalloc((void**)&c->h_misc, 16 * sizeof(uint32_t), hipHostMallocDefault);
+    if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
+    if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(4) != hipSuccess) {
+        kb_destroy(c);
+        return fail(KB_ENOMEM, "device alloc");
+    }
+    *out = c;
+    return KB_OK;
+}
+
+static void free_batches(kb_ctx* c) {
+    for (auto& b : c->batches) {
+        if (b.own_words) (void)hipFree(b.own_words);
+        if (b.own_lens) (void)hipFree(b.own_lens);
+        if (b.kmer_base) (void)hipFree(b.kmer_base);
+        if (b.ids) (void)hipFree(b.ids);
+    }
+    c->batches.clear();
+    c->n_reads = 0;
+    c->n_occ = 0;
+}
+
+extern "C" void kb_destroy(kb_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->dev);
+    if (c->s) (void)hipStreamSynchronize(c->s);
+    free_batches(c);
+    c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_slot.release();
+    c->read_ids.release(); c->slot_entry.release(); c->e_mmer.release(); c->e_cnt.release();
+    c->cursor.release(); c->lists.release(); c->e_hi.release(); c->e_lo.release();
+    c->e_off.release(); c->ids_ord.release(); c->ids_tmp.release(); c->ids_out.release();
+    c->scratch.release(); c->misc.release(); c->totals.release();
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->h_misc) (void)hipHostFree(c->h_misc);
+    for (auto& ev : c->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->s) (void)hipStreamDestroy(c->s);
+    delete c;
+}
+
+extern "C" int kb_reset(kb_ctx* c) {
+    if (!c) return fail(KB_EINVAL, "null ctx");
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->s));
+    free_batches(c);
+    c->finalized = false;
+    c->exported = false;
+    c->n_entries = c->n_ids = c->n_distinct = 0;
+    return KB_OK;
+}
+
+// k-mer offsets of a batch (device scan) and its occurrence total (host sync)
+static int batch_offsets(kb_ctx* c, Batch& b) {
+    HIPCHK(hipMalloc((void**)&b.kmer_base, (b.n_reads + 1) * sizeof(uint64_t)));
+    const uint64_t need = kmer_base_scratch_elems(b.n_reads);
+    HIPCHK(c->scratch.ensure(std::max<uint64_t>(need, c->scratch.cap)));
+    HIPCHK(launch_kmer_base(b.lens, b.n_reads, c->p.K, b.kmer_base, c->scratch.p, c->scratch.cap, c->s));
+    uint64_t tot = 0;
+    HIPCHK(hipMemcpyAsync(&tot, b.kmer_base + b.n_reads, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    b.n_occ = tot;
+    return KB_OK;
+}
+
+static int submit_common(kb_ctx* c, const char* bases, const uint32_t* lens, uint64_t n_reads,
+                         const int32_t* ids, int32_t first_id) {
+    if (!c) return fail(KB_EINVAL, "null ctx");
+    if (c->finalized) return fail(KB_ESTATE, "submit after finalize (call kb_reset)");
+    if (n_reads == 0) return KB_OK;
+    if (!bases || !lens) return fail(KB_EINVAL, "null bases/lens");
+    if (c->n_reads + n_reads > 0xFFFFFFFFull)
+        return fail(KB_EOVERFLOW, "more than 2^32 reads per context");
+    int rc = set_device(c);
+    if (rc) return rc;
+    // host-side validation (lengths) and offsets
+    std::vector<uint64_t> off(n_reads + 1);
+    off[0] = 0;
+    uint32_t maxlen = 0;
+    for (uint64_t r = 0; r < n_reads; r++) {
+        if (lens[r] > (uint32_t)c->p.max_read_len)
+            return fail(KB_ETOOLONG, "read %llu has %u bases > max_read_len %d",
+                        (unsigned long long)r, lens[r], c->p.max_read_len);
+        maxlen = std::max(maxlen, lens[r]);
+        off[r + 1] = off[r] + lens[r];
+    }
+    const uint64_t nb = off[n_reads];
+    const int RW = (int)((std::max<uint32_t>(maxlen, 1) + 31) / 32);
+    // stage through pinned memory (the caller may reuse its buffer on return)
+    if (c->h_stage_cap < nb) {
+        if (c->h_stage) (void)hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->h_stage_cap = 0;
+        HIPCHK(hipHostMalloc((void**)&c->h_stage, std::max<uint64_t>(nb, 1), hipHostMallocDefault));
+        c->h_stage_cap = std::max<uint64_t>(nb, 1);
+    }
+    HIPCHK(hipStreamSynchronize(c->s));  // staging buffer reuse
+    memcpy(c->h_stage, bases, nb);
+    HIPCHK(c->d_bases.ensure(nb));
+    HIPCHK(c->d_off.ensure(n_reads + 1));
+    HIPCHK(hipMemcpyAsync(c->d_bases.p, c->h_stage, nb, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d_off.p, off.data(), (n_reads + 1) * sizeof(uint64_t),
+                          hipMemcpyHostToDevice, c->s));
+    Batch b;
+    b.n_reads = n_reads;
+    b.RW = RW;
+    b.ord_base = c->n_reads;
+    HIPCHK(hipMalloc((void**)&b.own_words, n_reads * (uint64_t)RW * sizeof(uint64_t)));
+    HIPCHK(hipMalloc((void**)&b.own_lens, n_reads * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void**)&b.ids, n_reads * sizeof(int32_t)));
+    b.words = b.own_words;
+    b.lens = b.own_lens;
+    HIPCHK(hipMemsetAsync(c->misc.p, 0, sizeof(uint32_t), c->s));
+    HIPCHK(launch_pack(c->d_bases.p, c->d_off.p, n_reads, RW, b.own_words, b.own_lens, c->misc.p, c->s));
+    if (ids)
+        HIPCHK(hipMemcpyAsync(b.ids, ids, n_reads * sizeof(int32_t), hipMemcpyHostToDevice, c->s));
+    else
+        HIPCHK(launch_fill_ids(b.ids, n_reads, first_id, c->s));
+    uint32_t st = 0;
+    HIPCHK(hipMemcpyAsync(&st, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (st & ST_ALPHABET) {
+        (void)hipFree(b.own_words); (void)hipFree(b.own_lens); (void)hipFree(b.ids);
+        return fail(KB_EALPHABET, "read byte outside {A,C,G,T} (see DESIGN.md: alphabet)");
+    }
+    rc = batch_offsets(c, b);
+    if (rc) {
+        (void)hipFree(b.own_words); (void)hipFree(b.own_lens); (void)hipFree(b.ids);
+        return rc;
+    }
+    b.occ_base = c->n_occ;
+    c->n_occ += b.n_occ;
+    c->n_reads += n_reads;
+    c->batches.push_back(b);
+    return KB_OK;
+}
+
+extern "C" int kb_submit(kb_ctx* c, const char* bases, const uint32_t* lens, uint64_t n_reads,
+                         int32_t first_id) {
+    return submit_common(c, bases, lens, n_reads, nullptr, first_id);
+}
+
+extern "C" int kb_submit_ids(kb_ctx* c, const char* bases, const uint32_t* lens, uint64_t n_reads,
+                             const int32_t* ids) {
+    if (n_reads && !ids) return fail(KB_EINVAL, "null ids");
+    return submit_common(c, bases, lens, n_reads, ids, 0);
+}
+
+extern "C" int kb_submit_packed_device(kb_ctx* c, const uint64_t* d_words, const uint32_t* d_lens,
+                                       uint64_t n_reads, uint32_t wpr, int32_t first_id) {
+    if (!c) return fail(KB_EINVAL, "null ctx");
+    if (c->finalized) return fail(KB_ESTATE, "submit after finalize (call kb_reset)");
+    if (n_reads == 0) return KB_OK;
+    if (!d_words || !d_lens) return fail(KB_EINVAL, "null device pointers");
+    if ((uint64_t)wpr * 32 < 1 || wpr > 2048) return fail(KB_EINVAL, "words_per_read=%u", wpr);
+    if ((uint64_t)wpr * 32 > (uint64_t)c->p.max_read_len + 31)
+        return fail(KB_ETOOLONG, "words_per_read=%u exceeds max_read_len %d", wpr, c->p.max_read_len);
+    if (c->n_reads + n_reads > 0xFFFFFFFFull)
+        return fail(KB_EOVERFLOW, "more than 2^32 reads per context");
+    int rc = set_device(c);
+    if (rc) return rc;
+    Batch b;
+    b.words = d_words;
+    b.lens = d_lens;
+    b.n_reads = n_reads;
+    b.RW = (int)wpr;
+    b.ord_base = c->n_reads;
+    HIPCHK(hipMalloc((void**)&b.ids, n_reads * sizeof(int32_t)));
+    HIPCHK(launch_fill_ids(b.ids, n_reads, first_id, c->s));
+    rc = batch_offsets(c, b);
+    if (rc) { (void)hipFree(b.ids); return rc; }
+    b.occ_base = c->n_occ;
+    c->n_occ += b.n_occ;
+    c->n_reads += n_reads;
+    c->batches.push_back(b);
+    return KB_OK;
+}
+
+static uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+extern "C" int kb_set_timing(kb_ctx* c, int enable) {
+    if (!c) return fail(KB_EINVAL, "null ctx");
+    c->timing = enable != 0;
+    return KB_OK;
+}
+
+extern "C" int kb_get_timing(kb_ctx* c, kb_timing* out) {
+    if (!c || !out) return fail(KB_EINVAL, "null argument");
+    *out = c->tm;
+    return KB_OK;
+}
+
+#define REC(i) \
+    do { if (c->timing) HIPCHK(hipEventRecord(c->ev[i], c->s)); } while (0)
+
+extern "C" int kb_finalize(kb_ctx* c, int prune) {
+    if (!c) return fail(KB_EINVAL, "null ctx");
+    if (c->finalized) return fail(KB_ESTATE, "already finalized (call kb_reset)");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (c->n_occ > 0xFFFFFFFFull * 64)
+        return fail(KB_EOVERFLOW, "too many k-mers for one context");
+    memset(&c->tm, 0, sizeof(c->tm));
+    const int SW = c->KW == 1 ? 2 : 4;
+    // ---- table plan
+    uint64_t slots = c->p.table_slots;
+    if (!slots) slots = c->learned_slots;
+    if (!slots) slots = next_pow2(std::max<uint64_t>(4096, c->n_occ / 4));
+    slots = std::max<uint64_t>(slots, 1024);
+    HIPCHK(c->occ_slot.ensure(c->n_occ));
+    // ordinal -> read id, concatenated over batches
+    HIPCHK(c->read_ids.ensure(c->n_reads));
+    for (auto& b : c->batches)
+        HIPCHK(hipMemcpyAsync(c->read_ids.p + b.ord_base, b.ids, b.n_reads * sizeof(int32_t),
+                              hipMemcpyDeviceToDevice, c->s));
+    uint32_t status = 0, ndist = 0;
+    for (int attempt = 0;; attempt++) {
+        if (slots > (1ull << 32))
+            return fail(KB_ENOMEM, "table would need more than 2^32 slots");
+        hipError_t e = c->table.ensure(slots * SW);
+        if (e != hipSuccess) return fail(KB_ENOMEM, "table of %llu slots: %s",
+                                         (unsigned long long)slots, hipGetErrorString(e));
+        c->slots = slots;
+        REC(0);
+        HIPCHK(hipMemsetAsync(c->table.p, 0, slots * SW * sizeof(uint64_t), c->s));
+        HIPCHK(hipMemsetAsync(c->misc.p, 0, 2 * sizeof(uint32_t), c->s));
+        REC(1);
+        for (auto& b : c->batches) {
+            ScanArgs a{};
+            a.words = b.words;
+            a.lens = b.lens;
+            a.kmer_base = b.kmer_base;
+            a.n_reads = b.n_reads;
+            a.table = c->table.p;
+            a.mask = slots - 1;
+            a.occ_slot = c->occ_slot.p + b.occ_base;
+            a.n_distinct = c->misc.p + 1;
+            a.status = c->misc.p;
+            a.max_distinct = (uint32_t)std::min<uint64_t>(slots - slots / 8, 0xFFFFFFFFull);
+            a.max_probe = (uint32_t)std::min<uint64_t>(slots, 1u << 20);
+            a.RW = b.RW;
+            a.K = c->p.K;
+            a.M = c->p.M;
+            HIPCHK(launch_scan_insert(a, c->KW, c->s));
+            c->tm.scan_insert_launches++;
+        }
+        REC(2);
+        HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));
+        status = c->h_misc[0];
+        ndist = c->h_misc[1];
+        if (!(status & (ST_TABLE_FULL | ST_PROBE_LIMIT))) break;
+        if (attempt >= 6) return fail(KB_ENOMEM, "table retries exhausted (status %u)", status);
+        slots *= 4;
+    }
+    c->n_distinct = ndist;
+    if (!c->p.table_slots) c->learned_slots = std::max<uint64_t>(1024, next_pow2((uint64_t)ndist * 2));
+    if (c->timing) {
+        HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));
+    }
+    // ---- prune + compact
+    const uint64_t ne_cap = (uint64_t)ndist + 1;
+    HIPCHK(c->slot_entry.ensure(slots));
+    HIPCHK(c->e_mmer.ensure(ne_cap));
+    HIPCHK(c->e_cnt.ensure(ne_cap));
+    HIPCHK(c->e_hi.ensure(ne_cap));
+    HIPCHK(c->e_lo.ensure(ne_cap));
+    HIPCHK(c->e_off.ensure(ne_cap));
+    HIPCHK(c->scratch.ensure(std::max<uint64_t>(compact_scratch_elems(slots), c->scratch.cap)));
+    const uint32_t keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
+    REC(3);
+    HIPCHK(launch_compact(c->table.p, slots, c->KW, c->p.K, keep_gt, c->slot_entry.p, c->e_mmer.p,
+                          c->e_hi.p, c->e_lo.p, c->e_cnt.p, c->e_off.p, c->scratch.p,
+                          c->scratch.cap, c->totals.p, c->s));
+    REC(4);
+    uint64_t tot[2];
+    HIPCHK(hipMemcpyAsync(tot, c->totals.p, sizeof(tot), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    c->n_entries = tot[0];
+    c->n_ids = tot[1];
+    // ---- place
+    HIPCHK(c->cursor.ensure(ne_cap));
+    HIPCHK(c->ids_ord.ensure(c->n_ids));
+    HIPCHK(c->ids_out.ensure(c->n_ids));
+    HIPCHK(hipMemsetAsync(c->cursor.p, 0, c->n_entries * sizeof(uint32_t), c->s));
+    for (auto& b : c->batches) {
+        PlaceArgs a{};
+        a.occ_slot = c->occ_slot.p + b.occ_base;
+        a.kmer_base = b.kmer_base;
+        a.n_reads = b.n_reads;
+        a.n_occ = b.n_occ;
+        a.slot_entry = c->slot_entry.p;
+        a.e_off = c->e_off.p;
+        a.cursor = c->cursor.p;
+        a.ids_ord = c->ids_ord.p;
+        a.ord_base = (uint32_t)b.ord_base;
+        HIPCHK(launch_place(a, c->s));
+    }
+    REC(5);
+    // ---- order ids per key
+    HIPCHK(c->lists.ensure(2 * ne_cap));
+    HIPCHK(c->ids_tmp.ensure(c->n_ids));
+    HIPCHK(launch_sort(c->e_off.p, c->e_cnt.p, c->n_entries, c->ids_ord.p, c->ids_tmp.p,
+                       c->read_ids.p, c->ids_out.p, c->lists.p, c->misc.p + 4, c->s));
+    REC(6);
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (c->timing) {
+        HIPCHK(hipEventElapsedTime(&c->tm.compact_ms, c->ev[3], c->ev[4]));
+        HIPCHK(hipEventElapsedTime(&c->tm.place_ms, c->ev[4], c->ev[5]));
+        HIPCHK(hipEventElapsedTime(&c->tm.sort_ms, c->ev[5], c->ev[6]));
+        HIPCHK(hipEventElapsedTime(&c->tm.total_ms, c->ev[0], c->ev[6]));
+    }
+    c->tm.table_slots = slots;
+    c->finalized = true;
+    c->exported = false;
+    return KB_OK;
+}
+
+extern "C" int kb_export_device(kb_ctx* c, kb_csr* out) {
+    if (!c || !out) return fail(KB_EINVAL, "null argument");
+    if (!c->finalized) return fail(KB_ESTATE, "export before finalize");
+    out->n_entries = c->n_entries;
+    out->n_ids = c->n_ids;
+    out->n_kmers = c->n_occ;
+    out->n_distinct = c->n_distinct;
+    out->mmer = c->e_mmer.p;
+    out->kmer_hi = c->e_hi.p;
+    out->kmer_lo = c->e_lo.p;
+    out->count = c->e_cnt.p;
+    out->offset = c->e_off.p;
+    out->ids = c->ids_out.p;
+    return KB_OK;
+}
+
+extern "C" int kb_export(kb_ctx* c, kb_csr* out) {
+    if (!c || !out) return fail(KB_EINVAL, "null argument");
+    if (!c->finalized) return fail(KB_ESTATE, "export before finalize");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (!c->exported) {
+        const uint64_t n = c->n_entries;
+        c->h_mmer.resize(n);
+        c->h_cnt.resize(n);
+        c->h_hi.resize(n);
+        c->h_lo.resize(n);
+        c->h_off.resize(n + 1);
+        c->h_ids.resize(c->n_ids);
+        if (n) {
+            HIPCHK(hipMemcpyAsync(c->h_mmer.data(), c->e_mmer.p, n * 4, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_cnt.data(), c->e_cnt.p, n * 4, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_hi.data(), c->e_hi.p, n * 8, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_lo.data(), c->e_lo.p, n * 8, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_off.data(), c->e_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->s));
+        } else {
+            c->h_off[0] = 0;
+        }
+        if (c->n_ids)
+            HIPCHK(hipMemcpyAsync(c->h_ids.data(), c->ids_out.p, c->n_ids * 4, hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));
+        c->exported = true;
+    }
+    out->n_entries = c->n_entries;
+    out->n_ids = c->n_ids;
+    out->n_kmers = c->n_occ;
+    out->n_distinct = c->n_distinct;
+    out->mmer = c->h_mmer.data();
+    out->kmer_hi = c->h_hi.data();
+    out->kmer_lo = c->h_lo.data();
+    out->count = c->h_cnt.data();
+    out->offset = c->h_off.data();
+    out->ids = c->h_ids.data();
+    return KB_OK;
+}
+
+extern "C" int kb_generate_reads_device(int device, uint64_t* d_words, uint32_t* d_lens,
+                                        uint64_t n_reads, uint32_t read_len, uint64_t genome_len,
+                                        uint32_t err_ppm, uint64_t seed) {
+    if (!d_words || !d_lens) return fail(KB_EINVAL, "null device pointers");
+    if (read_len < 1 || genome_len < read_len) return fail(KB_EINVAL, "bad read_len/genome_len");
+    if (err_ppm > 1000000) return fail(KB_EINVAL, "err_per_million > 1e6");
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(launch_generate(d_words, d_lens, n_reads, read_len, genome_len, err_ppm, seed, 0));
+    HIPCHK(hipStreamSynchronize(0));
+    return KB_OK;
+}
+
+extern "C" int kb_unpack_reads_to_host(int device, const uint64_t* d_words, const uint32_t* d_lens,
+                                       uint64_t n_reads, uint32_t wpr, char* h_bases,
+                                       uint32_t* h_lens) {
+    if (!d_words || !d_lens || !h_bases || !h_lens) return fail(KB_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(device));
+    if (!n_reads) return KB_OK;
+    HIPCHK(hipMemcpy(h_lens, d_lens, n_reads * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::vector<uint64_t> off(n_reads + 1);
+    off[0] = 0;
+    for (uint64_t r = 0; r < n_reads; r++) off[r + 1] = off[r] + h_lens[r];
+    uint64_t *d_off = nullptr;
+    uint8_t* d_out = nullptr;
+    HIPCHK(hipMalloc((void**)&d_off, (n_reads + 1) * 8));
+    hipError_t e = hipMalloc((void**)&d_out, std::max<uint64_t>(off[n_reads], 1));
+    if (e != hipSuccess) { (void)hipFree(d_off); return fail(KB_ENOMEM, "unpack alloc"); }
+    e = hipMemcpy(d_off, off.data(), (n_reads + 1) * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_unpack(d_words, d_lens, n_reads, (int)wpr, d_off, d_out, 0);
+    if (e == hipSuccess) e = hipMemcpy(h_bases, d_out, off[n_reads], hipMemcpyDeviceToHost);
+    (void)hipFree(d_off);
+    (void)hipFree(d_out);
+    if (e != hipSuccess) return fail(KB_EDEVICE, "unpack: %s", hipGetErrorString(e));
+    return KB_OK;
+}

@@ -1,0 +1,290 @@
+"""ctypes binding of libkbin.so -- the MI355X k-mer binning engine.
+
+Mirrors the reference operator surface (binning.c process_read / prune_data)
+for Python callers: an :class:`Engine` is one two-level mmer->kmer table
+(binning.c:1151 zcreate_hash_table), :meth:`Engine.submit` stands for the
+stream of process_read calls (binning.c:1165) and :meth:`Engine.finalize`
+for prune_data (binning.c:1169).  Results come back as a :class:`Result`
+CSR.  The engine is HIP-only: importing works anywhere, but creating an
+Engine without the built library or a GPU raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = pathlib.Path(__file__).resolve().parent
+PKG_ROOT = _HERE.parent                       # genome-assembly_amd/
+REPO_ROOT = PKG_ROOT.parent
+LIB_DIR = PKG_ROOT / "lib"
+LIB_PATH = LIB_DIR / "libkbin.so"
+HOST_LIB_PATH = LIB_DIR / "libkbin_host.so"
+INCLUDE_DIR = REPO_ROOT / "include"
+
+KB_OK, KB_EINVAL, KB_ENOMEM, KB_EDEVICE, KB_EALPHABET, KB_ETOOLONG, KB_ESTATE, KB_EOVERFLOW = range(8)
+_ERRNAMES = {0: "KB_OK", 1: "KB_EINVAL", 2: "KB_ENOMEM", 3: "KB_EDEVICE", 4: "KB_EALPHABET",
+             5: "KB_ETOOLONG", 6: "KB_ESTATE", 7: "KB_EOVERFLOW"}
+
+# symbols include/kbin.h declares (tests check every one is exported)
+EXPORTED = [
+    "kb_create", "kb_destroy", "kb_submit", "kb_submit_ids", "kb_submit_packed_device",
+    "kb_finalize", "kb_export", "kb_export_device", "kb_reset", "kb_set_timing",
+    "kb_get_timing", "kb_generate_reads_device", "kb_unpack_reads_to_host", "kb_stream",
+    "kb_last_error", "kb_abi_version",
+]
+
+
+class KbError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class kb_params(C.Structure):
+    _fields_ = [("K", C.c_int32), ("M", C.c_int32), ("cutoff", C.c_int32),
+                ("max_read_len", C.c_int32), ("device", C.c_int32), ("reserved", C.c_int32),
+                ("table_slots", C.c_uint64)]
+
+
+class kb_csr(C.Structure):
+    _fields_ = [("n_entries", C.c_uint64), ("n_ids", C.c_uint64), ("n_kmers", C.c_uint64),
+                ("n_distinct", C.c_uint64),
+                ("mmer", C.POINTER(C.c_uint32)), ("kmer_hi", C.POINTER(C.c_uint64)),
+                ("kmer_lo", C.POINTER(C.c_uint64)), ("count", C.POINTER(C.c_uint32)),
+                ("offset", C.POINTER(C.c_uint64)), ("ids", C.POINTER(C.c_int32))]
+
+
+class kb_timing(C.Structure):
+    _fields_ = [("scan_insert_ms", C.c_float), ("compact_ms", C.c_float),
+                ("place_ms", C.c_float), ("sort_ms", C.c_float), ("total_ms", C.c_float),
+                ("scan_insert_launches", C.c_uint32), ("reserved", C.c_uint32),
+                ("table_slots", C.c_uint64)]
+
+
+_lib = None
+
+
+def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
+    """Load libkbin.so (raises if it is not built -- no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = pathlib.Path(path) if path else LIB_PATH
+    # One HIP runtime per process: torch ships its own libamdhip64.so (same
+    # SONAME as /opt/rocm's).  If torch is importable it must be loaded first so
+    # libkbin.so binds to that copy instead of pulling in a second runtime.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not p.exists():
+        raise FileNotFoundError(f"{p} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(str(p))
+    vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int32
+    lib.kb_create.argtypes = [C.POINTER(kb_params), C.POINTER(vp)]
+    lib.kb_destroy.argtypes = [vp]
+    lib.kb_destroy.restype = None
+    lib.kb_submit.argtypes = [vp, C.c_char_p, C.POINTER(u32), u64, i32]
+    lib.kb_submit_ids.argtypes = [vp, C.c_char_p, C.POINTER(u32), u64, C.POINTER(i32)]
+    lib.kb_submit_packed_device.argtypes = [vp, vp, vp, u64, u32, i32]
+    lib.kb_finalize.argtypes = [vp, C.c_int]
+    lib.kb_export.argtypes = [vp, C.POINTER(kb_csr)]
+    lib.kb_export_device.argtypes = [vp, C.POINTER(kb_csr)]
+    lib.kb_reset.argtypes = [vp]
+    lib.kb_set_timing.argtypes = [vp, C.c_int]
+    lib.kb_get_timing.argtypes = [vp, C.POINTER(kb_timing)]
+    lib.kb_generate_reads_device.argtypes = [C.c_int, vp, vp, u64, u32, u64, u32, u64]
+    lib.kb_unpack_reads_to_host.argtypes = [C.c_int, vp, vp, u64, u32, C.c_char_p, C.POINTER(u32)]
+    lib.kb_stream.argtypes = [vp]
+    lib.kb_stream.restype = vp
+    lib.kb_last_error.argtypes = []
+    lib.kb_last_error.restype = C.c_char_p
+    lib.kb_abi_version.restype = C.c_int
+    for name in EXPORTED:
+        if name not in ("kb_destroy", "kb_stream", "kb_last_error"):
+            getattr(lib, name).restype = C.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(lib, rc: int) -> None:
+    if rc != KB_OK:
+        raise KbError(rc, lib.kb_last_error().decode(errors="replace"))
+
+
+@dataclass
+class Result:
+    """Post-prune CSR: entry e is the key (mmer[e], kmer_hi[e]:kmer_lo[e]) with
+    count[e] read ids ids[offset[e]:offset[e+1]] in reverse call order."""
+    mmer: np.ndarray
+    kmer_hi: np.ndarray
+    kmer_lo: np.ndarray
+    count: np.ndarray
+    offset: np.ndarray
+    ids: np.ndarray
+    n_kmers: int
+    n_distinct: int
+
+    @property
+    def n_entries(self) -> int:
+        return int(self.mmer.shape[0])
+
+    def canonical(self) -> "Result":
+        """Entries in canonical dump order: bytewise (mmer, kmer) ascending,
+        i.e. descending codes (A=3 > C=2 > G=1 > T=0)."""
+        order = np.lexsort((self.kmer_lo, self.kmer_hi, self.mmer))[::-1]
+        cnt = self.count[order]
+        off = np.zeros(len(order) + 1, dtype=np.uint64)
+        np.cumsum(cnt, out=off[1:])
+        if len(order):
+            starts = self.offset[:-1][order].astype(np.int64)
+            idx = np.repeat(starts - off[:-1].astype(np.int64), cnt.astype(np.int64)) + \
+                np.arange(int(off[-1]), dtype=np.int64)
+            ids = self.ids[idx]
+        else:
+            ids = self.ids[:0]
+        return Result(self.mmer[order], self.kmer_hi[order], self.kmer_lo[order], cnt, off, ids,
+                      self.n_kmers, self.n_distinct)
+
+
+_BP = np.frombuffer(b"TGCA", dtype=np.uint8)  # getbp (binning.c:69-88)
+
+
+def decode(code_hi: int, code_lo: int, n: int) -> str:
+    """Key string of an n-base code (first base most significant)."""
+    v = (int(code_hi) << 64) | int(code_lo)
+    out = bytearray(n)
+    for j in range(n - 1, -1, -1):
+        out[j] = _BP[v & 3]
+        v >>= 2
+    return out.decode()
+
+
+def dump_lines(res: Result, K: int, M: int):
+    """Canonical dump lines: mmer\\tkmer\\tcount\\tids."""
+    r = res.canonical()
+    for e in range(r.n_entries):
+        ids = r.ids[int(r.offset[e]):int(r.offset[e + 1])]
+        yield "%s\t%s\t%d\t%s\n" % (decode(0, r.mmer[e], M), decode(r.kmer_hi[e], r.kmer_lo[e], K),
+                                    int(r.count[e]), ",".join(str(int(x)) for x in ids))
+
+
+def pack_reads(reads) -> tuple[bytes, np.ndarray]:
+    """list of str/bytes reads -> (concatenated bytes, uint32 lengths)."""
+    bs = [r.encode() if isinstance(r, str) else bytes(r) for r in reads]
+    lens = np.fromiter((len(b) for b in bs), dtype=np.uint32, count=len(bs))
+    return b"".join(bs), lens
+
+
+class Engine:
+    """One binning context on one GPU (C-ABI kb_ctx)."""
+
+    def __init__(self, K: int, M: int, cutoff: int = 1, max_read_len: int = 1024,
+                 device: int = 0, table_slots: int = 0, lib_path=None):
+        self.lib = load_library(lib_path)
+        self.K, self.M, self.cutoff = K, M, cutoff
+        p = kb_params(K=K, M=M, cutoff=cutoff, max_read_len=max_read_len, device=device,
+                      reserved=0, table_slots=table_slots)
+        h = C.c_void_p()
+        _check(self.lib, self.lib.kb_create(C.byref(p), C.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.kb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def submit(self, reads=None, *, bases: bytes | None = None, lens=None, first_id: int = 0,
+               ids=None) -> None:
+        """Append reads (list of strings, or bases+lens).  Read r gets id
+        first_id + r unless `ids` is given (process_read's read_id)."""
+        if reads is not None:
+            bases, lens = pack_reads(reads)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = int(lens.shape[0])
+        lp = lens.ctypes.data_as(C.POINTER(C.c_uint32))
+        if ids is not None:
+            ids = np.ascontiguousarray(ids, dtype=np.int32)
+            _check(self.lib, self.lib.kb_submit_ids(self._h, bases, lp, n,
+                                                    ids.ctypes.data_as(C.POINTER(C.c_int32))))
+        else:
+            _check(self.lib, self.lib.kb_submit(self._h, bases, lp, n, int(first_id)))
+
+    def submit_packed_device(self, words_ptr: int, lens_ptr: int, n_reads: int,
+                             words_per_read: int, first_id: int = 0) -> None:
+        _check(self.lib, self.lib.kb_submit_packed_device(self._h, C.c_void_p(words_ptr),
+                                                          C.c_void_p(lens_ptr), n_reads,
+                                                          words_per_read, int(first_id)))
+
+    def finalize(self, prune: bool = True) -> None:
+        _check(self.lib, self.lib.kb_finalize(self._h, 1 if prune else 0))
+
+    def reset(self) -> None:
+        _check(self.lib, self.lib.kb_reset(self._h))
+
+    def set_timing(self, on: bool = True) -> None:
+        _check(self.lib, self.lib.kb_set_timing(self._h, 1 if on else 0))
+
+    def timing(self) -> dict:
+        t = kb_timing()
+        _check(self.lib, self.lib.kb_get_timing(self._h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in kb_timing._fields_ if f != "reserved"}
+
+    def stream(self) -> int:
+        return self.lib.kb_stream(self._h) or 0
+
+    def export(self) -> Result:
+        c = kb_csr()
+        _check(self.lib, self.lib.kb_export(self._h, C.byref(c)))
+        n, m = int(c.n_entries), int(c.n_ids)
+
+        def arr(ptr, count, dt):
+            if count == 0:
+                return np.zeros(0, dtype=dt)
+            return np.ctypeslib.as_array(ptr, shape=(count,)).astype(dt, copy=True)
+
+        return Result(arr(c.mmer, n, np.uint32), arr(c.kmer_hi, n, np.uint64),
+                      arr(c.kmer_lo, n, np.uint64), arr(c.count, n, np.uint32),
+                      arr(c.offset, n + 1, np.uint64), arr(c.ids, m, np.int32),
+                      int(c.n_kmers), int(c.n_distinct))
+
+    def export_device(self) -> dict:
+        c = kb_csr()
+        _check(self.lib, self.lib.kb_export_device(self._h, C.byref(c)))
+        return {f: (getattr(c, f) if f.startswith("n_") else C.cast(getattr(c, f), C.c_void_p).value)
+                for f, _ in kb_csr._fields_}
+
+
+def generate_reads_device(words_ptr: int, lens_ptr: int, n_reads: int, read_len: int,
+                          genome_len: int, err_per_million: int, seed: int, device: int = 0) -> None:
+    lib = load_library()
+    _check(lib, lib.kb_generate_reads_device(device, C.c_void_p(words_ptr), C.c_void_p(lens_ptr),
+                                             n_reads, read_len, genome_len, err_per_million, seed))
+
+
+def unpack_reads_to_host(words_ptr: int, lens_ptr: int, n_reads: int, words_per_read: int,
+                         total_bases: int, device: int = 0) -> tuple[bytes, np.ndarray]:
+    lib = load_library()
+    buf = C.create_string_buffer(max(total_bases, 1))
+    lens = np.zeros(n_reads, dtype=np.uint32)
+    _check(lib, lib.kb_unpack_reads_to_host(device, C.c_void_p(words_ptr), C.c_void_p(lens_ptr),
+                                            n_reads, words_per_read, buf,
+                                            lens.ctypes.data_as(C.POINTER(C.c_uint32))))
+    return buf.raw[:int(lens.sum())], lens

@@ -1,0 +1,166 @@
+/*
+ * kbin.h -- C-ABI of the MI355X k-mer binning engine (libkbin.so).
+ *
+ * This is the device-side replacement for the reference hot path
+ *   binning.c:902-1076  struct ZHashTable *process_read(struct ZHashTable*, char *read, int read_id)
+ *   binning.c:1085-1144 prune_kmers / prune_data
+ * and for the containers it drives (zhash.c chained string hash, llist.c
+ * read-id lists).  The host keeps the reference's C surface (see
+ * include/binning_gpu.h); that shim batches reads and forwards here.
+ *
+ * Plain C types only: pointers, sizes, status codes.  One host thread per
+ * context; all device work runs on the context's own HIP stream and is
+ * synchronised inside kb_finalize / kb_export.
+ *
+ * Semantics:
+ *   - encoding getval: T=0 G=1 C=2 A=3 (binning.c:91-111); bytes outside ACGT
+ *     are rejected with KB_EALPHABET (the reference silently maps them to 'A'
+ *     for scoring but keeps them verbatim in forward keys -- not representable
+ *     in 2 bits);
+ *   - signature = complement-canonical mmer, leftmost strict argmax, "sticky"
+ *     recompute only when the k-mer start passes it (binning.c:922-989);
+ *   - key = (mmer, kmer), both complemented (no reversal) when the complement
+ *     wins (binning.c:1029-1040);
+ *   - per key the read ids in REVERSE CALL ORDER with duplicates
+ *     (binning.c:1061-1068);
+ *   - prune: keep a key iff its list length > cutoff (binning.c:1094-1102).
+ *
+ * Codes: a key string s of n bases is exported as the 2n-bit integer
+ * sum_j getval(s[j]) * 4^(n-1-j) (getscore order, binning.c:114-124), split
+ * into (hi, lo) 64-bit words for k-mers.
+ */
+#ifndef KBIN_H
+#define KBIN_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define KB_OK 0
+#define KB_EINVAL 1      /* bad argument / parameter combination */
+#define KB_ENOMEM 2      /* device or host allocation failed */
+#define KB_EDEVICE 3     /* HIP runtime error */
+#define KB_EALPHABET 4   /* a read byte outside {A,C,G,T} */
+#define KB_ETOOLONG 5    /* a read longer than max_read_len */
+#define KB_ESTATE 6      /* call out of order (e.g. export before finalize) */
+#define KB_EOVERFLOW 7   /* k-mer count beyond the 32-bit occurrence index */
+
+typedef struct kb_ctx kb_ctx;
+
+typedef struct {
+    int32_t K;              /* KMER_SIZE       (binning.c:11); 2 <= K <= 63      */
+    int32_t M;              /* MMER_SIZE       (binning.c:10); 1 <= M <= 8, K >= 2M */
+    int32_t cutoff;         /* ABUNDANCE_CUTOFF (binning.c:12); >= 0            */
+    int32_t max_read_len;   /* longest read accepted (READ_LENGTH-2 for fgets)  */
+    int32_t device;         /* HIP device ordinal                               */
+    int32_t reserved;
+    uint64_t table_slots;   /* hash-table slots hint (power of two); 0 = auto   */
+} kb_params;
+
+/* Exported result (CSR).  Entry order is unspecified (hash order), exactly as
+ * the reference's bucket order is not part of its contract. */
+typedef struct {
+    uint64_t n_entries;     /* surviving (mmer, kmer) keys                      */
+    uint64_t n_ids;         /* sum of counts                                    */
+    uint64_t n_kmers;       /* k-mer occurrences scanned (all submitted reads)  */
+    uint64_t n_distinct;    /* distinct keys before the prune                   */
+    const uint32_t *mmer;   /* [n_entries] canonical mmer code                  */
+    const uint64_t *kmer_hi;/* [n_entries] k-mer code bits 64..127 (0 if K<=32) */
+    const uint64_t *kmer_lo;/* [n_entries] k-mer code bits 0..63                */
+    const uint32_t *count;  /* [n_entries] list length (duplicates kept)        */
+    const uint64_t *offset; /* [n_entries+1] into ids                           */
+    const int32_t *ids;     /* [n_ids] read ids, reverse call order per entry   */
+} kb_csr;
+
+/* per-phase device time of the last kb_finalize (HIP events on the context
+ * stream; only filled when timing is enabled) */
+typedef struct {
+    float scan_insert_ms;   /* fused signature scan + table insert/count        */
+    float compact_ms;       /* prune + stream compaction (3 launches)           */
+    float place_ms;         /* read-id placement                                */
+    float sort_ms;          /* per-key descending id order                      */
+    float total_ms;         /* first to last event of the finalize              */
+    uint32_t scan_insert_launches;
+    uint32_t reserved;
+    uint64_t table_slots;   /* slots used by the last finalize                  */
+} kb_timing;
+
+/* Create a context (kb_create replaces zcreate_hash_table for the level-1
+ * table, zhash.c:19-35). */
+int kb_create(const kb_params *params, kb_ctx **out);
+void kb_destroy(kb_ctx *ctx);
+
+/* Append a batch of reads from host memory.  Reads are concatenated in
+ * `bases`, `lens[r]` bytes each; read r gets id first_id + r and call ordinal
+ * (its position in the stream of all submitted reads).  The bytes are copied
+ * before return (the caller may reuse its buffer, as binning.c:1154/1158 does).
+ * Replaces the per-call process_read(hash, read, id) (binning.c:902). */
+int kb_submit(kb_ctx *ctx, const char *bases, const uint32_t *lens,
+              uint64_t n_reads, int32_t first_id);
+
+/* Same, with an explicit id per read (process_read's caller-supplied id). */
+int kb_submit_ids(kb_ctx *ctx, const char *bases, const uint32_t *lens,
+                  uint64_t n_reads, const int32_t *ids);
+
+/* Append reads already resident in device memory in the engine's packed
+ * layout: read r occupies words_per_read uint64 words at d_words + r*wpr, base
+ * j of the read in word j/32 at bits [62-2(j%32), 63-2(j%32)] (getval codes,
+ * first base most significant); d_lens[r] bases.  The device buffers are
+ * referenced, not copied, until kb_reset/kb_destroy. */
+int kb_submit_packed_device(kb_ctx *ctx, const uint64_t *d_words,
+                            const uint32_t *d_lens, uint64_t n_reads,
+                            uint32_t words_per_read, int32_t first_id);
+
+/* Scan + insert + count, prune (keep count > cutoff when prune != 0), place
+ * and order the read ids.  Replaces the insert half of process_read and
+ * prune_data (binning.c:1130-1144). */
+int kb_finalize(kb_ctx *ctx, int prune);
+
+/* Copy the result to host memory owned by the context (valid until the next
+ * kb_finalize / kb_reset / kb_destroy). */
+int kb_export(kb_ctx *ctx, kb_csr *out);
+
+/* Device pointers of the same result (no copy). */
+int kb_export_device(kb_ctx *ctx, kb_csr *out);
+
+/* Drop all submitted reads and results; keeps allocations for reuse. */
+int kb_reset(kb_ctx *ctx);
+
+/* Per-phase timing of the last finalize (enable before kb_finalize). */
+int kb_set_timing(kb_ctx *ctx, int enable);
+int kb_get_timing(kb_ctx *ctx, kb_timing *out);
+
+/* Synthetic reads generated on device (mirroring
+ * generate_reads.py:93-112: iid uniform genome, uniform start, forward strand,
+ * iid substitutions at rate err_per_million/1e6), written in the packed
+ * layout above into caller-owned device buffers.  Deterministic in seed
+ * (splitmix64 counters).  d_words needs n_reads*ceil(read_len/32) words. */
+int kb_generate_reads_device(int device, uint64_t *d_words, uint32_t *d_lens,
+                             uint64_t n_reads, uint32_t read_len,
+                             uint64_t genome_len, uint32_t err_per_million,
+                             uint64_t seed);
+
+/* Unpack device packed reads to host ASCII (bases concatenated, lens). */
+int kb_unpack_reads_to_host(int device, const uint64_t *d_words,
+                            const uint32_t *d_lens, uint64_t n_reads,
+                            uint32_t words_per_read, char *h_bases,
+                            uint32_t *h_lens);
+
+/* Stream used by the context (hipStream_t as void*), for callers that want
+ * to order their own work against the engine. */
+void *kb_stream(kb_ctx *ctx);
+
+/* Message for the last failing call on this thread. */
+const char *kb_last_error(void);
+
+/* ABI version (bumped on incompatible change) */
+int kb_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KBIN_H */

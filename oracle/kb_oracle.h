@@ -1,0 +1,32 @@
+/* kb_oracle.h -- TEST INFRASTRUCTURE ONLY (parity oracle; see kb_oracle.c). */
+#ifndef KB_ORACLE_H
+#define KB_ORACLE_H
+#include <stdint.h>
+
+#define KBO_OK 0
+#define KBO_EINVAL 1
+#define KBO_ENOMEM 2
+#define KBO_EIO 3
+
+typedef struct {
+    uint64_t n_entries;
+    uint32_t *mmer;     /* mmer code per entry */
+    uint64_t *kmer_hi;  /* k-mer code, high 64 bits (0 when K <= 32) */
+    uint64_t *kmer_lo;  /* k-mer code, low 64 bits */
+    uint32_t *count;    /* list length (occurrences, duplicates kept) */
+    uint64_t *offset;   /* n_entries + 1 */
+    int32_t *ids;       /* read ids per entry, reverse call order */
+    uint64_t n_kmers;   /* k-mer occurrences scanned */
+    int alphabet_ok;    /* 0 if any byte outside ACGT was seen */
+} kbo_result;
+
+int kbo_bin(const char *bases, const uint64_t *read_off, uint64_t n_reads,
+            const int32_t *read_ids, int K, int M, int cutoff, int prune,
+            kbo_result *out);
+void kbo_free(kbo_result *r);
+int kbo_write_dump(const kbo_result *r, int K, int M, const char *path);
+int kbo_read_fgets(const char *path, int read_length, char **bases_out,
+                   uint64_t **off_out, uint64_t *n_out);
+void kbo_free_reads(char *bases, uint64_t *off);
+
+#endif

@@ -1,0 +1,135 @@
+"""GPU parity: the HIP path (through the C-ABI, libkbin.so) against
+  (1) the known-answer digests of the compiled reference (tests/golden), and
+  (2) the CPU oracle (oracle/, clean-room restatement) on the same inputs,
+bit-exact on every (mmer, kmer) key, count and read-id list."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import kbin
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_result(bases, lens, K, M, cutoff=1, prune=True, ids=None, batches=1, max_read_len=1024):
+    with kbin.Engine(K, M, cutoff=cutoff, max_read_len=max_read_len) as eng:
+        n = len(lens)
+        off = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(np.asarray(lens, dtype=np.int64), out=off[1:])
+        cuts = np.linspace(0, n, batches + 1).astype(int)
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            if b <= a:
+                continue
+            sub = bases[off[a]:off[b]]
+            if ids is None:
+                eng.submit(bases=sub, lens=lens[a:b], first_id=int(a))
+            else:
+                eng.submit(bases=sub, lens=lens[a:b], ids=ids[a:b])
+        eng.finalize(prune=prune)
+        return eng.export()
+
+
+def assert_same(res, ora):
+    c = res.canonical()
+    assert c.n_entries == ora.n_entries
+    np.testing.assert_array_equal(c.mmer, ora.mmer)
+    np.testing.assert_array_equal(c.kmer_hi, ora.kmer_hi)
+    np.testing.assert_array_equal(c.kmer_lo, ora.kmer_lo)
+    np.testing.assert_array_equal(c.count, ora.count)
+    np.testing.assert_array_equal(c.offset, ora.offset)
+    np.testing.assert_array_equal(c.ids, ora.ids)
+
+
+def dump_sha(res, K, M):
+    h = hashlib.sha256()
+    for line in kbin.dump_lines(res, K, M):
+        h.update(line.encode())
+    return h.hexdigest()
+
+
+def test_known_answer_digests(digests, golden_dir):
+    for row in digests:
+        bases, lens = oracle.read_fgets(golden_dir / row["input"], row["read_length"])
+        res = gpu_result(bases, lens, row["K"], row["M"], row["cutoff"], row["prune"])
+        assert res.n_entries == row["entries"], row
+        assert int(res.count.sum()) == row["sum_count"], row
+        assert len(set(res.mmer.tolist())) == row["mmers"], row
+        assert dump_sha(res, row["K"], row["M"]) == row["sha256"], row
+
+
+@pytest.mark.parametrize("K,M", [(31, 7), (6, 3), (21, 5), (32, 8), (33, 7), (63, 7), (40, 1), (2, 1)])
+def test_random_vs_oracle(K, M):
+    rng = np.random.default_rng(K * 100 + M)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=3000)
+    reads = []
+    for _ in range(1500):
+        L = int(rng.integers(0, 260))
+        s = int(rng.integers(0, 3000 - L))
+        r = genome[s:s + L].copy()
+        m = rng.random(L) < 0.01
+        r[m] = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=int(m.sum()))
+        reads.append(r.tobytes())
+    bases, lens = kbin.pack_reads(reads)
+    for prune in (False, True):
+        ora = oracle.bin_reads(bases, lens, K, M, 1, prune)
+        res = gpu_result(bases, lens, K, M, 1, prune, batches=3)
+        assert res.n_kmers == ora.n_kmers
+        assert_same(res, ora)
+
+
+def test_explicit_ids_nonmonotone():
+    """ids are caller-supplied (process_read's read_id): lists keep REVERSE CALL
+    order, not id order (binning.c:1065-1068)."""
+    rng = np.random.default_rng(7)
+    reads = [b"ACGTACGTAC" * 5] * 20 + [rng.choice(np.frombuffer(b"ACGT", np.uint8), 60).tobytes() for _ in range(50)]
+    bases, lens = kbin.pack_reads(reads)
+    ids = rng.permutation(len(reads)).astype(np.int32) * 3 - 7
+    ora = oracle.bin_reads(bases, lens, 11, 4, 1, True, ids=ids)
+    res = gpu_result(bases, lens, 11, 4, 1, True, ids=ids, batches=2)
+    assert_same(res, ora)
+
+
+def test_large_lists():
+    """a key seen > 4096 times takes the chunk-sort + merge path"""
+    reads = [b"A" * 40] * 3000 + [b"ACGT" * 10] * 200
+    bases, lens = kbin.pack_reads(reads)
+    ora = oracle.bin_reads(bases, lens, 9, 3, 1, True)
+    res = gpu_result(bases, lens, 9, 3, 1, True)
+    assert int(res.count.max()) > 4096 * 4
+    assert_same(res, ora)
+
+
+def test_cutoffs():
+    bases, lens = oracle.read_fgets(kbin.REPO_ROOT / "tests/golden/reads.txt", 101)
+    for cutoff in (0, 2, 5):
+        ora = oracle.bin_reads(bases, lens, 15, 5, cutoff, True)
+        res = gpu_result(bases, lens, 15, 5, cutoff, True)
+        assert_same(res, ora)
+
+
+def test_device_generator_roundtrip():
+    import torch
+    n, L = 20000, 150
+    wpr = (L + 31) // 32
+    words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, 200000, 1000, 5)
+    torch.cuda.synchronize()
+    bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n, wpr, n * L)
+    assert (hl == L).all() and len(bases) == n * L
+    ora = oracle.bin_reads(bases, hl, 31, 7, 1, True)
+    with kbin.Engine(31, 7, cutoff=1, max_read_len=L) as eng:
+        eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
+        eng.finalize(True)
+        res = eng.export()
+    assert_same(res, ora)
+
+
+def test_alphabet_rejected():
+    """bytes outside ACGT are rejected loudly (alphabet)"""
+    with kbin.Engine(11, 4) as eng:
+        with pytest.raises(kbin.KbError) as ei:
+            eng.submit([b"ACGTNACGTACGTACG"])
+        assert ei.value.code == kbin.KB_EALPHABET
