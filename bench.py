@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Headline benchmark: canonical k-mers binned per second (BASELINE.json).
+
+One step = one full pass of the hot path over one resident batch of synthetic
+reads: k-mer offsets -> fused signature scan + (mmer,kmer) table insert/count
+-> low-abundance prune + compaction -> read-id placement -> per-key id order.
+Inputs are generated on the device before the timed region (seeded, SURVEY
+§8(d) C2 at N=1: 1M x 150 bp, genome 5 Mbp, 0.1% substitutions, seed 2,
+K=31 M=7, cutoff 1); outputs stay device-resident (CSR).
+
+N>1 (torchrun, one rank per GPU): every rank owns its own 1M-read shard
+(weak scaling) and k-mers are routed to the GPU that owns their canonical mmer
+with an RCCL all-to-all (genome-assembly_amd/kbin/dist.py).
+
+Prints ONE JSON line on rank 0 (contract in the task statement); extra
+objects: "roofline" for the dominant kernel (scan_insert) and "cpu_baseline"
+(the CPU oracle on a bounded sample of the same workload, rank 0 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+REPO = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "genome-assembly_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (loaded before libkbin: one HIP runtime per process)
+
+import kbin  # noqa: E402
+
+METRIC = "canonical k-mers binned/sec, 150bp k=31, at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes_per_read(L: int, K: int) -> float:
+    """ceil(L/4) (2-bit read) + n_k * (Kb + 12) per read, Kb = 8 B
+    (K<=32) or 16 B: per k-mer a slot-key read, a 4-B count read + 4-B write,
+    a 4-B occurrence/id write."""
+    nk = max(0, L - K + 1)
+    kb = 8 if K <= 32 else 16
+    return (L + 3) // 4 + nk * (kb + 12)
+
+
+def cpu_baseline(words, lens, n_sample, wpr, L, K, M, cutoff):
+    """CPU oracle (oracle/liboracle.so, single thread) on the first n_sample
+    reads of the same workload."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle  # test-infrastructure checker, used here only as the CPU baseline leg
+    bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n_sample, wpr,
+                                          n_sample * L)
+    t0 = time.perf_counter()
+    r = oracle.bin_reads(bases, hl, K, M, cutoff, True)
+    dt = time.perf_counter() - t0
+    return {"value": r.n_kmers / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+            "sample": f"first {n_sample} reads of the bench workload ({r.n_kmers} k-mers), "
+                      f"oracle/kb_oracle.c single-threaded, {dt:.2f} s, host nproc={os.cpu_count()}"}
+
+
+def load_traffic(tag: str):
+    """Per-launch HBM bytes of scan_insert from the committed rocprofv3 --pmc
+    passes (profiles/traffic.json, written by profiles/pmc_traffic.py)."""
+    p = REPO / "profiles" / "traffic.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get(tag)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU")
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--K", type=int, default=31)
+    ap.add_argument("--M", type=int, default=7)
+    ap.add_argument("--cutoff", type=int, default=1)
+    ap.add_argument("--genome", type=int, default=5_000_000)
+    ap.add_argument("--err-ppm", type=int, default=1000)
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=300_000,
+                    help="reads timed on the CPU oracle (0 = skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+
+    L, K, M = args.read_len, args.K, args.M
+    wpr = (L + 31) // 32
+    n = args.reads
+    words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    # rank r draws read indices [r*n, (r+1)*n) of one global stream: seed is
+    # per rank-shard so shards are disjoint slices of the same genome
+    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, args.genome,
+                               args.err_ppm, args.seed * 1000003 + rank, device=local)
+    torch.cuda.synchronize()
+
+    if world > 1:
+        from kbin import dist as kdist
+        runner = kdist.ShardedBinner(K, M, args.cutoff, L, device=local, group=None)
+        step = lambda: runner.step(words, lens, n, wpr, first_id=rank * n)  # noqa: E731
+        eng = runner.engine
+    else:
+        eng = kbin.Engine(K, M, cutoff=args.cutoff, max_read_len=L, device=local)
+
+        def step():
+            eng.reset()
+            eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, first_id=0)
+            eng.finalize(prune=True)
+
+    eng.set_timing(True)
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    scan_ms = []
+    tim = []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        t = eng.timing()
+        tim.append(t)
+        scan_ms.append(t["scan_insert_ms"] / max(1, t["scan_insert_launches"]))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    dev = eng.export_device()
+    n_kmers = int(dev["n_kmers"])          # occurrences this rank inserted (owned)
+    scanned = n * max(0, L - K + 1)         # occurrences this rank scanned
+    total_scanned = scanned * world
+    value = total_scanned * args.steps / elapsed
+
+    bpr = algorithmic_bytes_per_read(L, K)
+    avg_scan_ms = float(np.mean(scan_ms))
+    achieved = (bpr * n) / (avg_scan_ms * 1e-3) / 1e9  # GB/s, per launch
+    tag = f"n{n}_L{L}_K{K}_M{M}"
+    traffic = load_traffic(tag)
+    roof = {"bound": "hbm", "kernel": "scan_insert_kernel<1>" if K <= 31 else "scan_insert_kernel<2>",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+            "kernel_ms": round(avg_scan_ms, 4),
+            "bytes_per_kmer": round(bpr / max(1, L - K + 1), 3)}
+    phases = {k: round(float(np.mean([t[k] for t in tim])), 4)
+              for k in ("scan_insert_ms", "compact_ms", "place_ms", "sort_ms", "total_ms")}
+
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": f"C2: {n} x {L}bp reads per GPU, genome {args.genome} bp, "
+                               f"{args.err_ppm / 1e4:.2f}% substitutions, seed {args.seed}, "
+                               f"K={K} M={M}, prune cutoff {args.cutoff}",
+                   "reads_per_gpu": n, "read_len": L, "K": K, "M": M, "cutoff": args.cutoff,
+                   "genome_len": args.genome, "err_ppm": args.err_ppm,
+                   "parallelism": f"mmer-sharded x{world}" if world > 1 else "single GPU"},
+        "roofline": roof,
+        "phases_ms": phases,
+        "result": {"entries": int(dev["n_entries"]), "ids": int(dev["n_ids"]),
+                   "distinct": int(dev["n_distinct"]), "kmers_owned": n_kmers,
+                   "table_slots": int(tim[-1]["table_slots"])},
+    }
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(words, lens, min(args.cpu_sample, n), wpr, L, K, M,
+                                           args.cutoff)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
