@@ -170,7 +170,7 @@ def main():
             "kernel_ms": round(avg_scan_ms, 4),
             "bytes_per_kmer": round(bpr / max(1, L - K + 1), 3)}
     phases = {k: round(float(np.mean([t[k] for t in tim])), 4)
-              for k in ("scan_insert_ms", "compact_ms", "place_ms", "sort_ms", "total_ms")}
+              for k in ("scan_insert_ms", "sort_ms", "runs_ms", "emit_ms", "total_ms")}
 
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world,

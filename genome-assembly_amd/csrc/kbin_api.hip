@@ -4,8 +4,9 @@
 // and sequences the kernels of kbin_kernels.hip:
 //   submit   : H2D (pinned staging) + pack, or adopt device-packed reads;
 //              per-read k-mer offsets (device scan)
-//   finalize : zero table -> scan_insert per batch -> [retry bigger on
-//              overflow] -> compact(prune) -> place -> sort
+//   finalize : zero table -> scan_insert per batch (records) -> [retry
+//              bigger on overflow] -> radix sort by slot -> runs/prune/CSR ->
+//              emit read ids
 //   export   : D2H of the CSR
 #include <hip/hip_runtime.h>
 
@@ -93,16 +94,18 @@ struct kb_ctx {
     // finalize working set
     DevBuf<uint64_t> table;
     uint64_t slots = 0, learned_slots = 0;
-    DevBuf<uint32_t> occ_slot;
+    DevBuf<uint64_t> occ_a, occ_b;  // occurrence records, radix ping-pong
+    uint64_t* sorted = nullptr;
+    DevBuf<uint32_t> rs_counts;
     DevBuf<int32_t> read_ids;
-    DevBuf<uint32_t> slot_entry;
-    DevBuf<uint32_t> e_mmer, e_cnt, cursor, lists;
+    DevBuf<uint32_t> starts;
+    DevBuf<uint32_t> e_mmer, e_cnt;
     DevBuf<uint64_t> e_hi, e_lo, e_off;
-    DevBuf<uint32_t> ids_ord, ids_tmp;
     DevBuf<int32_t> ids_out;
     DevBuf<uint64_t> scratch;
-    DevBuf<uint32_t> misc;    // [0] status [1] n_distinct [4..8) list counts
-    DevBuf<uint64_t> totals;  // [0] n_entries [1] n_ids
+    DevBuf<uint32_t> misc;    // [0] status [1] n_distinct
+    DevBuf<uint64_t> totals;  // [0] n_entries [1] n_ids [2] runs
+    uint64_t* h_totals = nullptr;
     uint32_t* h_misc = nullptr;
 
     // results
@@ -160,6 +163,8 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     }
     e = hipHostMalloc((void**)&c->h_misc, 16 * sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
+    e = hipHostMalloc((void**)&c->h_totals, 4 * sizeof(uint64_t), hipHostMallocDefault);
+    if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
     if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(4) != hipSuccess) {
         kb_destroy(c);
         return fail(KB_ENOMEM, "device alloc");
@@ -185,11 +190,12 @@ extern "C" void kb_destroy(kb_ctx* c) {
     (void)hipSetDevice(c->dev);
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
-    c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_slot.release();
-    c->read_ids.release(); c->slot_entry.release(); c->e_mmer.release(); c->e_cnt.release();
-    c->cursor.release(); c->lists.release(); c->e_hi.release(); c->e_lo.release();
-    c->e_off.release(); c->ids_ord.release(); c->ids_tmp.release(); c->ids_out.release();
-    c->scratch.release(); c->misc.release(); c->totals.release();
+    c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
+    c->occ_b.release(); c->rs_counts.release(); c->read_ids.release(); c->starts.release();
+    c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
+    c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
+    c->misc.release(); c->totals.release();
+    if (c->h_totals) (void)hipHostFree(c->h_totals);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
     for (auto& ev : c->ev)
@@ -357,21 +363,31 @@ extern "C" int kb_get_timing(kb_ctx* c, kb_timing* out) {
 #define REC(i) \
     do { if (c->timing) HIPCHK(hipEventRecord(c->ev[i], c->s)); } while (0)
 
+static int log2u(uint64_t x) {
+    int b = 0;
+    while ((1ull << b) < x) b++;
+    return b;
+}
+
 extern "C" int kb_finalize(kb_ctx* c, int prune) {
     if (!c) return fail(KB_EINVAL, "null ctx");
     if (c->finalized) return fail(KB_ESTATE, "already finalized (call kb_reset)");
     int rc = set_device(c);
     if (rc) return rc;
-    if (c->n_occ > 0xFFFFFFFFull * 64)
-        return fail(KB_EOVERFLOW, "too many k-mers for one context");
+    if (c->n_occ >= 0xFFFFFFFFull)
+        return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
+                    (unsigned long long)c->n_occ);
     memset(&c->tm, 0, sizeof(c->tm));
     const int SW = c->KW == 1 ? 2 : 4;
-    // ---- table plan
+    const uint64_t N = c->n_occ;
+    // ---- table plan: ~0.6 load for the expected distinct keys
     uint64_t slots = c->p.table_slots;
     if (!slots) slots = c->learned_slots;
-    if (!slots) slots = next_pow2(std::max<uint64_t>(4096, c->n_occ / 4));
+    if (!slots) slots = next_pow2(std::max<uint64_t>(4096, N / 6));
     slots = std::max<uint64_t>(slots, 1024);
-    HIPCHK(c->occ_slot.ensure(c->n_occ));
+    HIPCHK(c->occ_a.ensure(N));
+    HIPCHK(c->occ_b.ensure(N));
+    HIPCHK(c->ids_out.ensure(N));
     // ordinal -> read id, concatenated over batches
     HIPCHK(c->read_ids.ensure(c->n_reads));
     for (auto& b : c->batches)
@@ -379,16 +395,18 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
                               hipMemcpyDeviceToDevice, c->s));
     uint32_t status = 0, ndist = 0;
     for (int attempt = 0;; attempt++) {
-        if (slots > (1ull << 32))
-            return fail(KB_ENOMEM, "table would need more than 2^32 slots");
+        if (slots > (1ull << 32) - 1)
+            return fail(KB_ENOMEM, "table would need 2^32 slots or more");
         hipError_t e = c->table.ensure(slots * SW);
-        if (e != hipSuccess) return fail(KB_ENOMEM, "table of %llu slots: %s",
-                                         (unsigned long long)slots, hipGetErrorString(e));
+        if (e != hipSuccess)
+            return fail(KB_ENOMEM, "table of %llu slots: %s", (unsigned long long)slots,
+                        hipGetErrorString(e));
         c->slots = slots;
         REC(0);
         HIPCHK(hipMemsetAsync(c->table.p, 0, slots * SW * sizeof(uint64_t), c->s));
         HIPCHK(hipMemsetAsync(c->misc.p, 0, 2 * sizeof(uint32_t), c->s));
         REC(1);
+        c->tm.scan_insert_launches = 0;
         for (auto& b : c->batches) {
             ScanArgs a{};
             a.words = b.words;
@@ -397,7 +415,10 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
             a.n_reads = b.n_reads;
             a.table = c->table.p;
             a.mask = slots - 1;
-            a.occ_slot = c->occ_slot.p + b.occ_base;
+            a.occ = c->occ_a.p;
+            a.occ_base = b.occ_base;
+            a.n_occ_total = N;
+            a.ord_base = (uint32_t)b.ord_base;
             a.n_distinct = c->misc.p + 1;
             a.status = c->misc.p;
             a.max_distinct = (uint32_t)std::min<uint64_t>(slots - slots / 8, 0xFFFFFFFFull);
@@ -418,61 +439,42 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
         slots *= 4;
     }
     c->n_distinct = ndist;
-    if (!c->p.table_slots) c->learned_slots = std::max<uint64_t>(1024, next_pow2((uint64_t)ndist * 2));
-    if (c->timing) {
-        HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));
-    }
-    // ---- prune + compact
+    // next finalize on this context: ~0.6 load for the distinct keys seen now
+    if (!c->p.table_slots)
+        c->learned_slots = std::max<uint64_t>(1024, next_pow2((uint64_t)ndist * 5 / 3 + 1));
+    // ---- stable radix sort of the records by slot
+    const int key_bits = log2u(slots);
+    HIPCHK(c->rs_counts.ensure(radix_counts_elems(N)));
     const uint64_t ne_cap = (uint64_t)ndist + 1;
-    HIPCHK(c->slot_entry.ensure(slots));
+    HIPCHK(c->scratch.ensure(std::max({radix_scratch_elems(N), runs_scratch_elems(N, ne_cap),
+                                       c->scratch.cap})));
+    HIPCHK(launch_radix_sort(c->occ_a.p, c->occ_b.p, N, key_bits, c->rs_counts.p, c->scratch.p,
+                             c->scratch.cap, &c->sorted, c->s));
+    c->tm.sort_passes = (uint32_t)((key_bits + 7) / 8);
+    REC(3);
+    // ---- runs -> counts -> prune -> CSR entries
+    HIPCHK(c->starts.ensure(ne_cap + 1));
     HIPCHK(c->e_mmer.ensure(ne_cap));
     HIPCHK(c->e_cnt.ensure(ne_cap));
     HIPCHK(c->e_hi.ensure(ne_cap));
     HIPCHK(c->e_lo.ensure(ne_cap));
     HIPCHK(c->e_off.ensure(ne_cap));
-    HIPCHK(c->scratch.ensure(std::max<uint64_t>(compact_scratch_elems(slots), c->scratch.cap)));
     const uint32_t keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
-    REC(3);
-    HIPCHK(launch_compact(c->table.p, slots, c->KW, c->p.K, keep_gt, c->slot_entry.p, c->e_mmer.p,
-                          c->e_hi.p, c->e_lo.p, c->e_cnt.p, c->e_off.p, c->scratch.p,
-                          c->scratch.cap, c->totals.p, c->s));
+    HIPCHK(launch_runs(c->sorted, N, c->table.p, c->KW, keep_gt, c->starts.p, c->read_ids.p,
+                       c->ids_out.p, ne_cap, c->e_mmer.p, c->e_hi.p, c->e_lo.p, c->e_cnt.p,
+                       c->e_off.p, c->scratch.p, c->scratch.cap, c->totals.p, c->s));
     REC(4);
-    uint64_t tot[2];
-    HIPCHK(hipMemcpyAsync(tot, c->totals.p, sizeof(tot), hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
-    c->n_entries = tot[0];
-    c->n_ids = tot[1];
-    // ---- place
-    HIPCHK(c->cursor.ensure(ne_cap));
-    HIPCHK(c->ids_ord.ensure(c->n_ids));
-    HIPCHK(c->ids_out.ensure(c->n_ids));
-    HIPCHK(hipMemsetAsync(c->cursor.p, 0, c->n_entries * sizeof(uint32_t), c->s));
-    for (auto& b : c->batches) {
-        PlaceArgs a{};
-        a.occ_slot = c->occ_slot.p + b.occ_base;
-        a.kmer_base = b.kmer_base;
-        a.n_reads = b.n_reads;
-        a.n_occ = b.n_occ;
-        a.slot_entry = c->slot_entry.p;
-        a.e_off = c->e_off.p;
-        a.cursor = c->cursor.p;
-        a.ids_ord = c->ids_ord.p;
-        a.ord_base = (uint32_t)b.ord_base;
-        HIPCHK(launch_place(a, c->s));
-    }
     REC(5);
-    // ---- order ids per key
-    HIPCHK(c->lists.ensure(2 * ne_cap));
-    HIPCHK(c->ids_tmp.ensure(c->n_ids));
-    HIPCHK(launch_sort(c->e_off.p, c->e_cnt.p, c->n_entries, c->ids_ord.p, c->ids_tmp.p,
-                       c->read_ids.p, c->ids_out.p, c->lists.p, c->misc.p + 4, c->s));
-    REC(6);
+    HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
+    c->n_entries = c->h_totals[0];
+    c->n_ids = c->h_totals[1];
     if (c->timing) {
-        HIPCHK(hipEventElapsedTime(&c->tm.compact_ms, c->ev[3], c->ev[4]));
-        HIPCHK(hipEventElapsedTime(&c->tm.place_ms, c->ev[4], c->ev[5]));
-        HIPCHK(hipEventElapsedTime(&c->tm.sort_ms, c->ev[5], c->ev[6]));
-        HIPCHK(hipEventElapsedTime(&c->tm.total_ms, c->ev[0], c->ev[6]));
+        HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));
+        HIPCHK(hipEventElapsedTime(&c->tm.sort_ms, c->ev[2], c->ev[3]));
+        HIPCHK(hipEventElapsedTime(&c->tm.runs_ms, c->ev[3], c->ev[4]));
+        HIPCHK(hipEventElapsedTime(&c->tm.emit_ms, c->ev[4], c->ev[5]));
+        HIPCHK(hipEventElapsedTime(&c->tm.total_ms, c->ev[0], c->ev[5]));
     }
     c->tm.table_slots = slots;
     c->finalized = true;

@@ -24,29 +24,20 @@ constexpr uint32_t ST_ALPHABET = 4u;     // byte outside ACGT in packed input
 struct ScanArgs {
     const uint64_t* words;     // packed reads, RW words per read
     const uint32_t* lens;      // bases per read
-    const uint64_t* kmer_base; // [n_reads+1] first occurrence index of read r
+    const uint64_t* kmer_base; // [n_reads+1] first occurrence index of read r (batch-local)
     uint64_t n_reads;
     uint64_t* table;           // slots * SW words
     uint64_t mask;             // slots - 1
-    uint32_t* occ_slot;        // [n_kmers of batch] slot of each occurrence
+    uint64_t* occ;             // [n_occ_total] records (slot << 32 | ordinal), reversed
+    uint64_t occ_base;         // first occurrence index of this batch
+    uint64_t n_occ_total;
+    uint32_t ord_base;         // call ordinal of the batch's first read
     uint32_t* n_distinct;      // global distinct-key counter
     uint32_t* status;
     uint32_t max_distinct;
     uint32_t max_probe;
     int RW;                    // words per read
     int K, M;
-};
-
-struct PlaceArgs {
-    const uint32_t* occ_slot;
-    const uint64_t* kmer_base; // [n_reads+1]
-    uint64_t n_reads;
-    uint64_t n_occ;
-    const uint32_t* slot_entry;
-    const uint64_t* e_off;
-    uint32_t* cursor;
-    uint32_t* ids_ord;         // ordinals placed per entry
-    uint32_t ord_base;
 };
 
 // launch helpers implemented in kbin_kernels.hip (all asynchronous on `s`)
@@ -58,17 +49,16 @@ hipError_t launch_kmer_base(const uint32_t* d_lens, uint64_t n_reads, int K,
                             hipStream_t s);
 uint64_t kmer_base_scratch_elems(uint64_t n_reads);
 hipError_t launch_scan_insert(const ScanArgs& a, int KW, hipStream_t s);
-hipError_t launch_compact(const uint64_t* table, uint64_t slots, int KW, int K,
-                          uint32_t cutoff_keep_gt, uint32_t* slot_entry,
-                          uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo,
-                          uint32_t* e_cnt, uint64_t* e_off,
-                          uint64_t* scratch, uint64_t scratch_n,
-                          uint64_t* d_totals, hipStream_t s);
-uint64_t compact_scratch_elems(uint64_t slots);
-hipError_t launch_place(const PlaceArgs& a, hipStream_t s);
-hipError_t launch_sort(const uint64_t* e_off, const uint32_t* e_cnt, uint64_t n_entries,
-                       uint32_t* ids_ord, uint32_t* ids_tmp, const int32_t* read_ids,
-                       int32_t* ids_out, uint32_t* lists, uint32_t* list_counts,
+uint64_t radix_counts_elems(uint64_t n);
+uint64_t radix_scratch_elems(uint64_t n);
+hipError_t launch_radix_sort(uint64_t* a, uint64_t* b, uint64_t n, int key_bits, uint32_t* counts,
+                             uint64_t* scratch, uint64_t scratch_n, uint64_t** sorted,
+                             hipStream_t s);
+uint64_t runs_scratch_elems(uint64_t n, uint64_t max_runs);
+hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int KW,
+                       uint32_t keep_gt, uint32_t* starts, const int32_t* read_ids,
+                       int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
+                       uint64_t* e_off, uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals,
                        hipStream_t s);
 hipError_t launch_fill_ids(int32_t* d_ids, uint64_t n, int32_t first, hipStream_t s);
 hipError_t launch_generate(uint64_t* d_words, uint32_t* d_lens, uint64_t n_reads,

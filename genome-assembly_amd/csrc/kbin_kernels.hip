@@ -8,12 +8,18 @@
 //                 reduction, the "sticky" signature chain walked wave-uniformly,
 //                 then every k-mer key inserted/counted in one open-addressed
 //                 (mmer, kmer) table with device atomics.
-//   compact       prune (count > cutoff) + stream compaction into a CSR.
-//   place         read-id placement per surviving key (atomic cursor).
-//   sort          per key, ids in reverse call order (descending ordinal),
-//                 mapped to the caller's read ids.
+//                 Each occurrence leaves one record (slot << 32 | call ordinal),
+//                 written in descending call order.
+//   radix sort    stable LSD sort of the records by slot (8-bit digits, LDS
+//                 multisplit): every key becomes one run whose ordinals are
+//                 already descending = the reference's prepend order.
+//   runs          run boundaries -> counts -> prune (count > cutoff) ->
+//                 CSR entries (stream compaction) and the surviving runs'
+//                 read ids, copied coalesced.
 //
 // All integer work: no MFMA.  Roofline = HBM.
+#include <algorithm>
+
 #include "kbin_internal.h"
 
 namespace kb {
@@ -346,13 +352,16 @@ struct Key {
     }
 };
 
-// Insert one occurrence; returns the slot index (NONE on probe-limit failure).
+
+// Find-or-insert one key; returns its slot index (NONE on probe-limit failure).
 // Protocol (DESIGN.md "Table protocol"): claim by 64-bit CAS of the claim word
 // on an empty slot; the winner then publishes the other words with atomic
-// stores, each carrying its own marker.  A reader that finds an unpublished
-// word re-reads it with an atomic RMW (coherent across XCD L2s) and, if still
-// unpublished, retries the same slot on its next loop trip -- no lane ever
-// waits inside a branch another lane of its wave must leave.
+// stores, each carrying its own marker (tag = mmer+1 != 0, PUB bit).  A reader
+// that finds an unpublished word re-reads it with an atomic RMW (coherent
+// across the XCD L2s) and, if still unpublished, retries the same slot on its
+// next loop trip -- no lane ever waits inside a branch that another lane of
+// its own wave has to leave first.  Words only ever go empty -> final, so a
+// stale read can only show an older state, which the CAS / RMW re-read fixes.
 template <int KW>
 DEV uint32_t table_insert(uint64_t* __restrict__ table, uint64_t mask, const Key<KW>& k,
                           uint32_t tag, uint32_t max_probe, bool& is_new) {
@@ -366,50 +375,54 @@ DEV uint32_t table_insert(uint64_t* __restrict__ table, uint64_t mask, const Key
         uint64_t w0 = atomic_load_u64(s);
         uint32_t t = atomic_load_u32(tagp);
         uint64_t w1 = 0;
-        if (KW == 2) w1 = atomic_load_u64(s + 1);
+        if constexpr (KW == 2) w1 = atomic_load_u64(s + 1);
         if (w0 == 0) {
             const uint64_t old = atomicCAS((unsigned long long*)s, 0ull, (unsigned long long)k.a);
             if (old == 0) {
-                if constexpr (KW == 2) __hip_atomic_store(s + 1, k.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if constexpr (KW == 2)
+                    __hip_atomic_store(s + 1, k.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(tagp, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicAdd(tagp + 1, 1u);
                 is_new = true;
                 return (uint32_t)idx;
             }
             w0 = old;
-            t = 0;   // anything loaded before the CAS may predate the claim
+            t = 0;  // anything loaded before the CAS may predate the claim
             w1 = 0;
         }
         if (w0 == k.a) {
             bool pending = false;
-            if (KW == 2) {
+            if constexpr (KW == 2) {
                 if (!(w1 & PUB)) w1 = atomicOr((unsigned long long*)(s + 1), 0ull);
                 if (!(w1 & PUB)) pending = true;
             }
             if (t == 0) t = atomicOr(tagp, 0u);
             if (t == 0) pending = true;
             if (pending) continue;  // claimed but not yet published: re-read next trip
-            if (t == tag && (KW == 1 || w1 == k.b)) {
-                atomicAdd(tagp + 1, 1u);
-                return (uint32_t)idx;
-            }
+            if (t == tag && (KW == 1 || w1 == k.b)) return (uint32_t)idx;
         }
         idx = (idx + 1) & mask;
         if (++probes > max_probe) return NONE;
     }
 }
 
+// One wavefront per read.  For every k-mer occurrence it emits the record
+//   (slot << 32) | call_ordinal
+// at position n_total-1-(global occurrence index): occurrences are written in
+// DESCENDING call order, so the stable radix sort by slot that follows leaves
+// each key's ordinals descending -- the reference's prepend order
+// (binning.c:1061-1068) -- with no per-key sort.
 template <int KW>
 __global__ __launch_bounds__(256) void scan_insert_kernel(ScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int RW = A.RW, K = A.K, M = A.M;
-    const int W = K - M + 1;                          // mmer starts per k-mer window
+    const int W = K - M + 1;                   // mmer starts per k-mer window (<= 64)
     const uint32_t maskM = (1u << (2 * M)) - 1u;
-    const uint32_t halfM = 1u << (2 * M - 1);         // s < halfM <=> first base T/G <=> complement wins
+    const uint32_t halfM = 1u << (2 * M - 1);  // s < halfM <=> first base T/G <=> complement wins
     uint64_t* sw = smem + wid * (RW + 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    uint64_t* const occ_end = A.occ + A.n_occ_total - 1 - A.occ_base;
     uint32_t local_new = 0;
     uint32_t st = 0;
 
@@ -422,7 +435,8 @@ __global__ __launch_bounds__(256) void scan_insert_kernel(ScanArgs A) {
         for (int w = lane; w < RW; w += 64) sw[w] = A.words[r * RW + w];
         if (lane == 0) sw[RW] = 0;
         wave_sync();
-        const uint64_t obase = A.kmer_base[r];
+        uint64_t* const orow = occ_end - A.kmer_base[r];
+        const uint64_t ordv = (uint64_t)(A.ord_base + (uint32_t)r);
 
         int seg_lo = 0, seg_hi = -1;  // current sticky segment [seg_lo, seg_hi], sig = seg_hi
         for (int i0 = 0; i0 < nK; i0 += 64) {
@@ -474,7 +488,7 @@ __global__ __launch_bounds__(256) void scan_insert_kernel(ScanArgs A) {
                 const uint32_t slot = table_insert<KW>(A.table, A.mask, key, mm + 1u, A.max_probe, is_new);
                 if (slot == NONE) st |= ST_PROBE_LIMIT;
                 local_new += is_new ? 1u : 0u;
-                A.occ_slot[obase + i] = slot;
+                *(orow - i) = ((uint64_t)slot << 32) | ordv;
             }
         }
     }
@@ -507,32 +521,251 @@ hipError_t launch_scan_insert(const ScanArgs& a, int KW, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// compact: prune (binning.c:1094-1102: keep iff count > cutoff) + CSR build
+// LSD radix sort of the occurrence records by their slot field (bits 32..),
+// 8-bit digits, stable: per pass a tile histogram, one device-wide exclusive
+// scan of the (digit-major, tile-minor) counts, and a scatter that ranks each
+// tile in LDS (wave multisplit by 8 ballots) and writes digit runs coalesced.
 // ---------------------------------------------------------------------------
-// scratch layout: [0, nb) kept-count partials, [nb, 2nb) id-count partials
-DEV void slot_info(const uint64_t* __restrict__ table, int SW, uint64_t slot, uint32_t keep_gt,
-                   uint32_t& kept, uint32_t& cnt) {
-    const uint64_t tc = table[slot * SW + (SW == 2 ? 1 : 2)];
-    const uint32_t tag = (uint32_t)tc;
-    cnt = (uint32_t)(tc >> 32);
-    kept = (tag != 0 && cnt > keep_gt) ? 1u : 0u;
+constexpr int RS_ITEMS = 16;
+constexpr int RS_TILE = 256 * RS_ITEMS;  // 4096 records per block
+
+__global__ __launch_bounds__(256) void rs_hist_kernel(const uint64_t* __restrict__ in, uint32_t n,
+                                                      int shift, uint32_t* __restrict__ counts,
+                                                      uint32_t n_tiles) {
+    __shared__ uint32_t h[4][256];
+    const int t = threadIdx.x, wid = t >> 6;
+#pragma unroll
+    for (int w = 0; w < 4; w++) h[w][t] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    uint32_t d[RS_ITEMS];
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++) {
+        const uint64_t k = base + (uint64_t)j * 256 + t;
+        d[j] = k < n ? (uint32_t)(in[k] >> shift) & 255u : 256u;
+    }
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++)
+        if (d[j] < 256u) atomicAdd(&h[wid][d[j]], 1u);
+    __syncthreads();
+    counts[(uint64_t)t * n_tiles + blockIdx.x] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
 }
 
-__global__ __launch_bounds__(256) void compact_partials_kernel(const uint64_t* __restrict__ table,
-                                                               uint64_t slots, int SW,
-                                                               uint32_t keep_gt,
-                                                               uint64_t* __restrict__ part,
-                                                               uint64_t nb) {
+__global__ __launch_bounds__(256) void rs_scatter_kernel(const uint64_t* __restrict__ in,
+                                                         uint64_t* __restrict__ out, uint32_t n,
+                                                         int shift, const uint32_t* __restrict__ offs,
+                                                         uint32_t n_tiles) {
+    __shared__ uint64_t buf[RS_TILE];  // 32 KiB: the tile in local digit order
+    __shared__ uint32_t wcnt[4][256];
+    __shared__ uint32_t lstart[256];
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t sh[4];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t base = (uint64_t)tile * RS_TILE;
+    const uint32_t tn = (uint32_t)min((uint64_t)RS_TILE, (uint64_t)n - base);
+    uint64_t v[RS_ITEMS];
+    uint32_t dg[RS_ITEMS];
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++) {
+        const uint32_t li = (uint32_t)j * 256u + t;
+        v[j] = li < tn ? in[base + li] : 0ull;
+        dg[j] = (uint32_t)(v[j] >> shift) & 255u;
+    }
+#pragma unroll
+    for (int w = 0; w < 4; w++) wcnt[w][t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++)
+        if ((uint32_t)j * 256u + t < tn) atomicAdd(&wcnt[wid][dg[j]], 1u);
+    __syncthreads();
+    const uint32_t c = wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan256<uint32_t>(c, sh, tot);
+    lstart[t] = ex;
+    run[t] = 0;
+    gbase[t] = offs[(uint64_t)t * n_tiles + tile];
+#pragma unroll
+    for (int w = 0; w < 4; w++) wcnt[w][t] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++) {
+        const bool valid = (uint32_t)j * 256u + t < tn;
+        const uint32_t d = dg[j];
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bl = __ballot(bit);
+            m &= bit ? bl : ~bl;
+        }
+        const uint32_t peer = (uint32_t)__popcll(m & lt);
+        if (valid && peer == 0) wcnt[wid][d] = (uint32_t)__popcll(m);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = lstart[d] + run[d] + peer;
+            for (int w = 0; w < wid; w++) pos += wcnt[w][d];
+            buf[pos] = v[j];
+        }
+        __syncthreads();
+        run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+        wcnt[0][t] = 0;
+        wcnt[1][t] = 0;
+        wcnt[2][t] = 0;
+        wcnt[3][t] = 0;
+        __syncthreads();
+    }
+    for (uint32_t i = t; i < tn; i += 256) {
+        const uint64_t e = buf[i];
+        const uint32_t d = (uint32_t)(e >> shift) & 255u;
+        out[gbase[d] + (i - lstart[d])] = e;
+    }
+}
+
+// generic exclusive scan of a u32 array (values sum < 2^32), in place
+__global__ __launch_bounds__(256) void scan_u32_partials_kernel(const uint32_t* __restrict__ a, uint64_t n,
+                                                                uint64_t* __restrict__ part) {
+    __shared__ uint64_t sh[4];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; j++)
+        if (base + j < n) s += a[base + j];
+    s = block_sum256(s, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void scan_u32_apply_kernel(uint32_t* __restrict__ a, uint64_t n,
+                                                             const uint64_t* __restrict__ part) {
+    __shared__ uint64_t sh[4];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; j++) {
+        v[j] = base + j < n ? a[base + j] : 0u;
+        s += v[j];
+    }
+    uint64_t tot;
+    uint64_t run = block_excl_scan256(s, sh, tot) + part[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; j++) {
+        if (base + j < n) a[base + j] = (uint32_t)run;
+        run += v[j];
+    }
+}
+
+static hipError_t scan_u32(uint32_t* a, uint64_t n, uint64_t* scratch, uint64_t scratch_n, hipStream_t s) {
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (!nb) return hipSuccess;
+    if (scratch_n < nb + 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(scan_u32_partials_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, n, scratch);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch, nb, scratch + nb);
+    hipLaunchKernelGGL(scan_u32_apply_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, n, scratch);
+    return hipGetLastError();
+}
+
+uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + RS_TILE - 1) / RS_TILE); }
+
+uint64_t radix_scratch_elems(uint64_t n) {
+    return (radix_counts_elems(n) + SCAN_TILE - 1) / SCAN_TILE + 2;
+}
+
+hipError_t launch_radix_sort(uint64_t* a, uint64_t* b, uint64_t n, int key_bits, uint32_t* counts,
+                             uint64_t* scratch, uint64_t scratch_n, uint64_t** sorted,
+                             hipStream_t s) {
+    *sorted = a;
+    if (n == 0) return hipSuccess;
+    if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t n_tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    uint64_t* src = a;
+    uint64_t* dst = b;
+    for (int lo = 0; lo < key_bits; lo += 8) {
+        const int shift = 32 + lo;
+        hipLaunchKernelGGL(rs_hist_kernel, dim3(n_tiles), dim3(256), 0, s, src, (uint32_t)n, shift,
+                           counts, n_tiles);
+        hipError_t e = scan_u32(counts, 256ull * n_tiles, scratch, scratch_n, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(rs_scatter_kernel, dim3(n_tiles), dim3(256), 0, s, src, dst, (uint32_t)n,
+                           shift, counts, n_tiles);
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+    }
+    *sorted = src;
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// runs: after the sort every key is one contiguous run of records.
+//   run length = list length (binning.c:1094-1100 counts the list);
+//   prune keeps runs longer than the cutoff (binning.c:1102);
+//   survivors become CSR entries in slot order (= hash order, like the
+//   reference's bucket order, not part of the contract).
+// ---------------------------------------------------------------------------
+DEV uint32_t slot_of(uint64_t rec) { return (uint32_t)(rec >> 32); }
+
+DEV uint32_t is_head(const uint64_t* __restrict__ S, uint64_t k) {
+    return (k == 0 || slot_of(S[k]) != slot_of(S[k - 1])) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void heads_partials_kernel(const uint64_t* __restrict__ S, uint64_t n,
+                                                             uint64_t* __restrict__ part) {
     __shared__ uint64_t sh[4];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
-    uint64_t nk = 0, ni = 0;
+    uint64_t c = 0;
     for (int j = 0; j < SCAN_ITEMS; j++) {
-        const uint64_t slot = base + (uint64_t)j * 256 + threadIdx.x;  // coalesced
-        if (slot < slots) {
-            uint32_t kept, cnt;
-            slot_info(table, SW, slot, keep_gt, kept, cnt);
-            nk += kept;
-            ni += kept ? cnt : 0;
+        const uint64_t k = base + (uint64_t)j * 256 + threadIdx.x;
+        if (k < n) c += is_head(S, k);
+    }
+    c = block_sum256(c, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(256) void heads_write_kernel(const uint64_t* __restrict__ S, uint64_t n,
+                                                          const uint64_t* __restrict__ part,
+                                                          uint32_t* __restrict__ starts) {
+    __shared__ uint64_t sh[4];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+    uint64_t run = part[blockIdx.x];
+    for (int j = 0; j < SCAN_ITEMS; j++) {
+        const uint64_t k = base + (uint64_t)j * 256 + threadIdx.x;
+        const uint32_t h = k < n ? is_head(S, k) : 0u;
+        uint64_t tot;
+        const uint64_t ex = block_excl_scan256((uint64_t)h, sh, tot);
+        if (h) starts[run + ex] = (uint32_t)k;
+        run += tot;
+    }
+}
+
+__global__ void runs_total_kernel(const uint64_t* __restrict__ tot_runs, uint64_t n,
+                                  uint32_t* __restrict__ starts, uint64_t* __restrict__ totals) {
+    const uint64_t D = *tot_runs;
+    starts[D] = (uint32_t)n;
+    totals[2] = D;
+}
+
+// per run: kept flag / kept length partials
+__global__ __launch_bounds__(256) void runs_partials_kernel(const uint32_t* __restrict__ starts,
+                                                            const uint64_t* __restrict__ totals,
+                                                            uint32_t keep_gt, uint64_t* __restrict__ part,
+                                                            uint64_t nb) {
+    __shared__ uint64_t sh[4];
+    const uint64_t D = totals[2];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+    uint64_t nk = 0, ni = 0;
+    if (base < D) {
+        for (int j = 0; j < SCAN_ITEMS; j++) {
+            const uint64_t r = base + (uint64_t)j * 256 + threadIdx.x;
+            if (r < D) {
+                const uint32_t len = starts[r + 1] - starts[r];
+                if (len > keep_gt) {
+                    nk++;
+                    ni += len;
+                }
+            }
         }
     }
     nk = block_sum256(nk, sh);
@@ -543,27 +776,45 @@ __global__ __launch_bounds__(256) void compact_partials_kernel(const uint64_t* _
     }
 }
 
-__global__ __launch_bounds__(256) void compact_write_kernel(
-    const uint64_t* __restrict__ table, uint64_t slots, int SW, int K, uint32_t keep_gt,
-    const uint64_t* __restrict__ part, uint64_t nb, uint32_t* __restrict__ slot_entry,
-    uint32_t* __restrict__ e_mmer, uint64_t* __restrict__ e_hi, uint64_t* __restrict__ e_lo,
-    uint32_t* __restrict__ e_cnt, uint64_t* __restrict__ e_off) {
+// per 256-run round: prune, write CSR entries, then the block copies the
+// round's records (a contiguous span of S) into the id array -- records are
+// already in descending call order inside each run (see scan_insert)
+__global__ __launch_bounds__(256) void runs_write_kernel(
+    const uint64_t* __restrict__ S, const uint32_t* __restrict__ starts,
+    const uint64_t* __restrict__ totals, uint32_t keep_gt, const uint64_t* __restrict__ part,
+    uint64_t nb, const uint64_t* __restrict__ table, int SW, const int32_t* __restrict__ read_ids,
+    int32_t* __restrict__ ids_out, uint32_t* __restrict__ e_mmer, uint64_t* __restrict__ e_hi,
+    uint64_t* __restrict__ e_lo, uint32_t* __restrict__ e_cnt, uint64_t* __restrict__ e_off) {
     __shared__ uint64_t sh[4];
+    __shared__ uint32_t rs[257];   // run starts of the round (+ end)
+    __shared__ uint32_t ro[256];   // id offset of each run, NONE if pruned
+    const uint64_t D = totals[2];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+    if (base >= D) return;  // uniform per block
     uint64_t ent = part[blockIdx.x];
     uint64_t ids = part[nb + blockIdx.x];
-    // process the tile in SCAN_ITEMS coalesced rounds of 256 slots
     for (int j = 0; j < SCAN_ITEMS; j++) {
-        const uint64_t slot = base + (uint64_t)j * 256 + threadIdx.x;
-        uint32_t kept = 0, cnt = 0;
-        if (slot < slots) slot_info(table, SW, slot, keep_gt, kept, cnt);
+        const uint64_t r0 = base + (uint64_t)j * 256;
+        if (r0 >= D) break;  // uniform
+        const uint64_t r = r0 + threadIdx.x;
+        uint32_t len = 0, kept = 0, st = 0;
+        if (r < D) {
+            st = starts[r];
+            len = starts[r + 1] - st;
+            kept = len > keep_gt ? 1u : 0u;
+        }
         uint64_t tk, ti;
         const uint64_t pk = block_excl_scan256((uint64_t)kept, sh, tk);
-        const uint64_t pi = block_excl_scan256((uint64_t)(kept ? cnt : 0), sh, ti);
-        if (slot < slots) {
+        const uint64_t pi = block_excl_scan256((uint64_t)(kept ? len : 0u), sh, ti);
+        const uint32_t nr = (uint32_t)min((uint64_t)256, D - r0);
+        if (r < D) {
+            rs[threadIdx.x] = st;
+            ro[threadIdx.x] = kept ? (uint32_t)(ids + pi) : NONE;
+            if (threadIdx.x == nr - 1) rs[nr] = st + len;
             if (kept) {
                 const uint64_t e = ent + pk;
-                const uint64_t* s = table + slot * SW;
+                const uint32_t slot = slot_of(S[st]);
+                const uint64_t* s = table + (uint64_t)slot * SW;
                 const uint64_t tc = s[SW == 2 ? 1 : 2];
                 e_mmer[e] = (uint32_t)tc - 1u;
                 if (SW == 2) {
@@ -575,323 +826,71 @@ __global__ __launch_bounds__(256) void compact_write_kernel(
                     e_hi[e] = a >> 1;
                     e_lo[e] = (a << 63) | b;
                 }
-                e_cnt[e] = cnt;
+                e_cnt[e] = len;
                 e_off[e] = ids + pi;
-                slot_entry[slot] = (uint32_t)e;
-            } else {
-                slot_entry[slot] = NONE;
             }
         }
+        __syncthreads();
+        // copy the round's records: [rs[0], rs[nr]) -- coalesced reads/writes
+        const uint32_t k_lo = rs[0], k_hi = rs[nr];
+        for (uint32_t k = k_lo + threadIdx.x; k < k_hi; k += 256) {
+            uint32_t lo = 0, hi = nr;  // last run with rs[run] <= k
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (rs[mid] <= k) lo = mid; else hi = mid;
+            }
+            const uint32_t off = ro[lo];
+            if (off != NONE) ids_out[off + (k - rs[lo])] = read_ids[(uint32_t)S[k]];
+        }
+        __syncthreads();
         ent += tk;
         ids += ti;
     }
-    (void)K;
 }
 
-uint64_t compact_scratch_elems(uint64_t slots) {
-    return 2 * ((slots + SCAN_TILE - 1) / SCAN_TILE) + 2;
+__global__ void entries_total_kernel(const uint64_t* __restrict__ tk, const uint64_t* __restrict__ ti,
+                                     uint64_t* __restrict__ e_off, uint64_t* __restrict__ totals) {
+    totals[0] = *tk;
+    totals[1] = *ti;
+    e_off[*tk] = *ti;
 }
 
-__global__ void compact_totals_kernel(const uint64_t* __restrict__ part, uint64_t nb,
-                                      const uint64_t* __restrict__ tot_k,
-                                      const uint64_t* __restrict__ tot_i,
-                                      uint64_t* __restrict__ e_off, uint64_t* __restrict__ totals) {
-    const uint64_t nk = *tot_k, ni = *tot_i;
-    totals[0] = nk;
-    totals[1] = ni;
-    e_off[nk] = ni;
-    (void)part;
-    (void)nb;
-}
-
-hipError_t launch_compact(const uint64_t* table, uint64_t slots, int KW, int K, uint32_t keep_gt,
-                          uint32_t* slot_entry, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo,
-                          uint32_t* e_cnt, uint64_t* e_off, uint64_t* scratch, uint64_t scratch_n,
-                          uint64_t* d_totals, hipStream_t s) {
+hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int KW,
+                       uint32_t keep_gt, uint32_t* starts, const int32_t* read_ids,
+                       int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
+                       uint64_t* e_off, uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals,
+                       hipStream_t s) {
     const int SW = KW == 1 ? 2 : 4;
-    const uint64_t nb = (slots + SCAN_TILE - 1) / SCAN_TILE;
-    if (scratch_n < 2 * nb + 2) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(compact_partials_kernel, dim3((unsigned)nb), dim3(256), 0, s, table, slots,
-                       SW, keep_gt, scratch, nb);
-    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch, nb,
-                       scratch + 2 * nb);
-    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch + nb, nb,
-                       scratch + 2 * nb + 1);
-    hipLaunchKernelGGL(compact_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, table, slots, SW,
-                       K, keep_gt, scratch, nb, slot_entry, e_mmer, e_hi, e_lo, e_cnt, e_off);
-    hipLaunchKernelGGL(compact_totals_kernel, dim3(1), dim3(1), 0, s, scratch, nb,
-                       scratch + 2 * nb, scratch + 2 * nb + 1, e_off, d_totals);
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const uint64_t nbr = (max_runs + SCAN_TILE - 1) / SCAN_TILE;
+    if (scratch_n < std::max(nb + 1, 2 * nbr + 2)) return hipErrorInvalidValue;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_totals, 0, 3 * sizeof(uint64_t), s);
+        if (e == hipSuccess) e = hipMemsetAsync(e_off, 0, sizeof(uint64_t), s);
+        return e;
+    }
+    hipLaunchKernelGGL(heads_partials_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch, nb, scratch + nb);
+    hipLaunchKernelGGL(heads_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch, starts);
+    hipLaunchKernelGGL(runs_total_kernel, dim3(1), dim3(1), 0, s, scratch + nb, n, starts, d_totals);
+    // runs -> prune -> entries (grid sized for the max possible run count;
+    // blocks past the real count exit)
+    hipLaunchKernelGGL(runs_partials_kernel, dim3((unsigned)nbr), dim3(256), 0, s, starts, d_totals,
+                       keep_gt, scratch, nbr);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch, nbr, scratch + 2 * nbr);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch + nbr, nbr,
+                       scratch + 2 * nbr + 1);
+    hipLaunchKernelGGL(runs_write_kernel, dim3((unsigned)nbr), dim3(256), 0, s, S, starts, d_totals,
+                       keep_gt, scratch, nbr, table, SW, read_ids, ids_out, e_mmer, e_hi, e_lo, e_cnt, e_off);
+    hipLaunchKernelGGL(entries_total_kernel, dim3(1), dim3(1), 0, s, scratch + 2 * nbr,
+                       scratch + 2 * nbr + 1, e_off, d_totals);
     return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------
-// place: every occurrence of a surviving key drops its read ordinal into the
-// key's id range (binning.c:1056-1068 builds the same multiset by prepend)
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void place_kernel(PlaceArgs A) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t k0 = wave * 64; k0 < A.n_occ; k0 += nwaves * 64) {
-        // read of occurrence k0: last r with kmer_base[r] <= k0 (wave-uniform search)
-        uint64_t lo = 0, hi = A.n_reads;  // answer in [lo, hi)
-        while (hi - lo > 1) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (A.kmer_base[mid] <= k0) lo = mid; else hi = mid;
-        }
-        const uint64_t k = k0 + lane;
-        if (k < A.n_occ) {
-            uint64_t r = lo;
-            while (A.kmer_base[r + 1] <= k) r++;
-            const uint32_t slot = A.occ_slot[k];
-            const uint32_t e = slot == NONE ? NONE : A.slot_entry[slot];
-            if (e != NONE) {
-                const uint32_t pos = atomicAdd(&A.cursor[e], 1u);
-                A.ids_ord[A.e_off[e] + pos] = A.ord_base + (uint32_t)r;
-            }
-        }
-    }
-}
-
-hipError_t launch_place(const PlaceArgs& a, hipStream_t s) {
-    if (!a.n_occ) return hipSuccess;
-    uint64_t blocks = (a.n_occ + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(place_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// sort: ids of each key in descending call ordinal (= prepend order,
-// binning.c:1061-1068), then ordinal -> caller read id
-// ---------------------------------------------------------------------------
-constexpr int SMALL_N = 32;
-constexpr int MED_N = 4096;  // block LDS bitonic (16 KB)
-
-// lists: [0, n_entries) medium entry ids, [n_entries, 2 n_entries) large;
-// list_counts: [0] medium count, [1] large count, [2] max large size
-__global__ __launch_bounds__(256) void sort_small_kernel(const uint64_t* __restrict__ e_off,
-                                                         const uint32_t* __restrict__ e_cnt,
-                                                         uint64_t n_entries,
-                                                         const uint32_t* __restrict__ ids_ord,
-                                                         const int32_t* __restrict__ read_ids,
-                                                         int32_t* __restrict__ ids_out,
-                                                         uint32_t* __restrict__ lists,
-                                                         uint32_t* __restrict__ list_counts) {
-    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n_entries;
-         e += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t n = e_cnt[e];
-        const uint64_t o = e_off[e];
-        if (n > SMALL_N) {
-            if (n > MED_N) {
-                const uint32_t at = atomicAdd(&list_counts[1], 1u);
-                lists[n_entries + at] = (uint32_t)e;
-                atomicMax(&list_counts[2], n);
-            } else {
-                const uint32_t at = atomicAdd(&list_counts[0], 1u);
-                lists[at] = (uint32_t)e;
-            }
-            continue;
-        }
-        uint32_t v[SMALL_N];
-#pragma unroll
-        for (int j = 0; j < SMALL_N; j++) v[j] = (uint32_t)j < n ? ids_ord[o + j] + 1u : 0u;
-        // bitonic network, descending
-#pragma unroll
-        for (int k = 2; k <= SMALL_N; k <<= 1) {
-#pragma unroll
-            for (int j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-                for (int i = 0; i < SMALL_N; i++) {
-                    const int l = i ^ j;
-                    if (l > i) {
-                        const uint32_t x = v[i], y = v[l];
-                        const bool desc = (i & k) == 0;
-                        const bool sw = desc ? (x < y) : (x > y);
-                        v[i] = sw ? y : x;
-                        v[l] = sw ? x : y;
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < SMALL_N; j++)
-            if ((uint32_t)j < n) ids_out[o + j] = read_ids[v[j] - 1u];
-    }
-}
-
-// one block per medium entry (grid-stride over the list), LDS bitonic
-__global__ __launch_bounds__(256) void sort_medium_kernel(const uint64_t* __restrict__ e_off,
-                                                          const uint32_t* __restrict__ e_cnt,
-                                                          const uint32_t* __restrict__ ids_ord,
-                                                          const int32_t* __restrict__ read_ids,
-                                                          int32_t* __restrict__ ids_out,
-                                                          const uint32_t* __restrict__ lists,
-                                                          const uint32_t* __restrict__ list_counts) {
-    __shared__ uint32_t buf[MED_N];
-    const uint32_t nmed = list_counts[0];
-    for (uint32_t li = blockIdx.x; li < nmed; li += gridDim.x) {
-        const uint32_t e = lists[li];
-        const uint32_t n = e_cnt[e];
-        const uint64_t o = e_off[e];
-        uint32_t P = 64;
-        while (P < n) P <<= 1;
-        for (uint32_t j = threadIdx.x; j < P; j += blockDim.x)
-            buf[j] = j < n ? ids_ord[o + j] + 1u : 0u;
-        __syncthreads();
-        for (uint32_t k = 2; k <= P; k <<= 1) {
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-                    const uint32_t l = i ^ j;
-                    if (l > i) {
-                        const uint32_t x = buf[i], y = buf[l];
-                        const bool desc = (i & k) == 0;
-                        if (desc ? (x < y) : (x > y)) {
-                            buf[i] = y;
-                            buf[l] = x;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) ids_out[o + j] = read_ids[buf[j] - 1u];
-        __syncthreads();
-    }
-}
-
-// large lists (> MED_N): sort MED_N chunks in LDS into tmp (descending), then
-// merge passes between tmp and ids_ord, one launch per pass.
-__global__ __launch_bounds__(256) void sort_large_chunks_kernel(const uint64_t* __restrict__ e_off,
-                                                                const uint32_t* __restrict__ e_cnt,
-                                                                uint64_t n_entries,
-                                                                const uint32_t* __restrict__ ids_ord,
-                                                                uint32_t* __restrict__ tmp,
-                                                                const uint32_t* __restrict__ lists,
-                                                                const uint32_t* __restrict__ list_counts) {
-    __shared__ uint32_t buf[MED_N];
-    const uint32_t nl = list_counts[1];
-    for (uint32_t li = 0; li < nl; li++) {
-        const uint32_t e = lists[n_entries + li];
-        const uint32_t n = e_cnt[e];
-        const uint64_t o = e_off[e];
-        const uint32_t nchunks = (n + MED_N - 1) / MED_N;
-        for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-            const uint32_t c0 = c * MED_N;
-            const uint32_t cn = min((uint32_t)MED_N, n - c0);
-            for (uint32_t j = threadIdx.x; j < MED_N; j += blockDim.x)
-                buf[j] = j < cn ? ids_ord[o + c0 + j] + 1u : 0u;
-            __syncthreads();
-            for (uint32_t k = 2; k <= (uint32_t)MED_N; k <<= 1) {
-                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    for (uint32_t i = threadIdx.x; i < (uint32_t)MED_N; i += blockDim.x) {
-                        const uint32_t l = i ^ j;
-                        if (l > i) {
-                            const uint32_t x = buf[i], y = buf[l];
-                            const bool desc = (i & k) == 0;
-                            if (desc ? (x < y) : (x > y)) {
-                                buf[i] = y;
-                                buf[l] = x;
-                            }
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-            for (uint32_t j = threadIdx.x; j < cn; j += blockDim.x) tmp[o + c0 + j] = buf[j];
-            __syncthreads();
-        }
-    }
-}
-
-// merge runs of width w (descending, values are ordinal+1) from src into dst
-__global__ __launch_bounds__(256) void merge_pass_kernel(const uint64_t* __restrict__ e_off,
-                                                         const uint32_t* __restrict__ e_cnt,
-                                                         uint64_t n_entries,
-                                                         const uint32_t* __restrict__ src,
-                                                         uint32_t* __restrict__ dst, uint32_t w,
-                                                         const uint32_t* __restrict__ lists,
-                                                         const uint32_t* __restrict__ list_counts) {
-    const uint32_t nl = list_counts[1];
-    for (uint32_t li = 0; li < nl; li++) {
-        const uint32_t e = lists[n_entries + li];
-        const uint32_t n = e_cnt[e];
-        const uint64_t o = e_off[e];
-        for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n;
-             t += (uint64_t)gridDim.x * blockDim.x) {
-            const uint32_t pair0 = (uint32_t)(t / (2ull * w)) * 2u * w;
-            const uint32_t a0 = pair0, an = min(w, n - a0);
-            const uint32_t b0 = a0 + an, bn = b0 < n ? min(w, n - b0) : 0u;
-            const uint32_t d = (uint32_t)t - pair0;  // output rank within the pair
-            // co-rank: find i in A, j = d - i in B with stable descending merge
-            uint32_t lo = d > bn ? d - bn : 0u, hi = min(d, an);
-            while (lo < hi) {
-                const uint32_t i = (lo + hi) >> 1;
-                const uint32_t j = d - i - 1;
-                // take more from A if A[i] >= B[j]
-                if (src[o + a0 + i] >= src[o + b0 + j]) lo = i + 1; else hi = i;
-            }
-            const uint32_t i = lo, j = d - lo;
-            uint32_t v;
-            if (i < an && (j >= bn || src[o + a0 + i] >= src[o + b0 + j])) v = src[o + a0 + i];
-            else v = src[o + b0 + j];
-            dst[o + t] = v;
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void large_finish_kernel(const uint64_t* __restrict__ e_off,
-                                                           const uint32_t* __restrict__ e_cnt,
-                                                           uint64_t n_entries,
-                                                           const uint32_t* __restrict__ src,
-                                                           const int32_t* __restrict__ read_ids,
-                                                           int32_t* __restrict__ ids_out,
-                                                           const uint32_t* __restrict__ lists,
-                                                           const uint32_t* __restrict__ list_counts) {
-    const uint32_t nl = list_counts[1];
-    for (uint32_t li = 0; li < nl; li++) {
-        const uint32_t e = lists[n_entries + li];
-        const uint32_t n = e_cnt[e];
-        const uint64_t o = e_off[e];
-        for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n;
-             t += (uint64_t)gridDim.x * blockDim.x)
-            ids_out[o + t] = read_ids[src[o + t] - 1u];
-    }
-}
-
-hipError_t launch_sort(const uint64_t* e_off, const uint32_t* e_cnt, uint64_t n_entries,
-                       uint32_t* ids_ord, uint32_t* ids_tmp, const int32_t* read_ids,
-                       int32_t* ids_out, uint32_t* lists, uint32_t* list_counts, hipStream_t s) {
-    if (!n_entries) return hipSuccess;
-    hipError_t err = hipMemsetAsync(list_counts, 0, 4 * sizeof(uint32_t), s);
-    if (err != hipSuccess) return err;
-    uint64_t blocks = (n_entries + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(sort_small_kernel, dim3((unsigned)blocks), dim3(256), 0, s, e_off, e_cnt,
-                       n_entries, ids_ord, read_ids, ids_out, lists, list_counts);
-    hipLaunchKernelGGL(sort_medium_kernel, dim3(2048), dim3(256), 0, s, e_off, e_cnt, ids_ord,
-                       read_ids, ids_out, lists, list_counts);
-    // large lists need the max size on the host to plan merge passes
-    uint32_t hc[4];
-    err = hipMemcpyAsync(hc, list_counts, sizeof(hc), hipMemcpyDeviceToHost, s);
-    if (err != hipSuccess) return err;
-    err = hipStreamSynchronize(s);
-    if (err != hipSuccess) return err;
-    if (hc[1] == 0) return hipGetLastError();
-    hipLaunchKernelGGL(sort_large_chunks_kernel, dim3(256), dim3(256), 0, s, e_off, e_cnt, n_entries,
-                       ids_ord, ids_tmp, lists, list_counts);
-    uint32_t* src = ids_tmp;
-    uint32_t* dst = ids_ord;
-    for (uint32_t w = MED_N; w < hc[2]; w <<= 1) {
-        hipLaunchKernelGGL(merge_pass_kernel, dim3(1024), dim3(256), 0, s, e_off, e_cnt, n_entries,
-                           src, dst, w, lists, list_counts);
-        uint32_t* t = src;
-        src = dst;
-        dst = t;
-    }
-    hipLaunchKernelGGL(large_finish_kernel, dim3(1024), dim3(256), 0, s, e_off, e_cnt, n_entries,
-                       src, read_ids, ids_out, lists, list_counts);
-    return hipGetLastError();
+uint64_t runs_scratch_elems(uint64_t n, uint64_t max_runs) {
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const uint64_t nbr = (max_runs + SCAN_TILE - 1) / SCAN_TILE;
+    return std::max(nb + 1, 2 * nbr + 2);
 }
 
 __global__ void fill_ids_kernel(int32_t* d, uint64_t n, int32_t first) {

@@ -59,9 +59,9 @@ class kb_csr(C.Structure):
 
 
 class kb_timing(C.Structure):
-    _fields_ = [("scan_insert_ms", C.c_float), ("compact_ms", C.c_float),
-                ("place_ms", C.c_float), ("sort_ms", C.c_float), ("total_ms", C.c_float),
-                ("scan_insert_launches", C.c_uint32), ("reserved", C.c_uint32),
+    _fields_ = [("scan_insert_ms", C.c_float), ("sort_ms", C.c_float),
+                ("runs_ms", C.c_float), ("emit_ms", C.c_float), ("total_ms", C.c_float),
+                ("scan_insert_launches", C.c_uint32), ("sort_passes", C.c_uint32),
                 ("table_slots", C.c_uint64)]
 
 

@@ -79,13 +79,13 @@ typedef struct {
 /* per-phase device time of the last kb_finalize (HIP events on the context
  * stream; only filled when timing is enabled) */
 typedef struct {
-    float scan_insert_ms;   /* fused signature scan + table insert/count        */
-    float compact_ms;       /* prune + stream compaction (3 launches)           */
-    float place_ms;         /* read-id placement                                */
-    float sort_ms;          /* per-key descending id order                      */
+    float scan_insert_ms;   /* fused signature scan + table find-or-insert      */
+    float sort_ms;          /* stable radix sort of the occurrence records      */
+    float runs_ms;          /* run counts + prune + CSR compaction              */
+    float emit_ms;          /* read-id emission                                 */
     float total_ms;         /* first to last event of the finalize              */
     uint32_t scan_insert_launches;
-    uint32_t reserved;
+    uint32_t sort_passes;
     uint64_t table_slots;   /* slots used by the last finalize                  */
 } kb_timing;
 
