@@ -1,0 +1,64 @@
+/*
+ * binning_gpu.h -- the reference's host-side C surface, backed by libkbin.so.
+ *
+ * Drop-in replacements (identical signatures and argument meaning):
+ *   struct ZHashTable *process_read(struct ZHashTable *, char *read, int read_id)
+ *       binning.c:902.  Copies `read` (borrowed for the call only, as main
+ *       reuses one stack buffer, binning.c:1154/1158) into a staging batch of
+ *       the context bound to `hash_table`; full batches go to kb_submit_ids.
+ *       Returns `hash_table` (binning.c:1075).
+ *   struct ZHashTable *prune_data(struct ZHashTable *)
+ *       binning.c:1130.  Flushes, runs the device scan/insert/prune
+ *       (kb_finalize), and MATERIALISES the surviving entries into
+ *       `hash_table` as real level-1 mmer -> level-2 kmer -> ll_node tables
+ *       (zhash.h / llist.h layout), so downstream reference code
+ *       (expand_read_id_list, find_kmer_extensions, print_kmers) runs
+ *       unchanged.  Returns `hash_table` (the reference has no return,
+ *       binning.c:1144).
+ *
+ * Error convention: like the reference (zhash.c:236/247 exit on OOM), any
+ * engine failure prints kb_last_error() to stderr and calls exit(EXIT_FAILURE).
+ *
+ * Configuration (the reference's compile-time #defines, binning.c:10-13):
+ * build with -DKMER_SIZE=.. -DMMER_SIZE=.. -DABUNDANCE_CUTOFF=.. matching the
+ * caller, or call kbh_configure() before the first process_read.
+ */
+#ifndef BINNING_GPU_H
+#define BINNING_GPU_H
+
+#include <stdint.h>
+#include <stdio.h>
+
+#include "kb_zhash.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct ZHashTable *process_read(struct ZHashTable *hash_table, char *read, int read_id);
+struct ZHashTable *prune_data(struct ZHashTable *hash_table);
+
+/* explicit configuration (else the compile-time defaults); device = HIP ordinal */
+int kbh_configure(int K, int M, int cutoff, int device);
+
+/* like prune_data but without the prune (every key kept) */
+struct ZHashTable *kbh_finish_unpruned(struct ZHashTable *hash_table);
+
+/* drop the engine context bound to hash_table (the tables stay) */
+void kbh_release(struct ZHashTable *hash_table);
+
+/* binning.c:1150-1166 read loop: fgets(buf, read_length) chunks, strip of the
+ * last byte, one id per chunk (empty chunks included).  Returns concatenated
+ * bases + lengths (malloc'd; free with kbh_free_reads). */
+int kbh_read_fgets(const char *path, int read_length, char **bases, uint32_t **lens,
+                   uint64_t *n_reads);
+void kbh_free_reads(char *bases, uint32_t *lens);
+
+/* canonical dump of a materialised two-level table:
+ * "mmer\tkmer\tcount\tid1,id2,...\n", lines sorted bytewise */
+int kbh_dump_table(struct ZHashTable *hash_table, FILE *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

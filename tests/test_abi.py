@@ -1,0 +1,75 @@
+"""C-ABI checks that need no GPU: every symbol the public headers declare is
+exported by the built libraries; parameter validation; and the product path
+fails loudly (no CPU fallback) when no HIP device is present."""
+import ctypes as C
+import pathlib
+import re
+import subprocess
+
+import pytest
+
+import kbin
+
+from conftest import gpu_available
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+
+
+def declared(header: str, prefix: str):
+    txt = (REPO / "include" / header).read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(" + prefix + r"\w+)\s*\(", txt)))
+
+
+def exported(lib: pathlib.Path):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(lib)], check=True,
+                         capture_output=True, text=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+def test_kbin_exports_every_declared_symbol():
+    decl = declared("kbin.h", "kb_")
+    assert decl, "no kb_ declarations parsed"
+    ex = exported(kbin.LIB_PATH)
+    missing = [d for d in decl if d not in ex]
+    assert not missing, missing
+    assert sorted(kbin.EXPORTED) == decl
+
+
+def test_host_exports_reference_surface():
+    ex = exported(kbin.HOST_LIB_PATH)
+    for sym in ["process_read", "prune_data"] + declared("binning_gpu.h", "kbh_"):
+        assert sym in ex, sym
+    # clean-room container API (zhash.h / llist.h names)
+    for sym in declared("kb_zhash.h", "z") + ["create_node_num", "create_node_item", "free_llist"]:
+        assert sym in ex, sym
+    # the drop-in archive must NOT define the containers (they come from the caller)
+    arch = subprocess.run(["nm", "--defined-only", str(kbin.LIB_DIR / "libkbin_host.a")],
+                          check=True, capture_output=True, text=True).stdout
+    assert " zhash_set" not in arch and " create_node_num" not in arch
+    assert " T process_read" in arch and " T prune_data" in arch
+
+
+def test_abi_version():
+    assert kbin.load_library().kb_abi_version() == 1
+
+
+@pytest.mark.parametrize("K,M,code", [(10, 6, kbin.KB_EINVAL), (64, 7, kbin.KB_EINVAL),
+                                      (31, 9, kbin.KB_EINVAL), (31, 0, kbin.KB_EINVAL)])
+def test_param_validation(K, M, code):
+    with pytest.raises(kbin.KbError) as ei:
+        kbin.Engine(K, M)
+    assert ei.value.code == code
+
+
+def test_no_silent_cpu_fallback():
+    if gpu_available():
+        pytest.skip("GPU present")
+    with pytest.raises(kbin.KbError) as ei:
+        kbin.Engine(31, 7)
+    assert ei.value.code == kbin.KB_EDEVICE
+
+
+def test_missing_library_raises(tmp_path):
+    with pytest.raises(FileNotFoundError):
+        kbin.load_library(tmp_path / "nope.so")

@@ -133,3 +133,16 @@ def test_alphabet_rejected():
         with pytest.raises(kbin.KbError) as ei:
             eng.submit([b"ACGTNACGTACGTACG"])
         assert ei.value.code == kbin.KB_EALPHABET
+
+
+def test_host_cli_process_read_prune_data(digests, golden_dir):
+    """The reference's C surface (process_read / prune_data over libkbin.so,
+    then a walk of the MATERIALISED ZHashTable/ll_node tables) reproduces the
+    known-answer digests: kbin_main = binning.c:1147-1169 up to the prune."""
+    import subprocess
+    exe = kbin.LIB_DIR / "kbin_main"
+    for row in digests[:8]:
+        out = subprocess.run([str(exe), str(golden_dir / row["input"]), str(row["K"]), str(row["M"]),
+                              str(row["read_length"]), str(row["cutoff"]), "1" if row["prune"] else "0"],
+                             check=True, capture_output=True, timeout=120).stdout
+        assert hashlib.sha256(out).hexdigest() == row["sha256"], row

@@ -1,0 +1,89 @@
+"""Host C layer (genome-assembly_amd/host) on CPU: the fgets-compat reader
+restates binning.c:1150-1166, and the clean-room containers behave like the
+reference zhash/llist (same bucket function, ladder and growth points)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import kbin
+import oracle
+
+
+@pytest.fixture(scope="module")
+def host():
+    lib = C.CDLL(str(kbin.HOST_LIB_PATH))
+    lib.kbh_read_fgets.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.POINTER(C.c_char)),
+                                   C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64)]
+    lib.kbh_free_reads.argtypes = [C.c_void_p, C.c_void_p]
+    lib.zcreate_hash_table.restype = C.c_void_p
+    lib.zhash_set.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p]
+    lib.zhash_get.argtypes = [C.c_void_p, C.c_char_p]
+    lib.zhash_get.restype = C.c_void_p
+    lib.zhash_delete.argtypes = [C.c_void_p, C.c_char_p]
+    lib.zhash_delete.restype = C.c_void_p
+    lib.zgenerate_hash.argtypes = [C.c_void_p, C.c_char_p]
+    lib.zgenerate_hash.restype = C.c_size_t
+    lib.zfree_hash_table.argtypes = [C.c_void_p]
+    return lib
+
+
+def host_read(host, path, rl):
+    bp = C.POINTER(C.c_char)()
+    lp = C.POINTER(C.c_uint32)()
+    n = C.c_uint64()
+    assert host.kbh_read_fgets(str(path).encode(), rl, C.byref(bp), C.byref(lp), C.byref(n)) == 0
+    lens = np.ctypeslib.as_array(lp, shape=(n.value,)).copy() if n.value else np.zeros(0, np.uint32)
+    bases = C.string_at(bp, int(lens.sum()))
+    host.kbh_free_reads(C.cast(bp, C.c_void_p), C.cast(lp, C.c_void_p))
+    return bases, lens
+
+
+@pytest.mark.parametrize("name,rl", [("input.txt", 101), ("reads.txt", 101), ("reads.txt", 102),
+                                     ("reads.txt", 40), ("synth_b.txt", 101), ("synth_c.txt", 9)])
+def test_fgets_reader_matches_oracle(host, golden_dir, name, rl):
+    hb, hl = host_read(host, golden_dir / name, rl)
+    ob, ol = oracle.read_fgets(golden_dir / name, rl)
+    assert hb == ob
+    np.testing.assert_array_equal(hl, ol)
+
+
+def test_fgets_edge_file(host, tmp_path):
+    p = tmp_path / "e.txt"
+    p.write_bytes(b"\n\nACGT\nAC" + b"G" * 300 + b"\nT")
+    hb, hl = host_read(host, p, 101)
+    ob, ol = oracle.read_fgets(p, 101)
+    assert hb == ob and hl.tolist() == ol.tolist()
+    assert hl.tolist()[:3] == [0, 0, 4]
+
+
+def test_zhash_bucket_function(host):
+    """bucket = fold (17h + c) mod 53 at the first ladder step (zhash.c:171-182)"""
+    t = host.zcreate_hash_table()
+    for key in [b"ACGT", b"A", b"TTTTTTTTTTTTTTTTTTTTTTTTTTTTTTT", b"CAGCCG"]:
+        h = 0
+        for ch in key:
+            h = (17 * h + ch) % 53
+        assert host.zgenerate_hash(t, key) == h
+    host.zfree_hash_table(t)
+
+
+def test_zhash_growth_and_lookup(host):
+    t = host.zcreate_hash_table()
+    keys = [("K%05d" % i).encode() for i in range(3000)]
+    for i, k in enumerate(keys):
+        host.zhash_set(t, k, C.c_void_p(i + 1))
+    size_index = C.cast(t, C.POINTER(C.c_size_t))[0]
+    entry_count = C.cast(t, C.POINTER(C.c_size_t))[1]
+    assert entry_count == 3000
+    # ladder 53,101,211,503,1553,3407,6803: 3000 > 3407/2 -> 6803 (index 6)
+    assert size_index == 6
+    for i, k in enumerate(keys):
+        assert host.zhash_get(t, k) == i + 1
+    assert host.zhash_get(t, b"nope") is None
+    for k in keys[:2990]:
+        host.zhash_delete(t, k)
+    assert C.cast(t, C.POINTER(C.c_size_t))[1] == 10
+    assert C.cast(t, C.POINTER(C.c_size_t))[0] < 6  # shrank below 1/8
+    assert host.zhash_get(t, keys[-1]) == 3000
+    host.zfree_hash_table(t)

@@ -1,0 +1,103 @@
+"""CPU tests of the parity oracle (oracle/): pinned to the reference's known
+answers (tests/golden/digests.json, produced by the compiled reference) and,
+where the reference is buildable (this container), to the reference binary on
+fresh seeded inputs -- including K < 2M, where the reference's incremental
+branch (binning.c:992-1021) is live."""
+import hashlib
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+
+
+def dump_bytes(res, K, M) -> bytes:
+    bp = b"TGCA"
+
+    def s(hi, lo, n):
+        v = (int(hi) << 64) | int(lo)
+        out = bytearray(n)
+        for j in range(n - 1, -1, -1):
+            out[j] = bp[v & 3]
+            v >>= 2
+        return bytes(out)
+
+    lines = []
+    for e in range(res.n_entries):
+        ids = res.ids[int(res.offset[e]):int(res.offset[e + 1])]
+        lines.append(b"%s\t%s\t%d\t%s\n" % (s(0, res.mmer[e], M), s(res.kmer_hi[e], res.kmer_lo[e], K),
+                                             int(res.count[e]), b",".join(b"%d" % x for x in ids)))
+    return b"".join(lines)
+
+
+def test_known_answer_digests(digests, golden_dir):
+    for row in digests:
+        bases, lens = oracle.read_fgets(golden_dir / row["input"], row["read_length"])
+        res = oracle.bin_reads(bases, lens, row["K"], row["M"], row["cutoff"], row["prune"])
+        d = dump_bytes(res, row["K"], row["M"])
+        assert res.n_entries == row["entries"], row
+        assert hashlib.sha256(d).hexdigest() == row["sha256"], row
+
+
+def test_full_dump_line_level(golden_dir):
+    bases, lens = oracle.read_fgets(golden_dir / "input.txt", 101)
+    res = oracle.bin_reads(bases, lens, 6, 3, 1, True)
+    assert dump_bytes(res, 6, 3) == (golden_dir / "input_k6m3_prune.tsv").read_bytes()
+    # first sorted lines
+    assert dump_bytes(res, 6, 3).startswith(b"ACC\tACCACG\t2\t15,8\nACC\tACCCAG\t2\t7,0\n")
+
+
+def test_fgets_chunking(tmp_path):
+    """binning.c:1158-1166: 100-bp lines with READ_LENGTH 101 split into a
+    99-bp read + an empty read; a last line without newline loses a base."""
+    p = tmp_path / "r.txt"
+    p.write_bytes(b"A" * 100 + b"\n" + b"C" * 10 + b"\n" + b"G" * 5)
+    _, lens = oracle.read_fgets(p, 101)
+    assert lens.tolist() == [99, 0, 10, 4]
+    _, lens = oracle.read_fgets(p, 40)
+    assert lens.tolist() == [38, 38, 22, 10, 4]
+
+
+def test_hand_trace_read0():
+    """SURVEY §8(c) hand trace of input.txt read 0 at k=6 m=3."""
+    r = b"CAGCCGCTGGGTCCG"
+    res = oracle.bin_reads(r, [len(r)], 6, 3, 1, False)
+    d = dump_bytes(res, 6, 3).decode().splitlines()
+    keys = {tuple(x.split("\t")[:2]) for x in d}
+    for mm, km in [("AGC", "CAGCCG"), ("AGC", "AGCCGC"), ("CCG", "GCCGCT"), ("CCG", "CCGCTG"),
+                   ("ACC", "GCGACC"), ("ACC", "CGACCC"), ("ACC", "GACCCA"), ("ACC", "ACCCAG"),
+                   ("AGG", "CCCAGG"), ("AGG", "CCAGGC")]:
+        assert (mm, km) in keys
+
+
+def _ref_or_skip(K, M, c=1):
+    exe = oracle.ref_binary(K, M, c)
+    if exe is None:
+        pytest.skip("reference not buildable here (no /root/reference)")
+    return exe
+
+
+@pytest.mark.parametrize("K,M,rl", [(31, 7, 152), (6, 3, 101), (10, 6, 80), (5, 4, 60), (40, 8, 130),
+                                    (63, 7, 260)])
+def test_oracle_vs_reference_binary(tmp_path, K, M, rl):
+    exe = _ref_or_skip(K, M)
+    rng = np.random.default_rng(K * 31 + M)
+    g = rng.choice(np.frombuffer(b"ACGT", np.uint8), 2500)
+    lines = []
+    for _ in range(300):
+        L = int(rng.integers(0, rl + 30))
+        s = int(rng.integers(0, 2500 - L))
+        r = g[s:s + L].copy()
+        m = rng.random(L) < 0.02
+        r[m] = rng.choice(np.frombuffer(b"ACGT", np.uint8), int(m.sum()))
+        lines.append(r.tobytes())
+    p = tmp_path / "reads.txt"
+    p.write_bytes(b"\n".join(lines) + b"\n")
+    for prune in (0, 1):
+        out = subprocess.run([str(exe), str(p), str(rl), str(prune)], check=True,
+                             capture_output=True).stdout
+        ref = b"".join(sorted(out.splitlines(keepends=True)))
+        bases, lens = oracle.read_fgets(p, rl)
+        res = oracle.bin_reads(bases, lens, K, M, 1, bool(prune))
+        assert dump_bytes(res, K, M) == ref
