@@ -101,6 +101,7 @@ struct kb_ctx {
     DevBuf<uint32_t> starts;
     DevBuf<uint32_t> e_mmer, e_cnt;
     DevBuf<uint64_t> e_hi, e_lo, e_off;
+    DevBuf<uint64_t> first, e_first;  // KB_TRACK_FIRST
     DevBuf<int32_t> ids_out;
     DevBuf<uint64_t> scratch;
     DevBuf<uint32_t> misc;    // [0] status [1] n_distinct
@@ -112,7 +113,7 @@ struct kb_ctx {
     bool finalized = false;
     uint64_t n_entries = 0, n_ids = 0, n_distinct = 0;
     std::vector<uint32_t> h_mmer, h_cnt;
-    std::vector<uint64_t> h_hi, h_lo, h_off;
+    std::vector<uint64_t> h_hi, h_lo, h_off, h_first;
     std::vector<int32_t> h_ids;
     bool exported = false;
 
@@ -147,6 +148,7 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     if (p.cutoff < 0) return fail(KB_EINVAL, "cutoff < 0");
     if (p.max_read_len < 1 || p.max_read_len > 65535)
         return fail(KB_EINVAL, "max_read_len=%d outside [1,65535]", p.max_read_len);
+    if (p.flags & ~KB_TRACK_FIRST) return fail(KB_EINVAL, "unknown flags 0x%x", p.flags);
     if (p.table_slots && (p.table_slots & (p.table_slots - 1)))
         return fail(KB_EINVAL, "table_slots must be a power of two");
     kb_ctx* c = new kb_ctx();
@@ -194,7 +196,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->occ_b.release(); c->rs_counts.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
-    c->misc.release(); c->totals.release();
+    c->misc.release(); c->totals.release(); c->first.release(); c->e_first.release();
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
@@ -380,6 +382,7 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     memset(&c->tm, 0, sizeof(c->tm));
     const int SW = c->KW == 1 ? 2 : 4;
     const uint64_t N = c->n_occ;
+    const bool track_first = (c->p.flags & KB_TRACK_FIRST) != 0;
     // ---- table plan: ~0.6 load for the expected distinct keys
     uint64_t slots = c->p.table_slots;
     if (!slots) slots = c->learned_slots;
@@ -405,6 +408,10 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
         REC(0);
         HIPCHK(hipMemsetAsync(c->table.p, 0, slots * SW * sizeof(uint64_t), c->s));
         HIPCHK(hipMemsetAsync(c->misc.p, 0, 2 * sizeof(uint32_t), c->s));
+        if (track_first) {
+            HIPCHK(c->first.ensure(slots));
+            HIPCHK(hipMemsetAsync(c->first.p, 0xFF, slots * sizeof(uint64_t), c->s));
+        }
         REC(1);
         c->tm.scan_insert_launches = 0;
         for (auto& b : c->batches) {
@@ -419,6 +426,7 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
             a.occ_base = b.occ_base;
             a.n_occ_total = N;
             a.ord_base = (uint32_t)b.ord_base;
+            a.first = track_first ? c->first.p : nullptr;
             a.n_distinct = c->misc.p + 1;
             a.status = c->misc.p;
             a.max_distinct = (uint32_t)std::min<uint64_t>(slots - slots / 8, 0xFFFFFFFFull);
@@ -459,10 +467,13 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     HIPCHK(c->e_hi.ensure(ne_cap));
     HIPCHK(c->e_lo.ensure(ne_cap));
     HIPCHK(c->e_off.ensure(ne_cap));
+    if (track_first) HIPCHK(c->e_first.ensure(ne_cap));
     const uint32_t keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
     HIPCHK(launch_runs(c->sorted, N, c->table.p, c->KW, keep_gt, c->starts.p, c->read_ids.p,
                        c->ids_out.p, ne_cap, c->e_mmer.p, c->e_hi.p, c->e_lo.p, c->e_cnt.p,
-                       c->e_off.p, c->scratch.p, c->scratch.cap, c->totals.p, c->s));
+                       c->e_off.p, track_first ? c->first.p : nullptr,
+                       track_first ? c->e_first.p : nullptr, c->scratch.p, c->scratch.cap,
+                       c->totals.p, c->s));
     REC(4);
     REC(5);
     HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
@@ -495,6 +506,7 @@ extern "C" int kb_export_device(kb_ctx* c, kb_csr* out) {
     out->count = c->e_cnt.p;
     out->offset = c->e_off.p;
     out->ids = c->ids_out.p;
+    out->first = (c->p.flags & KB_TRACK_FIRST) ? c->e_first.p : nullptr;
     return KB_OK;
 }
 
@@ -510,6 +522,8 @@ extern "C" int kb_export(kb_ctx* c, kb_csr* out) {
         c->h_hi.resize(n);
         c->h_lo.resize(n);
         c->h_off.resize(n + 1);
+        const bool tf = (c->p.flags & KB_TRACK_FIRST) != 0;
+        c->h_first.resize(tf ? n : 0);
         c->h_ids.resize(c->n_ids);
         if (n) {
             HIPCHK(hipMemcpyAsync(c->h_mmer.data(), c->e_mmer.p, n * 4, hipMemcpyDeviceToHost, c->s));
@@ -517,6 +531,8 @@ extern "C" int kb_export(kb_ctx* c, kb_csr* out) {
             HIPCHK(hipMemcpyAsync(c->h_hi.data(), c->e_hi.p, n * 8, hipMemcpyDeviceToHost, c->s));
             HIPCHK(hipMemcpyAsync(c->h_lo.data(), c->e_lo.p, n * 8, hipMemcpyDeviceToHost, c->s));
             HIPCHK(hipMemcpyAsync(c->h_off.data(), c->e_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->s));
+            if (tf)
+                HIPCHK(hipMemcpyAsync(c->h_first.data(), c->e_first.p, n * 8, hipMemcpyDeviceToHost, c->s));
         } else {
             c->h_off[0] = 0;
         }
@@ -535,6 +551,7 @@ extern "C" int kb_export(kb_ctx* c, kb_csr* out) {
     out->count = c->h_cnt.data();
     out->offset = c->h_off.data();
     out->ids = c->h_ids.data();
+    out->first = (c->p.flags & KB_TRACK_FIRST) ? c->h_first.data() : nullptr;
     return KB_OK;
 }
 

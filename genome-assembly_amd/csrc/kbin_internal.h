@@ -32,6 +32,7 @@ struct ScanArgs {
     uint64_t occ_base;         // first occurrence index of this batch
     uint64_t n_occ_total;
     uint32_t ord_base;         // call ordinal of the batch's first read
+    uint64_t* first;           // [slots] min(ordinal << 16 | i) per key, or null
     uint32_t* n_distinct;      // global distinct-key counter
     uint32_t* status;
     uint32_t max_distinct;
@@ -58,8 +59,8 @@ uint64_t runs_scratch_elems(uint64_t n, uint64_t max_runs);
 hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int KW,
                        uint32_t keep_gt, uint32_t* starts, const int32_t* read_ids,
                        int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
-                       uint64_t* e_off, uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals,
-                       hipStream_t s);
+                       uint64_t* e_off, const uint64_t* first, uint64_t* e_first,
+                       uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s);
 hipError_t launch_fill_ids(int32_t* d_ids, uint64_t n, int32_t first, hipStream_t s);
 hipError_t launch_generate(uint64_t* d_words, uint32_t* d_lens, uint64_t n_reads,
                            uint32_t read_len, uint64_t genome_len, uint32_t err_ppm,

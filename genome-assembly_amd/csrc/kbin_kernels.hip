@@ -489,6 +489,8 @@ __global__ __launch_bounds__(256) void scan_insert_kernel(ScanArgs A) {
                 if (slot == NONE) st |= ST_PROBE_LIMIT;
                 local_new += is_new ? 1u : 0u;
                 *(orow - i) = ((uint64_t)slot << 32) | ordv;
+                if (A.first && slot != NONE)  // insertion order of the reference (KB_TRACK_FIRST)
+                    atomicMin((unsigned long long*)&A.first[slot], (unsigned long long)((ordv << 16) | (uint64_t)i));
             }
         }
     }
@@ -784,7 +786,8 @@ __global__ __launch_bounds__(256) void runs_write_kernel(
     const uint64_t* __restrict__ totals, uint32_t keep_gt, const uint64_t* __restrict__ part,
     uint64_t nb, const uint64_t* __restrict__ table, int SW, const int32_t* __restrict__ read_ids,
     int32_t* __restrict__ ids_out, uint32_t* __restrict__ e_mmer, uint64_t* __restrict__ e_hi,
-    uint64_t* __restrict__ e_lo, uint32_t* __restrict__ e_cnt, uint64_t* __restrict__ e_off) {
+    uint64_t* __restrict__ e_lo, uint32_t* __restrict__ e_cnt, uint64_t* __restrict__ e_off,
+    const uint64_t* __restrict__ first, uint64_t* __restrict__ e_first) {
     __shared__ uint64_t sh[4];
     __shared__ uint32_t rs[257];   // run starts of the round (+ end)
     __shared__ uint32_t ro[256];   // id offset of each run, NONE if pruned
@@ -828,6 +831,7 @@ __global__ __launch_bounds__(256) void runs_write_kernel(
                 }
                 e_cnt[e] = len;
                 e_off[e] = ids + pi;
+                if (first) e_first[e] = first[slot];
             }
         }
         __syncthreads();
@@ -858,8 +862,8 @@ __global__ void entries_total_kernel(const uint64_t* __restrict__ tk, const uint
 hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int KW,
                        uint32_t keep_gt, uint32_t* starts, const int32_t* read_ids,
                        int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
-                       uint64_t* e_off, uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals,
-                       hipStream_t s) {
+                       uint64_t* e_off, const uint64_t* first, uint64_t* e_first,
+                       uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s) {
     const int SW = KW == 1 ? 2 : 4;
     const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     const uint64_t nbr = (max_runs + SCAN_TILE - 1) / SCAN_TILE;
@@ -881,7 +885,8 @@ hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int
     hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch + nbr, nbr,
                        scratch + 2 * nbr + 1);
     hipLaunchKernelGGL(runs_write_kernel, dim3((unsigned)nbr), dim3(256), 0, s, S, starts, d_totals,
-                       keep_gt, scratch, nbr, table, SW, read_ids, ids_out, e_mmer, e_hi, e_lo, e_cnt, e_off);
+                       keep_gt, scratch, nbr, table, SW, read_ids, ids_out, e_mmer, e_hi, e_lo, e_cnt, e_off,
+                       first, e_first);
     hipLaunchKernelGGL(entries_total_kernel, dim3(1), dim3(1), 0, s, scratch + 2 * nbr,
                        scratch + 2 * nbr + 1, e_off, d_totals);
     return hipGetLastError();

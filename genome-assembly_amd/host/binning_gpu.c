@@ -30,6 +30,13 @@
 #define KBH_BATCH_BYTES (256u << 20)
 #endif
 
+/* bucket counts of the level tables (zhash.c:13-17 ladder; the reference keeps
+ * it file-static, so the walker carries its own copy) */
+static const size_t LADDER[23] = {
+    53, 101, 211, 503, 1553, 3407, 6803, 12503, 25013, 50261, 104729, 250007,
+    500009, 1000003, 2000029, 4000037, 10000019, 25000009, 50000047, 104395301,
+    217645177, 512927357, 1000000007};
+
 static int g_K = KMER_SIZE, g_M = MMER_SIZE, g_cutoff = ABUNDANCE_CUTOFF, g_device = 0;
 
 /* one engine context per level-1 table the caller uses */
@@ -86,6 +93,7 @@ static binding_t *binding(struct ZHashTable *t, int create)
     p.cutoff = g_cutoff;
     p.max_read_len = 65535;
     p.device = g_device;
+    p.flags = KB_TRACK_FIRST;
     if (kb_create(&p, &free_slot->ctx) != KB_OK) die("kb_create");
     free_slot->table = t;
     free_slot->cap_reads = 4096;
@@ -141,12 +149,30 @@ static void code_to_str(uint64_t hi, uint64_t lo, int n, char *s)
     s[n] = '\0';
 }
 
-/* build reference-layout tables from the CSR: level 1 mmer -> level 2 table,
- * level 2 kmer -> ll_node list in stored order (reverse call order) */
+static const uint64_t *g_first; /* qsort context */
+
+static int cmp_first(const void *a, const void *b)
+{
+    const uint64_t x = g_first[*(const uint64_t *)a], y = g_first[*(const uint64_t *)b];
+    return x < y ? -1 : x > y;
+}
+
+/* Rebuild the reference's two-level table from the CSR.  Keys are inserted in
+ * the order the reference inserts them -- first occurrence (call ordinal,
+ * k-mer position), binning.c:1045-1057 -- so bucket chains, table sizes and
+ * rehash history come out identical; level-2 values are the id lists in
+ * stored order (reverse call order). */
 static void materialise(struct ZHashTable *level1, const kb_csr *r)
 {
     char ms[17], ks[129];
-    for (uint64_t e = 0; e < r->n_entries; e++) {
+    uint64_t *order = xmalloc(r->n_entries * sizeof(uint64_t));
+    for (uint64_t e = 0; e < r->n_entries; e++) order[e] = e;
+    if (r->first) {
+        g_first = r->first;
+        qsort(order, r->n_entries, sizeof(uint64_t), cmp_first);
+    }
+    for (uint64_t o = 0; o < r->n_entries; o++) {
+        const uint64_t e = order[o];
         code_to_str(0, r->mmer[e], g_M, ms);
         code_to_str(r->kmer_hi[e], r->kmer_lo[e], g_K, ks);
         struct ZHashTable *level2 = zhash_get(level1, ms);
@@ -161,16 +187,61 @@ static void materialise(struct ZHashTable *level1, const kb_csr *r)
         }
         zhash_set(level2, ks, head);
     }
+    free(order);
+}
+
+/* prune_kmers / prune_data semantics on the materialised table
+ * (binning.c:1085-1144): unlink every entry whose list has <= cutoff nodes
+ * without resizing (the reference deletes through its iterators, which never
+ * rehash), drop emptied level-2 tables and their level-1 entries. */
+static void prune_materialised(struct ZHashTable *level1, int cutoff)
+{
+    const size_t m1 = LADDER[level1->size_index];
+    for (size_t b1 = 0; b1 < m1; b1++) {
+        struct ZHashEntry **l1 = &level1->entries[b1];
+        while (*l1) {
+            struct ZHashTable *level2 = (*l1)->val;
+            const size_t m2 = LADDER[level2->size_index];
+            for (size_t b2 = 0; b2 < m2; b2++) {
+                struct ZHashEntry **l2 = &level2->entries[b2];
+                while (*l2) {
+                    int cnt = 0;
+                    for (ll_node *t = (*l2)->val; t && cnt <= cutoff; t = t->next) cnt++;
+                    if (cnt <= cutoff) {
+                        struct ZHashEntry *dead = *l2;
+                        *l2 = dead->next;
+                        free_llist(dead->val);
+                        zfree_entry(dead, false);
+                        level2->entry_count--;
+                    } else {
+                        l2 = &(*l2)->next;
+                    }
+                }
+            }
+            if (level2->entry_count == 0) {
+                struct ZHashEntry *dead = *l1;
+                *l1 = dead->next;
+                free(level2->entries);
+                free(level2);
+                zfree_entry(dead, false);
+                level1->entry_count--;
+            } else {
+                l1 = &(*l1)->next;
+            }
+        }
+    }
 }
 
 static struct ZHashTable *finish(struct ZHashTable *hash_table, int prune)
 {
     binding_t *b = binding(hash_table, 1);
     flush(b);
-    if (kb_finalize(b->ctx, prune) != KB_OK) die("kb_finalize");
+    /* every key, pruned ones included, takes part in the insertion history */
+    if (kb_finalize(b->ctx, 0) != KB_OK) die("kb_finalize");
     kb_csr r;
     if (kb_export(b->ctx, &r) != KB_OK) die("kb_export");
     materialise(hash_table, &r);
+    if (prune) prune_materialised(hash_table, g_cutoff);
     kbh_release(hash_table);
     return hash_table;
 }
@@ -244,11 +315,11 @@ int kbh_dump_table(struct ZHashTable *level1, FILE *out)
 {
     size_t cap = 1024, n = 0;
     char **lines = xmalloc(cap * sizeof(char *));
-    const size_t m1 = kb_zhash_sizes[level1->size_index];
+    const size_t m1 = LADDER[level1->size_index];
     for (size_t b1 = 0; b1 < m1; b1++) {
         for (struct ZHashEntry *me = level1->entries[b1]; me; me = me->next) {
             struct ZHashTable *level2 = me->val;
-            const size_t m2 = kb_zhash_sizes[level2->size_index];
+            const size_t m2 = LADDER[level2->size_index];
             for (size_t b2 = 0; b2 < m2; b2++) {
                 for (struct ZHashEntry *ke = level2->entries[b2]; ke; ke = ke->next) {
                     size_t cnt = 0, sz = strlen(me->key) + strlen(ke->key) + 32;

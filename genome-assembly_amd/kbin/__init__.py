@@ -46,7 +46,7 @@ class KbError(RuntimeError):
 
 class kb_params(C.Structure):
     _fields_ = [("K", C.c_int32), ("M", C.c_int32), ("cutoff", C.c_int32),
-                ("max_read_len", C.c_int32), ("device", C.c_int32), ("reserved", C.c_int32),
+                ("max_read_len", C.c_int32), ("device", C.c_int32), ("flags", C.c_int32),
                 ("table_slots", C.c_uint64)]
 
 
@@ -55,7 +55,11 @@ class kb_csr(C.Structure):
                 ("n_distinct", C.c_uint64),
                 ("mmer", C.POINTER(C.c_uint32)), ("kmer_hi", C.POINTER(C.c_uint64)),
                 ("kmer_lo", C.POINTER(C.c_uint64)), ("count", C.POINTER(C.c_uint32)),
-                ("offset", C.POINTER(C.c_uint64)), ("ids", C.POINTER(C.c_int32))]
+                ("offset", C.POINTER(C.c_uint64)), ("ids", C.POINTER(C.c_int32)),
+                ("first", C.POINTER(C.c_uint64))]
+
+
+KB_TRACK_FIRST = 1
 
 
 class kb_timing(C.Structure):
@@ -129,6 +133,7 @@ class Result:
     ids: np.ndarray
     n_kmers: int
     n_distinct: int
+    first: np.ndarray | None = None  # (ordinal << 16 | i) with KB_TRACK_FIRST
 
     @property
     def n_entries(self) -> int:
@@ -149,7 +154,8 @@ class Result:
         else:
             ids = self.ids[:0]
         return Result(self.mmer[order], self.kmer_hi[order], self.kmer_lo[order], cnt, off, ids,
-                      self.n_kmers, self.n_distinct)
+                      self.n_kmers, self.n_distinct,
+                      None if self.first is None else self.first[order])
 
 
 _BP = np.frombuffer(b"TGCA", dtype=np.uint8)  # getbp (binning.c:69-88)
@@ -185,11 +191,11 @@ class Engine:
     """One binning context on one GPU (C-ABI kb_ctx)."""
 
     def __init__(self, K: int, M: int, cutoff: int = 1, max_read_len: int = 1024,
-                 device: int = 0, table_slots: int = 0, lib_path=None):
+                 device: int = 0, table_slots: int = 0, flags: int = 0, lib_path=None):
         self.lib = load_library(lib_path)
         self.K, self.M, self.cutoff = K, M, cutoff
         p = kb_params(K=K, M=M, cutoff=cutoff, max_read_len=max_read_len, device=device,
-                      reserved=0, table_slots=table_slots)
+                      flags=flags, table_slots=table_slots)
         h = C.c_void_p()
         _check(self.lib, self.lib.kb_create(C.byref(p), C.byref(h)))
         self._h = h
@@ -263,7 +269,8 @@ class Engine:
         return Result(arr(c.mmer, n, np.uint32), arr(c.kmer_hi, n, np.uint64),
                       arr(c.kmer_lo, n, np.uint64), arr(c.count, n, np.uint32),
                       arr(c.offset, n + 1, np.uint64), arr(c.ids, m, np.int32),
-                      int(c.n_kmers), int(c.n_distinct))
+                      int(c.n_kmers), int(c.n_distinct),
+                      arr(c.first, n, np.uint64) if bool(c.first) else None)
 
     def export_device(self) -> dict:
         c = kb_csr()

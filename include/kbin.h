@@ -49,6 +49,12 @@ extern "C" {
 #define KB_ESTATE 6      /* call out of order (e.g. export before finalize) */
 #define KB_EOVERFLOW 7   /* k-mer count beyond the 32-bit occurrence index */
 
+/* kb_params.flags */
+#define KB_TRACK_FIRST 1 /* keep (call ordinal << 16 | k-mer position) of every
+                            key's first occurrence -- the order in which the
+                            reference inserts keys (binning.c:1045-1057), needed
+                            to rebuild its exact zhash layout */
+
 typedef struct kb_ctx kb_ctx;
 
 typedef struct {
@@ -57,7 +63,7 @@ typedef struct {
     int32_t cutoff;         /* ABUNDANCE_CUTOFF (binning.c:12); >= 0            */
     int32_t max_read_len;   /* longest read accepted (READ_LENGTH-2 for fgets)  */
     int32_t device;         /* HIP device ordinal                               */
-    int32_t reserved;
+    int32_t flags;          /* KB_TRACK_FIRST: record each key's first occurrence */
     uint64_t table_slots;   /* hash-table slots hint (power of two); 0 = auto   */
 } kb_params;
 
@@ -74,6 +80,8 @@ typedef struct {
     const uint32_t *count;  /* [n_entries] list length (duplicates kept)        */
     const uint64_t *offset; /* [n_entries+1] into ids                           */
     const int32_t *ids;     /* [n_ids] read ids, reverse call order per entry   */
+    const uint64_t *first;  /* [n_entries] first occurrence (ordinal << 16 | i)
+                               with KB_TRACK_FIRST, else NULL                    */
 } kb_csr;
 
 /* per-phase device time of the last kb_finalize (HIP events on the context

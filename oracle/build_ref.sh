@@ -1,21 +1,37 @@
 #!/usr/bin/env bash
 # build_ref.sh -- TEST INFRASTRUCTURE ONLY.
 #
-# Compiles the reference hot path (binning.c + zhash.c + llist.c, straight from
-# /root/reference) together with our own ref_harness.c into
-#   oracle/_ref/ref_k<K>_m<M>_c<C>
-# The reference hard-codes KMER_SIZE/MMER_SIZE/ABUNDANCE_CUTOFF with plain
-# #defines (binning.c:10-12), so a guarded copy of binning.c is produced in a
-# private temp dir (deleted on exit) -- no reference source is ever written
-# into the repository tree.  Only the binary lands in oracle/_ref/ (git-ignored).
+# Compiles the reference (binning.c + zhash.c + llist.c, straight from
+# /root/reference) into oracle/_ref/ (git-ignored).  The reference hard-codes
+# KMER_SIZE/MMER_SIZE/ABUNDANCE_CUTOFF with plain #defines (binning.c:10-12),
+# so a guarded copy of binning.c is produced in a private temp dir that is
+# deleted on exit -- no reference source is ever written into the repository.
 #
-# Usage: oracle/build_ref.sh K M [CUTOFF]      (no-op when /root/reference is absent)
+#   build_ref.sh K M [C]          ref_k<K>_m<M>_c<C>: reference hot path + our
+#                                 ref_harness.c main -> canonical post-prune dump
+#   build_ref.sh full K M [C]     full_k<K>_m<M>_c<C>: the reference program as
+#                                 shipped (its own main: bin, prune, expand,
+#                                 unitig extension, print_kmers)
+#   build_ref.sh dropin K M [C]   dropin_k<K>_m<M>_c<C>: the SAME reference
+#                                 program, but its process_read/prune_data are
+#                                 weakened and the GPU shim's strong definitions
+#                                 (genome-assembly_amd/host/binning_gpu.c over
+#                                 libkbin.so) win at link time -- the drop-in
+#                                 integration described in INTEGRATION.md
+# No-op when /root/reference is absent (e.g. on the GPU box).
 set -euo pipefail
+MODE=harness
+if [ "${1:-}" = "full" ] || [ "${1:-}" = "dropin" ]; then MODE=$1; shift; fi
 K=${1:?K}; M=${2:?M}; C=${3:-1}
 REF=${KB_REFERENCE_DIR:-/root/reference}
 HERE="$(cd "$(dirname "$0")" && pwd)"
+REPO="$(cd "$HERE/.." && pwd)"
 OUT="$HERE/_ref"
-BIN="$OUT/ref_k${K}_m${M}_c${C}"
+case $MODE in
+  harness) BIN="$OUT/ref_k${K}_m${M}_c${C}" ;;
+  full)    BIN="$OUT/full_k${K}_m${M}_c${C}" ;;
+  dropin)  BIN="$OUT/dropin_k${K}_m${M}_c${C}" ;;
+esac
 if [ ! -f "$REF/binning.c" ]; then
   echo "reference not present at $REF; skipping" >&2
   exit 0
@@ -28,10 +44,33 @@ sed -e 's/^#define MMER_SIZE \(.*\)$/#ifndef MMER_SIZE\n#define MMER_SIZE \1\n#e
     -e 's/^#define KMER_SIZE \(.*\)$/#ifndef KMER_SIZE\n#define KMER_SIZE \1\n#endif/' \
     -e 's/^#define ABUNDANCE_CUTOFF \(.*\)$/#ifndef ABUNDANCE_CUTOFF\n#define ABUNDANCE_CUTOFF \1\n#endif/' \
     "$REF/binning.c" > "$TMP/binning_guarded.c"
-gcc -O2 -w -I"$REF" -DKMER_SIZE="$K" -DMMER_SIZE="$M" -DABUNDANCE_CUTOFF="$C" \
-    -Dmain=binning_main -c "$TMP/binning_guarded.c" -o "$TMP/binning.o"
-gcc -O2 -w -I"$REF" -c "$REF/zhash.c" -o "$TMP/zhash.o"
-gcc -O2 -w -I"$REF" -c "$REF/llist.c" -o "$TMP/llist.o"
-gcc -O2 -w -I"$REF" -c "$HERE/ref_harness.c" -o "$TMP/harness.o"
-gcc -O2 "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/harness.o" -o "$BIN"
+DEFS="-DKMER_SIZE=$K -DMMER_SIZE=$M -DABUNDANCE_CUTOFF=$C"
+case $MODE in
+  harness)
+    gcc -O2 -w -I"$REF" $DEFS -Dmain=binning_main -c "$TMP/binning_guarded.c" -o "$TMP/binning.o"
+    gcc -O2 -w -I"$REF" -c "$REF/zhash.c" -o "$TMP/zhash.o"
+    gcc -O2 -w -I"$REF" -c "$REF/llist.c" -o "$TMP/llist.o"
+    gcc -O2 -w -I"$REF" -c "$HERE/ref_harness.c" -o "$TMP/harness.o"
+    gcc -O2 "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/harness.o" -o "$BIN"
+    ;;
+  full|dropin)
+    # makefile:2-5 flags (-g, no -O): calls stay relocations against the
+    # global symbols, so a strong definition elsewhere can replace them
+    gcc -g -O0 -fno-inline -w -I"$REF" $DEFS -c "$TMP/binning_guarded.c" -o "$TMP/binning.o"
+    gcc -g -O0 -w -I"$REF" -c "$REF/zhash.c" -o "$TMP/zhash.o"
+    gcc -g -O0 -w -I"$REF" -c "$REF/llist.c" -o "$TMP/llist.o"
+    if [ "$MODE" = full ]; then
+      gcc "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" -o "$BIN"
+    else
+      LIB="$REPO/genome-assembly_amd/lib"
+      [ -f "$LIB/libkbin.so" ] || { echo "build libkbin.so first" >&2; exit 1; }
+      objcopy --weaken-symbol=process_read --weaken-symbol=prune_data "$TMP/binning.o"
+      # the shim includes our kb_zhash.h (same layout as zhash.h/llist.h); its
+      # container calls resolve to the reference's zhash.o / llist.o
+      gcc -O2 -w $DEFS -c "$REPO/genome-assembly_amd/host/binning_gpu.c" -o "$TMP/shim.o"
+      gcc "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/shim.o" -L"$LIB" -lkbin \
+          -Wl,-rpath,"\$ORIGIN/../../genome-assembly_amd/lib" -o "$BIN"
+    fi
+    ;;
+esac
 echo "built $BIN"

@@ -101,6 +101,22 @@ def main():
             (HERE / "input_k6m3_prune.tsv").write_bytes(d)
     (HERE / "digests.json").write_text(json.dumps(out, indent=1) + "\n")
 
+    # whole-program outputs of the reference as shipped (binning.c main: bin,
+    # prune, expand, unitig extension, print_kmers; READ_LENGTH 101) -- the
+    # drop-in test runs the same program with the GPU process_read/prune_data
+    uni = []
+    for f, K, M in [("reads.txt", 31, 4), ("input.txt", 6, 3), ("reads.txt", 6, 3),
+                    ("reads.txt", 31, 7), ("synth_a.txt", 21, 5), ("reads.txt", 63, 7)]:
+        subprocess.run(["bash", str(REPO / "oracle" / "build_ref.sh"), "full", str(K), str(M), "1"],
+                       check=True, capture_output=True)
+        exe = REPO / "oracle" / "_ref" / f"full_k{K}_m{M}_c1"
+        outb = subprocess.run([str(exe), str(HERE / f)], check=True, capture_output=True).stdout
+        row = {"input": f, "K": K, "M": M, "cutoff": 1, "lines": outb.count(b"\n"),
+               "sha256": hashlib.sha256(outb).hexdigest()}
+        print(row)
+        uni.append(row)
+    (HERE / "unitigs.json").write_text(json.dumps(uni, indent=1) + "\n")
+
 
 if __name__ == "__main__":
     main()

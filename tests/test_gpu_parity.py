@@ -146,3 +146,26 @@ def test_host_cli_process_read_prune_data(digests, golden_dir):
                               str(row["read_length"]), str(row["cutoff"]), "1" if row["prune"] else "0"],
                              check=True, capture_output=True, timeout=120).stdout
         assert hashlib.sha256(out).hexdigest() == row["sha256"], row
+
+
+def test_dropin_reference_program(golden_dir):
+    """DROP-IN: the reference program itself (binning.c main + its unitig
+    extension + print_kmers, compiled from /root/reference into oracle/_ref in
+    the build container) with ONLY process_read/prune_data replaced by the GPU
+    shim at link time.  Its stdout must equal the reference program's stdout
+    byte for byte -- which requires the materialised ZHashTable layout (bucket
+    chains, sizes, rehash history) to match the reference's exactly."""
+    import json
+    import subprocess
+    rows = json.loads((golden_dir / "unitigs.json").read_text())
+    ran = 0
+    for row in rows:
+        exe = kbin.REPO_ROOT / "oracle" / "_ref" / f"dropin_k{row['K']}_m{row['M']}_c1"
+        if not exe.exists():
+            continue
+        out = subprocess.run([str(exe), str(golden_dir / row["input"])], check=True,
+                             capture_output=True, timeout=300).stdout
+        assert hashlib.sha256(out).hexdigest() == row["sha256"], row
+        ran += 1
+    if not ran:
+        pytest.skip("drop-in binaries not built (needs the reference at build time)")
