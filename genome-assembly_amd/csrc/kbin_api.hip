@@ -75,6 +75,13 @@ struct Batch {
     uint64_t ord_base = 0;
     uint64_t occ_base = 0;
     uint64_t n_occ = 0;
+    // multi-GPU routing
+    bool superkmers = false;          // a batch of received super-k-mer records
+    const uint64_t* recs = nullptr;   // (superkmers) caller's device records
+    uint32_t* rec_base = nullptr;     // (superkmers) owned, per-record occurrence base
+    bool routed = false;              // (reads) shipped by kb_route_pack: not scanned here
+    uint32_t* route_offs = nullptr;   // (reads) owned [G][n_reads]
+    std::vector<uint64_t> route_tot;  // (reads) records per destination
 };
 
 struct kb_ctx {
@@ -84,6 +91,7 @@ struct kb_ctx {
     hipStream_t s = nullptr;
     std::vector<Batch> batches;
     uint64_t n_reads = 0, n_occ = 0;
+    uint32_t route_G = 0;  // destinations of the last kb_route_plan
 
     // staging for host submissions
     char* h_stage = nullptr;
@@ -181,7 +189,10 @@ static void free_batches(kb_ctx* c) {
         if (b.own_lens) (void)hipFree(b.own_lens);
         if (b.kmer_base) (void)hipFree(b.kmer_base);
         if (b.ids) (void)hipFree(b.ids);
+        if (b.rec_base) (void)hipFree(b.rec_base);
+        if (b.route_offs) (void)hipFree(b.route_offs);
     }
+    c->route_G = 0;
     c->batches.clear();
     c->n_reads = 0;
     c->n_occ = 0;
@@ -365,6 +376,144 @@ extern "C" int kb_get_timing(kb_ctx* c, kb_timing* out) {
 #define REC(i) \
     do { if (c->timing) HIPCHK(hipEventRecord(c->ev[i], c->s)); } while (0)
 
+// words per routed super-k-mer record: header + span of n + K - 1 <= 2K - M bases
+static int rec_words(const kb_ctx* c) { return 1 + (2 * c->p.K - c->p.M + 31) / 32; }
+
+extern "C" int kb_record_words(kb_ctx* c, uint32_t* out) {
+    if (!c || !out) return fail(KB_EINVAL, "null argument");
+    *out = (uint32_t)rec_words(c);
+    return KB_OK;
+}
+
+extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
+    if (!c || !h_counts) return fail(KB_EINVAL, "null argument");
+    if (n_dest < 1 || n_dest > 64) return fail(KB_EINVAL, "n_dest=%u outside [1,64]", n_dest);
+    if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
+    int rc = set_device(c);
+    if (rc) return rc;
+    std::vector<uint64_t> tot(n_dest, 0);
+    for (auto& b : c->batches) {
+        if (b.superkmers || b.routed) continue;
+        const uint64_t cells = (uint64_t)n_dest * b.n_reads;
+        if (b.route_offs) (void)hipFree(b.route_offs);
+        b.route_offs = nullptr;
+        HIPCHK(hipMalloc((void**)&b.route_offs, std::max<uint64_t>(cells, 1) * sizeof(uint32_t)));
+        RouteArgs a{};
+        a.words = b.words;
+        a.lens = b.lens;
+        a.ids = b.ids;
+        a.n_reads = b.n_reads;
+        a.offs = b.route_offs;
+        a.G = n_dest;
+        a.rec_words = rec_words(c);
+        a.RW = b.RW;
+        a.K = c->p.K;
+        a.M = c->p.M;
+        HIPCHK(launch_route(a, false, c->s));
+        // dest-major exclusive scan -> every (dest, read) slot in a dest-major buffer
+        HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(cells), c->scratch.cap)));
+        std::vector<uint32_t> edge(n_dest + 1, 0);
+        HIPCHK(launch_scan_u32(b.route_offs, cells, c->scratch.p, c->scratch.cap, c->s));
+        uint64_t grand = 0;
+        const uint64_t nb = scan_u32_scratch_elems(cells) - 2;
+        HIPCHK(hipMemcpyAsync(&grand, c->scratch.p + nb, 8, hipMemcpyDeviceToHost, c->s));
+        for (uint32_t d = 0; d < n_dest; d++)
+            HIPCHK(hipMemcpyAsync(&edge[d], b.route_offs + (uint64_t)d * b.n_reads, 4,
+                                  hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));
+        edge[n_dest] = (uint32_t)grand;
+        b.route_tot.assign(n_dest, 0);
+        for (uint32_t d = 0; d < n_dest; d++) {
+            b.route_tot[d] = (uint64_t)edge[d + 1] - edge[d];
+            tot[d] += b.route_tot[d];
+        }
+    }
+    c->route_G = n_dest;
+    for (uint32_t d = 0; d < n_dest; d++) h_counts[d] = tot[d];
+    return KB_OK;
+}
+
+extern "C" int kb_route_pack(kb_ctx* c, uint64_t* d_send) {
+    if (!c) return fail(KB_EINVAL, "null ctx");
+    if (!c->route_G) return fail(KB_ESTATE, "kb_route_pack before kb_route_plan");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const uint32_t G = c->route_G;
+    // destination d's records start at sum_{d'<d} total(d'); inside it, batches in order
+    std::vector<uint64_t> dest_base(G, 0), seen(G, 0);
+    {
+        std::vector<uint64_t> tot(G, 0);
+        for (auto& b : c->batches)
+            if (!b.superkmers && !b.routed && b.route_offs)
+                for (uint32_t d = 0; d < G; d++) tot[d] += b.route_tot[d];
+        uint64_t acc = 0;
+        for (uint32_t d = 0; d < G; d++) {
+            dest_base[d] = acc;
+            acc += tot[d];
+        }
+        if (acc && !d_send) return fail(KB_EINVAL, "null send buffer");
+        if (acc > 0xFFFFFFFFull) return fail(KB_EOVERFLOW, "more than 2^32 routed records");
+    }
+    DevBuf<uint64_t> adj;
+    HIPCHK(adj.ensure(G));
+    for (auto& b : c->batches) {
+        if (b.superkmers || b.routed || !b.route_offs) continue;
+        std::vector<uint64_t> h_adj(G);
+        uint64_t below = 0;  // sum_{d'<d} total_b(d'): already inside the scanned offsets
+        for (uint32_t d = 0; d < G; d++) {
+            h_adj[d] = dest_base[d] + seen[d] - below;
+            below += b.route_tot[d];
+            seen[d] += b.route_tot[d];
+        }
+        HIPCHK(hipMemcpyAsync(adj.p, h_adj.data(), G * 8, hipMemcpyHostToDevice, c->s));
+        RouteArgs a{};
+        a.words = b.words;
+        a.lens = b.lens;
+        a.ids = b.ids;
+        a.n_reads = b.n_reads;
+        a.offs = b.route_offs;
+        a.adj = adj.p;
+        a.out = d_send;
+        a.G = G;
+        a.rec_words = rec_words(c);
+        a.RW = b.RW;
+        a.K = c->p.K;
+        a.M = c->p.M;
+        HIPCHK(launch_route(a, true, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));  // h_adj / adj reuse
+        b.routed = true;
+    }
+    adj.release();
+    c->route_G = 0;
+    return KB_OK;
+}
+
+extern "C" int kb_submit_superkmers_device(kb_ctx* c, const uint64_t* d_recs, uint64_t n_rec) {
+    if (!c) return fail(KB_EINVAL, "null ctx");
+    if (c->finalized) return fail(KB_ESTATE, "submit after finalize (call kb_reset)");
+    if (n_rec == 0) return KB_OK;
+    if (!d_recs) return fail(KB_EINVAL, "null records");
+    if (n_rec > 0xFFFFFFFFull) return fail(KB_EOVERFLOW, "more than 2^32 records");
+    int rc = set_device(c);
+    if (rc) return rc;
+    Batch b;
+    b.superkmers = true;
+    b.recs = d_recs;
+    b.n_reads = n_rec;
+    HIPCHK(hipMalloc((void**)&b.rec_base, n_rec * sizeof(uint32_t)));
+    HIPCHK(launch_sk_counts(d_recs, n_rec, rec_words(c), b.rec_base, c->s));
+    HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(n_rec), c->scratch.cap)));
+    HIPCHK(launch_scan_u32(b.rec_base, n_rec, c->scratch.p, c->scratch.cap, c->s));
+    uint64_t tot = 0;
+    const uint64_t nb = scan_u32_scratch_elems(n_rec) - 2;
+    HIPCHK(hipMemcpyAsync(&tot, c->scratch.p + nb, 8, hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    b.n_occ = tot;
+    c->n_occ += tot;
+    c->batches.push_back(b);
+    return KB_OK;
+}
+
 static int log2u(uint64_t x) {
     int b = 0;
     while ((1ull << b) < x) b++;
@@ -376,12 +525,23 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     if (c->finalized) return fail(KB_ESTATE, "already finalized (call kb_reset)");
     int rc = set_device(c);
     if (rc) return rc;
-    if (c->n_occ >= 0xFFFFFFFFull)
+    // active batches: unrouted reads, or received super-k-mers (not both)
+    bool any_reads = false, any_sk = false;
+    uint64_t N = 0;
+    for (auto& b : c->batches) {
+        if (b.routed) continue;
+        (b.superkmers ? any_sk : any_reads) = true;
+        b.occ_base = N;
+        N += b.n_occ;
+    }
+    if (any_reads && any_sk)
+        return fail(KB_ESTATE, "a context bins either its own reads or received super-k-mers");
+    c->n_occ = N;
+    if (N >= 0xFFFFFFFFull)
         return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
-                    (unsigned long long)c->n_occ);
+                    (unsigned long long)N);
     memset(&c->tm, 0, sizeof(c->tm));
     const int SW = c->KW == 1 ? 2 : 4;
-    const uint64_t N = c->n_occ;
     const bool track_first = (c->p.flags & KB_TRACK_FIRST) != 0;
     // ---- table plan: ~0.6 load for the expected distinct keys
     uint64_t slots = c->p.table_slots;
@@ -394,8 +554,9 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     // ordinal -> read id, concatenated over batches
     HIPCHK(c->read_ids.ensure(c->n_reads));
     for (auto& b : c->batches)
-        HIPCHK(hipMemcpyAsync(c->read_ids.p + b.ord_base, b.ids, b.n_reads * sizeof(int32_t),
-                              hipMemcpyDeviceToDevice, c->s));
+        if (!b.superkmers && b.n_reads)
+            HIPCHK(hipMemcpyAsync(c->read_ids.p + b.ord_base, b.ids, b.n_reads * sizeof(int32_t),
+                                  hipMemcpyDeviceToDevice, c->s));
     uint32_t status = 0, ndist = 0;
     for (int attempt = 0;; attempt++) {
         if (slots > (1ull << 32) - 1)
@@ -415,6 +576,29 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
         REC(1);
         c->tm.scan_insert_launches = 0;
         for (auto& b : c->batches) {
+            if (b.routed) continue;
+            if (b.superkmers) {
+                SkArgs a{};
+                a.recs = b.recs;
+                a.rec_base = b.rec_base;
+                a.n_rec = b.n_reads;
+                a.rec_words = rec_words(c);
+                a.table = c->table.p;
+                a.mask = slots - 1;
+                a.occ = c->occ_a.p;
+                a.occ_base = b.occ_base;
+                a.n_occ_total = N;
+                a.first = track_first ? c->first.p : nullptr;
+                a.n_distinct = c->misc.p + 1;
+                a.status = c->misc.p;
+                a.max_distinct = (uint32_t)std::min<uint64_t>(slots - slots / 8, 0xFFFFFFFFull);
+                a.max_probe = (uint32_t)std::min<uint64_t>(slots, 1u << 20);
+                a.K = c->p.K;
+                a.M = c->p.M;
+                HIPCHK(launch_insert_sk(a, c->KW, c->s));
+                c->tm.scan_insert_launches++;
+                continue;
+            }
             ScanArgs a{};
             a.words = b.words;
             a.lens = b.lens;
@@ -469,7 +653,8 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     HIPCHK(c->e_off.ensure(ne_cap));
     if (track_first) HIPCHK(c->e_first.ensure(ne_cap));
     const uint32_t keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
-    HIPCHK(launch_runs(c->sorted, N, c->table.p, c->KW, keep_gt, c->starts.p, c->read_ids.p,
+    HIPCHK(launch_runs(c->sorted, N, c->table.p, c->KW, keep_gt, c->starts.p,
+                       any_sk ? nullptr : c->read_ids.p,
                        c->ids_out.p, ne_cap, c->e_mmer.p, c->e_hi.p, c->e_lo.p, c->e_cnt.p,
                        c->e_off.p, track_first ? c->first.p : nullptr,
                        track_first ? c->e_first.p : nullptr, c->scratch.p, c->scratch.cap,

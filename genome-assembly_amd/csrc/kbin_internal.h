@@ -41,6 +41,37 @@ struct ScanArgs {
     int K, M;
 };
 
+struct RouteArgs {
+    const uint64_t* words;
+    const uint32_t* lens;
+    const int32_t* ids;        // read ids (carried in the records)
+    uint64_t n_reads;
+    uint32_t* offs;            // [G][n_reads] counts (count pass) / scanned offsets (pack pass)
+    const uint64_t* adj;       // [G] per-destination base adjustment (pack pass)
+    uint64_t* out;             // send buffer (pack pass)
+    uint32_t G;
+    int rec_words;
+    int RW, K, M;
+};
+
+struct SkArgs {
+    const uint64_t* recs;      // received super-k-mer records
+    const uint32_t* rec_base;  // [n_rec] first occurrence index of each record (batch-local)
+    uint64_t n_rec;
+    int rec_words;
+    uint64_t* table;
+    uint64_t mask;
+    uint64_t* occ;
+    uint64_t occ_base;
+    uint64_t n_occ_total;
+    uint64_t* first;
+    uint32_t* n_distinct;
+    uint32_t* status;
+    uint32_t max_distinct;
+    uint32_t max_probe;
+    int K, M;
+};
+
 // launch helpers implemented in kbin_kernels.hip (all asynchronous on `s`)
 hipError_t launch_pack(const uint8_t* d_bases, const uint64_t* d_off, uint64_t n_reads,
                        int RW, uint64_t* d_words, uint32_t* d_lens, uint32_t* d_status,
@@ -61,6 +92,11 @@ hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int
                        int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
                        uint64_t* e_off, const uint64_t* first, uint64_t* e_first,
                        uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s);
+hipError_t launch_route(const RouteArgs& a, bool pack, hipStream_t s);
+hipError_t launch_sk_counts(const uint64_t* recs, uint64_t n_rec, int rw, uint32_t* nk, hipStream_t s);
+hipError_t launch_insert_sk(const SkArgs& a, int KW, hipStream_t s);
+hipError_t launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* scratch, uint64_t scratch_n, hipStream_t s);
+uint64_t scan_u32_scratch_elems(uint64_t n);
 hipError_t launch_fill_ids(int32_t* d_ids, uint64_t n, int32_t first, hipStream_t s);
 hipError_t launch_generate(uint64_t* d_words, uint32_t* d_lens, uint64_t n_reads,
                            uint32_t read_len, uint64_t genome_len, uint32_t err_ppm,

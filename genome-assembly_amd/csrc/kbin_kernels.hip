@@ -523,6 +523,198 @@ hipError_t launch_scan_insert(const ScanArgs& a, int KW, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// Multi-GPU routing: a read's k-mers fall into consecutive
+// runs that share one signature (super-k-mers, ~10 per 150-bp read at k31/m7).
+// The owner of a super-k-mer is a hash of its canonical mmer; each super-k-mer
+// travels as one fixed-size record
+//   w0 = ord (bits 0-31) | i0 (32-47) | n (48-53) | sig_off (54-59)
+//   w1.. = bases [i0, i0 + n + K - 1) packed like the reads (first base in the MSBs)
+// where ord is the read's id, i0 its first k-mer position, n its k-mer count
+// and sig_off = signature position - i0.
+// route_kernel<false> counts records per (destination, read), dest-major, so
+// one exclusive scan gives every record its slot in a dest-major send buffer
+// in read order; route_kernel<true> writes them.
+// ---------------------------------------------------------------------------
+DEV uint32_t owner_of(uint32_t mmer, uint32_t G) {
+    return (uint32_t)((mix64((uint64_t)mmer + 0x5851F42D4C957F2Dull) >> 32) % G);
+}
+
+template <bool PACK>
+__global__ __launch_bounds__(256) void route_kernel(RouteArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int RW = A.RW, K = A.K, M = A.M;
+    const int W = K - M + 1;
+    const uint32_t maskM = (1u << (2 * M)) - 1u;
+    const uint32_t halfM = 1u << (2 * M - 1);
+    uint64_t* sw = smem + wid * (RW + 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    for (uint64_t r = (uint64_t)blockIdx.x * 4 + wid; r < A.n_reads; r += nwaves) {
+        const int L = rfl((int)A.lens[r]);
+        const int nK = L - K + 1;
+        uint32_t run = 0;  // lane d: records of read r for destination d
+        if (PACK && lane < (int)A.G) run = A.offs[(uint64_t)lane * A.n_reads + r] + (uint32_t)A.adj[lane];
+        if (nK > 0) {
+            wave_sync();
+            for (int w = lane; w < RW; w += 64) sw[w] = A.words[r * RW + w];
+            if (lane == 0) sw[RW] = 0;
+            wave_sync();
+            const uint32_t ordv = PACK ? (uint32_t)A.ids[r] : 0u;
+            int seg_lo = 0;
+            while (seg_lo < nK) {
+                const int d = (lane - seg_lo) & 63;
+                uint32_t key = 0;
+                if (d < W) {
+                    const int p = seg_lo + d;
+                    const uint32_t sm = (uint32_t)(window64(sw, p) >> (64 - 2 * M));
+                    const uint32_t c = sm >= halfM ? sm : maskM - sm;
+                    key = (c << 16) | (0xFFFFu - (uint32_t)p);
+                }
+                key = wave_max_u32(key);
+                const int sig = rfl((int)(0xFFFFu - (key & 0xFFFFu)));
+                const uint32_t c = key >> 16;
+                const int n = min(sig, nK - 1) - seg_lo + 1;
+                const uint32_t dest = owner_of(c, A.G);
+                if (PACK) {
+                    const uint64_t pos = (uint64_t)(uint32_t)__shfl((int)run, (int)dest, 64);
+                    uint64_t* rec = A.out + pos * (uint64_t)A.rec_words;
+                    if (lane == 0)
+                        rec[0] = (uint64_t)ordv | ((uint64_t)seg_lo << 32) | ((uint64_t)n << 48) |
+                                 ((uint64_t)(sig - seg_lo) << 54);
+                    else if (lane < A.rec_words) {
+                        const int p = seg_lo + 32 * (lane - 1);
+                        rec[lane] = p < L ? window64(sw, p) : 0ull;
+                    }
+                }
+                if (lane == (int)dest) run++;
+                seg_lo = sig + 1;
+            }
+        }
+        if (!PACK && lane < (int)A.G) A.offs[(uint64_t)lane * A.n_reads + r] = run;
+    }
+}
+
+hipError_t launch_route(const RouteArgs& a, bool pack, hipStream_t s) {
+    if (!a.n_reads) return hipSuccess;
+    uint64_t blocks = (a.n_reads + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
+    const size_t lds = (size_t)4 * (a.RW + 1) * sizeof(uint64_t);
+    if (pack)
+        hipLaunchKernelGGL(route_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+    else
+        hipLaunchKernelGGL(route_kernel<false>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* scratch, uint64_t scratch_n, hipStream_t s);
+
+// k-mers per received record -> exclusive scan gives each record's first
+// occurrence index (records arrive in ascending id order: by source rank,
+// then read order)
+__global__ void sk_counts_kernel(const uint64_t* __restrict__ recs, uint64_t n_rec, int rw,
+                                 uint32_t* __restrict__ nk) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n_rec;
+         t += (uint64_t)gridDim.x * blockDim.x)
+        nk[t] = (uint32_t)(recs[t * rw] >> 48) & 63u;
+}
+
+hipError_t launch_sk_counts(const uint64_t* recs, uint64_t n_rec, int rw, uint32_t* nk, hipStream_t s) {
+    if (!n_rec) return hipSuccess;
+    uint64_t blocks = (n_rec + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(sk_counts_kernel, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, nk);
+    return hipGetLastError();
+}
+
+// 64-bit window of a record's span words (s0..s3 in registers, no scratch)
+DEV uint64_t span_window(uint64_t s0, uint64_t s1, uint64_t s2, uint64_t s3, int p) {
+    const int w = p >> 5, sh = (p & 31) << 1;
+    const uint64_t a = w == 0 ? s0 : w == 1 ? s1 : w == 2 ? s2 : s3;
+    const uint64_t b = w == 0 ? s1 : w == 1 ? s2 : w == 2 ? s3 : 0ull;
+    return sh ? (a << sh) | (b >> (64 - sh)) : a;
+}
+
+// receiver: insert every k-mer of every received super-k-mer (one thread per
+// record); emits the same occurrence records as scan_insert
+template <int KW>
+__global__ __launch_bounds__(256) void insert_sk_kernel(SkArgs A) {
+    const int K = A.K, M = A.M;
+    const uint32_t maskM = (1u << (2 * M)) - 1u;
+    const uint32_t halfM = 1u << (2 * M - 1);
+    uint64_t* const occ_end = A.occ + A.n_occ_total - 1 - A.occ_base;
+    uint32_t local_new = 0, st = 0;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < A.n_rec;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t* rec = A.recs + t * A.rec_words;
+        const uint64_t h = rec[0];
+        const uint64_t ordv = (uint32_t)h;
+        const int i0 = (int)((h >> 32) & 0xFFFFu);
+        const int n = (int)((h >> 48) & 63u);
+        const int so = (int)((h >> 54) & 63u);
+        const uint64_t s0 = rec[1];
+        const uint64_t s1 = A.rec_words > 2 ? rec[2] : 0ull;
+        const uint64_t s2 = A.rec_words > 3 ? rec[3] : 0ull;
+        const uint64_t s3 = A.rec_words > 4 ? rec[4] : 0ull;
+        const uint32_t sm = (uint32_t)(span_window(s0, s1, s2, s3, so) >> (64 - 2 * M));
+        const bool rev = sm < halfM;
+        const uint32_t mm = rev ? maskM - sm : sm;
+        uint64_t* const orow = occ_end - A.rec_base[t];
+        for (int j = 0; j < n; j++) {
+            Key<KW> key;
+            if constexpr (KW == 1) {
+                uint64_t code = span_window(s0, s1, s2, s3, j) >> (64 - 2 * K);
+                if (rev) code ^= (1ull << (2 * K)) - 1ull;
+                key.a = code + 1ull;
+            } else {
+                const int kh = K - 32;
+                uint64_t hi = kh ? (span_window(s0, s1, s2, s3, j) >> (64 - 2 * kh)) : 0ull;
+                uint64_t lo = span_window(s0, s1, s2, s3, j + kh);
+                if (rev) {
+                    hi ^= kh ? ((1ull << (2 * kh)) - 1ull) : 0ull;
+                    lo = ~lo;
+                }
+                key.a = ((hi << 1) | (lo >> 63)) + 1ull;
+                key.b = (lo & ~PUB) | PUB;
+            }
+            bool is_new;
+            const uint32_t slot = table_insert<KW>(A.table, A.mask, key, mm + 1u, A.max_probe, is_new);
+            if (slot == NONE) st |= ST_PROBE_LIMIT;
+            local_new += is_new ? 1u : 0u;
+            *(orow - j) = ((uint64_t)slot << 32) | ordv;
+            if (A.first && slot != NONE)
+                atomicMin((unsigned long long*)&A.first[slot],
+                          (unsigned long long)((ordv << 16) | (uint64_t)(i0 + j)));
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    uint32_t tot = local_new;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tot += (uint32_t)__shfl_xor((int)tot, off, 64);
+    uint32_t stw = st;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) stw |= (uint32_t)__shfl_xor((int)stw, off, 64);
+    if (lane == 0) {
+        if (tot) {
+            const uint32_t before = atomicAdd(A.n_distinct, tot);
+            if ((uint64_t)before + tot > A.max_distinct) stw |= ST_TABLE_FULL;
+        }
+        if (stw) atomicOr(A.status, stw);
+    }
+}
+
+hipError_t launch_insert_sk(const SkArgs& a, int KW, hipStream_t s) {
+    if (!a.n_rec) return hipSuccess;
+    uint64_t blocks = (a.n_rec + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (KW == 1)
+        hipLaunchKernelGGL(insert_sk_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(insert_sk_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // LSD radix sort of the occurrence records by their slot field (bits 32..),
 // 8-bit digits, stable: per pass a tile histogram, one device-wide exclusive
 // scan of the (digit-major, tile-minor) counts, and a scatter that ranks each
@@ -659,7 +851,7 @@ __global__ __launch_bounds__(256) void scan_u32_apply_kernel(uint32_t* __restric
     }
 }
 
-static hipError_t scan_u32(uint32_t* a, uint64_t n, uint64_t* scratch, uint64_t scratch_n, hipStream_t s) {
+hipError_t launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* scratch, uint64_t scratch_n, hipStream_t s) {
     const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (!nb) return hipSuccess;
     if (scratch_n < nb + 1) return hipErrorInvalidValue;
@@ -668,6 +860,8 @@ static hipError_t scan_u32(uint32_t* a, uint64_t n, uint64_t* scratch, uint64_t 
     hipLaunchKernelGGL(scan_u32_apply_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, n, scratch);
     return hipGetLastError();
 }
+
+uint64_t scan_u32_scratch_elems(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 2; }
 
 uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + RS_TILE - 1) / RS_TILE); }
 
@@ -688,7 +882,7 @@ hipError_t launch_radix_sort(uint64_t* a, uint64_t* b, uint64_t n, int key_bits,
         const int shift = 32 + lo;
         hipLaunchKernelGGL(rs_hist_kernel, dim3(n_tiles), dim3(256), 0, s, src, (uint32_t)n, shift,
                            counts, n_tiles);
-        hipError_t e = scan_u32(counts, 256ull * n_tiles, scratch, scratch_n, s);
+        hipError_t e = launch_scan_u32(counts, 256ull * n_tiles, scratch, scratch_n, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(rs_scatter_kernel, dim3(n_tiles), dim3(256), 0, s, src, dst, (uint32_t)n,
                            shift, counts, n_tiles);
@@ -844,7 +1038,10 @@ __global__ __launch_bounds__(256) void runs_write_kernel(
                 if (rs[mid] <= k) lo = mid; else hi = mid;
             }
             const uint32_t off = ro[lo];
-            if (off != NONE) ids_out[off + (k - rs[lo])] = read_ids[(uint32_t)S[k]];
+            if (off != NONE) {
+                const uint32_t o = (uint32_t)S[k];
+                ids_out[off + (k - rs[lo])] = read_ids ? read_ids[o] : (int32_t)o;
+            }
         }
         __syncthreads();
         ent += tk;

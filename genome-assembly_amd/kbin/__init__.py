@@ -34,7 +34,8 @@ EXPORTED = [
     "kb_create", "kb_destroy", "kb_submit", "kb_submit_ids", "kb_submit_packed_device",
     "kb_finalize", "kb_export", "kb_export_device", "kb_reset", "kb_set_timing",
     "kb_get_timing", "kb_generate_reads_device", "kb_unpack_reads_to_host", "kb_stream",
-    "kb_last_error", "kb_abi_version",
+    "kb_last_error", "kb_abi_version", "kb_record_words", "kb_route_plan", "kb_route_pack",
+    "kb_submit_superkmers_device",
 ]
 
 
@@ -103,6 +104,10 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_get_timing.argtypes = [vp, C.POINTER(kb_timing)]
     lib.kb_generate_reads_device.argtypes = [C.c_int, vp, vp, u64, u32, u64, u32, u64]
     lib.kb_unpack_reads_to_host.argtypes = [C.c_int, vp, vp, u64, u32, C.c_char_p, C.POINTER(u32)]
+    lib.kb_record_words.argtypes = [vp, C.POINTER(u32)]
+    lib.kb_route_plan.argtypes = [vp, u32, C.POINTER(u64)]
+    lib.kb_route_pack.argtypes = [vp, vp]
+    lib.kb_submit_superkmers_device.argtypes = [vp, vp, u64]
     lib.kb_stream.argtypes = [vp]
     lib.kb_stream.restype = vp
     lib.kb_last_error.argtypes = []
@@ -238,6 +243,26 @@ class Engine:
         _check(self.lib, self.lib.kb_submit_packed_device(self._h, C.c_void_p(words_ptr),
                                                           C.c_void_p(lens_ptr), n_reads,
                                                           words_per_read, int(first_id)))
+
+    # ---- multi-GPU routing (include/kbin.h; driven by kbin.dist) ----
+    def record_words(self) -> int:
+        w = C.c_uint32()
+        _check(self.lib, self.lib.kb_record_words(self._h, C.byref(w)))
+        return int(w.value)
+
+    def route_plan(self, n_dest: int) -> np.ndarray:
+        """super-k-mer records per destination for the reads submitted so far"""
+        cnt = np.zeros(n_dest, dtype=np.uint64)
+        _check(self.lib, self.lib.kb_route_plan(self._h, n_dest,
+                                                cnt.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return cnt
+
+    def route_pack(self, send_ptr: int) -> None:
+        _check(self.lib, self.lib.kb_route_pack(self._h, C.c_void_p(send_ptr)))
+
+    def submit_superkmers_device(self, recs_ptr: int, n_records: int) -> None:
+        _check(self.lib, self.lib.kb_submit_superkmers_device(self._h, C.c_void_p(recs_ptr),
+                                                              int(n_records)))
 
     def finalize(self, prune: bool = True) -> None:
         _check(self.lib, self.lib.kb_finalize(self._h, 1 if prune else 0))

@@ -1,0 +1,104 @@
+"""Multi-GPU binning: one process per GPU, the canonical-mmer space sharded
+over the ranks.
+
+The reference has no distributed mode; FAQ.md:11 only asks how bins would be
+merged across nodes.  Here the level-1 key of binning.c (the mmer,
+binning.c:1045) is the shard key: every (mmer, kmer) entry lives on rank
+owner(mmer), so per-rank results are disjoint and their union is the
+single-GPU result.  The one exchange step is an all-to-all of super-k-mer
+records (a run of consecutive k-mers of a read that share one signature,
+~10 per 150-bp read at k31/m7 -- about 2 B per k-mer on the wire instead of
+a 12-16 B per-k-mer record) over RCCL (torch.distributed "nccl") / xGMI.
+
+Per step on every rank:
+  kb_route_plan (counts per destination)  ->  kb_route_pack (dest-major send
+  buffer)  ->  all_to_all_single (counts, then records)  ->
+  kb_submit_superkmers_device (received, concatenated by source rank)  ->
+  kb_finalize (table insert, radix sort, prune, CSR).
+Read ids must increase with the global call order (rank r's ids below rank
+r+1's): they are the reverse-call-order key of every id list.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import Engine
+
+_MIX_SALT = 0x5851F42D4C957F2D
+_M64 = (1 << 64) - 1
+
+
+def _mix64(x: int) -> int:
+    x &= _M64
+    x ^= x >> 30
+    x = (x * 0xBF58476D1CE4E5B9) & _M64
+    x ^= x >> 27
+    x = (x * 0x94D049BB133111EB) & _M64
+    x ^= x >> 31
+    return x
+
+
+def owner_of(mmer_code: int, n_dest: int) -> int:
+    """Owning rank of a canonical mmer (same function as owner_of() in
+    csrc/kbin_kernels.hip)."""
+    return (_mix64(mmer_code + _MIX_SALT) >> 32) % n_dest
+
+
+def exchange_records(send: torch.Tensor, counts, rec_words: int, group=None):
+    """All-to-all of fixed-size records.  `send` holds sum(counts) records
+    (rec_words int64 each), destination-major; returns (received records
+    concatenated by source rank, per-source counts).  Device-agnostic: RCCL
+    for cuda tensors, gloo for cpu tensors."""
+    dev = send.device
+    cnt = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    rc = [int(x) for x in rcnt.cpu().tolist()]
+    recv = torch.empty(sum(rc) * rec_words, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv, send[: int(sum(counts)) * rec_words].contiguous(),
+                           output_split_sizes=[c * rec_words for c in rc],
+                           input_split_sizes=[int(c) * rec_words for c in counts], group=group)
+    return recv, rc
+
+
+class ShardedBinner:
+    """One rank's share of a mmer-sharded binning job."""
+
+    def __init__(self, K: int, M: int, cutoff: int, max_read_len: int, device: int = 0,
+                 group=None, flags: int = 0):
+        self.engine = Engine(K, M, cutoff=cutoff, max_read_len=max_read_len, device=device,
+                             flags=flags)
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.rec_words = self.engine.record_words()
+        self.device = torch.device("cuda", device)
+        self._send = torch.empty(0, dtype=torch.int64, device=self.device)
+        self._recv = None
+        self.last_counts = None
+
+    def _send_buffer(self, words: int) -> torch.Tensor:
+        if self._send.numel() < words:
+            self._send = torch.empty(int(words * 1.25) + 1024, dtype=torch.int64, device=self.device)
+        return self._send
+
+    def step(self, words: torch.Tensor, lens: torch.Tensor, n_reads: int, words_per_read: int,
+             first_id: int, prune: bool = True) -> None:
+        """Bin this rank's resident packed reads (ids first_id..first_id+n-1)
+        together with every other rank's; the result this rank owns stays in
+        self.engine (export / export_device)."""
+        eng = self.engine
+        eng.reset()
+        eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n_reads, words_per_read,
+                                 first_id)
+        counts = eng.route_plan(self.world)
+        total = int(counts.sum())
+        send = self._send_buffer(total * self.rec_words)
+        eng.route_pack(send.data_ptr())  # synchronises the engine stream
+        recv, rc = exchange_records(send, counts.tolist(), self.rec_words, self.group)
+        torch.cuda.current_stream(self.device).synchronize()
+        self._recv = recv  # referenced by the engine until the next reset
+        self.last_counts = (counts.tolist(), rc)
+        eng.submit_superkmers_device(recv.data_ptr(), recv.numel() // self.rec_words)
+        eng.finalize(prune=prune)

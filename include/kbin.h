@@ -158,6 +158,22 @@ int kb_unpack_reads_to_host(int device, const uint64_t *d_words,
                             uint32_t words_per_read, char *h_bases,
                             uint32_t *h_lens);
 
+/* ---- multi-GPU routing ------------------------------
+ * The canonical-mmer space shards: a super-k-mer (a run of consecutive k-mers
+ * of one read sharing a signature) is owned by GPU owner(mmer) of n_dest.
+ * Sender: kb_route_plan counts the records per destination for every read
+ * batch submitted so far; kb_route_pack writes them, destination-major and in
+ * read order, into d_send (sum(counts) * kb_record_words u64 words) and marks
+ * those batches as shipped.  The caller moves the buffers (RCCL all-to-all,
+ * kbin/dist.py).  Receiver: kb_submit_superkmers_device adopts the records it
+ * got, concatenated by source rank, and kb_finalize bins them.  Record ids are
+ * the senders' read ids: across all ranks they must increase with call order
+ * (rank r's ids below rank r+1's) and be >= 0; they are the list order key. */
+int kb_record_words(kb_ctx *ctx, uint32_t *out);
+int kb_route_plan(kb_ctx *ctx, uint32_t n_dest, uint64_t *h_counts);
+int kb_route_pack(kb_ctx *ctx, uint64_t *d_send);
+int kb_submit_superkmers_device(kb_ctx *ctx, const uint64_t *d_records, uint64_t n_records);
+
 /* Stream used by the context (hipStream_t as void*), for callers that want
  * to order their own work against the engine. */
 void *kb_stream(kb_ctx *ctx);

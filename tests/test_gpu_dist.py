@@ -1,0 +1,100 @@
+"""GPU side of the multi-GPU path on ONE device with G virtual shards
+(SURVEY §4.5): the HIP route kernels pack exactly the records of the format
+restatement (tests/skmer_ref.py), every shard bins its records through the
+receiver kernels, and the union of the shards equals the oracle."""
+import numpy as np
+import pytest
+import torch
+
+import kbin
+import kbin.dist
+import oracle
+import skmer_ref
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _reads(n=700, rl=102):
+    bases, lens = oracle.read_fgets(GOLDEN / "reads.txt", rl)
+    off = np.concatenate([[0], np.cumsum(lens.astype(np.int64))]).astype(np.int64)
+    rng = np.random.default_rng(3)
+    extra = [rng.choice(np.frombuffer(b"ACGT", np.uint8), int(rng.integers(0, 200))).tobytes()
+             for _ in range(100)] + [b"A" * 120, b"ACGT" * 40, b""]
+    reads = [bases[off[i]:off[i + 1]] for i in range(n)] + extra
+    return reads
+
+
+def _result_dict(res):
+    c = res.canonical()
+    out = {}
+    for e in range(c.n_entries):
+        key = (int(c.mmer[e]), (int(c.kmer_hi[e]) << 64) | int(c.kmer_lo[e]))
+        out[key] = [int(x) for x in c.ids[int(c.offset[e]):int(c.offset[e + 1])]]
+    return out
+
+
+@pytest.mark.parametrize("K,M,G", [(31, 7, 1), (31, 7, 2), (31, 7, 3), (21, 5, 8), (63, 7, 4),
+                                   (40, 6, 5)])
+def test_virtual_shards(K, M, G):
+    reads = _reads()
+    bases, lens = kbin.pack_reads(reads)
+    ids = np.arange(len(reads), dtype=np.int32) * 2 + 5  # increasing, not ordinals
+    rw = skmer_ref.rec_words(K, M)
+    with kbin.Engine(K, M, cutoff=1, max_read_len=300) as eng:
+        assert eng.record_words() == rw
+        eng.submit(bases=bases, lens=lens, ids=ids)
+        counts = eng.route_plan(G)
+        total = int(counts.sum())
+        send = torch.zeros(max(1, total * rw), dtype=torch.int64, device="cuda")
+        eng.route_pack(send.data_ptr())
+        torch.cuda.synchronize()
+        got = send.cpu().numpy().view(np.uint64)[: total * rw]
+    want, wcounts = skmer_ref.encode(reads, ids.tolist(), K, M, G)
+    assert counts.tolist() == wcounts
+    np.testing.assert_array_equal(got, want)
+
+    ora = skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, True, ids=ids))
+    union = {}
+    edges = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    for d in range(G):
+        seg = send[int(edges[d]) * rw:int(edges[d + 1]) * rw]
+        with kbin.Engine(K, M, cutoff=1, max_read_len=300) as shard:
+            shard.submit_superkmers_device(seg.data_ptr(), int(counts[d]))
+            shard.finalize(prune=True)
+            part = _result_dict(shard.export())
+        assert all(kbin.dist.owner_of(mm, G) == d for mm, _ in part)
+        assert not (set(part) & set(union))
+        union.update(part)
+    assert union == ora
+
+
+def test_track_first_through_routing():
+    """first occurrence (id << 16 | position) survives the exchange"""
+    reads = _reads(300)
+    bases, lens = kbin.pack_reads(reads)
+    ids = np.arange(len(reads), dtype=np.int32)
+    K, M, G = 31, 7, 3
+    rw = skmer_ref.rec_words(K, M)
+    with kbin.Engine(K, M, max_read_len=300, flags=kbin.KB_TRACK_FIRST) as whole:
+        whole.submit(bases=bases, lens=lens, ids=ids)
+        whole.finalize(prune=False)
+        ref = whole.export().canonical()
+    firsts = {(int(ref.mmer[e]), int(ref.kmer_lo[e])): int(ref.first[e]) for e in range(ref.n_entries)}
+    with kbin.Engine(K, M, max_read_len=300) as eng:
+        eng.submit(bases=bases, lens=lens, ids=ids)
+        counts = eng.route_plan(G)
+        send = torch.zeros(max(1, int(counts.sum()) * rw), dtype=torch.int64, device="cuda")
+        eng.route_pack(send.data_ptr())
+        torch.cuda.synchronize()
+    edges = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    seen = 0
+    for d in range(G):
+        with kbin.Engine(K, M, max_read_len=300, flags=kbin.KB_TRACK_FIRST) as shard:
+            shard.submit_superkmers_device(send[int(edges[d]) * rw:].data_ptr(), int(counts[d]))
+            shard.finalize(prune=False)
+            r = shard.export()
+            for e in range(r.n_entries):
+                assert firsts[(int(r.mmer[e]), int(r.kmer_lo[e]))] == int(r.first[e])
+                seen += 1
+    assert seen == ref.n_entries
