@@ -96,11 +96,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # one rank per GPU; KB_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
+    backend = os.environ.get("KB_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % ndev if backend == "gloo" else local
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
         dist = tdist
 
     L, K, M = args.read_len, args.K, args.M
@@ -148,7 +155,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64,
+                          device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 

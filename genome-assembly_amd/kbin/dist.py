@@ -51,6 +51,11 @@ def exchange_records(send: torch.Tensor, counts, rec_words: int, group=None):
     concatenated by source rank, per-source counts).  Device-agnostic: RCCL
     for cuda tensors, gloo for cpu tensors."""
     dev = send.device
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        # rehearsal mode (several ranks sharing one GPU, gloo): stage via host
+        recv, rc = exchange_records(send[: int(sum(counts)) * rec_words].cpu(), counts, rec_words,
+                                    group)
+        return recv.to(dev), rc
     cnt = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
     rcnt = torch.empty_like(cnt)
     dist.all_to_all_single(rcnt, cnt, group=group)

@@ -98,3 +98,39 @@ def test_track_first_through_routing():
                 assert firsts[(int(r.mmer[e]), int(r.kmer_lo[e]))] == int(r.first[e])
                 seen += 1
     assert seen == ref.n_entries
+
+
+def test_ranks_rehearsal(tmp_path):
+    """Two real ranks (torch.distributed.run, gloo rehearsal on one GPU) run
+    kbin.dist.ShardedBinner end to end; the union of what they own equals a
+    single-GPU engine over both shards' reads."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    n, L, K, M = 20000, 150, 31, 7
+    env = dict(__import__("os").environ, KB_DIST_BACKEND="gloo")
+    worker = kbin.REPO_ROOT / "tests" / "dist_worker.py"
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(port), str(worker),
+                    str(tmp_path), str(n), str(L), str(K), str(M)], check=True, env=env, timeout=300)
+    wpr = (L + 31) // 32
+    words = np.concatenate([np.load(tmp_path / f"words{r}.npy") for r in range(2)])
+    dw = torch.from_numpy(words).cuda()
+    dl = torch.full((2 * n,), L, dtype=torch.int32, device="cuda")
+    with kbin.Engine(K, M, cutoff=1, max_read_len=L) as eng:
+        eng.submit_packed_device(dw.data_ptr(), dl.data_ptr(), 2 * n, wpr, 0)
+        eng.finalize(True)
+        want = _result_dict(eng.export())
+    union = {}
+    for r in range(2):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        res = kbin.Result(z["mmer"], z["hi"], z["lo"], z["count"], z["offset"], z["ids"], 0, 0)
+        part = _result_dict(res)
+        assert all(kbin.dist.owner_of(mm, 2) == r for mm, _ in part)
+        assert not (set(part) & set(union))
+        union.update(part)
+        assert z["sent"].sum() > 0 and z["recv"].sum() > 0
+    assert union == want
