@@ -75,6 +75,8 @@ struct Batch {
     uint64_t ord_base = 0;
     uint64_t occ_base = 0;
     uint64_t n_occ = 0;
+    bool affine = false;              // ids = first_id + r
+    int64_t first_id = 0;
     // multi-GPU routing
     bool superkmers = false;          // a batch of received super-k-mer records
     const uint64_t* recs = nullptr;   // (superkmers) caller's device records
@@ -104,7 +106,9 @@ struct kb_ctx {
     uint64_t slots = 0, learned_slots = 0;
     DevBuf<uint64_t> occ_a, occ_b;  // occurrence records, radix ping-pong
     uint64_t* sorted = nullptr;
-    DevBuf<uint32_t> rs_counts;
+    DevBuf<uint64_t> os_flags;        // onesweep look-back words
+    DevBuf<uint32_t> os_aux;          // histograms/bases, tickets, error word
+    uint32_t os_epoch = 0;
     DevBuf<int32_t> read_ids;
     DevBuf<uint32_t> starts;
     DevBuf<uint32_t> e_mmer, e_cnt;
@@ -173,9 +177,9 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     }
     e = hipHostMalloc((void**)&c->h_misc, 16 * sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
-    e = hipHostMalloc((void**)&c->h_totals, 4 * sizeof(uint64_t), hipHostMallocDefault);
+    e = hipHostMalloc((void**)&c->h_totals, 8 * sizeof(uint64_t), hipHostMallocDefault);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
-    if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(4) != hipSuccess) {
+    if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(8) != hipSuccess) {
         kb_destroy(c);
         return fail(KB_ENOMEM, "device alloc");
     }
@@ -204,7 +208,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
-    c->occ_b.release(); c->rs_counts.release(); c->read_ids.release(); c->starts.release();
+    c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
     c->misc.release(); c->totals.release(); c->first.release(); c->e_first.release();
@@ -291,10 +295,13 @@ static int submit_common(kb_ctx* c, const char* bases, const uint32_t* lens, uin
     b.lens = b.own_lens;
     HIPCHK(hipMemsetAsync(c->misc.p, 0, sizeof(uint32_t), c->s));
     HIPCHK(launch_pack(c->d_bases.p, c->d_off.p, n_reads, RW, b.own_words, b.own_lens, c->misc.p, c->s));
-    if (ids)
+    if (ids) {
         HIPCHK(hipMemcpyAsync(b.ids, ids, n_reads * sizeof(int32_t), hipMemcpyHostToDevice, c->s));
-    else
+    } else {
         HIPCHK(launch_fill_ids(b.ids, n_reads, first_id, c->s));
+        b.affine = true;
+        b.first_id = first_id;
+    }
     uint32_t st = 0;
     HIPCHK(hipMemcpyAsync(&st, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
@@ -346,6 +353,8 @@ extern "C" int kb_submit_packed_device(kb_ctx* c, const uint64_t* d_words, const
     b.ord_base = c->n_reads;
     HIPCHK(hipMalloc((void**)&b.ids, n_reads * sizeof(int32_t)));
     HIPCHK(launch_fill_ids(b.ids, n_reads, first_id, c->s));
+    b.affine = true;
+    b.first_id = first_id;
     rc = batch_offsets(c, b);
     if (rc) { (void)hipFree(b.ids); return rc; }
     b.occ_base = c->n_occ;
@@ -631,17 +640,28 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
         slots *= 4;
     }
     c->n_distinct = ndist;
+#ifdef KB_ABLATE_TABLE
+    if (c->timing) HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));
+    c->n_entries = c->n_ids = 0;
+    c->finalized = true;
+    return KB_OK;
+#endif
     // next finalize on this context: ~0.6 load for the distinct keys seen now
     if (!c->p.table_slots)
         c->learned_slots = std::max<uint64_t>(1024, next_pow2((uint64_t)ndist * 5 / 3 + 1));
     // ---- stable radix sort of the records by slot
     const int key_bits = log2u(slots);
-    HIPCHK(c->rs_counts.ensure(radix_counts_elems(N)));
     const uint64_t ne_cap = (uint64_t)ndist + 1;
-    HIPCHK(c->scratch.ensure(std::max({radix_scratch_elems(N), runs_scratch_elems(N, ne_cap),
-                                       c->scratch.cap})));
-    HIPCHK(launch_radix_sort(c->occ_a.p, c->occ_b.p, N, key_bits, c->rs_counts.p, c->scratch.p,
-                             c->scratch.cap, &c->sorted, c->s));
+    HIPCHK(c->scratch.ensure(std::max(runs_scratch_elems(N, ne_cap), c->scratch.cap)));
+    const uint64_t nflags = onesweep_flag_elems(N);
+    if (c->os_flags.cap < nflags || c->os_epoch > (1u << 24) - 8) {
+        HIPCHK(c->os_flags.ensure(nflags));
+        HIPCHK(hipMemsetAsync(c->os_flags.p, 0, c->os_flags.cap * sizeof(uint64_t), c->s));
+        c->os_epoch = 0;
+    }
+    HIPCHK(c->os_aux.ensure(4 * 256 + 8));
+    HIPCHK(launch_onesweep(c->occ_a.p, c->occ_b.p, N, key_bits, c->os_flags.p, c->os_aux.p,
+                           &c->os_epoch, &c->sorted, c->s));
     c->tm.sort_passes = (uint32_t)((key_bits + 7) / 8);
     REC(3);
     // ---- runs -> counts -> prune -> CSR entries
@@ -653,16 +673,33 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     HIPCHK(c->e_off.ensure(ne_cap));
     if (track_first) HIPCHK(c->e_first.ensure(ne_cap));
     const uint32_t keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
+    // ids: affine fast path (id = ordinal + c for every batch) avoids the gather
+    bool affine = !any_sk;
+    int64_t id_c = 0;
+    bool first_b = true;
+    for (auto& b : c->batches) {
+        if (b.routed || b.superkmers) continue;
+        const int64_t cb = b.first_id - (int64_t)b.ord_base;
+        if (!b.affine || (!first_b && cb != id_c)) affine = false;
+        id_c = cb;
+        first_b = false;
+    }
     HIPCHK(launch_runs(c->sorted, N, c->table.p, c->KW, keep_gt, c->starts.p,
-                       any_sk ? nullptr : c->read_ids.p,
+                       (any_sk || affine) ? nullptr : c->read_ids.p, (uint32_t)(affine ? id_c : 0),
                        c->ids_out.p, ne_cap, c->e_mmer.p, c->e_hi.p, c->e_lo.p, c->e_cnt.p,
                        c->e_off.p, track_first ? c->first.p : nullptr,
                        track_first ? c->e_first.p : nullptr, c->scratch.p, c->scratch.cap,
                        c->totals.p, c->s));
     REC(4);
     REC(5);
-    HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+    if (N) HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    else c->h_misc[8] = 0;
     HIPCHK(hipStreamSynchronize(c->s));
+    if (c->h_misc[8]) return fail(KB_EDEVICE, "radix look-back timed out (device error word %u)", c->h_misc[8]);
+    if (c->h_totals[3])
+        return fail(KB_EDEVICE, "internal: %llu runs > %llu distinct keys", (unsigned long long)c->h_totals[3],
+                    (unsigned long long)ne_cap);
     c->n_entries = c->h_totals[0];
     c->n_ids = c->h_totals[1];
     if (c->timing) {

@@ -86,10 +86,13 @@ uint64_t radix_scratch_elems(uint64_t n);
 hipError_t launch_radix_sort(uint64_t* a, uint64_t* b, uint64_t n, int key_bits, uint32_t* counts,
                              uint64_t* scratch, uint64_t scratch_n, uint64_t** sorted,
                              hipStream_t s);
+uint64_t onesweep_flag_elems(uint64_t n);
+hipError_t launch_onesweep(uint64_t* a, uint64_t* b, uint64_t n, int key_bits, uint64_t* flags,
+                           uint32_t* aux, uint32_t* epoch, uint64_t** sorted, hipStream_t s);
 uint64_t runs_scratch_elems(uint64_t n, uint64_t max_runs);
 hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int KW,
                        uint32_t keep_gt, uint32_t* starts, const int32_t* read_ids,
-                       int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
+                       uint32_t id_off, int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
                        uint64_t* e_off, const uint64_t* first, uint64_t* e_first,
                        uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s);
 hipError_t launch_route(const RouteArgs& a, bool pack, hipStream_t s);

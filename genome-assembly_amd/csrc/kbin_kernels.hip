@@ -484,8 +484,12 @@ __global__ __launch_bounds__(256) void scan_insert_kernel(ScanArgs A) {
                     key.a = ((hi << 1) | (lo >> 63)) + 1ull;
                     key.b = (lo & ~PUB) | PUB;
                 }
-                bool is_new;
+                bool is_new = false;
+#ifdef KB_ABLATE_TABLE  // timing experiment only: no table, slot = hash (kbin_api stops after the scan)
+                const uint32_t slot = (uint32_t)(key.hash(mm + 1u) & A.mask);
+#else
                 const uint32_t slot = table_insert<KW>(A.table, A.mask, key, mm + 1u, A.max_probe, is_new);
+#endif
                 if (slot == NONE) st |= ST_PROBE_LIMIT;
                 local_new += is_new ? 1u : 0u;
                 *(orow - i) = ((uint64_t)slot << 32) | ordv;
@@ -720,6 +724,7 @@ hipError_t launch_insert_sk(const SkArgs& a, int KW, hipStream_t s) {
 // scan of the (digit-major, tile-minor) counts, and a scatter that ranks each
 // tile in LDS (wave multisplit by 8 ballots) and writes digit runs coalesced.
 // ---------------------------------------------------------------------------
+constexpr int RUN_SPAN = 8192;  // records of one 256-run round mapped in LDS
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = 256 * RS_ITEMS;  // 4096 records per block
 
@@ -745,49 +750,42 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const uint64_t* __restrict
     counts[(uint64_t)t * n_tiles + blockIdx.x] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
 }
 
+// Each wave ranks its own contiguous 1024-record chunk of the tile (16 rounds
+// of 64) against wave-private digit counters -- multisplit by 8 ballots, no
+// block barrier inside the rounds; tile order = (wave, round, lane), so the
+// ranking is stable.  Three block barriers per tile in all.
 __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint64_t* __restrict__ in,
                                                          uint64_t* __restrict__ out, uint32_t n,
                                                          int shift, const uint32_t* __restrict__ offs,
                                                          uint32_t n_tiles) {
     __shared__ uint64_t buf[RS_TILE];  // 32 KiB: the tile in local digit order
-    __shared__ uint32_t wcnt[4][256];
+    __shared__ uint32_t wcnt[4][256];  // per-wave digit counters, then per-wave digit bases
     __shared__ uint32_t lstart[256];
-    __shared__ uint32_t run[256];
     __shared__ uint32_t gbase[256];
     __shared__ uint32_t sh[4];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t base = (uint64_t)tile * RS_TILE;
     const uint32_t tn = (uint32_t)min((uint64_t)RS_TILE, (uint64_t)n - base);
-    uint64_t v[RS_ITEMS];
-    uint32_t dg[RS_ITEMS];
-#pragma unroll
-    for (int j = 0; j < RS_ITEMS; j++) {
-        const uint32_t li = (uint32_t)j * 256u + t;
-        v[j] = li < tn ? in[base + li] : 0ull;
-        dg[j] = (uint32_t)(v[j] >> shift) & 255u;
-    }
+    const uint32_t wbase = (uint32_t)wid * (RS_TILE / 4);
 #pragma unroll
     for (int w = 0; w < 4; w++) wcnt[w][t] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < RS_ITEMS; j++)
-        if ((uint32_t)j * 256u + t < tn) atomicAdd(&wcnt[wid][dg[j]], 1u);
-    __syncthreads();
-    const uint32_t c = wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan256<uint32_t>(c, sh, tot);
-    lstart[t] = ex;
-    run[t] = 0;
     gbase[t] = offs[(uint64_t)t * n_tiles + tile];
-#pragma unroll
-    for (int w = 0; w < 4; w++) wcnt[w][t] = 0;
-    __syncthreads();
-    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t v[RS_ITEMS];
 #pragma unroll
     for (int j = 0; j < RS_ITEMS; j++) {
-        const bool valid = (uint32_t)j * 256u + t < tn;
-        const uint32_t d = dg[j];
+        const uint32_t li = wbase + (uint32_t)j * 64u + lane;
+        v[j] = li < tn ? in[base + li] : 0ull;
+    }
+    __syncthreads();
+    // phase 1: wave-local stable ranks
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t rk[RS_ITEMS];
+    uint32_t* const cw = wcnt[wid];
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++) {
+        const bool valid = wbase + (uint32_t)j * 64u + lane < tn;
+        const uint32_t d = (uint32_t)(v[j] >> shift) & 255u;
         uint64_t m = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
@@ -796,26 +794,223 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint64_t* __restr
             m &= bit ? bl : ~bl;
         }
         const uint32_t peer = (uint32_t)__popcll(m & lt);
-        if (valid && peer == 0) wcnt[wid][d] = (uint32_t)__popcll(m);
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = lstart[d] + run[d] + peer;
-            for (int w = 0; w < wid; w++) pos += wcnt[w][d];
-            buf[pos] = v[j];
-        }
-        __syncthreads();
-        run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-        wcnt[0][t] = 0;
-        wcnt[1][t] = 0;
-        wcnt[2][t] = 0;
-        wcnt[3][t] = 0;
-        __syncthreads();
+        const uint32_t before = valid ? cw[d] : 0u;
+        wave_sync();
+        if (valid && peer == 0) cw[d] = before + (uint32_t)__popcll(m);
+        wave_sync();
+        rk[j] = before + peer;
     }
+    __syncthreads();
+    // phase 2: thread t = digit t: tile digit starts and per-wave bases
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan256<uint32_t>(c0 + c1 + c2 + c3, sh, tot);
+    lstart[t] = ex;
+    wcnt[0][t] = ex;
+    wcnt[1][t] = ex + c0;
+    wcnt[2][t] = ex + c0 + c1;
+    wcnt[3][t] = ex + c0 + c1 + c2;
+    __syncthreads();
+    // phase 3: place in LDS, then write digit runs out coalesced
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++) {
+        if (wbase + (uint32_t)j * 64u + lane < tn) {
+            const uint32_t d = (uint32_t)(v[j] >> shift) & 255u;
+            buf[cw[d] + rk[j]] = v[j];
+        }
+    }
+    __syncthreads();
     for (uint32_t i = t; i < tn; i += 256) {
         const uint64_t e = buf[i];
         const uint32_t d = (uint32_t)(e >> shift) & 255u;
         out[gbase[d] + (i - lstart[d])] = e;
     }
+}
+
+// ---- onesweep variant: one up-front histogram for all digits, then one
+// scatter launch per digit whose tiles obtain their global digit offsets by
+// decoupled look-back (tiles take tickets in launch order; each publishes its
+// digit counts and then its inclusive prefix as single 8-byte words
+// {epoch:24 | flag:2 | value:38}, written and polled with agent-scope atomics
+// -- the value-is-the-flag hand-off of MI355X_MICROARCH.md "Valid forms").
+constexpr int OS_MAX_PASSES = 4;
+constexpr uint64_t OS_VAL_MASK = (1ull << 38) - 1;
+constexpr uint64_t OS_AGG = 1ull << 38, OS_INC = 2ull << 38;
+constexpr int OS_WIN = 16;  // look-back window (tiles per round trip)
+
+__global__ __launch_bounds__(256) void os_hist_kernel(const uint64_t* __restrict__ in, uint32_t n,
+                                                      int npass, uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t h[OS_MAX_PASSES][256];
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < OS_MAX_PASSES; p++) h[p][t] = 0;
+    __syncthreads();
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + t; k < n; k += (uint64_t)gridDim.x * 256) {
+        const uint64_t e = in[k];
+        for (int p = 0; p < npass; p++) atomicAdd(&h[p][(uint32_t)(e >> (32 + 8 * p)) & 255u], 1u);
+    }
+    __syncthreads();
+    for (int p = 0; p < npass; p++)
+        if (h[p][t]) atomicAdd(&ghist[p * 256 + t], h[p][t]);
+}
+
+__global__ __launch_bounds__(256) void os_bases_kernel(uint32_t* __restrict__ ghist, int npass) {
+    __shared__ uint32_t sh[4];
+    for (int p = 0; p < npass; p++) {
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan256<uint32_t>(ghist[p * 256 + threadIdx.x], sh, tot);
+        ghist[p * 256 + threadIdx.x] = ex;
+    }
+}
+
+__global__ __launch_bounds__(256) void os_scatter_kernel(const uint64_t* __restrict__ in,
+                                                         uint64_t* __restrict__ out, uint32_t n,
+                                                         int shift, const uint32_t* __restrict__ dbase,
+                                                         uint64_t* __restrict__ flags,
+                                                         uint32_t* __restrict__ ticket, uint32_t epoch,
+                                                         uint32_t* __restrict__ err) {
+    __shared__ uint64_t buf[RS_TILE];
+    __shared__ uint32_t wcnt[4][256];
+    __shared__ uint32_t lstart[256];
+    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t sh[4];
+    __shared__ uint32_t s_tile;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (t == 0) s_tile = atomicAdd(ticket, 1u);
+#pragma unroll
+    for (int w = 0; w < 4; w++) wcnt[w][t] = 0;
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t base = (uint64_t)tile * RS_TILE;
+    const uint32_t tn = (uint32_t)min((uint64_t)RS_TILE, (uint64_t)n - base);
+    const uint32_t wbase = (uint32_t)wid * (RS_TILE / 4);
+    uint64_t v[RS_ITEMS];
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++) {
+        const uint32_t li = wbase + (uint32_t)j * 64u + lane;
+        v[j] = li < tn ? in[base + li] : 0ull;
+    }
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t rk[RS_ITEMS];
+    uint32_t* const cw = wcnt[wid];
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++) {
+        const bool valid = wbase + (uint32_t)j * 64u + lane < tn;
+        const uint32_t d = (uint32_t)(v[j] >> shift) & 255u;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bl = __ballot(bit);
+            m &= bit ? bl : ~bl;
+        }
+        const uint32_t peer = (uint32_t)__popcll(m & lt);
+        const uint32_t before = valid ? cw[d] : 0u;
+        wave_sync();
+        if (valid && peer == 0) cw[d] = before + (uint32_t)__popcll(m);
+        wave_sync();
+        rk[j] = before + peer;
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t c = c0 + c1 + c2 + c3;
+    // decoupled look-back for digit t
+    const uint64_t ep = (uint64_t)epoch << 40;
+    uint64_t* const fl = flags + (uint64_t)tile * 256 + t;
+    uint64_t prefix = 0;
+    if (tile == 0) {
+        __hip_atomic_store(fl, ep | OS_INC | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_store(fl, ep | OS_AGG | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // windowed look-back: OS_WIN predecessor words per round trip
+        int64_t tp = (int64_t)tile - 1;
+        uint32_t spins = 0;
+        while (tp >= 0) {
+            uint64_t w[OS_WIN];
+#pragma unroll
+            for (int i = 0; i < OS_WIN; i++)
+                w[i] = tp - i >= 0 ? __hip_atomic_load(flags + (uint64_t)(tp - i) * 256 + t,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0ull;
+            int used = 0;       // words consumed from the window
+            bool done = false, blocked = false;
+#pragma unroll
+            for (int i = 0; i < OS_WIN; i++) {
+                if (!done && !blocked) {
+                    if (tp - i < 0) {
+                        done = true;  // cannot happen (tile 0 publishes INC), kept for safety
+                    } else if ((w[i] >> 40) != epoch || !(w[i] & (OS_AGG | OS_INC))) {
+                        blocked = true;
+                    } else {
+                        prefix += w[i] & OS_VAL_MASK;
+                        used = i + 1;
+                        if (w[i] & OS_INC) done = true;
+                    }
+                }
+            }
+            if (done) break;
+            tp -= used;
+            if (blocked) {
+                if (++spins > (1u << 22)) {  // bounded: report, never hang the device
+                    atomicOr(err, 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __hip_atomic_store(fl, ep | OS_INC | (prefix + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    gbase[t] = dbase[t] + (uint32_t)prefix;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan256<uint32_t>(c, sh, tot);
+    lstart[t] = ex;
+    wcnt[0][t] = ex;
+    wcnt[1][t] = ex + c0;
+    wcnt[2][t] = ex + c0 + c1;
+    wcnt[3][t] = ex + c0 + c1 + c2;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; j++) {
+        if (wbase + (uint32_t)j * 64u + lane < tn) {
+            const uint32_t d = (uint32_t)(v[j] >> shift) & 255u;
+            buf[cw[d] + rk[j]] = v[j];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < tn; i += 256) {
+        const uint64_t e = buf[i];
+        const uint32_t d = (uint32_t)(e >> shift) & 255u;
+        out[gbase[d] + (i - lstart[d])] = e;
+    }
+}
+
+uint64_t onesweep_flag_elems(uint64_t n) { return 256ull * ((n + RS_TILE - 1) / RS_TILE); }
+
+// aux: [0, 4*256) digit histograms -> bases, [1024, 1028) tickets, [1028] error
+hipError_t launch_onesweep(uint64_t* a, uint64_t* b, uint64_t n, int key_bits, uint64_t* flags,
+                           uint32_t* aux, uint32_t* epoch, uint64_t** sorted, hipStream_t s) {
+    *sorted = a;
+    if (n == 0) return hipSuccess;
+    if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const int npass = (key_bits + 7) / 8;
+    if (npass > OS_MAX_PASSES) return hipErrorInvalidValue;
+    const uint32_t n_tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    hipError_t e = hipMemsetAsync(aux, 0, (4 * 256 + 8) * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(os_hist_kernel, dim3(1024), dim3(256), 0, s, a, (uint32_t)n, npass, aux);
+    hipLaunchKernelGGL(os_bases_kernel, dim3(1), dim3(256), 0, s, aux, npass);
+    uint64_t* src = a;
+    uint64_t* dst = b;
+    for (int p = 0; p < npass; p++) {
+        const uint32_t ep = ++*epoch;
+        hipLaunchKernelGGL(os_scatter_kernel, dim3(n_tiles), dim3(256), 0, s, src, dst, (uint32_t)n,
+                           32 + 8 * p, aux + p * 256, flags, aux + 1024 + p, ep, aux + 1028);
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+    }
+    *sorted = src;
+    return hipGetLastError();
 }
 
 // generic exclusive scan of a u32 array (values sum < 2^32), in place
@@ -922,7 +1117,8 @@ __global__ __launch_bounds__(256) void heads_partials_kernel(const uint64_t* __r
 
 __global__ __launch_bounds__(256) void heads_write_kernel(const uint64_t* __restrict__ S, uint64_t n,
                                                           const uint64_t* __restrict__ part,
-                                                          uint32_t* __restrict__ starts) {
+                                                          uint32_t* __restrict__ starts,
+                                                          uint64_t max_runs) {
     __shared__ uint64_t sh[4];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
     uint64_t run = part[blockIdx.x];
@@ -931,14 +1127,20 @@ __global__ __launch_bounds__(256) void heads_write_kernel(const uint64_t* __rest
         const uint32_t h = k < n ? is_head(S, k) : 0u;
         uint64_t tot;
         const uint64_t ex = block_excl_scan256((uint64_t)h, sh, tot);
-        if (h) starts[run + ex] = (uint32_t)k;
+        if (h && run + ex < max_runs) starts[run + ex] = (uint32_t)k;
         run += tot;
     }
 }
 
 __global__ void runs_total_kernel(const uint64_t* __restrict__ tot_runs, uint64_t n,
-                                  uint32_t* __restrict__ starts, uint64_t* __restrict__ totals) {
-    const uint64_t D = *tot_runs;
+                                  uint32_t* __restrict__ starts, uint64_t* __restrict__ totals,
+                                  uint64_t max_runs) {
+    uint64_t D = *tot_runs;
+    totals[3] = 0;
+    if (D > max_runs) {  // cannot happen (runs == distinct keys); never write out of bounds
+        totals[3] = D;
+        D = max_runs;
+    }
     starts[D] = (uint32_t)n;
     totals[2] = D;
 }
@@ -979,12 +1181,13 @@ __global__ __launch_bounds__(256) void runs_write_kernel(
     const uint64_t* __restrict__ S, const uint32_t* __restrict__ starts,
     const uint64_t* __restrict__ totals, uint32_t keep_gt, const uint64_t* __restrict__ part,
     uint64_t nb, const uint64_t* __restrict__ table, int SW, const int32_t* __restrict__ read_ids,
-    int32_t* __restrict__ ids_out, uint32_t* __restrict__ e_mmer, uint64_t* __restrict__ e_hi,
+    uint32_t id_off, int32_t* __restrict__ ids_out, uint32_t* __restrict__ e_mmer, uint64_t* __restrict__ e_hi,
     uint64_t* __restrict__ e_lo, uint32_t* __restrict__ e_cnt, uint64_t* __restrict__ e_off,
     const uint64_t* __restrict__ first, uint64_t* __restrict__ e_first) {
     __shared__ uint64_t sh[4];
     __shared__ uint32_t rs[257];   // run starts of the round (+ end)
     __shared__ uint32_t ro[256];   // id offset of each run, NONE if pruned
+    __shared__ uint8_t rofk[RUN_SPAN];  // run (within the round) of each record of the span
     const uint64_t D = totals[2];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
     if (base >= D) return;  // uniform per block
@@ -1031,16 +1234,24 @@ __global__ __launch_bounds__(256) void runs_write_kernel(
         __syncthreads();
         // copy the round's records: [rs[0], rs[nr]) -- coalesced reads/writes
         const uint32_t k_lo = rs[0], k_hi = rs[nr];
+        const bool filled = k_hi - k_lo <= (uint32_t)RUN_SPAN;  // uniform
+        if (filled && r < D)
+            for (uint32_t k = st; k < st + len; k++) rofk[k - k_lo] = (uint8_t)threadIdx.x;
+        __syncthreads();
         for (uint32_t k = k_lo + threadIdx.x; k < k_hi; k += 256) {
             uint32_t lo = 0, hi = nr;  // last run with rs[run] <= k
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (rs[mid] <= k) lo = mid; else hi = mid;
+            if (filled) {
+                lo = rofk[k - k_lo];
+            } else {
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (rs[mid] <= k) lo = mid; else hi = mid;
+                }
             }
             const uint32_t off = ro[lo];
             if (off != NONE) {
                 const uint32_t o = (uint32_t)S[k];
-                ids_out[off + (k - rs[lo])] = read_ids ? read_ids[o] : (int32_t)o;
+                ids_out[off + (k - rs[lo])] = read_ids ? read_ids[o] : (int32_t)(o + id_off);
             }
         }
         __syncthreads();
@@ -1058,7 +1269,7 @@ __global__ void entries_total_kernel(const uint64_t* __restrict__ tk, const uint
 
 hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int KW,
                        uint32_t keep_gt, uint32_t* starts, const int32_t* read_ids,
-                       int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
+                       uint32_t id_off, int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
                        uint64_t* e_off, const uint64_t* first, uint64_t* e_first,
                        uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s) {
     const int SW = KW == 1 ? 2 : 4;
@@ -1072,8 +1283,10 @@ hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int
     }
     hipLaunchKernelGGL(heads_partials_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch);
     hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch, nb, scratch + nb);
-    hipLaunchKernelGGL(heads_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch, starts);
-    hipLaunchKernelGGL(runs_total_kernel, dim3(1), dim3(1), 0, s, scratch + nb, n, starts, d_totals);
+    hipLaunchKernelGGL(heads_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch, starts,
+                       max_runs);
+    hipLaunchKernelGGL(runs_total_kernel, dim3(1), dim3(1), 0, s, scratch + nb, n, starts, d_totals,
+                       max_runs);
     // runs -> prune -> entries (grid sized for the max possible run count;
     // blocks past the real count exit)
     hipLaunchKernelGGL(runs_partials_kernel, dim3((unsigned)nbr), dim3(256), 0, s, starts, d_totals,
@@ -1082,7 +1295,7 @@ hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int
     hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch + nbr, nbr,
                        scratch + 2 * nbr + 1);
     hipLaunchKernelGGL(runs_write_kernel, dim3((unsigned)nbr), dim3(256), 0, s, S, starts, d_totals,
-                       keep_gt, scratch, nbr, table, SW, read_ids, ids_out, e_mmer, e_hi, e_lo, e_cnt, e_off,
+                       keep_gt, scratch, nbr, table, SW, read_ids, id_off, ids_out, e_mmer, e_hi, e_lo, e_cnt, e_off,
                        first, e_first);
     hipLaunchKernelGGL(entries_total_kernel, dim3(1), dim3(1), 0, s, scratch + 2 * nbr,
                        scratch + 2 * nbr + 1, e_off, d_totals);

@@ -78,7 +78,8 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = pathlib.Path(path) if path else LIB_PATH
+    # KB_LIB_PATH: load an alternative build (A/B experiments)
+    p = pathlib.Path(path) if path else pathlib.Path(os.environ.get("KB_LIB_PATH", LIB_PATH))
     # One HIP runtime per process: torch ships its own libamdhip64.so (same
     # SONAME as /opt/rocm's).  If torch is importable it must be loaded first so
     # libkbin.so binds to that copy instead of pulling in a second runtime.
