@@ -195,7 +195,9 @@ def main():
         "phases_ms": phases,
         "result": {"entries": int(dev["n_entries"]), "ids": int(dev["n_ids"]),
                    "distinct": int(dev["n_distinct"]), "kmers_owned": n_kmers,
-                   "table_slots": int(tim[-1]["table_slots"])},
+                   "table_slots": int(tim[-1]["table_slots"]),
+                   "engine": {1: "table", 2: "binned"}.get(int(tim[-1]["engine"]), "?"),
+                   "bins": int(tim[-1]["n_bins"]), "superkmers": int(tim[-1]["n_superkmers"])},
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(words, lens, min(args.cpu_sample, n), wpr, L, K, M,

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -117,7 +118,14 @@ struct kb_ctx {
     DevBuf<int32_t> ids_out;
     DevBuf<uint64_t> scratch;
     DevBuf<uint32_t> misc;    // [0] status [1] n_distinct
-    DevBuf<uint64_t> totals;  // [0] n_entries [1] n_ids [2] runs
+    DevBuf<uint64_t> totals;  // [0] n_entries [1] n_ids [2] runs [4..6] binned counters
+    // binned engine
+    DevBuf<uint32_t> seg;      // super-k-mers per read -> exclusive scan
+    DevBuf<uint64_t> pay;      // super-k-mer records, call order (3 words each)
+    DevBuf<uint64_t> srec;     // the same, bin order, structure of arrays
+    DevBuf<uint32_t> kbase;    // first occurrence index of each bin-ordered record
+    DevBuf<uint64_t> stage;    // per-occurrence (slot, ordinal) staging
+    float rho = 0.f;           // learned distinct / occurrences
     uint64_t* h_totals = nullptr;
     uint32_t* h_misc = nullptr;
 
@@ -160,7 +168,7 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     if (p.cutoff < 0) return fail(KB_EINVAL, "cutoff < 0");
     if (p.max_read_len < 1 || p.max_read_len > 65535)
         return fail(KB_EINVAL, "max_read_len=%d outside [1,65535]", p.max_read_len);
-    if (p.flags & ~KB_TRACK_FIRST) return fail(KB_EINVAL, "unknown flags 0x%x", p.flags);
+    if (p.flags & ~(KB_TRACK_FIRST | KB_ENGINE_TABLE | KB_ENGINE_BINNED)) return fail(KB_EINVAL, "unknown flags 0x%x", p.flags);
     if (p.table_slots && (p.table_slots & (p.table_slots - 1)))
         return fail(KB_EINVAL, "table_slots must be a power of two");
     kb_ctx* c = new kb_ctx();
@@ -208,6 +216,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->kbase.release(); c->stage.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
@@ -529,6 +538,173 @@ static int log2u(uint64_t x) {
     return b;
 }
 
+// ---------------------------------------------------------------------------
+// binned engine (kbin_bins.hip): super-k-mers -> sort by mmer -> one LDS
+// table per bin.  Eligible for K <= 31 reads binned here, no first-occurrence
+// tracking.
+// ---------------------------------------------------------------------------
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
+static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
+    const int M = c->p.M;
+    const uint64_t nr = c->n_reads;
+    c->tm.engine = KB_ENG_BINNED;
+    REC(0);
+    HIPCHK(c->seg.ensure(nr + 1));
+    HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(nr + 1), c->scratch.cap)));
+    HIPCHK(c->totals.ensure(8));
+    HIPCHK(hipMemsetAsync(c->totals.p, 0, 8 * sizeof(uint64_t), c->s));
+    HIPCHK(hipMemsetAsync(c->misc.p, 0, 2 * sizeof(uint32_t), c->s));
+    REC(1);
+    // ---- phase A: super-k-mers per read, scan, records
+    c->tm.scan_insert_launches = 0;
+    for (auto& b : c->batches) {
+        SkScanArgs a{};
+        a.words = b.words;
+        a.lens = b.lens;
+        a.n_reads = b.n_reads;
+        a.seg_count = c->seg.p + b.ord_base;
+        a.RW = b.RW;
+        a.K = c->p.K;
+        a.M = M;
+        HIPCHK(launch_sk(a, false, c->s));
+        c->tm.scan_insert_launches++;
+    }
+    HIPCHK(launch_scan_u32(c->seg.p, nr, c->scratch.p, c->scratch.cap, c->s));
+    const uint64_t nbs = scan_u32_scratch_elems(nr) - 2;
+    HIPCHK(hipMemcpyAsync(c->h_totals + 7, c->scratch.p + nbs, 8, hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    const uint64_t R = nr ? c->h_totals[7] : 0;
+    if (R > N) return fail(KB_EDEVICE, "internal: %llu super-k-mers > %llu k-mers", (unsigned long long)R,
+                           (unsigned long long)N);
+    HIPCHK(c->pay.ensure(3 * R));
+    HIPCHK(c->srec.ensure(3 * R));
+    HIPCHK(c->occ_a.ensure(std::max<uint64_t>(R, N / 2 + 1)));
+    HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 1)));
+    for (auto& b : c->batches) {
+        SkScanArgs a{};
+        a.words = b.words;
+        a.lens = b.lens;
+        a.n_reads = b.n_reads;
+        a.rec_base = c->seg.p + b.ord_base;
+        a.pay = c->pay.p;
+        a.keys = c->occ_a.p;
+        a.ord_base = (uint32_t)b.ord_base;
+        a.RW = b.RW;
+        a.K = c->p.K;
+        a.M = M;
+        HIPCHK(launch_sk(a, true, c->s));
+        c->tm.scan_insert_launches++;
+    }
+    REC(2);
+    // ---- stable sort of the records by canonical mmer, bin boundaries
+    const int key_bits = 2 * M;
+    const uint64_t nflags = onesweep_flag_elems(R);
+    if (c->os_flags.cap < nflags || c->os_epoch > (1u << 24) - 8) {
+        HIPCHK(c->os_flags.ensure(nflags));
+        HIPCHK(hipMemsetAsync(c->os_flags.p, 0, c->os_flags.cap * sizeof(uint64_t), c->s));
+        c->os_epoch = 0;
+    }
+    HIPCHK(c->os_aux.ensure(4 * 256 + 8));
+    HIPCHK(hipMemsetAsync(c->os_aux.p + 1028, 0, sizeof(uint32_t), c->s));
+    HIPCHK(launch_onesweep(c->occ_a.p, c->occ_b.p, R, key_bits, c->os_flags.p, c->os_aux.p,
+                           &c->os_epoch, &c->sorted, c->s));
+    c->tm.sort_passes = (uint32_t)((key_bits + 7) / 8);
+    const uint64_t max_bins = std::max<uint64_t>(1, std::min<uint64_t>(R, 1ull << (2 * M - 1)));
+    HIPCHK(c->starts.ensure(max_bins + 1));
+    HIPCHK(c->scratch.ensure(std::max(runs_scratch_elems(R, max_bins), c->scratch.cap)));
+    HIPCHK(launch_heads(c->sorted, R, c->starts.p, max_bins, c->scratch.p, c->scratch.cap,
+                        c->totals.p, c->s));
+    HIPCHK(c->kbase.ensure(R + 1));
+    HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
+    HIPCHK(launch_sk_gather(c->sorted, c->pay.p, R, c->srec.p, c->kbase.p, c->s));
+    HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(R + 1), c->scratch.cap)));
+    HIPCHK(launch_scan_u32(c->kbase.p, R, c->scratch.p, c->scratch.cap, c->s));
+    REC(3);
+    // ---- one workgroup per bin
+    const uint64_t ecap = N + 1;
+    HIPCHK(c->e_mmer.ensure(ecap));
+    HIPCHK(c->e_cnt.ensure(ecap));
+    HIPCHK(c->e_hi.ensure(ecap));
+    HIPCHK(c->e_lo.ensure(ecap));
+    HIPCHK(c->e_off.ensure(ecap));
+    HIPCHK(c->ids_out.ensure(std::max<uint64_t>(N, 1)));
+    bool affine = true;
+    int64_t id_c = 0;
+    for (size_t i = 0; i < c->batches.size(); i++) {
+        const Batch& b = c->batches[i];
+        const int64_t cb = b.first_id - (int64_t)b.ord_base;
+        if (!b.affine || (i && cb != id_c)) affine = false;
+        id_c = cb;
+    }
+    // >= 10: the sort phase carves 8 wave windows of 256 ids out of the table
+    const int ts_log2 = std::min(13, std::max(10, env_int("KB_BIN_TS_LOG2", 13)));
+    BinArgs a{};
+    a.keys = c->sorted;
+    a.hdr = c->srec.p;
+    a.w0 = c->srec.p + R;
+    a.w1 = c->srec.p + 2 * R;
+    a.bstart = c->starts.p;
+    a.kbase = c->kbase.p;
+    a.stage = c->stage.p;
+    a.totals = c->totals.p;
+    a.K = c->p.K;
+    a.M = M;
+    a.keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
+    a.ts_log2 = (uint32_t)ts_log2;
+    a.rho = c->rho > 0.f ? c->rho : 0.25f;
+    a.gcount = reinterpret_cast<unsigned long long*>(c->totals.p + 4);
+    a.status = c->misc.p;
+    a.e_mmer = c->e_mmer.p;
+    a.e_hi = c->e_hi.p;
+    a.e_lo = c->e_lo.p;
+    a.e_cnt = c->e_cnt.p;
+    a.e_off = c->e_off.p;
+    a.ids_ord = reinterpret_cast<uint32_t*>(c->sorted == c->occ_a.p ? c->occ_b.p : c->occ_a.p);
+    a.ids_out = c->ids_out.p;
+    a.read_ids = affine ? nullptr : c->read_ids.p;
+    a.id_off = (uint32_t)(affine ? id_c : 0);
+    a.max_entries = N;
+    a.max_ids = N;
+    HIPCHK(launch_bins(a, max_bins, c->s));
+#ifdef KB_BIN_PROF
+    bins_prof_report(c->s);
+#endif
+    REC(4);
+    HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries, c->s));
+    REC(5);
+    HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    if (R) HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    else c->h_misc[8] = 0;
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (c->h_misc[8]) return fail(KB_EDEVICE, "radix look-back timed out (device error word %u)", c->h_misc[8]);
+    if (c->h_totals[3]) return fail(KB_EDEVICE, "internal: %llu bins > %llu", (unsigned long long)c->h_totals[3],
+                                    (unsigned long long)max_bins);
+    if (c->h_misc[0] & ST_TABLE_FULL) return fail(KB_EDEVICE, "internal: CSR capacity exceeded");
+    if (c->h_misc[0] & ST_PROBE_LIMIT) return fail(KB_ENOMEM, "a bin exceeded the partition depth");
+    c->n_entries = c->h_totals[0];
+    c->n_ids = c->h_totals[1];
+    c->n_distinct = c->h_totals[6];
+    if (N) c->rho = (float)((double)c->n_distinct / (double)N);
+    if (c->timing) {
+        HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));
+        HIPCHK(hipEventElapsedTime(&c->tm.sort_ms, c->ev[2], c->ev[3]));
+        HIPCHK(hipEventElapsedTime(&c->tm.runs_ms, c->ev[3], c->ev[4]));
+        HIPCHK(hipEventElapsedTime(&c->tm.emit_ms, c->ev[4], c->ev[5]));
+        HIPCHK(hipEventElapsedTime(&c->tm.total_ms, c->ev[0], c->ev[5]));
+    }
+    c->tm.table_slots = 1ull << ts_log2;
+    c->tm.n_bins = (uint32_t)c->h_totals[2];
+    c->tm.n_superkmers = R;
+    c->finalized = true;
+    c->exported = false;
+    return KB_OK;
+}
+
 extern "C" int kb_finalize(kb_ctx* c, int prune) {
     if (!c) return fail(KB_EINVAL, "null ctx");
     if (c->finalized) return fail(KB_ESTATE, "already finalized (call kb_reset)");
@@ -552,6 +728,22 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     memset(&c->tm, 0, sizeof(c->tm));
     const int SW = c->KW == 1 ? 2 : 4;
     const bool track_first = (c->p.flags & KB_TRACK_FIRST) != 0;
+    bool any_routed = false;
+    for (auto& b : c->batches) any_routed |= b.routed;
+    // ids of the reads, ordinal-indexed (both engines)
+    HIPCHK(c->read_ids.ensure(c->n_reads));
+    for (auto& b : c->batches)
+        if (!b.superkmers && b.n_reads)
+            HIPCHK(hipMemcpyAsync(c->read_ids.p + b.ord_base, b.ids, b.n_reads * sizeof(int32_t),
+                                  hipMemcpyDeviceToDevice, c->s));
+    // engine choice: flags, then KB_ENGINE=table|binned (A/B runs), then the default
+    bool binned = false;
+    if (c->p.flags & KB_ENGINE_BINNED) binned = true;
+    else if (c->p.flags & KB_ENGINE_TABLE) binned = false;
+    else if (const char* e = getenv("KB_ENGINE")) binned = strcmp(e, "binned") == 0;
+    if (binned && c->KW == 1 && !track_first && !any_sk && !any_routed)
+        return finalize_binned(c, prune, N);
+    c->tm.engine = KB_ENG_TABLE;
     // ---- table plan: ~0.6 load for the expected distinct keys
     uint64_t slots = c->p.table_slots;
     if (!slots) slots = c->learned_slots;
@@ -560,12 +752,6 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     HIPCHK(c->occ_a.ensure(N));
     HIPCHK(c->occ_b.ensure(N));
     HIPCHK(c->ids_out.ensure(N));
-    // ordinal -> read id, concatenated over batches
-    HIPCHK(c->read_ids.ensure(c->n_reads));
-    for (auto& b : c->batches)
-        if (!b.superkmers && b.n_reads)
-            HIPCHK(hipMemcpyAsync(c->read_ids.p + b.ord_base, b.ids, b.n_reads * sizeof(int32_t),
-                                  hipMemcpyDeviceToDevice, c->s));
     uint32_t status = 0, ndist = 0;
     for (int attempt = 0;; attempt++) {
         if (slots > (1ull << 32) - 1)

@@ -1,0 +1,756 @@
+// kbin_bins.hip -- the binned engine ("v2") for K <= 31.
+//
+// The reference's level-1 key is the signature mmer (binning.c:1045): every
+// (mmer, kmer) entry lives in exactly one mmer bin, and prune_kmers runs per
+// mmer table (binning.c:1085, 1136).  v2 uses that as the unit of locality:
+//
+//   sk_count / sk_write  one wavefront per read walks the sticky signature
+//                        chain (as scan_insert does) and emits one record per
+//                        super-k-mer (run of k-mers sharing a signature):
+//                        payload {ord | i0 | n | sig_off}, sort key (mmer, t)
+//   onesweep             stable sort of the keys by mmer (2 passes at M=7)
+//   heads                bin boundaries
+//   bin_kernel           ONE WORKGROUP PER BIN: an LDS open-addressed table
+//                        keyed by the k-mer alone (the mmer is the bin -- this
+//                        is the per-mmer bucket of the north star), counts by
+//                        LDS atomics, prune, CSR allocation, read-id placement
+//                        and per-key reverse-call-order lists, all LDS/L2-local.
+//                        A bin whose keys overflow the LDS table is split by
+//                        k-mer hash into sub-partitions, recursively.
+//
+// Nothing in the hot loops touches HBM at random except the read-word gathers
+// (L2/MALL-resident packed reads) and the output writes.
+#include <algorithm>
+#include <cstdio>
+
+#include "kbin_internal.h"
+#include "kbin_device.h"
+
+namespace kb {
+
+// ---------------------------------------------------------------------------
+// phase A: super-k-mer extraction
+// ---------------------------------------------------------------------------
+// One segment of the sticky chain per call: leftmost strict argmax of the
+// complement-canonical mmer score over [lo, lo + K - M]  (binning.c:922-988).
+DEV void segment_at(const uint64_t* sw, int lo, int lane, int W, int M, uint32_t maskM,
+                    uint32_t halfM, int& sig, uint32_t& canon) {
+    const int d = (lane - lo) & 63;
+    uint32_t key = 0;
+    if (d < W) {
+        const int p = lo + d;
+        const uint32_t s = (uint32_t)(window64(sw, p) >> (64 - 2 * M));
+        const uint32_t c = s >= halfM ? s : maskM - s;
+        key = (c << 16) | (0xFFFFu - (uint32_t)p);
+    }
+    key = wave_max_u32(key);
+    sig = rfl((int)(0xFFFFu - (key & 0xFFFFu)));
+    canon = (uint32_t)rfl((int)(key >> 16));
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int RW = A.RW, K = A.K, M = A.M;
+    const int W = K - M + 1;
+    const uint32_t maskM = (1u << (2 * M)) - 1u;
+    const uint32_t halfM = 1u << (2 * M - 1);
+    uint64_t* sw = smem + wid * (RW + 2);  // two zero words: span windows never leave the read
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    for (uint64_t r = (uint64_t)blockIdx.x * 4 + wid; r < A.n_reads; r += nwaves) {
+        const int L = rfl((int)A.lens[r]);
+        const int nK = L - K + 1;
+        uint32_t nseg = 0;
+        if (nK > 0) {
+            wave_sync();
+            for (int w = lane; w < RW + 2; w += 64) sw[w] = w < RW ? A.words[r * RW + w] : 0ull;
+            wave_sync();
+            const uint64_t rbase = WRITE ? A.rec_base[r] : 0;
+            const uint64_t ordv = (uint64_t)(A.ord_base + (uint32_t)r);
+            int lo = 0;
+            while (lo < nK) {
+                int sig;
+                uint32_t canon;
+                segment_at(sw, lo, lane, W, M, maskM, halfM, sig, canon);
+                if (WRITE && lane == 0) {
+                    // one super-k-mer: k-mers lo..min(sig, nK-1) share the
+                    // signature at sig (binning.c:1004-1040 with the sticky
+                    // window).  Span = bases lo .. lo+n+K-2 (<= 56 for K <= 31).
+                    const uint64_t t = rbase + nseg;
+                    const int n = min(sig, nK - 1) - lo + 1;
+                    const uint32_t sm = (uint32_t)(window64(sw, sig) >> (64 - 2 * M));
+                    const uint64_t rev = sm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
+                    A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44);
+                    A.pay[3 * t + 1] = window64(sw, lo);
+                    A.pay[3 * t + 2] = window64(sw, lo + 32);
+                    A.keys[t] = ((uint64_t)canon << 32) | (uint32_t)t;
+                }
+                nseg++;
+                lo = sig + 1;
+            }
+        }
+        if (!WRITE && lane == 0) A.seg_count[r] = nseg;
+    }
+}
+
+// Thread-per-read variant for short reads (RW <= SK_THREAD_RW): a block
+// stages 256 reads in LDS rows and each lane walks its own read's sticky
+// chain serially.  The wave-per-read kernel above keeps 64 lanes busy on a
+// window of only K-M+1 positions; one lane per read does the same argmax
+// with no cross-lane reduction and no idle lanes.
+constexpr int SK_THREAD_RW = 16;
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    const int RW = A.RW, K = A.K, M = A.M;
+    const int W = K - M + 1;
+    const int RS = RW + 2;  // row stride: two zero words past the read
+    const int sh = 64 - 2 * M;
+    const uint32_t maskM = (1u << (2 * M)) - 1u;
+    const uint32_t halfM = 1u << (2 * M - 1);
+    const uint32_t tid = threadIdx.x;
+    for (uint64_t r0 = (uint64_t)blockIdx.x * 256; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * 256) {
+        const uint32_t nrows = (uint32_t)min<uint64_t>(256, A.n_reads - r0);
+        __syncthreads();
+        for (uint32_t i = tid; i < nrows * (uint32_t)RW; i += 256) {
+            const uint32_t row = i / (uint32_t)RW, col = i - row * (uint32_t)RW;
+            smem[row * RS + col] = A.words[r0 * RW + i];
+        }
+        if (tid < nrows) {
+            smem[tid * RS + RW] = 0;
+            smem[tid * RS + RW + 1] = 0;
+        }
+        __syncthreads();
+        if (tid >= nrows) continue;
+        const uint64_t r = r0 + tid;
+        const uint64_t* sw = smem + tid * RS;
+        const int nK = (int)A.lens[r] - K + 1;
+        uint32_t nseg = 0;
+        const uint64_t rbase = WRITE ? A.rec_base[r] : 0;
+        const uint64_t ordv = (uint64_t)(A.ord_base + (uint32_t)r);
+        int lo = 0;
+        while (lo < nK) {
+            // leftmost strict argmax of the canonical score over the window
+            int best = -1, sig = lo;
+            for (int p = lo; p < lo + W; p++) {
+                const uint32_t sm = (uint32_t)(window64(sw, p) >> sh);
+                const int c = (int)(sm >= halfM ? sm : maskM - sm);
+                if (c > best) {
+                    best = c;
+                    sig = p;
+                }
+            }
+            if (WRITE) {
+                const uint64_t t = rbase + nseg;
+                const int n = min(sig, nK - 1) - lo + 1;
+                const uint32_t sm = (uint32_t)(window64(sw, sig) >> sh);
+                const uint64_t rev = sm < halfM ? 1ull : 0ull;
+                A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44);
+                A.pay[3 * t + 1] = window64(sw, lo);
+                A.pay[3 * t + 2] = window64(sw, lo + 32);
+                A.keys[t] = ((uint64_t)(uint32_t)best << 32) | (uint32_t)t;
+            }
+            nseg++;
+            lo = sig + 1;
+        }
+        if (!WRITE) A.seg_count[r] = nseg;
+    }
+}
+
+hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s) {
+    if (!a.n_reads) return hipSuccess;
+    if (a.RW <= SK_THREAD_RW) {
+        const uint64_t blocks = std::min<uint64_t>((a.n_reads + 255) / 256, 8192);
+        const size_t lds = (size_t)256 * (a.RW + 2) * sizeof(uint64_t);
+        if (write)
+            hipLaunchKernelGGL(sk_thread_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+        else
+            hipLaunchKernelGGL(sk_thread_kernel<false>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+        return hipGetLastError();
+    }
+    uint64_t blocks = (a.n_reads + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
+    const size_t lds = (size_t)4 * (a.RW + 2) * sizeof(uint64_t);
+    if (write)
+        hipLaunchKernelGGL(sk_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+    else
+        hipLaunchKernelGGL(sk_kernel<false>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+// records into bin order, structure of arrays (the bin kernel streams them)
+__global__ __launch_bounds__(256) void sk_gather_kernel(const uint64_t* __restrict__ keys,
+                                                        const uint64_t* __restrict__ pay, uint64_t R,
+                                                        uint64_t* __restrict__ srec, uint32_t* __restrict__ nk) {
+    for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < R; k += (uint64_t)gridDim.x * 256) {
+        const uint64_t t = (uint32_t)keys[k];
+        const uint64_t hd = pay[3 * t];
+        srec[k] = hd;
+        nk[k] = (uint32_t)(hd >> 32) & 63u;
+        srec[R + k] = pay[3 * t + 1];
+        srec[2 * R + k] = pay[3 * t + 2];
+    }
+}
+
+hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
+                            uint32_t* nk, hipStream_t s) {
+    if (!R) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((R + 255) / 256, 8192);
+    hipLaunchKernelGGL(sk_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, s, keys, pay, R, srec, nk);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// phase B: one workgroup per mmer bin
+// ---------------------------------------------------------------------------
+#ifdef KB_BIN_PROF
+// per-phase cycle accounting (tid 0, between barriers): a diagnostic build only
+__device__ unsigned long long g_bin_prof[16];
+#define PROF_MARK(ph)                                              \
+    do {                                                           \
+        if (tid == 0) {                                            \
+            const unsigned long long _t = clock64();               \
+            pacc[ph] += _t - pt;                                   \
+            pt = _t;                                               \
+        }                                                          \
+    } while (0)
+#define PROF_CNT(i, v) do { if (tid == 0) pacc[i] += (v); } while (0)
+#else
+#define PROF_MARK(ph) do {} while (0)
+#define PROF_CNT(i, v) do {} while (0)
+#endif
+
+constexpr int BIN_THREADS = 512;
+constexpr int BIN_SORT_CAP = 8192;  // largest id list ordered in LDS in one piece
+constexpr int BIN_STACK = 32;
+
+DEV uint64_t lds_load_u64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// find-or-insert a k-mer (stored as code + 1) in the bin's LDS table
+DEV int lds_insert(uint64_t* claim, uint32_t mask, uint64_t key, uint32_t h, uint32_t* n_keys,
+                   uint32_t limit) {
+    uint32_t idx = h & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+        const uint64_t v = lds_load_u64(&claim[idx]);
+        if (v == key) return (int)idx;
+        if (v == 0) {
+            const uint64_t old = atomicCAS((unsigned long long*)&claim[idx], 0ull, (unsigned long long)key);
+            if (old == 0) {
+                if (atomicAdd(n_keys, 1u) >= limit) return -2;
+                return (int)idx;
+            }
+            if (old == key) return (int)idx;
+        }
+        idx = (idx + 1) & mask;
+    }
+    return -1;
+}
+
+DEV int lds_find(const uint64_t* claim, uint32_t mask, uint64_t key, uint32_t h) {
+    uint32_t idx = h & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+        const uint64_t v = claim[idx];
+        if (v == key) return (int)idx;
+        if (v == 0) return -1;
+        idx = (idx + 1) & mask;
+    }
+    return -1;
+}
+
+// map a call ordinal to the caller's read id
+DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
+    return read_ids ? read_ids[ord] : (int32_t)(ord + id_off);
+}
+
+struct alignas(16) BinShared {
+    uint32_t n_keys, overflow, sp, cur_p, cur_l, n_big, n_stage, pad0;
+    unsigned long long e0, i0;
+    uint32_t stack_p[BIN_STACK], stack_l[BIN_STACK];
+    uint64_t red[BIN_THREADS / 64];
+};
+static_assert(sizeof(BinShared) % 16 == 0, "LDS carve must stay 16-B aligned (guide G17)");
+
+// block-wide exclusive scan of two u32 quantities packed in a u64 (each lane's
+// value < 2^32, totals < 2^32)
+DEV uint64_t block_excl_scan_u64(uint64_t v, uint64_t* red, uint64_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) red[wid] = inc;
+    __syncthreads();
+    uint64_t wp = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < BIN_THREADS / 64; w++) {
+        const uint64_t x = red[w];
+        if (w < wid) wp += x;
+        tot += x;
+    }
+    __syncthreads();
+    total = tot;
+    return wp + inc - v;
+}
+
+constexpr int BIN_WAVES = BIN_THREADS / 64;
+constexpr int BIN_Q = 128;  // per-wave k-mer queue (64 pending + 64 pushed)
+
+DEV uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Expand the k-mers of the bin's records that fall in partition (p, l) and
+// hand each to f(code_plus1, ord, sidx).  Records are the bin's super-k-mers,
+// streamed from the bin-ordered SoA arrays, one record per lane.  Matching
+// k-mers are compacted through a per-wave LDS queue so f always runs on 64
+// k-mers at once, whatever the record lengths and the partition filter;
+// sidx is a block-unique index (0 .. k-mers of the partition - 1) taken from
+// *ctr.  The partition filter is one multiply; the table hash (mix64) is
+// computed by f on the compacted k-mers only.
+DEV uint32_t part_of(uint64_t code) { return (uint32_t)((code * 0x9E3779B97F4A7C15ull) >> 40); }
+
+template <typename F>
+DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, uint32_t l,
+                       uint64_t* qk, uint32_t* qo, uint32_t* ctr, F&& f) {
+    const int K = A.K;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t kmask = (1ull << (2 * K)) - 1ull;
+    const uint32_t pmask = (1u << l) - 1u;
+    uint32_t qn = 0;  // wave-uniform queue fill
+    for (uint32_t base = lo + wid * 64; base < hi; base += BIN_THREADS) {
+        const uint32_t rec = base + lane;
+        uint64_t hd = 0, s0 = 0, s1 = 0;
+        if (rec < hi) {
+            hd = A.hdr[rec];
+            s0 = A.w0[rec];
+            s1 = A.w1[rec];
+        }
+        const int n = (int)((hd >> 32) & 63u);
+        const uint32_t ord = (uint32_t)hd;
+        const uint64_t flip = ((hd >> 44) & 1ull) ? kmask : 0ull;
+        const int nmax = rfl((int)wave_max_u32((uint32_t)n));
+        for (int j = 0; j < nmax; j++) {
+            const uint64_t code = (span_window(s0, s1, 0ull, 0ull, j) >> (64 - 2 * K)) ^ flip;
+            const bool take = j < n && (l == 0 || (part_of(code) & pmask) == p);
+            const uint64_t m = __ballot(take);
+            if (take) {
+                const uint32_t pos = qn + lanes_below(m);
+                qk[pos] = code + 1ull;
+                qo[pos] = ord;
+            }
+            qn += (uint32_t)__popcll(m);
+            if (qn >= 64) {
+                wave_sync();
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(ctr, 64u);
+                b = (uint32_t)__shfl((int)b, 0, 64);
+                f(qk[lane], qo[lane], b + lane);
+                if (lane + 64 < qn) {
+                    const uint64_t k2 = qk[lane + 64];
+                    const uint32_t o2 = qo[lane + 64];
+                    qk[lane] = k2;
+                    qo[lane] = o2;
+                }
+                qn -= 64;
+                wave_sync();
+            }
+        }
+    }
+    wave_sync();
+    if (qn) {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(ctr, qn);
+        b = (uint32_t)__shfl((int)b, 0, 64);
+        if ((uint32_t)lane < qn) f(qk[lane], qo[lane], b + lane);
+    }
+    wave_sync();
+}
+
+__global__ __launch_bounds__(BIN_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void bin_kernel(BinArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    BinShared& S = *reinterpret_cast<BinShared*>(smem);      // all LDS in one dynamic array
+    const uint32_t TS = 1u << A.ts_log2, tmask = TS - 1;
+    uint64_t* claim = smem + sizeof(BinShared) / 8;          // [TS] k-mer code + 1
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(claim + TS);  // [TS] count, then cursor
+    uint32_t* big = cnt;                                      // sort phase: big-list entry ids
+    uint64_t* qk = reinterpret_cast<uint64_t*>(cnt + TS) + (threadIdx.x >> 6) * BIN_Q;
+    uint32_t* qo = reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(cnt + TS) + BIN_WAVES * BIN_Q) +
+                   (threadIdx.x >> 6) * BIN_Q;
+    const uint64_t nbins = A.totals[2];
+    const uint32_t tid = threadIdx.x;
+#ifdef KB_BIN_PROF
+    unsigned long long pacc[16] = {};
+    unsigned long long pt = clock64();
+#endif
+
+    for (uint64_t b = blockIdx.x; b < nbins; b += gridDim.x) {
+        const uint32_t lo = A.bstart[b], hi = A.bstart[b + 1];
+        const uint32_t mmer = (uint32_t)(A.keys[lo] >> 32);
+        uint64_t* stage = A.stage + A.kbase[lo];  // the bin's k-mer range, reused per partition
+        // occurrences of the bin -> first partition depth
+        uint64_t occ = 0;
+        for (uint32_t rec = lo + tid; rec < hi; rec += BIN_THREADS)
+            occ += (A.hdr[rec] >> 32) & 63u;
+        uint64_t occ_tot;
+        (void)block_excl_scan_u64(occ, S.red, occ_tot);
+        PROF_CNT(11, 1);
+        PROF_CNT(14, occ_tot);
+        uint32_t l0 = 0;  // uniform: initial partition depth from the expected distinct keys
+        {
+            const double want = (double)occ_tot * A.rho / (0.6 * TS);
+            while ((double)(1u << l0) < want && l0 < 16) l0++;
+        }
+        for (uint32_t p0 = 0; p0 < (1u << l0); p0++) {
+        if (tid == 0) {
+            S.sp = 1;
+            S.stack_p[0] = p0;
+            S.stack_l[0] = l0;
+        }
+        __syncthreads();
+        while (true) {
+            if (tid == 0) {
+                if (S.sp == 0) {
+                    S.cur_l = 0xFFFFFFFFu;
+                } else {
+                    S.sp--;
+                    S.cur_p = S.stack_p[S.sp];
+                    S.cur_l = S.stack_l[S.sp];
+                }
+                S.n_keys = 0;
+                S.overflow = 0;
+                S.n_big = 0;
+                S.n_stage = 0;
+            }
+            for (uint32_t i = tid; i < TS; i += BIN_THREADS) {
+                claim[i] = 0;
+                cnt[i] = 0;
+            }
+            __syncthreads();
+            PROF_MARK(1);
+            const uint32_t P = S.cur_p, Lv = S.cur_l;
+            if (Lv == 0xFFFFFFFFu) break;  // uniform
+            PROF_CNT(8, 1);
+            const uint32_t limit = TS - TS / 4;
+            // ---- sweep 1: insert + count (binning.c:1042-1069 semantics per key)
+            // each occurrence is staged as (slot, ordinal) for sweep 2
+            for_each_kmer(A, lo, hi, P, Lv, qk, qo, &S.n_stage, [&](uint64_t key, uint32_t ord, uint32_t si) {
+                const int ls = lds_insert(claim, tmask, key, (uint32_t)mix64(key - 1ull), &S.n_keys, limit);
+                if (ls < 0) {
+                    S.overflow = 1;
+                } else {
+                    atomicAdd(&cnt[ls], 1u);
+                    stage[si] = ((uint64_t)ls << 32) | ord;
+                }
+            });
+            __syncthreads();
+            PROF_MARK(2);
+            if (S.overflow) {  // uniform: split this partition in two and redo both
+                PROF_CNT(9, 1);
+                if (tid == 0) {
+                    if (Lv >= 20 || S.sp + 2 > BIN_STACK) {
+                        atomicOr(A.status, ST_PROBE_LIMIT);
+                    } else {
+                        S.stack_p[S.sp] = P;
+                        S.stack_l[S.sp] = Lv + 1;
+                        S.stack_p[S.sp + 1] = P + (1u << Lv);
+                        S.stack_l[S.sp + 1] = Lv + 1;
+                        S.sp += 2;
+                    }
+                }
+                __syncthreads();
+                continue;
+            }
+            // ---- prune (binning.c:1094-1102) + CSR allocation
+            uint64_t mine = 0;  // (ids << 32) | entries over this thread's slots
+            const uint32_t per = TS / BIN_THREADS;  // TS >= BIN_THREADS
+            for (uint32_t k = 0; k < per; k++) {
+                const uint32_t i = tid * per + k;
+                const uint32_t c = cnt[i];
+                if (claim[i] && c > A.keep_gt) mine += ((uint64_t)c << 32) + 1ull;
+            }
+            uint64_t tot;
+            uint64_t ex = block_excl_scan_u64(mine, S.red, tot);
+            if (tid == 0) {
+                const uint32_t ne = (uint32_t)tot, ni = (uint32_t)(tot >> 32);
+                atomicAdd(&A.gcount[2], (unsigned long long)S.n_keys);  // distinct before prune
+                S.e0 = ne ? atomicAdd((unsigned long long*)&A.gcount[0], (unsigned long long)ne) : 0ull;
+                S.i0 = ni ? atomicAdd((unsigned long long*)&A.gcount[1], (unsigned long long)ni) : 0ull;
+                if (S.e0 + ne > A.max_entries || S.i0 + ni > A.max_ids) atomicOr(A.status, ST_TABLE_FULL);
+            }
+            __syncthreads();
+            const unsigned long long e0 = S.e0, i0 = S.i0;
+            const bool room = !(e0 + (uint32_t)tot > A.max_entries || i0 + (uint32_t)(tot >> 32) > A.max_ids);
+            {
+                uint32_t e = (uint32_t)ex, off = (uint32_t)(ex >> 32);
+                for (uint32_t k = 0; k < per; k++) {
+                    const uint32_t i = tid * per + k;
+                    const uint32_t c = cnt[i];
+                    if (claim[i] && c > A.keep_gt) {
+                        if (room) {
+                            const uint64_t ge = e0 + e;
+                            A.e_mmer[ge] = mmer;
+                            A.e_hi[ge] = 0;
+                            A.e_lo[ge] = claim[i] - 1ull;
+                            A.e_cnt[ge] = c;
+                            A.e_off[ge] = i0 + off;
+                        }
+                        cnt[i] = off;  // cursor (relative to i0)
+                        e++;
+                        off += c;
+                    } else {
+                        cnt[i] = NONE;
+                    }
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+            PROF_MARK(3);
+            if (!room) continue;
+            // ---- sweep 2: drop every surviving occurrence's call ordinal in place
+            {
+                const uint32_t ns = S.n_stage;
+                for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
+                    const uint64_t v = stage[i];
+                    const uint32_t ls = (uint32_t)(v >> 32);
+                    if (cnt[ls] != NONE) {
+                        const uint32_t pos = atomicAdd(&cnt[ls], 1u);
+                        A.ids_ord[i0 + pos] = (uint32_t)v;
+                    }
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+            PROF_MARK(4);
+            // ---- per key: reverse call order = descending ordinal (binning.c:1061-1068)
+            const uint32_t ne = (uint32_t)tot;
+            for (uint32_t e = tid; e < ne; e += BIN_THREADS) {
+                const uint64_t ge = e0 + e;
+                const uint32_t n = A.e_cnt[ge];
+                const uint64_t o = A.e_off[ge];
+                if (n > 32) {
+                    big[atomicAdd(&S.n_big, 1u)] = e;
+                    continue;
+                }
+                uint32_t v[32];
+#pragma unroll
+                for (int j = 0; j < 32; j++) v[j] = (uint32_t)j < n ? A.ids_ord[o + j] + 1u : 0u;
+#pragma unroll
+                for (int kk = 2; kk <= 32; kk <<= 1) {
+#pragma unroll
+                    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+#pragma unroll
+                        for (int i = 0; i < 32; i++) {
+                            const int l2 = i ^ jj;
+                            if (l2 > i) {
+                                const uint32_t x = v[i], y = v[l2];
+                                const bool desc = (i & kk) == 0;
+                                const bool sw = desc ? (x < y) : (x > y);
+                                v[i] = sw ? y : x;
+                                v[l2] = sw ? x : y;
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 32; j++)
+                    if ((uint32_t)j < n) A.ids_out[o + j] = id_of(v[j] - 1u, A.read_ids, A.id_off);
+            }
+            __syncthreads();
+            PROF_MARK(5);
+            // longer lists.  33..256: one wavefront per list, LDS bitonic in a
+            // private 256-entry window, no block barriers.  Longer: the whole
+            // block.  The table is no longer needed: its LDS is the sort space.
+            uint32_t* buf = reinterpret_cast<uint32_t*>(claim);  // TS * 2 u32 of room
+            const uint32_t nbig = S.n_big;
+            PROF_CNT(10, nbig);
+            {
+                const int lane = tid & 63, wid = tid >> 6;
+                uint32_t* wb = buf + wid * 256;
+                for (uint32_t q = wid; q < nbig; q += BIN_THREADS / 64) {
+                    const uint64_t ge = e0 + big[q];
+                    const uint32_t n = A.e_cnt[ge];
+                    if (n > 256) continue;
+                    const uint64_t o = A.e_off[ge];
+                    uint32_t Pw = 64;
+                    while (Pw < n) Pw <<= 1;
+                    for (uint32_t j = lane; j < Pw; j += 64) wb[j] = j < n ? A.ids_ord[o + j] + 1u : 0u;
+                    wave_sync();
+                    for (uint32_t kk = 2; kk <= Pw; kk <<= 1) {
+                        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                            for (uint32_t i = lane; i < Pw; i += 64) {
+                                const uint32_t l2 = i ^ jj;
+                                if (l2 > i) {
+                                    const uint32_t x = wb[i], y = wb[l2];
+                                    const bool desc = (i & kk) == 0;
+                                    if (desc ? (x < y) : (x > y)) {
+                                        wb[i] = y;
+                                        wb[l2] = x;
+                                    }
+                                }
+                            }
+                            wave_sync();
+                        }
+                    }
+                    for (uint32_t j = lane; j < n; j += 64) A.ids_out[o + j] = id_of(wb[j] - 1u, A.read_ids, A.id_off);
+                    wave_sync();
+                }
+            }
+            __syncthreads();
+            PROF_MARK(7);
+            for (uint32_t q = 0; q < nbig; q++) {
+                const uint64_t ge = e0 + big[q];
+                const uint32_t n = A.e_cnt[ge];
+                const uint64_t o = A.e_off[ge];
+                if (n <= 256) continue;  // uniform
+                if (n <= (uint32_t)min(BIN_SORT_CAP, (int)(2 * TS))) {
+                    uint32_t Pw = 64;
+                    while (Pw < n) Pw <<= 1;
+                    for (uint32_t j = tid; j < Pw; j += BIN_THREADS) buf[j] = j < n ? A.ids_ord[o + j] + 1u : 0u;
+                    __syncthreads();
+                    for (uint32_t kk = 2; kk <= Pw; kk <<= 1) {
+                        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                            for (uint32_t i = tid; i < Pw; i += BIN_THREADS) {
+                                const uint32_t l2 = i ^ jj;
+                                if (l2 > i) {
+                                    const uint32_t x = buf[i], y = buf[l2];
+                                    const bool desc = (i & kk) == 0;
+                                    if (desc ? (x < y) : (x > y)) {
+                                        buf[i] = y;
+                                        buf[l2] = x;
+                                    }
+                                }
+                            }
+                            __syncthreads();
+                        }
+                    }
+                    for (uint32_t j = tid; j < n; j += BIN_THREADS)
+                        A.ids_out[o + j] = id_of(buf[j] - 1u, A.read_ids, A.id_off);
+                    __syncthreads();
+                } else {
+                    // very long list: sort LDS-sized chunks, then merge passes
+                    // through ids_out (as scratch) and ids_ord, ordinals + 1
+                    const uint32_t C = (uint32_t)min(BIN_SORT_CAP, (int)(2 * TS));
+                    uint32_t* src = A.ids_ord + o;
+                    uint32_t* dst = reinterpret_cast<uint32_t*>(A.ids_out + o);
+                    for (uint32_t c0 = 0; c0 < n; c0 += C) {
+                        const uint32_t cn = min(C, n - c0);
+                        for (uint32_t j = tid; j < C; j += BIN_THREADS) buf[j] = j < cn ? src[c0 + j] + 1u : 0u;
+                        __syncthreads();
+                        for (uint32_t kk = 2; kk <= C; kk <<= 1) {
+                            for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                                for (uint32_t i = tid; i < C; i += BIN_THREADS) {
+                                    const uint32_t l2 = i ^ jj;
+                                    if (l2 > i) {
+                                        const uint32_t x = buf[i], y = buf[l2];
+                                        const bool desc = (i & kk) == 0;
+                                        if (desc ? (x < y) : (x > y)) {
+                                            buf[i] = y;
+                                            buf[l2] = x;
+                                        }
+                                    }
+                                }
+                                __syncthreads();
+                            }
+                        }
+                        for (uint32_t j = tid; j < cn; j += BIN_THREADS) dst[c0 + j] = buf[j];
+                        __syncthreads();
+                    }
+                    __threadfence_block();
+                    __syncthreads();
+                    // merge runs of width wd from dst into src, alternating
+                    uint32_t* a = dst;
+                    uint32_t* bb = src;
+                    for (uint32_t wd = C; wd < n; wd <<= 1) {
+                        for (uint32_t t = tid; t < n; t += BIN_THREADS) {
+                            const uint32_t pair0 = (t / (2 * wd)) * 2 * wd;
+                            const uint32_t an = min(wd, n - pair0);
+                            const uint32_t b0 = pair0 + an, bn = b0 < n ? min(wd, n - b0) : 0u;
+                            const uint32_t d = t - pair0;
+                            uint32_t l1 = d > bn ? d - bn : 0u, h1 = min(d, an);
+                            while (l1 < h1) {
+                                const uint32_t i = (l1 + h1) >> 1;
+                                if (a[pair0 + i] >= a[b0 + d - i - 1]) l1 = i + 1; else h1 = i;
+                            }
+                            const uint32_t i = l1, j = d - l1;
+                            bb[t] = (i < an && (j >= bn || a[pair0 + i] >= a[b0 + j])) ? a[pair0 + i] : a[b0 + j];
+                        }
+                        __threadfence_block();
+                        __syncthreads();
+                        uint32_t* tmp = a;
+                        a = bb;
+                        bb = tmp;
+                    }
+                    // a holds the merged ordinals + 1; map into ids_out
+                    if (a == dst) {  // ids_out holds them already: map in place
+                        for (uint32_t t = tid; t < n; t += BIN_THREADS)
+                            A.ids_out[o + t] = id_of(dst[t] - 1u, A.read_ids, A.id_off);
+                    } else {
+                        for (uint32_t t = tid; t < n; t += BIN_THREADS)
+                            A.ids_out[o + t] = id_of(a[t] - 1u, A.read_ids, A.id_off);
+                    }
+                    __threadfence_block();
+                    __syncthreads();
+                }
+            }
+            __syncthreads();
+            PROF_MARK(6);
+        }
+        }  // initial partitions
+        __syncthreads();
+    }
+#ifdef KB_BIN_PROF
+    if (tid == 0)
+        for (int i = 0; i < 16; i++) atomicAdd(&g_bin_prof[i], pacc[i]);
+#endif
+}
+
+#ifdef KB_BIN_PROF
+void bins_prof_report(hipStream_t s) {
+    unsigned long long h[16];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bin_prof), sizeof(h));
+    static const char* nm[16] = {"occ", "zero", "sweep1", "prune/entries", "sweep2", "small sort", "big sort", "-",
+                                 "partitions", "overflows", "big lists", "bins", "-", "-", "occ", "-"};
+    fprintf(stderr, "[bin_prof]");
+    for (int i = 0; i < 16; i++)
+        if (h[i]) fprintf(stderr, " %s=%llu", nm[i], h[i]);
+    fprintf(stderr, "\n");
+    unsigned long long z[16] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bin_prof), z, sizeof(z));
+}
+#endif
+
+size_t bins_lds_bytes(uint32_t ts_log2) {
+    const size_t TS = (size_t)1 << ts_log2;
+    return sizeof(BinShared) + TS * (sizeof(uint64_t) + sizeof(uint32_t)) +
+           (size_t)BIN_WAVES * BIN_Q * (sizeof(uint64_t) + sizeof(uint32_t));
+}
+
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s) {
+    if (!max_bins) return hipSuccess;
+    const uint32_t TS = 1u << a.ts_log2;
+    if (TS < 1024 || bins_lds_bytes(a.ts_log2) > 160 * 1024) return hipErrorInvalidValue;  // wave sort windows: 8 x 256 u32 in the 2*TS u32 table space
+    const size_t lds = bins_lds_bytes(a.ts_log2);
+    uint64_t blocks = std::min<uint64_t>(max_bins, 65535);
+    hipLaunchKernelGGL(bin_kernel, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a);
+    return hipGetLastError();
+}
+
+__global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
+                                  uint64_t max_entries) {
+    // on overflow the counters ran past the capacity (status says so): clamp
+    const uint64_t ne = gcount[0] < max_entries ? gcount[0] : max_entries;
+    totals[0] = ne;
+    totals[1] = gcount[1];
+    e_off[ne] = gcount[1];
+}
+
+hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
+                             uint64_t max_entries, hipStream_t s) {
+    hipLaunchKernelGGL(bins_final_kernel, dim3(1), dim3(1), 0, s, gcount, e_off, totals, max_entries);
+    return hipGetLastError();
+}
+
+}  // namespace kb

@@ -72,6 +72,58 @@ struct SkArgs {
     int K, M;
 };
 
+// ---- binned engine (kbin_bins.hip)
+
+struct SkScanArgs {
+    const uint64_t* words;
+    const uint32_t* lens;
+    uint64_t n_reads;
+    uint32_t* seg_count;       // count pass: segments per read
+    const uint32_t* rec_base;  // write pass: exclusive scan of seg_count
+    uint64_t* pay;             // [3R] {ord | n << 32 | sig_off << 38 | rev << 44, span w0, w1}
+    uint64_t* keys;            // [R] canonical mmer << 32 | record index
+    uint32_t ord_base;
+    int RW, K, M;
+};
+
+struct BinArgs {
+    const uint64_t* keys;      // sorted by mmer
+    const uint64_t* hdr;       // [R] bin-ordered record headers (see SkScanArgs::pay)
+    const uint64_t* w0;        // [R] span bases 0..31
+    const uint64_t* w1;        // [R] span bases 32..63
+    const uint32_t* bstart;    // [nbins + 1]
+    const uint32_t* kbase;     // [R] first k-mer (occurrence) index of each bin-ordered record
+    uint64_t* stage;           // [N] (LDS slot << 32 | ordinal) per occurrence, bin-local ranges
+    const uint64_t* totals;    // totals[2] = nbins
+    int K, M;
+    uint32_t keep_gt;
+    uint32_t ts_log2;
+    float rho;                 // expected distinct keys per occurrence
+    unsigned long long* gcount;  // [0] entries [1] ids [2] distinct keys before prune
+    uint32_t* status;
+    uint32_t* e_mmer;
+    uint64_t* e_hi;
+    uint64_t* e_lo;
+    uint32_t* e_cnt;
+    uint64_t* e_off;
+    uint32_t* ids_ord;
+    int32_t* ids_out;
+    const int32_t* read_ids;
+    uint32_t id_off;
+    uint64_t max_entries, max_ids;
+};
+
+hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s);
+hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
+                            uint32_t* nk, hipStream_t s);
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s);
+size_t bins_lds_bytes(uint32_t ts_log2);
+#ifdef KB_BIN_PROF
+void bins_prof_report(hipStream_t s);
+#endif
+hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
+                             uint64_t max_entries, hipStream_t s);
+
 // launch helpers implemented in kbin_kernels.hip (all asynchronous on `s`)
 hipError_t launch_pack(const uint8_t* d_bases, const uint64_t* d_off, uint64_t n_reads,
                        int RW, uint64_t* d_words, uint32_t* d_lens, uint32_t* d_status,
@@ -89,6 +141,8 @@ hipError_t launch_radix_sort(uint64_t* a, uint64_t* b, uint64_t n, int key_bits,
 uint64_t onesweep_flag_elems(uint64_t n);
 hipError_t launch_onesweep(uint64_t* a, uint64_t* b, uint64_t n, int key_bits, uint64_t* flags,
                            uint32_t* aux, uint32_t* epoch, uint64_t** sorted, hipStream_t s);
+hipError_t launch_heads(const uint64_t* S, uint64_t n, uint32_t* starts, uint64_t max_runs,
+                        uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s);
 uint64_t runs_scratch_elems(uint64_t n, uint64_t max_runs);
 hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int KW,
                        uint32_t keep_gt, uint32_t* starts, const int32_t* read_ids,

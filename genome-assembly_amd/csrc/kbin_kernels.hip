@@ -21,87 +21,9 @@
 #include <algorithm>
 
 #include "kbin_internal.h"
+#include "kbin_device.h"
 
 namespace kb {
-
-#define DEV __device__ __forceinline__
-
-DEV uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
-    x ^= x >> 30;
-    x *= 0xbf58476d1ce4e5b9ull;
-    x ^= x >> 27;
-    x *= 0x94d049bb133111ebull;
-    x ^= x >> 31;
-    return x;
-}
-
-DEV int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-DEV void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-DEV uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        uint32_t o = (uint32_t)__shfl_xor((int)v, off, 64);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
-template <typename T>
-DEV T wave_incl_scan(T v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        T t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
-
-// exclusive scan over a 256-thread block; sh must hold 4 elements
-template <typename T>
-DEV T block_excl_scan256(T v, T* sh, T& total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    T inc = wave_incl_scan(v, lane);
-    if (lane == 63) sh[wid] = inc;
-    __syncthreads();
-    T wp = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        T x = sh[w];
-        if (w < wid) wp += x;
-        tot += x;
-    }
-    __syncthreads();
-    total = tot;
-    return wp + inc - v;
-}
-
-template <typename T>
-DEV T block_sum256(T v, T* sh) {
-    T tot;
-    (void)block_excl_scan256(v, sh, tot);
-    return tot;
-}
-
-// 64-bit window of the packed read starting at base p (first base in the MSBs)
-DEV uint64_t window64(const uint64_t* sw, int p) {
-    const int w = p >> 5, sh = (p & 31) << 1;
-    uint64_t x = sw[w];
-    if (sh) x = (x << sh) | (sw[w + 1] >> (64 - sh));
-    return x;
-}
-
-DEV uint64_t atomic_load_u64(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-DEV uint32_t atomic_load_u32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // ---------------------------------------------------------------------------
 // pack: ASCII reads -> 2-bit getval codes (binning.c:91-111), 32 bases/word
@@ -629,14 +551,6 @@ hipError_t launch_sk_counts(const uint64_t* recs, uint64_t n_rec, int rw, uint32
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(sk_counts_kernel, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, nk);
     return hipGetLastError();
-}
-
-// 64-bit window of a record's span words (s0..s3 in registers, no scratch)
-DEV uint64_t span_window(uint64_t s0, uint64_t s1, uint64_t s2, uint64_t s3, int p) {
-    const int w = p >> 5, sh = (p & 31) << 1;
-    const uint64_t a = w == 0 ? s0 : w == 1 ? s1 : w == 2 ? s2 : s3;
-    const uint64_t b = w == 0 ? s1 : w == 1 ? s2 : w == 2 ? s3 : 0ull;
-    return sh ? (a << sh) | (b >> (64 - sh)) : a;
 }
 
 // receiver: insert every k-mer of every received super-k-mer (one thread per
@@ -1267,6 +1181,21 @@ __global__ void entries_total_kernel(const uint64_t* __restrict__ tk, const uint
     e_off[*tk] = *ti;
 }
 
+// run starts of a sorted record array (key = bits 32..): starts[0..D], D in d_totals[2]
+hipError_t launch_heads(const uint64_t* S, uint64_t n, uint32_t* starts, uint64_t max_runs,
+                        uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s) {
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (scratch_n < nb + 1) return hipErrorInvalidValue;
+    if (n == 0) return hipMemsetAsync(d_totals, 0, 4 * sizeof(uint64_t), s);
+    hipLaunchKernelGGL(heads_partials_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch, nb, scratch + nb);
+    hipLaunchKernelGGL(heads_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch, starts,
+                       max_runs);
+    hipLaunchKernelGGL(runs_total_kernel, dim3(1), dim3(1), 0, s, scratch + nb, n, starts, d_totals,
+                       max_runs);
+    return hipGetLastError();
+}
+
 hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int KW,
                        uint32_t keep_gt, uint32_t* starts, const int32_t* read_ids,
                        uint32_t id_off, int32_t* ids_out, uint64_t max_runs, uint32_t* e_mmer, uint64_t* e_hi, uint64_t* e_lo, uint32_t* e_cnt,
@@ -1281,12 +1210,8 @@ hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int
         if (e == hipSuccess) e = hipMemsetAsync(e_off, 0, sizeof(uint64_t), s);
         return e;
     }
-    hipLaunchKernelGGL(heads_partials_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch);
-    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch, nb, scratch + nb);
-    hipLaunchKernelGGL(heads_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch, starts,
-                       max_runs);
-    hipLaunchKernelGGL(runs_total_kernel, dim3(1), dim3(1), 0, s, scratch + nb, n, starts, d_totals,
-                       max_runs);
+    hipError_t he = launch_heads(S, n, starts, max_runs, scratch, scratch_n, d_totals, s);
+    if (he != hipSuccess) return he;
     // runs -> prune -> entries (grid sized for the max possible run count;
     // blocks past the real count exit)
     hipLaunchKernelGGL(runs_partials_kernel, dim3((unsigned)nbr), dim3(256), 0, s, starts, d_totals,

@@ -54,6 +54,17 @@ extern "C" {
                             key's first occurrence -- the order in which the
                             reference inserts keys (binning.c:1045-1057), needed
                             to rebuild its exact zhash layout */
+#define KB_ENGINE_TABLE 2  /* force the global-table engine                      */
+#define KB_ENGINE_BINNED 4 /* prefer the binned engine; it applies to K <= 31
+                              reads binned in this context without
+                              KB_TRACK_FIRST, else the table engine runs.
+                              Neither flag: KB_ENGINE=table|binned from the
+                              environment, else the table engine.  Results are
+                              identical either way. */
+
+/* kb_timing.engine */
+#define KB_ENG_TABLE 1   /* scan + global find-or-insert + sort by slot + runs  */
+#define KB_ENG_BINNED 2  /* super-k-mers + sort by mmer + one LDS table per bin */
 
 typedef struct kb_ctx kb_ctx;
 
@@ -87,14 +98,18 @@ typedef struct {
 /* per-phase device time of the last kb_finalize (HIP events on the context
  * stream; only filled when timing is enabled) */
 typedef struct {
-    float scan_insert_ms;   /* fused signature scan + table find-or-insert      */
-    float sort_ms;          /* stable radix sort of the occurrence records      */
-    float runs_ms;          /* run counts + prune + CSR compaction              */
-    float emit_ms;          /* read-id emission                                 */
+    float scan_insert_ms;   /* table: fused signature scan + find-or-insert;
+                               binned: super-k-mer extraction (count + write)  */
+    float sort_ms;          /* table: radix sort by slot; binned: by mmer + bins */
+    float runs_ms;          /* table: runs/prune/CSR; binned: per-bin kernel    */
+    float emit_ms;          /* read-id emission / totals                        */
     float total_ms;         /* first to last event of the finalize              */
     uint32_t scan_insert_launches;
     uint32_t sort_passes;
-    uint64_t table_slots;   /* slots used by the last finalize                  */
+    uint64_t table_slots;   /* table: global slots; binned: LDS slots per bin   */
+    uint32_t engine;        /* KB_ENG_TABLE or KB_ENG_BINNED                     */
+    uint32_t n_bins;        /* binned: non-empty mmer bins                       */
+    uint64_t n_superkmers;  /* binned: super-k-mer records                       */
 } kb_timing;
 
 /* Create a context (kb_create replaces zcreate_hash_table for the level-1

@@ -13,6 +13,15 @@ import oracle
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["table", "binned"], autouse=True)
+def engine(request, monkeypatch):
+    """every parity case runs on both engines (KB_ENGINE; the binned engine
+    applies to K <= 31 without first-occurrence tracking, else the table
+    engine runs -- test_binned_engine_selected checks which ran)"""
+    monkeypatch.setenv("KB_ENGINE", request.param)
+    return request.param
+
+
 def gpu_result(bases, lens, K, M, cutoff=1, prune=True, ids=None, batches=1, max_read_len=1024):
     with kbin.Engine(K, M, cutoff=cutoff, max_read_len=max_read_len) as eng:
         n = len(lens)
@@ -77,6 +86,23 @@ def test_random_vs_oracle(K, M):
         res = gpu_result(bases, lens, K, M, 1, prune, batches=3)
         assert res.n_kmers == ora.n_kmers
         assert_same(res, ora)
+
+
+def test_binned_engine_selected(engine):
+    """the engine the environment asks for is the one that runs (K <= 31)"""
+    rng = np.random.default_rng(3)
+    reads = [rng.choice(np.frombuffer(b"ACGT", np.uint8), 150).tobytes() for _ in range(500)]
+    bases, lens = kbin.pack_reads(reads)
+    ora = oracle.bin_reads(bases, lens, 31, 7, 1, True)
+    with kbin.Engine(31, 7, cutoff=1, max_read_len=150) as eng:
+        eng.set_timing(True)
+        eng.submit(bases=bases, lens=lens, first_id=0)
+        eng.finalize(prune=True)
+        t = eng.timing()
+        assert_same(eng.export(), ora)
+    assert t["engine"] == (kbin.KB_ENG_BINNED if engine == "binned" else kbin.KB_ENG_TABLE)
+    if engine == "binned":
+        assert t["n_superkmers"] > 0 and t["n_bins"] > 0
 
 
 def test_explicit_ids_nonmonotone():
