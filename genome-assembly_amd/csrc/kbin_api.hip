@@ -125,7 +125,9 @@ struct kb_ctx {
     DevBuf<uint64_t> srec;     // the same, bin order, structure of arrays
     DevBuf<uint32_t> kbase;    // first occurrence index of each bin-ordered record
     DevBuf<uint64_t> stage;    // per-occurrence (slot, ordinal) staging
+    DevBuf<uint32_t> border;   // bin processing order
     float rho = 0.f;           // learned distinct / occurrences
+    uint64_t n_occ_entries_hint = 0;  // entries of the last finalize (lists grid)
     uint64_t* h_totals = nullptr;
     uint32_t* h_misc = nullptr;
 
@@ -216,7 +218,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->kbase.release(); c->stage.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->kbase.release(); c->stage.release(); c->border.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
@@ -623,6 +625,9 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
     HIPCHK(launch_sk_gather(c->sorted, c->pay.p, R, c->srec.p, c->kbase.p, c->s));
     HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(R + 1), c->scratch.cap)));
     HIPCHK(launch_scan_u32(c->kbase.p, R, c->scratch.p, c->scratch.cap, c->s));
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(c->kbase.p + R), (int)(uint32_t)N, 1, c->s));
+    HIPCHK(c->border.ensure(max_bins));
+    HIPCHK(launch_bins_order(c->starts.p, c->kbase.p, c->totals.p, c->border.p, c->s));
     REC(3);
     // ---- one workgroup per bin
     const uint64_t ecap = N + 1;
@@ -649,6 +654,8 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
     a.w1 = c->srec.p + 2 * R;
     a.bstart = c->starts.p;
     a.kbase = c->kbase.p;
+    a.order = c->border.p;
+    a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
     a.stage = c->stage.p;
     a.totals = c->totals.p;
     a.K = c->p.K;
@@ -673,8 +680,17 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
 #ifdef KB_BIN_PROF
     bins_prof_report(c->s);
 #endif
-    REC(4);
     HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries, c->s));
+    REC(4);
+    ListArgs la{};
+    la.totals = c->totals.p;
+    la.e_cnt = c->e_cnt.p;
+    la.e_off = c->e_off.p;
+    la.ids_ord = a.ids_ord;
+    la.ids_out = c->ids_out.p;
+    la.read_ids = a.read_ids;
+    la.id_off = a.id_off;
+    HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : N / 8 + 1, c->s));
     REC(5);
     HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
@@ -689,6 +705,7 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
     c->n_entries = c->h_totals[0];
     c->n_ids = c->h_totals[1];
     c->n_distinct = c->h_totals[6];
+    c->n_occ_entries_hint = c->n_entries;
     if (N) c->rho = (float)((double)c->n_distinct / (double)N);
     if (c->timing) {
         HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));

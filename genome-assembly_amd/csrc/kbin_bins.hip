@@ -223,8 +223,7 @@ __device__ unsigned long long g_bin_prof[16];
 #define PROF_CNT(i, v) do {} while (0)
 #endif
 
-constexpr int BIN_THREADS = 512;
-constexpr int BIN_SORT_CAP = 8192;  // largest id list ordered in LDS in one piece
+constexpr int BIN_THREADS = 1024;
 constexpr int BIN_STACK = 32;
 
 DEV uint64_t lds_load_u64(const uint64_t* p) {
@@ -268,7 +267,7 @@ DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
 }
 
 struct alignas(16) BinShared {
-    uint32_t n_keys, overflow, sp, cur_p, cur_l, n_big, n_stage, pad0;
+    uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, pad0;
     unsigned long long e0, i0;
     uint32_t stack_p[BIN_STACK], stack_l[BIN_STACK];
     uint64_t red[BIN_THREADS / 64];
@@ -295,20 +294,20 @@ DEV uint64_t block_excl_scan_u64(uint64_t v, uint64_t* red, uint64_t& total) {
 }
 
 constexpr int BIN_WAVES = BIN_THREADS / 64;
-constexpr int BIN_Q = 128;  // per-wave k-mer queue (64 pending + 64 pushed)
+constexpr uint32_t BIN_Q = 256;  // per-wave k-mer ring (flushes of 128 = 2 per lane)
 
 DEV uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // Expand the k-mers of the bin's records that fall in partition (p, l) and
-// hand each to f(code_plus1, ord, sidx).  Records are the bin's super-k-mers,
-// streamed from the bin-ordered SoA arrays, one record per lane.  Matching
-// k-mers are compacted through a per-wave LDS queue so f always runs on 64
-// k-mers at once, whatever the record lengths and the partition filter;
-// sidx is a block-unique index (0 .. k-mers of the partition - 1) taken from
-// *ctr.  The partition filter is one multiply; the table hash (mix64) is
-// computed by f on the compacted k-mers only.
+// hand them to f.  Records are the bin's super-k-mers, streamed from the
+// bin-ordered SoA arrays, one record per lane, the next chunk's loads issued
+// before the current chunk is expanded.  Matching k-mers are compacted into a
+// per-wave LDS ring; every 128 of them f(k0, o0, s0, k1, o1, s1, v1) runs with
+// two k-mers per lane (independent LDS chains interleave), s = block-unique
+// index from *ctr (0 .. k-mers of the partition - 1).  The partition filter is
+// one multiply; the table hash (mix64) is computed by f on compacted k-mers.
 DEV uint32_t part_of(uint64_t code) { return (uint32_t)((code * 0x9E3779B97F4A7C15ull) >> 40); }
 
 template <typename F>
@@ -318,14 +317,34 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t kmask = (1ull << (2 * K)) - 1ull;
     const uint32_t pmask = (1u << l) - 1u;
-    uint32_t qn = 0;  // wave-uniform queue fill
-    for (uint32_t base = lo + wid * 64; base < hi; base += BIN_THREADS) {
-        const uint32_t rec = base + lane;
-        uint64_t hd = 0, s0 = 0, s1 = 0;
-        if (rec < hi) {
-            hd = A.hdr[rec];
-            s0 = A.w0[rec];
-            s1 = A.w1[rec];
+    uint32_t head = 0, fill = 0;  // wave-uniform ring state
+    auto flush = [&](uint32_t cnt) {  // cnt <= 128 entries from head
+        wave_sync();
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(ctr, cnt);
+        b = (uint32_t)__shfl((int)b, 0, 64);
+        const uint32_t i0 = (head + lane) & (BIN_Q - 1), i1 = (head + 64 + lane) & (BIN_Q - 1);
+        const bool v0 = (uint32_t)lane < cnt, v1 = (uint32_t)lane + 64 < cnt;
+        f(qk[i0], qo[i0], b + lane, v0, qk[i1], qo[i1], b + 64 + lane, v1);
+        head = (head + cnt) & (BIN_Q - 1);
+        fill -= cnt;
+        wave_sync();
+    };
+    uint32_t base = lo + wid * 64;
+    uint64_t nhd = 0, ns0 = 0, ns1 = 0;
+    if (base + lane < hi) {
+        nhd = A.hdr[base + lane];
+        ns0 = A.w0[base + lane];
+        ns1 = A.w1[base + lane];
+    }
+    for (; base < hi; base += BIN_THREADS) {
+        const uint64_t hd = nhd, s0 = ns0, s1 = ns1;
+        const uint32_t nxt = base + BIN_THREADS + lane;
+        nhd = 0;
+        if (nxt < hi) {  // prefetch the next chunk
+            nhd = A.hdr[nxt];
+            ns0 = A.w0[nxt];
+            ns1 = A.w1[nxt];
         }
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
@@ -336,48 +355,27 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
             const bool take = j < n && (l == 0 || (part_of(code) & pmask) == p);
             const uint64_t m = __ballot(take);
             if (take) {
-                const uint32_t pos = qn + lanes_below(m);
+                const uint32_t pos = (head + fill + lanes_below(m)) & (BIN_Q - 1);
                 qk[pos] = code + 1ull;
                 qo[pos] = ord;
             }
-            qn += (uint32_t)__popcll(m);
-            if (qn >= 64) {
-                wave_sync();
-                uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(ctr, 64u);
-                b = (uint32_t)__shfl((int)b, 0, 64);
-                f(qk[lane], qo[lane], b + lane);
-                if (lane + 64 < qn) {
-                    const uint64_t k2 = qk[lane + 64];
-                    const uint32_t o2 = qo[lane + 64];
-                    qk[lane] = k2;
-                    qo[lane] = o2;
-                }
-                qn -= 64;
-                wave_sync();
-            }
+            fill += (uint32_t)__popcll(m);
+            if (fill >= 128) flush(128);
         }
     }
-    wave_sync();
-    if (qn) {
-        uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(ctr, qn);
-        b = (uint32_t)__shfl((int)b, 0, 64);
-        if ((uint32_t)lane < qn) f(qk[lane], qo[lane], b + lane);
-    }
-    wave_sync();
+    if (fill) flush(fill);
 }
 
-__global__ __launch_bounds__(BIN_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void bin_kernel(BinArgs A) {
+__global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     BinShared& S = *reinterpret_cast<BinShared*>(smem);      // all LDS in one dynamic array
     const uint32_t TS = 1u << A.ts_log2, tmask = TS - 1;
     uint64_t* claim = smem + sizeof(BinShared) / 8;          // [TS] k-mer code + 1
     uint32_t* cnt = reinterpret_cast<uint32_t*>(claim + TS);  // [TS] count, then cursor
-    uint32_t* big = cnt;                                      // sort phase: big-list entry ids
     uint64_t* qk = reinterpret_cast<uint64_t*>(cnt + TS) + (threadIdx.x >> 6) * BIN_Q;
     uint32_t* qo = reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(cnt + TS) + BIN_WAVES * BIN_Q) +
                    (threadIdx.x >> 6) * BIN_Q;
+    const uint32_t limit = TS - TS / 4;
     const uint64_t nbins = A.totals[2];
     const uint32_t tid = threadIdx.x;
 #ifdef KB_BIN_PROF
@@ -385,7 +383,13 @@ __global__ __launch_bounds__(BIN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
     unsigned long long pt = clock64();
 #endif
 
-    for (uint64_t b = blockIdx.x; b < nbins; b += gridDim.x) {
+    while (true) {
+        // persistent blocks take bins from a shared counter, largest first
+        __syncthreads();
+        if (tid == 0) S.item = (uint32_t)atomicAdd(A.work, 1ull);
+        __syncthreads();
+        if (S.item >= nbins) break;  // uniform
+        const uint32_t b = A.order[S.item];
         const uint32_t lo = A.bstart[b], hi = A.bstart[b + 1];
         const uint32_t mmer = (uint32_t)(A.keys[lo] >> 32);
         uint64_t* stage = A.stage + A.kbase[lo];  // the bin's k-mer range, reused per partition
@@ -420,7 +424,6 @@ __global__ __launch_bounds__(BIN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
                 }
                 S.n_keys = 0;
                 S.overflow = 0;
-                S.n_big = 0;
                 S.n_stage = 0;
             }
             for (uint32_t i = tid; i < TS; i += BIN_THREADS) {
@@ -432,16 +435,35 @@ __global__ __launch_bounds__(BIN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
             const uint32_t P = S.cur_p, Lv = S.cur_l;
             if (Lv == 0xFFFFFFFFu) break;  // uniform
             PROF_CNT(8, 1);
-            const uint32_t limit = TS - TS / 4;
             // ---- sweep 1: insert + count (binning.c:1042-1069 semantics per key)
             // each occurrence is staged as (slot, ordinal) for sweep 2
-            for_each_kmer(A, lo, hi, P, Lv, qk, qo, &S.n_stage, [&](uint64_t key, uint32_t ord, uint32_t si) {
-                const int ls = lds_insert(claim, tmask, key, (uint32_t)mix64(key - 1ull), &S.n_keys, limit);
-                if (ls < 0) {
-                    S.overflow = 1;
-                } else {
-                    atomicAdd(&cnt[ls], 1u);
-                    stage[si] = ((uint64_t)ls << 32) | ord;
+            for_each_kmer(A, lo, hi, P, Lv, qk, qo, &S.n_stage,
+                          [&](uint64_t k0, uint32_t o0, uint32_t s0, bool v0, uint64_t k1, uint32_t o1,
+                              uint32_t s1, bool v1) {
+                const uint32_t h0 = (uint32_t)mix64(k0 - 1ull), h1 = (uint32_t)mix64(k1 - 1ull);
+                // first probes of both k-mers in flight together; the rest
+                // (empty slot, collision chain) takes the full insert path
+                const uint64_t c0 = v0 ? lds_load_u64(&claim[h0 & tmask]) : 0ull;
+                const uint64_t c1 = v1 ? lds_load_u64(&claim[h1 & tmask]) : 0ull;
+                int l0 = c0 == k0 ? (int)(h0 & tmask) : -3;
+                int l1 = c1 == k1 ? (int)(h1 & tmask) : -3;
+                if (v0 && l0 == -3) l0 = lds_insert(claim, tmask, k0, h0, &S.n_keys, limit);
+                if (v1 && l1 == -3) l1 = lds_insert(claim, tmask, k1, h1, &S.n_keys, limit);
+                if (v0) {
+                    if (l0 < 0) {
+                        S.overflow = 1;
+                    } else {
+                        atomicAdd(&cnt[l0], 1u);
+                        stage[s0] = ((uint64_t)l0 << 32) | o0;
+                    }
+                }
+                if (v1) {
+                    if (l1 < 0) {
+                        S.overflow = 1;
+                    } else {
+                        atomicAdd(&cnt[l1], 1u);
+                        stage[s1] = ((uint64_t)l1 << 32) | o1;
+                    }
                 }
             });
             __syncthreads();
@@ -475,8 +497,13 @@ __global__ __launch_bounds__(BIN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
             if (tid == 0) {
                 const uint32_t ne = (uint32_t)tot, ni = (uint32_t)(tot >> 32);
                 atomicAdd(&A.gcount[2], (unsigned long long)S.n_keys);  // distinct before prune
-                S.e0 = ne ? atomicAdd((unsigned long long*)&A.gcount[0], (unsigned long long)ne) : 0ull;
-                S.i0 = ni ? atomicAdd((unsigned long long*)&A.gcount[1], (unsigned long long)ni) : 0ull;
+                // entries and ids from ONE packed counter (entries << 32 | ids; both
+                // totals < 2^32): consecutive entries own consecutive id ranges,
+                // so offset[e + 1] ends entry e's list (the CSR contract)
+                const unsigned long long got =
+                    tot ? atomicAdd(&A.gcount[0], ((unsigned long long)ne << 32) | ni) : 0ull;
+                S.e0 = got >> 32;
+                S.i0 = got & 0xFFFFFFFFull;
                 if (S.e0 + ne > A.max_entries || S.i0 + ni > A.max_ids) atomicOr(A.status, ST_TABLE_FULL);
             }
             __syncthreads();
@@ -523,177 +550,7 @@ __global__ __launch_bounds__(BIN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
             __threadfence_block();
             __syncthreads();
             PROF_MARK(4);
-            // ---- per key: reverse call order = descending ordinal (binning.c:1061-1068)
-            const uint32_t ne = (uint32_t)tot;
-            for (uint32_t e = tid; e < ne; e += BIN_THREADS) {
-                const uint64_t ge = e0 + e;
-                const uint32_t n = A.e_cnt[ge];
-                const uint64_t o = A.e_off[ge];
-                if (n > 32) {
-                    big[atomicAdd(&S.n_big, 1u)] = e;
-                    continue;
-                }
-                uint32_t v[32];
-#pragma unroll
-                for (int j = 0; j < 32; j++) v[j] = (uint32_t)j < n ? A.ids_ord[o + j] + 1u : 0u;
-#pragma unroll
-                for (int kk = 2; kk <= 32; kk <<= 1) {
-#pragma unroll
-                    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-#pragma unroll
-                        for (int i = 0; i < 32; i++) {
-                            const int l2 = i ^ jj;
-                            if (l2 > i) {
-                                const uint32_t x = v[i], y = v[l2];
-                                const bool desc = (i & kk) == 0;
-                                const bool sw = desc ? (x < y) : (x > y);
-                                v[i] = sw ? y : x;
-                                v[l2] = sw ? x : y;
-                            }
-                        }
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 32; j++)
-                    if ((uint32_t)j < n) A.ids_out[o + j] = id_of(v[j] - 1u, A.read_ids, A.id_off);
-            }
-            __syncthreads();
-            PROF_MARK(5);
-            // longer lists.  33..256: one wavefront per list, LDS bitonic in a
-            // private 256-entry window, no block barriers.  Longer: the whole
-            // block.  The table is no longer needed: its LDS is the sort space.
-            uint32_t* buf = reinterpret_cast<uint32_t*>(claim);  // TS * 2 u32 of room
-            const uint32_t nbig = S.n_big;
-            PROF_CNT(10, nbig);
-            {
-                const int lane = tid & 63, wid = tid >> 6;
-                uint32_t* wb = buf + wid * 256;
-                for (uint32_t q = wid; q < nbig; q += BIN_THREADS / 64) {
-                    const uint64_t ge = e0 + big[q];
-                    const uint32_t n = A.e_cnt[ge];
-                    if (n > 256) continue;
-                    const uint64_t o = A.e_off[ge];
-                    uint32_t Pw = 64;
-                    while (Pw < n) Pw <<= 1;
-                    for (uint32_t j = lane; j < Pw; j += 64) wb[j] = j < n ? A.ids_ord[o + j] + 1u : 0u;
-                    wave_sync();
-                    for (uint32_t kk = 2; kk <= Pw; kk <<= 1) {
-                        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-                            for (uint32_t i = lane; i < Pw; i += 64) {
-                                const uint32_t l2 = i ^ jj;
-                                if (l2 > i) {
-                                    const uint32_t x = wb[i], y = wb[l2];
-                                    const bool desc = (i & kk) == 0;
-                                    if (desc ? (x < y) : (x > y)) {
-                                        wb[i] = y;
-                                        wb[l2] = x;
-                                    }
-                                }
-                            }
-                            wave_sync();
-                        }
-                    }
-                    for (uint32_t j = lane; j < n; j += 64) A.ids_out[o + j] = id_of(wb[j] - 1u, A.read_ids, A.id_off);
-                    wave_sync();
-                }
-            }
-            __syncthreads();
-            PROF_MARK(7);
-            for (uint32_t q = 0; q < nbig; q++) {
-                const uint64_t ge = e0 + big[q];
-                const uint32_t n = A.e_cnt[ge];
-                const uint64_t o = A.e_off[ge];
-                if (n <= 256) continue;  // uniform
-                if (n <= (uint32_t)min(BIN_SORT_CAP, (int)(2 * TS))) {
-                    uint32_t Pw = 64;
-                    while (Pw < n) Pw <<= 1;
-                    for (uint32_t j = tid; j < Pw; j += BIN_THREADS) buf[j] = j < n ? A.ids_ord[o + j] + 1u : 0u;
-                    __syncthreads();
-                    for (uint32_t kk = 2; kk <= Pw; kk <<= 1) {
-                        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-                            for (uint32_t i = tid; i < Pw; i += BIN_THREADS) {
-                                const uint32_t l2 = i ^ jj;
-                                if (l2 > i) {
-                                    const uint32_t x = buf[i], y = buf[l2];
-                                    const bool desc = (i & kk) == 0;
-                                    if (desc ? (x < y) : (x > y)) {
-                                        buf[i] = y;
-                                        buf[l2] = x;
-                                    }
-                                }
-                            }
-                            __syncthreads();
-                        }
-                    }
-                    for (uint32_t j = tid; j < n; j += BIN_THREADS)
-                        A.ids_out[o + j] = id_of(buf[j] - 1u, A.read_ids, A.id_off);
-                    __syncthreads();
-                } else {
-                    // very long list: sort LDS-sized chunks, then merge passes
-                    // through ids_out (as scratch) and ids_ord, ordinals + 1
-                    const uint32_t C = (uint32_t)min(BIN_SORT_CAP, (int)(2 * TS));
-                    uint32_t* src = A.ids_ord + o;
-                    uint32_t* dst = reinterpret_cast<uint32_t*>(A.ids_out + o);
-                    for (uint32_t c0 = 0; c0 < n; c0 += C) {
-                        const uint32_t cn = min(C, n - c0);
-                        for (uint32_t j = tid; j < C; j += BIN_THREADS) buf[j] = j < cn ? src[c0 + j] + 1u : 0u;
-                        __syncthreads();
-                        for (uint32_t kk = 2; kk <= C; kk <<= 1) {
-                            for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-                                for (uint32_t i = tid; i < C; i += BIN_THREADS) {
-                                    const uint32_t l2 = i ^ jj;
-                                    if (l2 > i) {
-                                        const uint32_t x = buf[i], y = buf[l2];
-                                        const bool desc = (i & kk) == 0;
-                                        if (desc ? (x < y) : (x > y)) {
-                                            buf[i] = y;
-                                            buf[l2] = x;
-                                        }
-                                    }
-                                }
-                                __syncthreads();
-                            }
-                        }
-                        for (uint32_t j = tid; j < cn; j += BIN_THREADS) dst[c0 + j] = buf[j];
-                        __syncthreads();
-                    }
-                    __threadfence_block();
-                    __syncthreads();
-                    // merge runs of width wd from dst into src, alternating
-                    uint32_t* a = dst;
-                    uint32_t* bb = src;
-                    for (uint32_t wd = C; wd < n; wd <<= 1) {
-                        for (uint32_t t = tid; t < n; t += BIN_THREADS) {
-                            const uint32_t pair0 = (t / (2 * wd)) * 2 * wd;
-                            const uint32_t an = min(wd, n - pair0);
-                            const uint32_t b0 = pair0 + an, bn = b0 < n ? min(wd, n - b0) : 0u;
-                            const uint32_t d = t - pair0;
-                            uint32_t l1 = d > bn ? d - bn : 0u, h1 = min(d, an);
-                            while (l1 < h1) {
-                                const uint32_t i = (l1 + h1) >> 1;
-                                if (a[pair0 + i] >= a[b0 + d - i - 1]) l1 = i + 1; else h1 = i;
-                            }
-                            const uint32_t i = l1, j = d - l1;
-                            bb[t] = (i < an && (j >= bn || a[pair0 + i] >= a[b0 + j])) ? a[pair0 + i] : a[b0 + j];
-                        }
-                        __threadfence_block();
-                        __syncthreads();
-                        uint32_t* tmp = a;
-                        a = bb;
-                        bb = tmp;
-                    }
-                    // a holds the merged ordinals + 1; map into ids_out
-                    if (a == dst) {  // ids_out holds them already: map in place
-                        for (uint32_t t = tid; t < n; t += BIN_THREADS)
-                            A.ids_out[o + t] = id_of(dst[t] - 1u, A.read_ids, A.id_off);
-                    } else {
-                        for (uint32_t t = tid; t < n; t += BIN_THREADS)
-                            A.ids_out[o + t] = id_of(a[t] - 1u, A.read_ids, A.id_off);
-                    }
-                    __threadfence_block();
-                    __syncthreads();
-                }
-            }
+            // lists are put in reverse call order by lists_kernel
             __syncthreads();
             PROF_MARK(6);
         }
@@ -722,6 +579,326 @@ void bins_prof_report(hipStream_t s) {
 }
 #endif
 
+// ---------------------------------------------------------------------------
+// phase C: every list into reverse call order (binning.c:1061-1068 prepends,
+// so a list reads newest call first = descending ordinal), ordinals -> ids.
+// A block takes 256 consecutive entries: lists of <= 32 ids are sorted in the
+// registers of one lane, 33..256 by one wavefront in LDS, longer ones by the
+// whole block (LDS bitonic up to LIST_CAP, else chunks + merge passes).
+// ---------------------------------------------------------------------------
+constexpr int LIST_THREADS = 256;
+constexpr uint32_t LIST_CAP = 8192;   // longest list sorted in LDS in one piece
+constexpr uint32_t LIST_SPAN = 8192;  // ids of 256 entries staged in LDS at once
+
+// descending bitonic sort of Pw (power of two) values in LDS by a group of G
+// lanes (G = 64: one wavefront, wave barriers; else the block)
+template <int G>
+DEV void bitonic_desc(uint32_t* a, uint32_t Pw, uint32_t r) {
+    for (uint32_t kk = 2; kk <= Pw; kk <<= 1) {
+        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t i = r; i < Pw; i += G) {
+                const uint32_t l2 = i ^ jj;
+                if (l2 > i) {
+                    const uint32_t x = a[i], y = a[l2];
+                    const bool desc = (i & kk) == 0;
+                    if (desc ? (x < y) : (x > y)) {
+                        a[i] = y;
+                        a[l2] = x;
+                    }
+                }
+            }
+            if (G == 64) wave_sync();
+            else __syncthreads();
+        }
+    }
+}
+
+// up to 32 values (ordinal + 1) sorted descending in one lane's registers, in place
+DEV void sort32_inplace(uint32_t* p, uint32_t n) {
+    uint32_t v[32];
+#pragma unroll
+    for (int j = 0; j < 32; j++) v[j] = (uint32_t)j < n ? p[j] : 0u;
+#pragma unroll
+    for (int kk = 2; kk <= 32; kk <<= 1) {
+#pragma unroll
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 32; i++) {
+                const int l2 = i ^ jj;
+                if (l2 > i) {
+                    const uint32_t x = v[i], y = v[l2];
+                    const bool desc = (i & kk) == 0;
+                    const bool sw = desc ? (x < y) : (x > y);
+                    v[i] = sw ? y : x;
+                    v[l2] = sw ? x : y;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 32; j++)
+        if ((uint32_t)j < n) p[j] = v[j];
+}
+
+__global__ __launch_bounds__(LIST_THREADS) void lists_kernel(ListArgs A) {
+    // staged chunks: ibuf = the chunk's ids (ordinal + 1), wave windows after
+    // it; other chunks: buf = block sort space (LIST_CAP), wave windows inside
+    __shared__ uint32_t lds[LIST_SPAN + 4 * 256];
+    static_assert(LIST_CAP <= LIST_SPAN, "block sort space aliases the staging area");
+    uint32_t* const ibuf = lds;
+    uint32_t* const buf = lds;
+    __shared__ uint32_t big[LIST_THREADS];
+    __shared__ uint32_t n_big;
+    const uint32_t tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    const uint64_t n_entries = A.totals[0];
+    for (uint64_t e0 = (uint64_t)blockIdx.x * LIST_THREADS; e0 < n_entries;
+         e0 += (uint64_t)gridDim.x * LIST_THREADS) {
+        const uint32_t ne = (uint32_t)min<uint64_t>(LIST_THREADS, n_entries - e0);
+        const uint64_t ob = A.e_off[e0], span = A.e_off[e0 + ne] - ob;
+        if (tid == 0) n_big = 0;
+        const bool long_list = tid < ne && A.e_cnt[e0 + tid] > 256;
+        if (!__syncthreads_or(long_list) && span <= LIST_SPAN) {
+            // staged: coalesced in, every list sorted in LDS, coalesced out
+            for (uint32_t i = tid; i < span; i += LIST_THREADS) ibuf[i] = A.ids_ord[ob + i] + 1u;
+            __syncthreads();
+            if (tid < ne) {
+                const uint32_t n = A.e_cnt[e0 + tid];
+                const uint32_t o = (uint32_t)(A.e_off[e0 + tid] - ob);
+                if (n <= 32) sort32_inplace(ibuf + o, n);
+                else big[atomicAdd(&n_big, 1u)] = tid;
+            }
+            __syncthreads();
+            const uint32_t nbig = n_big;
+            uint32_t* wb = lds + LIST_SPAN + wid * 256;
+            for (uint32_t q = wid; q < nbig; q += LIST_THREADS / 64) {
+                const uint32_t n = A.e_cnt[e0 + big[q]];
+                const uint32_t o = (uint32_t)(A.e_off[e0 + big[q]] - ob);
+                uint32_t Pw = 64;
+                while (Pw < n) Pw <<= 1;
+                for (uint32_t j = lane; j < Pw; j += 64) wb[j] = j < n ? ibuf[o + j] : 0u;
+                wave_sync();
+                bitonic_desc<64>(wb, Pw, lane);
+                for (uint32_t j = lane; j < n; j += 64) ibuf[o + j] = wb[j];
+                wave_sync();
+            }
+            __syncthreads();
+            for (uint32_t i = tid; i < span; i += LIST_THREADS)
+                A.ids_out[ob + i] = id_of(ibuf[i] - 1u, A.read_ids, A.id_off);
+            __syncthreads();
+            continue;
+        }
+        __syncthreads();
+        for (uint32_t e = tid; e < ne; e += LIST_THREADS) {
+            const uint64_t ge = e0 + e;
+            const uint32_t n = A.e_cnt[ge];
+            const uint64_t o = A.e_off[ge];
+            if (n > 32) {
+                big[atomicAdd(&n_big, 1u)] = e;
+                continue;
+            }
+            uint32_t v[32];
+#pragma unroll
+            for (int j = 0; j < 32; j++) v[j] = (uint32_t)j < n ? A.ids_ord[o + j] + 1u : 0u;
+#pragma unroll
+            for (int kk = 2; kk <= 32; kk <<= 1) {
+#pragma unroll
+                for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+#pragma unroll
+                    for (int i = 0; i < 32; i++) {
+                        const int l2 = i ^ jj;
+                        if (l2 > i) {
+                            const uint32_t x = v[i], y = v[l2];
+                            const bool desc = (i & kk) == 0;
+                            const bool sw = desc ? (x < y) : (x > y);
+                            v[i] = sw ? y : x;
+                            v[l2] = sw ? x : y;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 32; j++)
+                if ((uint32_t)j < n) A.ids_out[o + j] = id_of(v[j] - 1u, A.read_ids, A.id_off);
+        }
+        __syncthreads();
+        // longer lists.  33..256: one wavefront per list, LDS bitonic in a
+        // private 256-entry window, no block barriers.  Longer: the whole block.
+        const uint32_t nbig = n_big;
+        {
+            const int lane = tid & 63, wid = tid >> 6;
+            uint32_t* wb = buf + wid * 256;
+            for (uint32_t q = wid; q < nbig; q += LIST_THREADS / 64) {
+                const uint64_t ge = e0 + big[q];
+                const uint32_t n = A.e_cnt[ge];
+                if (n > 256) continue;
+                const uint64_t o = A.e_off[ge];
+                uint32_t Pw = 64;
+                while (Pw < n) Pw <<= 1;
+                for (uint32_t j = lane; j < Pw; j += 64) wb[j] = j < n ? A.ids_ord[o + j] + 1u : 0u;
+                wave_sync();
+                for (uint32_t kk = 2; kk <= Pw; kk <<= 1) {
+                    for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                        for (uint32_t i = lane; i < Pw; i += 64) {
+                            const uint32_t l2 = i ^ jj;
+                            if (l2 > i) {
+                                const uint32_t x = wb[i], y = wb[l2];
+                                const bool desc = (i & kk) == 0;
+                                if (desc ? (x < y) : (x > y)) {
+                                    wb[i] = y;
+                                    wb[l2] = x;
+                                }
+                            }
+                        }
+                        wave_sync();
+                    }
+                }
+                for (uint32_t j = lane; j < n; j += 64) A.ids_out[o + j] = id_of(wb[j] - 1u, A.read_ids, A.id_off);
+                wave_sync();
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = 0; q < nbig; q++) {
+            const uint64_t ge = e0 + big[q];
+            const uint32_t n = A.e_cnt[ge];
+            const uint64_t o = A.e_off[ge];
+            if (n <= 256) continue;  // uniform
+            if (n <= (uint32_t)LIST_CAP) {
+                uint32_t Pw = 64;
+                while (Pw < n) Pw <<= 1;
+                for (uint32_t j = tid; j < Pw; j += LIST_THREADS) buf[j] = j < n ? A.ids_ord[o + j] + 1u : 0u;
+                __syncthreads();
+                for (uint32_t kk = 2; kk <= Pw; kk <<= 1) {
+                    for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                        for (uint32_t i = tid; i < Pw; i += LIST_THREADS) {
+                            const uint32_t l2 = i ^ jj;
+                            if (l2 > i) {
+                                const uint32_t x = buf[i], y = buf[l2];
+                                const bool desc = (i & kk) == 0;
+                                if (desc ? (x < y) : (x > y)) {
+                                    buf[i] = y;
+                                    buf[l2] = x;
+                                }
+                            }
+                        }
+                        __syncthreads();
+                    }
+                }
+                for (uint32_t j = tid; j < n; j += LIST_THREADS)
+                    A.ids_out[o + j] = id_of(buf[j] - 1u, A.read_ids, A.id_off);
+                __syncthreads();
+            } else {
+                // very long list: sort LDS-sized chunks, then merge passes
+                // through ids_out (as scratch) and ids_ord, ordinals + 1
+                const uint32_t C = (uint32_t)LIST_CAP;
+                uint32_t* src = A.ids_ord + o;
+                uint32_t* dst = reinterpret_cast<uint32_t*>(A.ids_out + o);
+                for (uint32_t c0 = 0; c0 < n; c0 += C) {
+                    const uint32_t cn = min(C, n - c0);
+                    for (uint32_t j = tid; j < C; j += LIST_THREADS) buf[j] = j < cn ? src[c0 + j] + 1u : 0u;
+                    __syncthreads();
+                    for (uint32_t kk = 2; kk <= C; kk <<= 1) {
+                        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                            for (uint32_t i = tid; i < C; i += LIST_THREADS) {
+                                const uint32_t l2 = i ^ jj;
+                                if (l2 > i) {
+                                    const uint32_t x = buf[i], y = buf[l2];
+                                    const bool desc = (i & kk) == 0;
+                                    if (desc ? (x < y) : (x > y)) {
+                                        buf[i] = y;
+                                        buf[l2] = x;
+                                    }
+                                }
+                            }
+                            __syncthreads();
+                        }
+                    }
+                    for (uint32_t j = tid; j < cn; j += LIST_THREADS) dst[c0 + j] = buf[j];
+                    __syncthreads();
+                }
+                __threadfence_block();
+                __syncthreads();
+                // merge runs of width wd from dst into src, alternating
+                uint32_t* a = dst;
+                uint32_t* bb = src;
+                for (uint32_t wd = C; wd < n; wd <<= 1) {
+                    for (uint32_t t = tid; t < n; t += LIST_THREADS) {
+                        const uint32_t pair0 = (t / (2 * wd)) * 2 * wd;
+                        const uint32_t an = min(wd, n - pair0);
+                        const uint32_t b0 = pair0 + an, bn = b0 < n ? min(wd, n - b0) : 0u;
+                        const uint32_t d = t - pair0;
+                        uint32_t l1 = d > bn ? d - bn : 0u, h1 = min(d, an);
+                        while (l1 < h1) {
+                            const uint32_t i = (l1 + h1) >> 1;
+                            if (a[pair0 + i] >= a[b0 + d - i - 1]) l1 = i + 1; else h1 = i;
+                        }
+                        const uint32_t i = l1, j = d - l1;
+                        bb[t] = (i < an && (j >= bn || a[pair0 + i] >= a[b0 + j])) ? a[pair0 + i] : a[b0 + j];
+                    }
+                    __threadfence_block();
+                    __syncthreads();
+                    uint32_t* tmp = a;
+                    a = bb;
+                    bb = tmp;
+                }
+                // a holds the merged ordinals + 1; map into ids_out
+                if (a == dst) {  // ids_out holds them already: map in place
+                    for (uint32_t t = tid; t < n; t += LIST_THREADS)
+                        A.ids_out[o + t] = id_of(dst[t] - 1u, A.read_ids, A.id_off);
+                } else {
+                    for (uint32_t t = tid; t < n; t += LIST_THREADS)
+                        A.ids_out[o + t] = id_of(a[t] - 1u, A.read_ids, A.id_off);
+                }
+                __threadfence_block();
+                __syncthreads();
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s) {
+    const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>(1, (max_entries + LIST_THREADS - 1) / LIST_THREADS), 16384);
+    hipLaunchKernelGGL(lists_kernel, dim3((unsigned)blocks), dim3(LIST_THREADS), 0, s, a);
+    return hipGetLastError();
+}
+
+// Bin processing order: descending log2(occurrences) (longest-processing-time
+// first for the persistent blocks).  One block; counting sort over 33 classes.
+__global__ __launch_bounds__(1024) void bins_order_kernel(const uint32_t* __restrict__ bstart,
+                                                          const uint32_t* __restrict__ kbase,
+                                                          const uint64_t* __restrict__ totals,
+                                                          uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[64];
+    const uint32_t nbins = (uint32_t)totals[2];
+    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
+        const uint32_t occ = kbase[bstart[b + 1]] - kbase[bstart[b]];
+        atomicAdd(&hist[32 - __clz(occ)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive offsets, class 32 first
+        uint32_t acc = 0;
+        for (int c = 32; c >= 0; c--) {
+            const uint32_t h = hist[c];
+            hist[c] = acc;
+            acc += h;
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
+        const uint32_t occ = kbase[bstart[b + 1]] - kbase[bstart[b]];
+        order[atomicAdd(&hist[32 - __clz(occ)], 1u)] = b;
+    }
+}
+
+hipError_t launch_bins_order(const uint32_t* bstart, const uint32_t* kbase, const uint64_t* totals,
+                             uint32_t* order, hipStream_t s) {
+    hipLaunchKernelGGL(bins_order_kernel, dim3(1), dim3(1024), 0, s, bstart, kbase, totals, order);
+    return hipGetLastError();
+}
+
 size_t bins_lds_bytes(uint32_t ts_log2) {
     const size_t TS = (size_t)1 << ts_log2;
     return sizeof(BinShared) + TS * (sizeof(uint64_t) + sizeof(uint32_t)) +
@@ -733,7 +910,12 @@ hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s) {
     const uint32_t TS = 1u << a.ts_log2;
     if (TS < 1024 || bins_lds_bytes(a.ts_log2) > 160 * 1024) return hipErrorInvalidValue;  // wave sort windows: 8 x 256 u32 in the 2*TS u32 table space
     const size_t lds = bins_lds_bytes(a.ts_log2);
-    uint64_t blocks = std::min<uint64_t>(max_bins, 65535);
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel, BIN_THREADS, lds);
+    if (e != hipSuccess) return e;
+    const uint64_t blocks = std::min<uint64_t>(max_bins, (uint64_t)std::max(1, cus) * std::max(1, per_cu));
     hipLaunchKernelGGL(bin_kernel, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a);
     return hipGetLastError();
 }
@@ -741,10 +923,11 @@ hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s) {
 __global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                                   uint64_t max_entries) {
     // on overflow the counters ran past the capacity (status says so): clamp
-    const uint64_t ne = gcount[0] < max_entries ? gcount[0] : max_entries;
+    const uint64_t ne0 = gcount[0] >> 32, ni = gcount[0] & 0xFFFFFFFFull;
+    const uint64_t ne = ne0 < max_entries ? ne0 : max_entries;
     totals[0] = ne;
-    totals[1] = gcount[1];
-    e_off[ne] = gcount[1];
+    totals[1] = ni;
+    e_off[ne] = ni;
 }
 
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,

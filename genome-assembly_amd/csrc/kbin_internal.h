@@ -92,14 +92,16 @@ struct BinArgs {
     const uint64_t* w0;        // [R] span bases 0..31
     const uint64_t* w1;        // [R] span bases 32..63
     const uint32_t* bstart;    // [nbins + 1]
-    const uint32_t* kbase;     // [R] first k-mer (occurrence) index of each bin-ordered record
+    const uint32_t* kbase;     // [R + 1] first k-mer (occurrence) index of each bin-ordered record
+    const uint32_t* order;     // [nbins] processing order (largest bins first)
+    unsigned long long* work;  // work counter (zeroed)
     uint64_t* stage;           // [N] (LDS slot << 32 | ordinal) per occurrence, bin-local ranges
     const uint64_t* totals;    // totals[2] = nbins
     int K, M;
     uint32_t keep_gt;
     uint32_t ts_log2;
     float rho;                 // expected distinct keys per occurrence
-    unsigned long long* gcount;  // [0] entries [1] ids [2] distinct keys before prune
+    unsigned long long* gcount;  // [0] entries << 32 | ids  [2] distinct keys before prune
     uint32_t* status;
     uint32_t* e_mmer;
     uint64_t* e_hi;
@@ -113,10 +115,23 @@ struct BinArgs {
     uint64_t max_entries, max_ids;
 };
 
+struct ListArgs {
+    const uint64_t* totals;    // totals[0] = entries
+    const uint32_t* e_cnt;
+    const uint64_t* e_off;
+    uint32_t* ids_ord;         // call ordinals per list (scratch for long lists)
+    int32_t* ids_out;
+    const int32_t* read_ids;
+    uint32_t id_off;
+};
+
+hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s);
 hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s);
 hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
                             uint32_t* nk, hipStream_t s);
 hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s);
+hipError_t launch_bins_order(const uint32_t* bstart, const uint32_t* kbase, const uint64_t* totals,
+                             uint32_t* order, hipStream_t s);
 size_t bins_lds_bytes(uint32_t ts_log2);
 #ifdef KB_BIN_PROF
 void bins_prof_report(hipStream_t s);

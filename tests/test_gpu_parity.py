@@ -40,7 +40,15 @@ def gpu_result(bases, lens, K, M, cutoff=1, prune=True, ids=None, batches=1, max
         return eng.export()
 
 
+def assert_csr(res):
+    """CSR contract (kbin.h): offset[e + 1] ends entry e's list, lists tile ids"""
+    off = np.asarray(res.offset, dtype=np.int64)
+    assert off[0] == 0 and off[-1] == len(res.ids)
+    np.testing.assert_array_equal(np.diff(off), np.asarray(res.count, dtype=np.int64))
+
+
 def assert_same(res, ora):
+    assert_csr(res)
     c = res.canonical()
     assert c.n_entries == ora.n_entries
     np.testing.assert_array_equal(c.mmer, ora.mmer)
@@ -195,3 +203,36 @@ def test_dropin_reference_program(golden_dir):
         ran += 1
     if not ran:
         pytest.skip("drop-in binaries not built (needs the reference at build time)")
+
+
+def test_full_scale_engines_agree(engine):
+    """BASELINE C2 size (1M x 150 bp, K31 M7, cutoff 1): both engines produce
+    the same canonical result; CSR contract, prune, list order by property
+    (affine ids: every list strictly non-increasing)"""
+    if engine == "binned":
+        pytest.skip("runs both engines itself")
+    import torch
+    n, L = 1_000_000, 150
+    wpr = (L + 31) // 32
+    words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, 5_000_000, 1000, 2)
+    torch.cuda.synchronize()
+    out = {}
+    for flag in (kbin.KB_ENGINE_TABLE, kbin.KB_ENGINE_BINNED):
+        with kbin.Engine(31, 7, cutoff=1, max_read_len=L, flags=flag) as eng:
+            eng.set_timing(True)
+            eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
+            eng.finalize(True)
+            assert eng.timing()["engine"] == (1 if flag == kbin.KB_ENGINE_TABLE else 2)
+            r = eng.export()
+        assert_csr(r)
+        assert int(np.asarray(r.count).min()) > 1
+        ok = np.diff(np.asarray(r.ids, dtype=np.int64)) <= 0
+        ok[np.asarray(r.offset[1:-1], dtype=np.int64) - 1] = True  # list boundaries
+        assert bool(ok.all())
+        out[flag] = r.canonical()
+    a, b = out[kbin.KB_ENGINE_TABLE], out[kbin.KB_ENGINE_BINNED]
+    assert a.n_entries == b.n_entries
+    for f in ("mmer", "kmer_hi", "kmer_lo", "count", "offset", "ids"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f))
