@@ -584,8 +584,8 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
                            (unsigned long long)N);
     HIPCHK(c->pay.ensure(3 * R));
     HIPCHK(c->srec.ensure(3 * R));
-    HIPCHK(c->occ_a.ensure(std::max<uint64_t>(R, N / 2 + 1)));
-    HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 1)));
+    HIPCHK(c->occ_a.ensure(std::max<uint64_t>(R, N / 2 + 4)));
+    HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4))  /* ids (u32) + 16-B over-read */);
     for (auto& b : c->batches) {
         SkScanArgs a{};
         a.words = b.words;
@@ -603,7 +603,7 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
     }
     REC(2);
     // ---- stable sort of the records by canonical mmer, bin boundaries
-    const int key_bits = 2 * M;
+    const int key_bits = 2 * M + 6;  // (mmer, 63 - n)
     const uint64_t nflags = onesweep_flag_elems(R);
     if (c->os_flags.cap < nflags || c->os_epoch > (1u << 24) - 8) {
         HIPCHK(c->os_flags.ensure(nflags));
@@ -619,7 +619,7 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
     HIPCHK(c->starts.ensure(max_bins + 1));
     HIPCHK(c->scratch.ensure(std::max(runs_scratch_elems(R, max_bins), c->scratch.cap)));
     HIPCHK(launch_heads(c->sorted, R, c->starts.p, max_bins, c->scratch.p, c->scratch.cap,
-                        c->totals.p, c->s));
+                        c->totals.p, c->s, 38));
     HIPCHK(c->kbase.ensure(R + 1));
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
     HIPCHK(launch_sk_gather(c->sorted, c->pay.p, R, c->srec.p, c->kbase.p, c->s));
@@ -663,6 +663,7 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
     a.keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
     a.ts_log2 = (uint32_t)ts_log2;
     a.rho = c->rho > 0.f ? c->rho : 0.25f;
+    a.ablate = env_int("KB_BIN_ABLATE", 0);
     a.gcount = reinterpret_cast<unsigned long long*>(c->totals.p + 4);
     a.status = c->misc.p;
     a.e_mmer = c->e_mmer.p;
@@ -691,6 +692,9 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
     la.read_ids = a.read_ids;
     la.id_off = a.id_off;
     HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : N / 8 + 1, c->s));
+#ifdef KB_BIN_PROF
+    lists_prof_report(c->s);
+#endif
     REC(5);
     HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
                     A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44);
                     A.pay[3 * t + 1] = window64(sw, lo);
                     A.pay[3 * t + 2] = window64(sw, lo + 32);
-                    A.keys[t] = ((uint64_t)canon << 32) | (uint32_t)t;
+                    A.keys[t] = ((uint64_t)canon << 38) | ((uint64_t)(63 - n) << 32) | (uint32_t)t;
                 }
                 nseg++;
                 lo = sig + 1;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                 A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44);
                 A.pay[3 * t + 1] = window64(sw, lo);
                 A.pay[3 * t + 2] = window64(sw, lo + 32);
-                A.keys[t] = ((uint64_t)(uint32_t)best << 32) | (uint32_t)t;
+                A.keys[t] = ((uint64_t)(uint32_t)best << 38) | ((uint64_t)(63 - n) << 32) | (uint32_t)t;
             }
             nseg++;
             lo = sig + 1;
@@ -349,9 +349,14 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
         const uint64_t flip = ((hd >> 44) & 1ull) ? kmask : 0ull;
-        const int nmax = rfl((int)wave_max_u32((uint32_t)n));
+        // records of a bin are sorted longest first: lane 0 holds the chunk's max
+        int nmax = rfl(n);
+        if (__ballot(n > nmax)) nmax = rfl((int)wave_max_u32((uint32_t)n));
+        uint64_t w = s0, x = s1;  // 64-base window at k-mer j, bases past it
         for (int j = 0; j < nmax; j++) {
-            const uint64_t code = (span_window(s0, s1, 0ull, 0ull, j) >> (64 - 2 * K)) ^ flip;
+            const uint64_t code = (w >> (64 - 2 * K)) ^ flip;
+            w = (w << 2) | (x >> 62);
+            x <<= 2;
             const bool take = j < n && (l == 0 || (part_of(code) & pmask) == p);
             const uint64_t m = __ballot(take);
             if (take) {
@@ -391,7 +396,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
         if (S.item >= nbins) break;  // uniform
         const uint32_t b = A.order[S.item];
         const uint32_t lo = A.bstart[b], hi = A.bstart[b + 1];
-        const uint32_t mmer = (uint32_t)(A.keys[lo] >> 32);
+        const uint32_t mmer = (uint32_t)(A.keys[lo] >> 38);
         uint64_t* stage = A.stage + A.kbase[lo];  // the bin's k-mer range, reused per partition
         // occurrences of the bin -> first partition depth
         uint64_t occ = 0;
@@ -440,6 +445,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             for_each_kmer(A, lo, hi, P, Lv, qk, qo, &S.n_stage,
                           [&](uint64_t k0, uint32_t o0, uint32_t s0, bool v0, uint64_t k1, uint32_t o1,
                               uint32_t s1, bool v1) {
+#ifdef KB_BIN_PROF
+                if (A.ablate == 1) return;  // expansion only
+#endif
                 const uint32_t h0 = (uint32_t)mix64(k0 - 1ull), h1 = (uint32_t)mix64(k1 - 1ull);
                 // first probes of both k-mers in flight together; the rest
                 // (empty slot, collision chain) takes the full insert path
@@ -454,6 +462,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                         S.overflow = 1;
                     } else {
                         atomicAdd(&cnt[l0], 1u);
+#ifdef KB_BIN_PROF
+                        if (A.ablate != 2)
+#endif
                         stage[s0] = ((uint64_t)l0 << 32) | o0;
                     }
                 }
@@ -462,6 +473,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                         S.overflow = 1;
                     } else {
                         atomicAdd(&cnt[l1], 1u);
+#ifdef KB_BIN_PROF
+                        if (A.ablate != 2)
+#endif
                         stage[s1] = ((uint64_t)l1 << 32) | o1;
                     }
                 }
@@ -537,7 +551,11 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             if (!room) continue;
             // ---- sweep 2: drop every surviving occurrence's call ordinal in place
             {
+#ifdef KB_BIN_PROF
+                const uint32_t ns = A.ablate ? 0u : S.n_stage;
+#else
                 const uint32_t ns = S.n_stage;
+#endif
                 for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
                     const uint64_t v = stage[i];
                     const uint32_t ls = (uint32_t)(v >> 32);
@@ -613,6 +631,55 @@ DEV void bitonic_desc(uint32_t* a, uint32_t Pw, uint32_t r) {
     }
 }
 
+// up to 256 values sorted descending by one wavefront, in registers: element
+// i = r * 64 + lane lives in v[r]; partners across lanes meet by xor-shuffle,
+// partners 64 or 128 apart are in the same lane.  In place in LDS.
+template <int R>
+DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane) {
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t i = (uint32_t)(r * 64 + lane);
+        v[r] = i < n ? p[i] : 0u;
+    }
+#pragma unroll
+    for (int kk = 2; kk <= R * 64; kk <<= 1) {
+#pragma unroll
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            if (jj >= 64) {
+                const int rj = jj >> 6;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const int r2 = r ^ rj;
+                    if (r2 > r) {
+                        const uint32_t i = (uint32_t)(r * 64 + lane);
+                        const bool desc = (i & kk) == 0;
+                        const uint32_t x = v[r], y = v[r2];
+                        const uint32_t hi = x > y ? x : y, lo = x > y ? y : x;
+                        v[r] = desc ? hi : lo;
+                        v[r2] = desc ? lo : hi;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const uint32_t i = (uint32_t)(r * 64 + lane);
+                    const uint32_t y = (uint32_t)__shfl_xor((int)v[r], jj, 64);
+                    const bool lower = (lane & jj) == 0;
+                    const bool desc = (i & kk) == 0;
+                    const uint32_t hi = v[r] > y ? v[r] : y, lo = v[r] > y ? y : v[r];
+                    v[r] = (lower == desc) ? hi : lo;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t i = (uint32_t)(r * 64 + lane);
+        if (i < n) p[i] = v[r];
+    }
+}
+
 // up to 32 values (ordinal + 1) sorted descending in one lane's registers, in place
 DEV void sort32_inplace(uint32_t* p, uint32_t n) {
     uint32_t v[32];
@@ -640,10 +707,28 @@ DEV void sort32_inplace(uint32_t* p, uint32_t n) {
         if ((uint32_t)j < n) p[j] = v[j];
 }
 
+#ifdef KB_BIN_PROF
+__device__ unsigned long long g_list_prof[8];
+#define LPROF(ph)                                                  \
+    do {                                                           \
+        if (tid == 0) {                                            \
+            const unsigned long long _t = clock64();               \
+            lacc[ph] += _t - lt;                                   \
+            lt = _t;                                               \
+        }                                                          \
+    } while (0)
+#else
+#define LPROF(ph) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(LIST_THREADS) void lists_kernel(ListArgs A) {
-    // staged chunks: ibuf = the chunk's ids (ordinal + 1), wave windows after
-    // it; other chunks: buf = block sort space (LIST_CAP), wave windows inside
-    __shared__ uint32_t lds[LIST_SPAN + 4 * 256];
+#ifdef KB_BIN_PROF
+    unsigned long long lacc[8] = {};
+    unsigned long long lt = clock64();
+#endif
+    // staged chunks: ibuf = the chunk's ids (ordinal + 1); other chunks: buf =
+    // block sort space (LIST_CAP), wave windows inside
+    __shared__ uint32_t lds[LIST_SPAN];
     static_assert(LIST_CAP <= LIST_SPAN, "block sort space aliases the staging area");
     uint32_t* const ibuf = lds;
     uint32_t* const buf = lds;
@@ -656,36 +741,74 @@ __global__ __launch_bounds__(LIST_THREADS) void lists_kernel(ListArgs A) {
          e0 += (uint64_t)gridDim.x * LIST_THREADS) {
         const uint32_t ne = (uint32_t)min<uint64_t>(LIST_THREADS, n_entries - e0);
         const uint64_t ob = A.e_off[e0], span = A.e_off[e0 + ne] - ob;
+        // staging is 16-B aligned: ibuf[j] holds id base + j, lists start at sh
+        const uint64_t base = ob & ~3ull;
+        const uint32_t sh = (uint32_t)(ob - base);
+        const uint32_t nv = (uint32_t)((sh + span + 3) >> 2);  // uint4 groups
         if (tid == 0) n_big = 0;
         const bool long_list = tid < ne && A.e_cnt[e0 + tid] > 256;
-        if (!__syncthreads_or(long_list) && span <= LIST_SPAN) {
-            // staged: coalesced in, every list sorted in LDS, coalesced out
-            for (uint32_t i = tid; i < span; i += LIST_THREADS) ibuf[i] = A.ids_ord[ob + i] + 1u;
-            __syncthreads();
+        if (!__syncthreads_or(long_list) && sh + span + 3 <= LIST_SPAN) {
+            // staged: coalesced 16-B in, every list sorted in LDS, 16-B out
+            LPROF(0);
+            const uint4* src4 = reinterpret_cast<const uint4*>(A.ids_ord + base);
+            uint4* ib4 = reinterpret_cast<uint4*>(ibuf);
+            for (uint32_t b = 0; b < nv; b += 4 * LIST_THREADS) {  // 4 x 16 B in flight
+                uint4 v[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t g = b + k * LIST_THREADS + tid;
+                    if (g < nv) v[k] = src4[g];  // may read up to 3 ids past the span: same allocation
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t g = b + k * LIST_THREADS + tid;
+                    if (g < nv) ib4[g] = make_uint4(v[k].x + 1u, v[k].y + 1u, v[k].z + 1u, v[k].w + 1u);
+                }
+            }            __syncthreads();
+            LPROF(1);
             if (tid < ne) {
                 const uint32_t n = A.e_cnt[e0 + tid];
-                const uint32_t o = (uint32_t)(A.e_off[e0 + tid] - ob);
+                const uint32_t o = (uint32_t)(A.e_off[e0 + tid] - base);
                 if (n <= 32) sort32_inplace(ibuf + o, n);
                 else big[atomicAdd(&n_big, 1u)] = tid;
             }
             __syncthreads();
+            LPROF(2);
             const uint32_t nbig = n_big;
-            uint32_t* wb = lds + LIST_SPAN + wid * 256;
             for (uint32_t q = wid; q < nbig; q += LIST_THREADS / 64) {
                 const uint32_t n = A.e_cnt[e0 + big[q]];
-                const uint32_t o = (uint32_t)(A.e_off[e0 + big[q]] - ob);
-                uint32_t Pw = 64;
-                while (Pw < n) Pw <<= 1;
-                for (uint32_t j = lane; j < Pw; j += 64) wb[j] = j < n ? ibuf[o + j] : 0u;
-                wave_sync();
-                bitonic_desc<64>(wb, Pw, lane);
-                for (uint32_t j = lane; j < n; j += 64) ibuf[o + j] = wb[j];
+                uint32_t* p = ibuf + (uint32_t)(A.e_off[e0 + big[q]] - base);
+                if (n <= 64) wave_sort_desc<1>(p, n, lane);
+                else if (n <= 128) wave_sort_desc<2>(p, n, lane);
+                else wave_sort_desc<4>(p, n, lane);
                 wave_sync();
             }
             __syncthreads();
-            for (uint32_t i = tid; i < span; i += LIST_THREADS)
-                A.ids_out[ob + i] = id_of(ibuf[i] - 1u, A.read_ids, A.id_off);
+            LPROF(3);
+            {
+                // full groups as 16-B stores, the partial first/last group per id
+                const uint32_t end = sh + (uint32_t)span;  // ibuf index past the span
+                int4* dst4 = reinterpret_cast<int4*>(A.ids_out + base);
+                for (uint32_t g = tid; g < nv; g += LIST_THREADS) {
+                    const uint32_t j0 = g * 4;
+                    const uint4 v = ib4[g];
+                    if (j0 >= sh && j0 + 4 <= end) {
+                        dst4[g] = make_int4(id_of(v.x - 1u, A.read_ids, A.id_off), id_of(v.y - 1u, A.read_ids, A.id_off),
+                                            id_of(v.z - 1u, A.read_ids, A.id_off), id_of(v.w - 1u, A.read_ids, A.id_off));
+                    } else {
+                        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            if (j0 + k >= sh && j0 + k < end)
+                                A.ids_out[base + j0 + k] = id_of(vv[k] - 1u, A.read_ids, A.id_off);
+                    }
+                }
+            }
             __syncthreads();
+            LPROF(4);
+#ifdef KB_BIN_PROF
+            if (tid == 0) lacc[5]++, lacc[6] += nbig;
+#endif
             continue;
         }
         __syncthreads();
@@ -855,7 +978,23 @@ __global__ __launch_bounds__(LIST_THREADS) void lists_kernel(ListArgs A) {
         }
         __syncthreads();
     }
+#ifdef KB_BIN_PROF
+    if (tid == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(&g_list_prof[i], lacc[i]);
+#endif
 }
+
+#ifdef KB_BIN_PROF
+void lists_prof_report(hipStream_t s) {
+    unsigned long long h[8];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_list_prof), sizeof(h));
+    fprintf(stderr, "[list_prof] pre=%llu load=%llu small=%llu mid=%llu store=%llu chunks=%llu mid_lists=%llu\n",
+            h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+    unsigned long long z[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_list_prof), z, sizeof(z));
+}
+#endif
 
 hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s) {
     const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>(1, (max_entries + LIST_THREADS - 1) / LIST_THREADS), 16384);

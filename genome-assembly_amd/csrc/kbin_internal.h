@@ -81,13 +81,15 @@ struct SkScanArgs {
     uint32_t* seg_count;       // count pass: segments per read
     const uint32_t* rec_base;  // write pass: exclusive scan of seg_count
     uint64_t* pay;             // [3R] {ord | n << 32 | sig_off << 38 | rev << 44, span w0, w1}
-    uint64_t* keys;            // [R] canonical mmer << 32 | record index
+    uint64_t* keys;            // [R] canonical mmer << 38 | (63 - n) << 32 | record index:
+                               // bins in mmer order, records of a bin longest first
+                               // (a wavefront's 64 records have near-equal k-mer counts)
     uint32_t ord_base;
     int RW, K, M;
 };
 
 struct BinArgs {
-    const uint64_t* keys;      // sorted by mmer
+    const uint64_t* keys;      // sorted by (mmer, 63 - n); mmer = key >> 38
     const uint64_t* hdr;       // [R] bin-ordered record headers (see SkScanArgs::pay)
     const uint64_t* w0;        // [R] span bases 0..31
     const uint64_t* w1;        // [R] span bases 32..63
@@ -101,6 +103,7 @@ struct BinArgs {
     uint32_t keep_gt;
     uint32_t ts_log2;
     float rho;                 // expected distinct keys per occurrence
+    int ablate;                // diagnostic build (KB_BIN_PROF) only: 1 expansion only, 2 no staging
     unsigned long long* gcount;  // [0] entries << 32 | ids  [2] distinct keys before prune
     uint32_t* status;
     uint32_t* e_mmer;
@@ -135,6 +138,7 @@ hipError_t launch_bins_order(const uint32_t* bstart, const uint32_t* kbase, cons
 size_t bins_lds_bytes(uint32_t ts_log2);
 #ifdef KB_BIN_PROF
 void bins_prof_report(hipStream_t s);
+void lists_prof_report(hipStream_t s);
 #endif
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                              uint64_t max_entries, hipStream_t s);
@@ -156,8 +160,10 @@ hipError_t launch_radix_sort(uint64_t* a, uint64_t* b, uint64_t n, int key_bits,
 uint64_t onesweep_flag_elems(uint64_t n);
 hipError_t launch_onesweep(uint64_t* a, uint64_t* b, uint64_t n, int key_bits, uint64_t* flags,
                            uint32_t* aux, uint32_t* epoch, uint64_t** sorted, hipStream_t s);
+// run starts of sorted keys, a run = equal S >> key_shift
 hipError_t launch_heads(const uint64_t* S, uint64_t n, uint32_t* starts, uint64_t max_runs,
-                        uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s);
+                        uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s,
+                        int key_shift = 32);
 uint64_t runs_scratch_elems(uint64_t n, uint64_t max_runs);
 hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int KW,
                        uint32_t keep_gt, uint32_t* starts, const int32_t* read_ids,

@@ -1012,18 +1012,18 @@ hipError_t launch_radix_sort(uint64_t* a, uint64_t* b, uint64_t n, int key_bits,
 // ---------------------------------------------------------------------------
 DEV uint32_t slot_of(uint64_t rec) { return (uint32_t)(rec >> 32); }
 
-DEV uint32_t is_head(const uint64_t* __restrict__ S, uint64_t k) {
-    return (k == 0 || slot_of(S[k]) != slot_of(S[k - 1])) ? 1u : 0u;
+DEV uint32_t is_head(const uint64_t* __restrict__ S, uint64_t k, int sh = 32) {
+    return (k == 0 || (S[k] >> sh) != (S[k - 1] >> sh)) ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(256) void heads_partials_kernel(const uint64_t* __restrict__ S, uint64_t n,
-                                                             uint64_t* __restrict__ part) {
+                                                             uint64_t* __restrict__ part, int key_sh) {
     __shared__ uint64_t sh[4];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
     uint64_t c = 0;
     for (int j = 0; j < SCAN_ITEMS; j++) {
         const uint64_t k = base + (uint64_t)j * 256 + threadIdx.x;
-        if (k < n) c += is_head(S, k);
+        if (k < n) c += is_head(S, k, key_sh);
     }
     c = block_sum256(c, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = c;
@@ -1032,13 +1032,13 @@ __global__ __launch_bounds__(256) void heads_partials_kernel(const uint64_t* __r
 __global__ __launch_bounds__(256) void heads_write_kernel(const uint64_t* __restrict__ S, uint64_t n,
                                                           const uint64_t* __restrict__ part,
                                                           uint32_t* __restrict__ starts,
-                                                          uint64_t max_runs) {
+                                                          uint64_t max_runs, int key_sh) {
     __shared__ uint64_t sh[4];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
     uint64_t run = part[blockIdx.x];
     for (int j = 0; j < SCAN_ITEMS; j++) {
         const uint64_t k = base + (uint64_t)j * 256 + threadIdx.x;
-        const uint32_t h = k < n ? is_head(S, k) : 0u;
+        const uint32_t h = k < n ? is_head(S, k, key_sh) : 0u;
         uint64_t tot;
         const uint64_t ex = block_excl_scan256((uint64_t)h, sh, tot);
         if (h && run + ex < max_runs) starts[run + ex] = (uint32_t)k;
@@ -1183,14 +1183,15 @@ __global__ void entries_total_kernel(const uint64_t* __restrict__ tk, const uint
 
 // run starts of a sorted record array (key = bits 32..): starts[0..D], D in d_totals[2]
 hipError_t launch_heads(const uint64_t* S, uint64_t n, uint32_t* starts, uint64_t max_runs,
-                        uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s) {
+                        uint64_t* scratch, uint64_t scratch_n, uint64_t* d_totals, hipStream_t s,
+                        int key_shift) {
     const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (scratch_n < nb + 1) return hipErrorInvalidValue;
     if (n == 0) return hipMemsetAsync(d_totals, 0, 4 * sizeof(uint64_t), s);
-    hipLaunchKernelGGL(heads_partials_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch);
+    hipLaunchKernelGGL(heads_partials_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch, key_shift);
     hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, scratch, nb, scratch + nb);
     hipLaunchKernelGGL(heads_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, scratch, starts,
-                       max_runs);
+                       max_runs, key_shift);
     hipLaunchKernelGGL(runs_total_kernel, dim3(1), dim3(1), 0, s, scratch + nb, n, starts, d_totals,
                        max_runs);
     return hipGetLastError();
