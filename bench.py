@@ -61,15 +61,19 @@ def cpu_baseline(words, lens, n_sample, wpr, L, K, M, cutoff):
                       f"oracle/kb_oracle.c single-threaded, {dt:.2f} s, host nproc={os.cpu_count()}"}
 
 
-def load_traffic(tag: str):
-    """Per-launch HBM bytes of scan_insert from the committed rocprofv3 --pmc
-    passes (profiles/traffic.json, written by profiles/pmc_traffic.py)."""
+def load_traffic(tag: str, kernel: str):
+    """Per-launch HBM bytes of the roofline kernel from the committed rocprofv3
+    --pmc passes (profiles/traffic.json, written by tools/pmc_traffic.py)."""
     p = REPO / "profiles" / "traffic.json"
     if not p.exists():
         return None
     try:
-        d = json.loads(p.read_text())
-        return d.get(tag)
+        d = json.loads(p.read_text()).get(tag)
+        if not d:
+            return None
+        k = kernel.split("<")[0]
+        row = next((v for name, v in d.get("per_kernel", {}).items() if k in name), None)
+        return {"hbm_bytes_per_launch": row["bytes"]} if row else None
     except Exception:
         return None
 
@@ -166,17 +170,24 @@ def main():
     total_scanned = scanned * world
     value = total_scanned * args.steps / elapsed
 
+    # roofline of the dominant kernel: SURVEY.md 8(d)'s algorithmic bytes per
+    # k-mer occurrence x the occurrences one launch processes / the launch's
+    # device time (HIP events on the engine stream, inside the timed loop)
     bpr = algorithmic_bytes_per_read(L, K)
-    avg_scan_ms = float(np.mean(scan_ms))
-    achieved = (bpr * n) / (avg_scan_ms * 1e-3) / 1e9  # GB/s, per launch
+    binned = int(tim[-1]["engine"]) == kbin.KB_ENG_BINNED
+    kname = "bin_kernel" if binned else ("scan_insert_kernel<1>" if K <= 31 else "scan_insert_kernel<2>")
+    avg_kernel_ms = float(np.mean([t["runs_ms"] for t in tim])) if binned else float(np.mean(scan_ms))
+    achieved = (bpr * n) / (avg_kernel_ms * 1e-3) / 1e9  # GB/s, per launch
     tag = f"n{n}_L{L}_K{K}_M{M}"
-    traffic = load_traffic(tag)
-    roof = {"bound": "hbm", "kernel": "scan_insert_kernel<1>" if K <= 31 else "scan_insert_kernel<2>",
+    traffic = load_traffic(tag, kname)
+    roof = {"bound": "hbm", "kernel": kname,
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
-            "kernel_ms": round(avg_scan_ms, 4),
-            "bytes_per_kmer": round(bpr / max(1, L - K + 1), 3)}
+            "kernel_ms": round(avg_kernel_ms, 4),
+            "bytes_per_kmer": round(bpr / max(1, L - K + 1), 3),
+            "path_frac": round(total_scanned * args.steps / elapsed * bpr / max(1, L - K + 1)
+                               / (world * HBM_PEAK_GBS * 1e9), 4)}
     phases = {k: round(float(np.mean([t[k] for t in tim])), 4)
               for k in ("scan_insert_ms", "sort_ms", "runs_ms", "emit_ms", "total_ms")}
 

@@ -76,7 +76,8 @@ struct Batch {
     uint64_t ord_base = 0;
     uint64_t occ_base = 0;
     uint64_t n_occ = 0;
-    bool affine = false;              // ids = first_id + r
+    bool affine = false;              // ids = first_id + r (no ids array until needed)
+    bool have_occ = false;            // kmer_base / n_occ computed (batch_offsets)
     int64_t first_id = 0;
     // multi-GPU routing
     bool superkmers = false;          // a batch of received super-k-mer records
@@ -126,6 +127,7 @@ struct kb_ctx {
     DevBuf<uint32_t> kbase;    // first occurrence index of each bin-ordered record
     DevBuf<uint64_t> stage;    // per-occurrence (slot, ordinal) staging
     DevBuf<uint32_t> border;   // bin processing order
+    DevBuf<uint64_t> kpart;    // per-block k-mer sums of the count pass
     float rho = 0.f;           // learned distinct / occurrences
     uint64_t n_occ_entries_hint = 0;  // entries of the last finalize (lists grid)
     uint64_t* h_totals = nullptr;
@@ -187,9 +189,9 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     }
     e = hipHostMalloc((void**)&c->h_misc, 16 * sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
-    e = hipHostMalloc((void**)&c->h_totals, 8 * sizeof(uint64_t), hipHostMallocDefault);
+    e = hipHostMalloc((void**)&c->h_totals, 16 * sizeof(uint64_t), hipHostMallocDefault);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
-    if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(8) != hipSuccess) {
+    if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(16) != hipSuccess) {
         kb_destroy(c);
         return fail(KB_ENOMEM, "device alloc");
     }
@@ -218,7 +220,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->kbase.release(); c->stage.release(); c->border.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->kbase.release(); c->stage.release(); c->border.release(); c->kpart.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
@@ -254,6 +256,15 @@ static int batch_offsets(kb_ctx* c, Batch& b) {
     HIPCHK(hipMemcpyAsync(&tot, b.kmer_base + b.n_reads, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     b.n_occ = tot;
+    b.have_occ = true;
+    return KB_OK;
+}
+
+// the ids array of an affine batch, materialised only where a path needs it
+static int batch_ids(kb_ctx* c, Batch& b) {
+    if (b.ids || b.superkmers) return KB_OK;
+    HIPCHK(hipMalloc((void**)&b.ids, std::max<uint64_t>(b.n_reads, 1) * sizeof(int32_t)));
+    HIPCHK(launch_fill_ids(b.ids, b.n_reads, (int32_t)b.first_id, c->s));
     return KB_OK;
 }
 
@@ -301,7 +312,7 @@ static int submit_common(kb_ctx* c, const char* bases, const uint32_t* lens, uin
     b.ord_base = c->n_reads;
     HIPCHK(hipMalloc((void**)&b.own_words, n_reads * (uint64_t)RW * sizeof(uint64_t)));
     HIPCHK(hipMalloc((void**)&b.own_lens, n_reads * sizeof(uint32_t)));
-    HIPCHK(hipMalloc((void**)&b.ids, n_reads * sizeof(int32_t)));
+    if (ids) HIPCHK(hipMalloc((void**)&b.ids, n_reads * sizeof(int32_t)));
     b.words = b.own_words;
     b.lens = b.own_lens;
     HIPCHK(hipMemsetAsync(c->misc.p, 0, sizeof(uint32_t), c->s));
@@ -309,7 +320,6 @@ static int submit_common(kb_ctx* c, const char* bases, const uint32_t* lens, uin
     if (ids) {
         HIPCHK(hipMemcpyAsync(b.ids, ids, n_reads * sizeof(int32_t), hipMemcpyHostToDevice, c->s));
     } else {
-        HIPCHK(launch_fill_ids(b.ids, n_reads, first_id, c->s));
         b.affine = true;
         b.first_id = first_id;
     }
@@ -320,13 +330,6 @@ static int submit_common(kb_ctx* c, const char* bases, const uint32_t* lens, uin
         (void)hipFree(b.own_words); (void)hipFree(b.own_lens); (void)hipFree(b.ids);
         return fail(KB_EALPHABET, "read byte outside {A,C,G,T} (see DESIGN.md: alphabet)");
     }
-    rc = batch_offsets(c, b);
-    if (rc) {
-        (void)hipFree(b.own_words); (void)hipFree(b.own_lens); (void)hipFree(b.ids);
-        return rc;
-    }
-    b.occ_base = c->n_occ;
-    c->n_occ += b.n_occ;
     c->n_reads += n_reads;
     c->batches.push_back(b);
     return KB_OK;
@@ -362,14 +365,8 @@ extern "C" int kb_submit_packed_device(kb_ctx* c, const uint64_t* d_words, const
     b.n_reads = n_reads;
     b.RW = (int)wpr;
     b.ord_base = c->n_reads;
-    HIPCHK(hipMalloc((void**)&b.ids, n_reads * sizeof(int32_t)));
-    HIPCHK(launch_fill_ids(b.ids, n_reads, first_id, c->s));
     b.affine = true;
     b.first_id = first_id;
-    rc = batch_offsets(c, b);
-    if (rc) { (void)hipFree(b.ids); return rc; }
-    b.occ_base = c->n_occ;
-    c->n_occ += b.n_occ;
     c->n_reads += n_reads;
     c->batches.push_back(b);
     return KB_OK;
@@ -415,6 +412,8 @@ extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
     for (auto& b : c->batches) {
         if (b.superkmers || b.routed) continue;
         const uint64_t cells = (uint64_t)n_dest * b.n_reads;
+        rc = batch_ids(c, b);
+        if (rc) return rc;
         if (b.route_offs) (void)hipFree(b.route_offs);
         b.route_offs = nullptr;
         HIPCHK(hipMalloc((void**)&b.route_offs, std::max<uint64_t>(cells, 1) * sizeof(uint32_t)));
@@ -529,6 +528,7 @@ extern "C" int kb_submit_superkmers_device(kb_ctx* c, const uint64_t* d_recs, ui
     HIPCHK(hipMemcpyAsync(&tot, c->scratch.p + nb, 8, hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     b.n_occ = tot;
+    b.have_occ = true;
     c->n_occ += tot;
     c->batches.push_back(b);
     return KB_OK;
@@ -550,36 +550,50 @@ static int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
-static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
+static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c) {
     const int M = c->p.M;
     const uint64_t nr = c->n_reads;
     c->tm.engine = KB_ENG_BINNED;
     REC(0);
     HIPCHK(c->seg.ensure(nr + 1));
     HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(nr + 1), c->scratch.cap)));
-    HIPCHK(c->totals.ensure(8));
-    HIPCHK(hipMemsetAsync(c->totals.p, 0, 8 * sizeof(uint64_t), c->s));
+    HIPCHK(c->totals.ensure(16));
+    HIPCHK(hipMemsetAsync(c->totals.p, 0, 16 * sizeof(uint64_t), c->s));
     HIPCHK(hipMemsetAsync(c->misc.p, 0, 2 * sizeof(uint32_t), c->s));
     REC(1);
     // ---- phase A: super-k-mers per read, scan, records
     c->tm.scan_insert_launches = 0;
+    {
+        uint64_t kp = 1;
+        for (auto& b : c->batches) kp = std::max(kp, sk_blocks(b.n_reads, b.RW));
+        HIPCHK(c->kpart.ensure(kp));
+    }
     for (auto& b : c->batches) {
         SkScanArgs a{};
         a.words = b.words;
         a.lens = b.lens;
         a.n_reads = b.n_reads;
         a.seg_count = c->seg.p + b.ord_base;
+        a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p);
         a.RW = b.RW;
         a.K = c->p.K;
         a.M = M;
         HIPCHK(launch_sk(a, false, c->s));
+        HIPCHK(launch_sk_kmers_total(reinterpret_cast<unsigned long long*>(c->kpart.p), sk_blocks(b.n_reads, b.RW),
+                                     reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
         c->tm.scan_insert_launches++;
     }
     HIPCHK(launch_scan_u32(c->seg.p, nr, c->scratch.p, c->scratch.cap, c->s));
     const uint64_t nbs = scan_u32_scratch_elems(nr) - 2;
     HIPCHK(hipMemcpyAsync(c->h_totals + 7, c->scratch.p + nbs, 8, hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
+    HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, 8, hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync: R and N size the rest
     const uint64_t R = nr ? c->h_totals[7] : 0;
+    const uint64_t N = nr ? c->h_totals[8] : 0;
+    c->n_occ = N;
+    if (N >= 0xFFFFFFFFull)
+        return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
+                    (unsigned long long)N);
     if (R > N) return fail(KB_EDEVICE, "internal: %llu super-k-mers > %llu k-mers", (unsigned long long)R,
                            (unsigned long long)N);
     HIPCHK(c->pay.ensure(3 * R));
@@ -637,14 +651,6 @@ static int finalize_binned(kb_ctx* c, int prune, uint64_t N) {
     HIPCHK(c->e_lo.ensure(ecap));
     HIPCHK(c->e_off.ensure(ecap));
     HIPCHK(c->ids_out.ensure(std::max<uint64_t>(N, 1)));
-    bool affine = true;
-    int64_t id_c = 0;
-    for (size_t i = 0; i < c->batches.size(); i++) {
-        const Batch& b = c->batches[i];
-        const int64_t cb = b.first_id - (int64_t)b.ord_base;
-        if (!b.affine || (i && cb != id_c)) affine = false;
-        id_c = cb;
-    }
     // >= 10: the sort phase carves 8 wave windows of 256 ids out of the table
     const int ts_log2 = std::min(13, std::max(10, env_int("KB_BIN_TS_LOG2", 13)));
     BinArgs a{};
@@ -733,38 +739,64 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     if (rc) return rc;
     // active batches: unrouted reads, or received super-k-mers (not both)
     bool any_reads = false, any_sk = false;
-    uint64_t N = 0;
     for (auto& b : c->batches) {
         if (b.routed) continue;
         (b.superkmers ? any_sk : any_reads) = true;
-        b.occ_base = N;
-        N += b.n_occ;
     }
     if (any_reads && any_sk)
         return fail(KB_ESTATE, "a context bins either its own reads or received super-k-mers");
-    c->n_occ = N;
-    if (N >= 0xFFFFFFFFull)
-        return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
-                    (unsigned long long)N);
     memset(&c->tm, 0, sizeof(c->tm));
     const int SW = c->KW == 1 ? 2 : 4;
     const bool track_first = (c->p.flags & KB_TRACK_FIRST) != 0;
     bool any_routed = false;
     for (auto& b : c->batches) any_routed |= b.routed;
-    // ids of the reads, ordinal-indexed (both engines)
-    HIPCHK(c->read_ids.ensure(c->n_reads));
-    for (auto& b : c->batches)
-        if (!b.superkmers && b.n_reads)
-            HIPCHK(hipMemcpyAsync(c->read_ids.p + b.ord_base, b.ids, b.n_reads * sizeof(int32_t),
-                                  hipMemcpyDeviceToDevice, c->s));
+    // ordinal -> read id: one affine map for the context, else an array
+    bool affine = !any_sk;
+    int64_t id_c = 0;
+    {
+        bool first_b = true;
+        for (auto& b : c->batches) {
+            if (b.routed || b.superkmers) continue;
+            const int64_t cb = b.first_id - (int64_t)b.ord_base;
+            if (!b.affine || (!first_b && cb != id_c)) affine = false;
+            id_c = cb;
+            first_b = false;
+        }
+    }
+    if (!affine && !any_sk) {
+        HIPCHK(c->read_ids.ensure(c->n_reads));
+        for (auto& b : c->batches) {
+            if (b.superkmers || !b.n_reads) continue;
+            if (b.ids)
+                HIPCHK(hipMemcpyAsync(c->read_ids.p + b.ord_base, b.ids, b.n_reads * sizeof(int32_t),
+                                      hipMemcpyDeviceToDevice, c->s));
+            else
+                HIPCHK(launch_fill_ids(c->read_ids.p + b.ord_base, b.n_reads, (int32_t)b.first_id, c->s));
+        }
+    }
     // engine choice: flags, then KB_ENGINE=table|binned (A/B runs), then the default
-    bool binned = false;
+    bool binned = true;
     if (c->p.flags & KB_ENGINE_BINNED) binned = true;
     else if (c->p.flags & KB_ENGINE_TABLE) binned = false;
-    else if (const char* e = getenv("KB_ENGINE")) binned = strcmp(e, "binned") == 0;
+    else if (const char* e = getenv("KB_ENGINE")) binned = strcmp(e, "table") != 0;
     if (binned && c->KW == 1 && !track_first && !any_sk && !any_routed)
-        return finalize_binned(c, prune, N);
+        return finalize_binned(c, prune, affine, id_c);
     c->tm.engine = KB_ENG_TABLE;
+    // per-read occurrence offsets (the table engine's record slots)
+    uint64_t N = 0;
+    for (auto& b : c->batches) {
+        if (b.routed) continue;
+        if (!b.superkmers && !b.have_occ) {
+            rc = batch_offsets(c, b);
+            if (rc) return rc;
+        }
+        b.occ_base = N;
+        N += b.n_occ;
+    }
+    c->n_occ = N;
+    if (N >= 0xFFFFFFFFull)
+        return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
+                    (unsigned long long)N);
     // ---- table plan: ~0.6 load for the expected distinct keys
     uint64_t slots = c->p.table_slots;
     if (!slots) slots = c->learned_slots;
@@ -881,16 +913,6 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     if (track_first) HIPCHK(c->e_first.ensure(ne_cap));
     const uint32_t keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
     // ids: affine fast path (id = ordinal + c for every batch) avoids the gather
-    bool affine = !any_sk;
-    int64_t id_c = 0;
-    bool first_b = true;
-    for (auto& b : c->batches) {
-        if (b.routed || b.superkmers) continue;
-        const int64_t cb = b.first_id - (int64_t)b.ord_base;
-        if (!b.affine || (!first_b && cb != id_c)) affine = false;
-        id_c = cb;
-        first_b = false;
-    }
     HIPCHK(launch_runs(c->sorted, N, c->table.p, c->KW, keep_gt, c->starts.p,
                        (any_sk || affine) ? nullptr : c->read_ids.p, (uint32_t)(affine ? id_c : 0),
                        c->ids_out.p, ne_cap, c->e_mmer.p, c->e_hi.p, c->e_lo.p, c->e_cnt.p,

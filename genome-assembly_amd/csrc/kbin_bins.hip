@@ -59,9 +59,11 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
     const uint32_t halfM = 1u << (2 * M - 1);
     uint64_t* sw = smem + wid * (RW + 2);  // two zero words: span windows never leave the read
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    uint64_t kmers = 0;
     for (uint64_t r = (uint64_t)blockIdx.x * 4 + wid; r < A.n_reads; r += nwaves) {
         const int L = rfl((int)A.lens[r]);
         const int nK = L - K + 1;
+        if (nK > 0) kmers += (uint64_t)nK;
         uint32_t nseg = 0;
         if (nK > 0) {
             wave_sync();
@@ -93,6 +95,11 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
         }
         if (!WRITE && lane == 0) A.seg_count[r] = nseg;
     }
+    if (!WRITE) {
+        __shared__ uint64_t sh[4];
+        const uint64_t tot = block_sum256((uint64_t)(lane == 0 ? kmers : 0), sh);
+        if (threadIdx.x == 0) A.n_kmers[blockIdx.x] = tot;
+    }
 }
 
 // Thread-per-read variant for short reads (RW <= SK_THREAD_RW): a block
@@ -112,6 +119,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     const uint32_t maskM = (1u << (2 * M)) - 1u;
     const uint32_t halfM = 1u << (2 * M - 1);
     const uint32_t tid = threadIdx.x;
+    uint64_t kmers = 0;
     for (uint64_t r0 = (uint64_t)blockIdx.x * 256; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * 256) {
         const uint32_t nrows = (uint32_t)min<uint64_t>(256, A.n_reads - r0);
         __syncthreads();
@@ -128,6 +136,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
         const uint64_t r = r0 + tid;
         const uint64_t* sw = smem + tid * RS;
         const int nK = (int)A.lens[r] - K + 1;
+        if (nK > 0) kmers += (uint64_t)nK;
         uint32_t nseg = 0;
         const uint64_t rbase = WRITE ? A.rec_base[r] : 0;
         const uint64_t ordv = (uint64_t)(A.ord_base + (uint32_t)r);
@@ -158,12 +167,38 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
         }
         if (!WRITE) A.seg_count[r] = nseg;
     }
+    if (!WRITE) {  // per-block partial sum (summed by sk_kmers_total_kernel)
+        __shared__ uint64_t sh[4];
+        const uint64_t tot = block_sum256(kmers, sh);
+        if (tid == 0) A.n_kmers[blockIdx.x] = tot;
+    }
+}
+
+uint64_t sk_blocks(uint64_t n_reads, int RW) {
+    if (!n_reads) return 0;
+    if (RW <= SK_THREAD_RW) return std::min<uint64_t>((n_reads + 255) / 256, 8192);
+    return std::min<uint64_t>((n_reads + 3) / 4, 4096);
+}
+
+__global__ void sk_kmers_total_kernel(const unsigned long long* part, uint64_t n, unsigned long long* out) {
+    __shared__ uint64_t sh[4];
+    uint64_t v = 0;
+    for (uint64_t i = threadIdx.x; i < n; i += 256) v += part[i];
+    v = block_sum256(v, sh);
+    if (threadIdx.x == 0) *out += v;
+}
+
+hipError_t launch_sk_kmers_total(const unsigned long long* part, uint64_t n, unsigned long long* out,
+                                 hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(sk_kmers_total_kernel, dim3(1), dim3(256), 0, s, part, n, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s) {
     if (!a.n_reads) return hipSuccess;
+    const uint64_t blocks = sk_blocks(a.n_reads, a.RW);
     if (a.RW <= SK_THREAD_RW) {
-        const uint64_t blocks = std::min<uint64_t>((a.n_reads + 255) / 256, 8192);
         const size_t lds = (size_t)256 * (a.RW + 2) * sizeof(uint64_t);
         if (write)
             hipLaunchKernelGGL(sk_thread_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);
@@ -171,8 +206,6 @@ hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s) {
             hipLaunchKernelGGL(sk_thread_kernel<false>, dim3((unsigned)blocks), dim3(256), lds, s, a);
         return hipGetLastError();
     }
-    uint64_t blocks = (a.n_reads + 3) / 4;
-    if (blocks > 4096) blocks = 4096;
     const size_t lds = (size_t)4 * (a.RW + 2) * sizeof(uint64_t);
     if (write)
         hipLaunchKernelGGL(sk_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);

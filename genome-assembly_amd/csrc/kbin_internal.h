@@ -79,6 +79,7 @@ struct SkScanArgs {
     const uint32_t* lens;
     uint64_t n_reads;
     uint32_t* seg_count;       // count pass: segments per read
+    unsigned long long* n_kmers;  // count pass: [sk_blocks()] per-block k-mer sums
     const uint32_t* rec_base;  // write pass: exclusive scan of seg_count
     uint64_t* pay;             // [3R] {ord | n << 32 | sig_off << 38 | rev << 44, span w0, w1}
     uint64_t* keys;            // [R] canonical mmer << 38 | (63 - n) << 32 | record index:
@@ -130,6 +131,9 @@ struct ListArgs {
 
 hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s);
 hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s);
+uint64_t sk_blocks(uint64_t n_reads, int RW);
+hipError_t launch_sk_kmers_total(const unsigned long long* part, uint64_t n, unsigned long long* out,
+                                 hipStream_t s);
 hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
                             uint32_t* nk, hipStream_t s);
 hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s);

@@ -55,12 +55,12 @@ extern "C" {
                             reference inserts keys (binning.c:1045-1057), needed
                             to rebuild its exact zhash layout */
 #define KB_ENGINE_TABLE 2  /* force the global-table engine                      */
-#define KB_ENGINE_BINNED 4 /* prefer the binned engine; it applies to K <= 31
-                              reads binned in this context without
-                              KB_TRACK_FIRST, else the table engine runs.
-                              Neither flag: KB_ENGINE=table|binned from the
-                              environment, else the table engine.  Results are
-                              identical either way. */
+#define KB_ENGINE_BINNED 4 /* force the binned engine where it applies (the
+                              default): K <= 31 reads binned in this context,
+                              no KB_TRACK_FIRST.  Elsewhere the table engine
+                              runs.  Neither flag: KB_ENGINE=table|binned from
+                              the environment (A/B runs), else binned.
+                              Results are identical either way. */
 
 /* kb_timing.engine */
 #define KB_ENG_TABLE 1   /* scan + global find-or-insert + sort by slot + runs  */

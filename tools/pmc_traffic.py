@@ -18,8 +18,10 @@ import sys
 
 def per_kernel(d):
     agg = collections.defaultdict(list)
-    for r in csv.DictReader(open(pathlib.Path(d) / "run_counter_collection.csv")):
-        agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+    files = sorted(pathlib.Path(d).rglob("*counter_collection.csv"))
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
@@ -28,7 +30,7 @@ def main():
     f, w = per_kernel(fetch), per_kernel(write)
     table = {k: {"fetch_kib": round(f.get(k, 0.0), 1), "write_kib": round(w.get(k, 0.0), 1),
                  "bytes": round((f.get(k, 0.0) + w.get(k, 0.0)) * 1024)} for k in sorted(set(f) | set(w))}
-    scan = [k for k in table if "scan_insert_kernel" in k]
+    scan = [k for k in table if "bin_kernel" in k] or [k for k in table if "scan_insert_kernel" in k]
     p = pathlib.Path(out)
     doc = json.loads(p.read_text()) if p.exists() else {}
     doc[tag] = {"hbm_bytes_per_launch": table[scan[0]]["bytes"] if scan else None,
