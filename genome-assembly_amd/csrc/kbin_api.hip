@@ -96,6 +96,11 @@ struct kb_ctx {
     std::vector<Batch> batches;
     uint64_t n_reads = 0, n_occ = 0;
     uint32_t route_G = 0;  // destinations of the last kb_route_plan
+    bool route_binned = false;  // the plan came from the super-k-mer record pass
+    uint64_t route_R = 0;
+    bool route_affine = false;
+    int64_t route_id_c = 0;
+    DevBuf<unsigned long long> rcount;  // records per destination
 
     // staging for host submissions
     char* h_stage = nullptr;
@@ -220,7 +225,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->kbase.release(); c->stage.release(); c->border.release(); c->kpart.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->kbase.release(); c->stage.release(); c->border.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
@@ -396,6 +401,108 @@ extern "C" int kb_get_timing(kb_ctx* c, kb_timing* out) {
 // words per routed super-k-mer record: header + span of n + K - 1 <= 2K - M bases
 static int rec_words(const kb_ctx* c) { return 1 + (2 * c->p.K - c->p.M + 31) / 32; }
 
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
+// the binned engine (kbin_bins.hip) serves K <= 31 without first-occurrence
+// tracking unless the table engine is forced (flag, or KB_ENGINE=table)
+static bool binned_applies(const kb_ctx* c) {
+    if (c->KW != 1 || (c->p.flags & KB_TRACK_FIRST)) return false;
+    if (c->p.flags & KB_ENGINE_BINNED) return true;
+    if (c->p.flags & KB_ENGINE_TABLE) return false;
+    const char* e = getenv("KB_ENGINE");
+    return !(e && strcmp(e, "table") == 0);
+}
+
+// ordinal -> read id over the unrouted read batches: one affine map (id =
+// ordinal + id_c) when every batch has affine ids that agree, else read_ids
+static int read_id_map(kb_ctx* c, bool& affine, int64_t& id_c) {
+    affine = true;
+    id_c = 0;
+    bool first_b = true;
+    for (auto& b : c->batches) {
+        if (b.routed || b.superkmers) continue;
+        const int64_t cb = b.first_id - (int64_t)b.ord_base;
+        if (!b.affine || (!first_b && cb != id_c)) affine = false;
+        id_c = cb;
+        first_b = false;
+    }
+    if (affine) return KB_OK;
+    HIPCHK(c->read_ids.ensure(std::max<uint64_t>(c->n_reads, 1)));
+    for (auto& b : c->batches) {
+        if (b.routed || b.superkmers || !b.n_reads) continue;
+        if (b.ids)
+            HIPCHK(hipMemcpyAsync(c->read_ids.p + b.ord_base, b.ids, b.n_reads * sizeof(int32_t),
+                                  hipMemcpyDeviceToDevice, c->s));
+        else
+            HIPCHK(launch_fill_ids(c->read_ids.p + b.ord_base, b.n_reads, (int32_t)b.first_id, c->s));
+    }
+    return KB_OK;
+}
+
+static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N);
+
+// routing through the binned engine's record pass: records in read order,
+// destination = owner(mmer); counts now, a stable sort by destination and
+// the pack in kb_route_pack (same record format and order as route_kernel)
+static int route_plan_binned(kb_ctx* c, uint32_t G, uint64_t* h_counts) {
+    HIPCHK(c->totals.ensure(16));
+    uint64_t R = 0, N = 0;
+    int rc = binned_read_records(c, R, N);
+    if (rc) return rc;
+    rc = read_id_map(c, c->route_affine, c->route_id_c);
+    if (rc) return rc;
+    HIPCHK(c->rcount.ensure(64));
+    HIPCHK(hipMemsetAsync(c->rcount.p, 0, 64 * sizeof(unsigned long long), c->s));
+    HIPCHK(launch_route_dest(c->occ_a.p, R, G, c->occ_b.p, c->rcount.p, c->s));
+    std::vector<unsigned long long> cnt(G);
+    HIPCHK(hipMemcpyAsync(cnt.data(), c->rcount.p, G * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    uint64_t tot = 0;
+    for (uint32_t d = 0; d < G; d++) {
+        h_counts[d] = cnt[d];
+        tot += h_counts[d];
+    }
+    if (tot != R) return fail(KB_EDEVICE, "internal: routed %llu of %llu records", (unsigned long long)tot,
+                              (unsigned long long)R);
+    if (R > 0xFFFFFFFFull) return fail(KB_EOVERFLOW, "more than 2^32 routed records");
+    c->route_binned = true;
+    c->route_R = R;
+    c->route_G = G;
+    return KB_OK;
+}
+
+static int route_pack_binned(kb_ctx* c, uint64_t* d_send) {
+    const uint64_t R = c->route_R;
+    if (R && !d_send) return fail(KB_EINVAL, "null send buffer");
+    int bits = 1;
+    while ((1u << bits) < c->route_G) bits++;
+    const uint64_t nflags = onesweep_flag_elems(R);
+    if (c->os_flags.cap < nflags || c->os_epoch > (1u << 24) - 8) {
+        HIPCHK(c->os_flags.ensure(nflags));
+        HIPCHK(hipMemsetAsync(c->os_flags.p, 0, c->os_flags.cap * sizeof(uint64_t), c->s));
+        c->os_epoch = 0;
+    }
+    HIPCHK(c->os_aux.ensure(4 * 256 + 8));
+    uint64_t* sorted = nullptr;
+    HIPCHK(launch_onesweep(c->occ_b.p, c->occ_a.p, R, bits, c->os_flags.p, c->os_aux.p, &c->os_epoch,
+                           &sorted, c->s));
+    HIPCHK(launch_route_pack_binned(sorted, c->pay.p, R, rec_words(c),
+                                    c->route_affine ? nullptr : c->read_ids.p,
+                                    (uint32_t)(c->route_affine ? c->route_id_c : 0), d_send, c->s));
+    if (R) HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    else c->h_misc[8] = 0;
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (c->h_misc[8]) return fail(KB_EDEVICE, "radix look-back timed out (device error word %u)", c->h_misc[8]);
+    for (auto& b : c->batches)
+        if (!b.superkmers) b.routed = true;
+    c->route_G = 0;
+    c->route_binned = false;
+    return KB_OK;
+}
+
 extern "C" int kb_record_words(kb_ctx* c, uint32_t* out) {
     if (!c || !out) return fail(KB_EINVAL, "null argument");
     *out = (uint32_t)rec_words(c);
@@ -408,6 +515,8 @@ extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
     if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
     int rc = set_device(c);
     if (rc) return rc;
+    if (binned_applies(c)) return route_plan_binned(c, n_dest, h_counts);
+    c->route_binned = false;
     std::vector<uint64_t> tot(n_dest, 0);
     for (auto& b : c->batches) {
         if (b.superkmers || b.routed) continue;
@@ -457,6 +566,7 @@ extern "C" int kb_route_pack(kb_ctx* c, uint64_t* d_send) {
     if (!c->route_G) return fail(KB_ESTATE, "kb_route_pack before kb_route_plan");
     int rc = set_device(c);
     if (rc) return rc;
+    if (c->route_binned) return route_pack_binned(c, d_send);
     const uint32_t G = c->route_G;
     // destination d's records start at sum_{d'<d} total(d'); inside it, batches in order
     std::vector<uint64_t> dest_base(G, 0), seen(G, 0);
@@ -545,30 +655,24 @@ static int log2u(uint64_t x) {
 // table per bin.  Eligible for K <= 31 reads binned here, no first-occurrence
 // tracking.
 // ---------------------------------------------------------------------------
-static int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
-}
 
-static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c) {
+// ---- phase A (reads): one record per super-k-mer of every unrouted read
+// batch -- pay[3t..3t+2] and keys[t] in occ_a, t in read order; returns the
+// record count R and the k-mer count N (one host sync)
+static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N) {
     const int M = c->p.M;
     const uint64_t nr = c->n_reads;
-    c->tm.engine = KB_ENG_BINNED;
-    REC(0);
     HIPCHK(c->seg.ensure(nr + 1));
+    HIPCHK(hipMemsetAsync(c->seg.p, 0, (nr + 1) * sizeof(uint32_t), c->s));
     HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(nr + 1), c->scratch.cap)));
-    HIPCHK(c->totals.ensure(16));
-    HIPCHK(hipMemsetAsync(c->totals.p, 0, 16 * sizeof(uint64_t), c->s));
-    HIPCHK(hipMemsetAsync(c->misc.p, 0, 2 * sizeof(uint32_t), c->s));
-    REC(1);
-    // ---- phase A: super-k-mers per read, scan, records
-    c->tm.scan_insert_launches = 0;
+    HIPCHK(hipMemsetAsync(c->totals.p + 8, 0, sizeof(uint64_t), c->s));
     {
         uint64_t kp = 1;
         for (auto& b : c->batches) kp = std::max(kp, sk_blocks(b.n_reads, b.RW));
         HIPCHK(c->kpart.ensure(kp));
     }
     for (auto& b : c->batches) {
+        if (b.routed || b.superkmers) continue;
         SkScanArgs a{};
         a.words = b.words;
         a.lens = b.lens;
@@ -588,9 +692,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c) {
     HIPCHK(hipMemcpyAsync(c->h_totals + 7, c->scratch.p + nbs, 8, hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, 8, hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync: R and N size the rest
-    const uint64_t R = nr ? c->h_totals[7] : 0;
-    const uint64_t N = nr ? c->h_totals[8] : 0;
-    c->n_occ = N;
+    R = nr ? c->h_totals[7] : 0;
+    N = nr ? c->h_totals[8] : 0;
     if (N >= 0xFFFFFFFFull)
         return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
                     (unsigned long long)N);
@@ -601,6 +704,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c) {
     HIPCHK(c->occ_a.ensure(std::max<uint64_t>(R, N / 2 + 4)));
     HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4))  /* ids (u32) + 16-B over-read */);
     for (auto& b : c->batches) {
+        if (b.routed || b.superkmers) continue;
         SkScanArgs a{};
         a.words = b.words;
         a.lens = b.lens;
@@ -615,6 +719,51 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c) {
         HIPCHK(launch_sk(a, true, c->s));
         c->tm.scan_insert_launches++;
     }
+    return KB_OK;
+}
+
+// ---- phase A (received): the routed super-k-mer records of every
+// kb_submit_superkmers_device batch, converted in place of phase A; the
+// record's read id is its ordinal (ids increase with the global call order)
+static int binned_sk_records(kb_ctx* c, uint64_t& R, uint64_t& N) {
+    R = 0;
+    N = 0;
+    for (auto& b : c->batches)
+        if (b.superkmers) {
+            R += b.n_reads;
+            N += b.n_occ;
+        }
+    if (N >= 0xFFFFFFFFull)
+        return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
+                    (unsigned long long)N);
+    HIPCHK(c->pay.ensure(3 * R));
+    HIPCHK(c->srec.ensure(3 * R));
+    HIPCHK(c->occ_a.ensure(std::max<uint64_t>(R, N / 2 + 4)));
+    HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));
+    uint64_t off = 0;
+    for (auto& b : c->batches) {
+        if (!b.superkmers) continue;
+        HIPCHK(launch_sk_convert(b.recs, b.n_reads, rec_words(c), off, c->p.M, c->pay.p, c->occ_a.p,
+                                 c->misc.p, c->s));
+        off += b.n_reads;
+        c->tm.scan_insert_launches++;
+    }
+    return KB_OK;
+}
+
+static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool received) {
+    const int M = c->p.M;
+    c->tm.engine = KB_ENG_BINNED;
+    REC(0);
+    HIPCHK(c->totals.ensure(16));
+    HIPCHK(hipMemsetAsync(c->totals.p, 0, 16 * sizeof(uint64_t), c->s));
+    HIPCHK(hipMemsetAsync(c->misc.p, 0, 2 * sizeof(uint32_t), c->s));
+    REC(1);
+    c->tm.scan_insert_launches = 0;
+    uint64_t R = 0, N = 0;
+    int rc = received ? binned_sk_records(c, R, N) : binned_read_records(c, R, N);
+    if (rc) return rc;
+    c->n_occ = N;
     REC(2);
     // ---- stable sort of the records by canonical mmer, bin boundaries
     const int key_bits = 2 * M + 6;  // (mmer, 63 - n)
@@ -711,6 +860,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c) {
     if (c->h_totals[3]) return fail(KB_EDEVICE, "internal: %llu bins > %llu", (unsigned long long)c->h_totals[3],
                                     (unsigned long long)max_bins);
     if (c->h_misc[0] & ST_TABLE_FULL) return fail(KB_EDEVICE, "internal: CSR capacity exceeded");
+    if (c->h_misc[0] & ST_NEG_ID)
+        return fail(KB_EINVAL, "routed read ids must be non-negative (they order the id lists)");
     if (c->h_misc[0] & ST_PROBE_LIMIT) return fail(KB_ENOMEM, "a bin exceeded the partition depth");
     c->n_entries = c->h_totals[0];
     c->n_ids = c->h_totals[1];
@@ -748,39 +899,18 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     memset(&c->tm, 0, sizeof(c->tm));
     const int SW = c->KW == 1 ? 2 : 4;
     const bool track_first = (c->p.flags & KB_TRACK_FIRST) != 0;
-    bool any_routed = false;
-    for (auto& b : c->batches) any_routed |= b.routed;
-    // ordinal -> read id: one affine map for the context, else an array
-    bool affine = !any_sk;
+    bool affine = false;
     int64_t id_c = 0;
-    {
-        bool first_b = true;
-        for (auto& b : c->batches) {
-            if (b.routed || b.superkmers) continue;
-            const int64_t cb = b.first_id - (int64_t)b.ord_base;
-            if (!b.affine || (!first_b && cb != id_c)) affine = false;
-            id_c = cb;
-            first_b = false;
-        }
+    if (any_sk) {
+        affine = false;
+    } else {
+        rc = read_id_map(c, affine, id_c);
+        if (rc) return rc;
     }
-    if (!affine && !any_sk) {
-        HIPCHK(c->read_ids.ensure(c->n_reads));
-        for (auto& b : c->batches) {
-            if (b.superkmers || !b.n_reads) continue;
-            if (b.ids)
-                HIPCHK(hipMemcpyAsync(c->read_ids.p + b.ord_base, b.ids, b.n_reads * sizeof(int32_t),
-                                      hipMemcpyDeviceToDevice, c->s));
-            else
-                HIPCHK(launch_fill_ids(c->read_ids.p + b.ord_base, b.n_reads, (int32_t)b.first_id, c->s));
-        }
+    if (binned_applies(c)) {
+        if (any_sk) return finalize_binned(c, prune, true, 0, true);  // ordinal = read id
+        return finalize_binned(c, prune, affine, id_c, false);
     }
-    // engine choice: flags, then KB_ENGINE=table|binned (A/B runs), then the default
-    bool binned = true;
-    if (c->p.flags & KB_ENGINE_BINNED) binned = true;
-    else if (c->p.flags & KB_ENGINE_TABLE) binned = false;
-    else if (const char* e = getenv("KB_ENGINE")) binned = strcmp(e, "table") != 0;
-    if (binned && c->KW == 1 && !track_first && !any_sk && !any_routed)
-        return finalize_binned(c, prune, affine, id_c);
     c->tm.engine = KB_ENG_TABLE;
     // per-read occurrence offsets (the table engine's record slots)
     uint64_t N = 0;

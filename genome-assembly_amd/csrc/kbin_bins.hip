@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
                     const int n = min(sig, nK - 1) - lo + 1;
                     const uint32_t sm = (uint32_t)(window64(sw, sig) >> (64 - 2 * M));
                     const uint64_t rev = sm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
-                    A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44);
+                    A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44) |
+                                       ((uint64_t)lo << 45);
                     A.pay[3 * t + 1] = window64(sw, lo);
                     A.pay[3 * t + 2] = window64(sw, lo + 32);
                     A.keys[t] = ((uint64_t)canon << 38) | ((uint64_t)(63 - n) << 32) | (uint32_t)t;
@@ -157,7 +158,8 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                 const int n = min(sig, nK - 1) - lo + 1;
                 const uint32_t sm = (uint32_t)(window64(sw, sig) >> sh);
                 const uint64_t rev = sm < halfM ? 1ull : 0ull;
-                A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44);
+                A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44) |
+                                   ((uint64_t)lo << 45);
                 A.pay[3 * t + 1] = window64(sw, lo);
                 A.pay[3 * t + 2] = window64(sw, lo + 32);
                 A.keys[t] = ((uint64_t)(uint32_t)best << 38) | ((uint64_t)(63 - n) << 32) | (uint32_t)t;
@@ -237,6 +239,106 @@ hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t 
 }
 
 // ---------------------------------------------------------------------------
+// routing (one process per GPU): the sender's records go to
+// owner(mmer) in the routed record format of route_kernel (kbin_kernels.hip)
+// -- header {id | i0 << 32 | n << 48 | sig_off << 54}, then the span words --
+// destination-major, read order within a destination; the receiver turns
+// them back into binned records.
+// ---------------------------------------------------------------------------
+// map a call ordinal to the caller's read id
+DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
+    return read_ids ? read_ids[ord] : (int32_t)(ord + id_off);
+}
+
+DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) {  // = owner_of() in kbin_kernels.hip
+    return (uint32_t)((mix64((uint64_t)mmer + 0x5851F42D4C957F2Dull) >> 32) % G);
+}
+
+__global__ __launch_bounds__(256) void route_dest_kernel(const uint64_t* __restrict__ keys, uint64_t R,
+                                                         uint32_t G, uint64_t* __restrict__ dkeys,
+                                                         unsigned long long* __restrict__ counts) {
+    __shared__ uint32_t hist[64];
+    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < R; t += (uint64_t)gridDim.x * 256) {
+        const uint32_t d = owner_of_mmer((uint32_t)(keys[t] >> 38), G);
+        dkeys[t] = ((uint64_t)d << 32) | (uint32_t)t;
+        atomicAdd(&hist[d], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < G && hist[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)hist[threadIdx.x]);
+}
+
+hipError_t launch_route_dest(const uint64_t* keys, uint64_t R, uint32_t G, uint64_t* dkeys,
+                             unsigned long long* counts, hipStream_t s) {
+    if (!R) return hipSuccess;
+    if (G < 1 || G > 64) return hipErrorInvalidValue;
+    const uint64_t blocks = std::min<uint64_t>((R + 255) / 256, 2048);
+    hipLaunchKernelGGL(route_dest_kernel, dim3((unsigned)blocks), dim3(256), 0, s, keys, R, G, dkeys, counts);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void route_pack_binned_kernel(const uint64_t* __restrict__ sorted,
+                                                                const uint64_t* __restrict__ pay, uint64_t R,
+                                                                int rw, const int32_t* __restrict__ read_ids,
+                                                                uint32_t id_off, uint64_t* __restrict__ out) {
+    for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < R; k += (uint64_t)gridDim.x * 256) {
+        const uint64_t t = (uint32_t)sorted[k];
+        const uint64_t hd = pay[3 * t];
+        const uint32_t id = (uint32_t)id_of((uint32_t)hd, read_ids, id_off);
+        const uint64_t n = (hd >> 32) & 63u, so = (hd >> 38) & 63u, lo = (hd >> 45) & 0xFFFFu;
+        uint64_t* o = out + k * (uint64_t)rw;
+        o[0] = (uint64_t)id | (lo << 32) | (n << 48) | (so << 54);
+        o[1] = pay[3 * t + 1];
+        if (rw >= 3) o[2] = pay[3 * t + 2];
+        for (int w = 3; w < rw; w++) o[w] = 0;  // (K <= 31 spans fit two words)
+    }
+}
+
+hipError_t launch_route_pack_binned(const uint64_t* sorted, const uint64_t* pay, uint64_t R, int rw,
+                                    const int32_t* read_ids, uint32_t id_off, uint64_t* out,
+                                    hipStream_t s) {
+    if (!R) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((R + 255) / 256, 8192);
+    hipLaunchKernelGGL(route_pack_binned_kernel, dim3((unsigned)blocks), dim3(256), 0, s, sorted, pay, R, rw,
+                       read_ids, id_off, out);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void sk_convert_kernel(const uint64_t* __restrict__ recs, uint64_t n_rec,
+                                                         int rw, uint64_t off, int M, uint64_t* __restrict__ pay,
+                                                         uint64_t* __restrict__ keys, uint32_t* status) {
+    const uint32_t maskM = (1u << (2 * M)) - 1u, halfM = 1u << (2 * M - 1);
+    bool neg = false;
+    for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < n_rec; k += (uint64_t)gridDim.x * 256) {
+        const uint64_t* r = recs + k * (uint64_t)rw;
+        const uint64_t h = r[0];
+        const uint64_t w0 = r[1], w1 = rw >= 3 ? r[2] : 0ull;
+        const uint32_t id = (uint32_t)h;
+        const uint64_t lo = (h >> 32) & 0xFFFFu, n = (h >> 48) & 63u, so = (h >> 54) & 63u;
+        const uint32_t sm = (uint32_t)(span_window(w0, w1, 0ull, 0ull, (int)so) >> (64 - 2 * M));
+        const bool rev = sm < halfM;  // complement wins (binning.c:1029-1040)
+        const uint32_t canon = rev ? maskM - sm : sm;
+        neg |= (int32_t)id < 0;
+        const uint64_t t = off + k;
+        pay[3 * t + 0] = (uint64_t)id | (n << 32) | (so << 38) | ((uint64_t)rev << 44) | (lo << 45);
+        pay[3 * t + 1] = w0;
+        pay[3 * t + 2] = w1;
+        keys[t] = ((uint64_t)canon << 38) | ((63ull - n) << 32) | (uint32_t)t;
+    }
+    if (neg) atomicOr(status, ST_NEG_ID);
+}
+
+hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint64_t off, int M,
+                             uint64_t* pay, uint64_t* keys, uint32_t* status, hipStream_t s) {
+    if (!n_rec) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((n_rec + 255) / 256, 8192);
+    hipLaunchKernelGGL(sk_convert_kernel, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, off, M, pay,
+                       keys, status);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // phase B: one workgroup per mmer bin
 // ---------------------------------------------------------------------------
 #ifdef KB_BIN_PROF
@@ -294,10 +396,6 @@ DEV int lds_find(const uint64_t* claim, uint32_t mask, uint64_t key, uint32_t h)
     return -1;
 }
 
-// map a call ordinal to the caller's read id
-DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
-    return read_ids ? read_ids[ord] : (int32_t)(ord + id_off);
-}
 
 struct alignas(16) BinShared {
     uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, pad0;

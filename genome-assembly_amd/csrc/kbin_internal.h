@@ -20,6 +20,7 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t ST_TABLE_FULL = 1u;   // distinct keys exceeded the load limit
 constexpr uint32_t ST_PROBE_LIMIT = 2u;  // a probe sequence exceeded max_probe
 constexpr uint32_t ST_ALPHABET = 4u;     // byte outside ACGT in packed input
+constexpr uint32_t ST_NEG_ID = 8u;       // a routed read id < 0 (the binned receiver orders lists by id)
 
 struct ScanArgs {
     const uint64_t* words;     // packed reads, RW words per read
@@ -131,6 +132,17 @@ struct ListArgs {
 
 hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s);
 hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s);
+// received routed records (rw words: {id | i0 << 32 | n << 48 | sig_off << 54}, span words)
+// -> binned records at t = off + k; ids < 0 set ST_NEG_ID in *status
+hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint64_t off, int M,
+                             uint64_t* pay, uint64_t* keys, uint32_t* status, hipStream_t s);
+// sender: destination of every record (owner of its mmer) -> dkeys = dest << 32 | t, counts[dest]
+hipError_t launch_route_dest(const uint64_t* keys, uint64_t R, uint32_t G, uint64_t* dkeys,
+                             unsigned long long* counts, hipStream_t s);
+// sender: records in destination-sorted order -> routed record format
+hipError_t launch_route_pack_binned(const uint64_t* sorted, const uint64_t* pay, uint64_t R, int rw,
+                                    const int32_t* read_ids, uint32_t id_off, uint64_t* out,
+                                    hipStream_t s);
 uint64_t sk_blocks(uint64_t n_reads, int RW);
 hipError_t launch_sk_kmers_total(const unsigned long long* part, uint64_t n, unsigned long long* out,
                                  hipStream_t s);

@@ -32,3 +32,11 @@ def golden_dir():
 def digests():
     import json
     return json.loads((GOLDEN / "digests.json").read_text())
+
+
+@pytest.fixture(params=["table", "binned"])
+def engine(request, monkeypatch):
+    """KB_ENGINE for the case: the binned engine applies to K <= 31 without
+    first-occurrence tracking (elsewhere the table engine runs either way)"""
+    monkeypatch.setenv("KB_ENGINE", request.param)
+    return request.param

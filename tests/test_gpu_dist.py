@@ -12,7 +12,8 @@ import oracle
 import skmer_ref
 from conftest import GOLDEN
 
-pytestmark = pytest.mark.gpu
+# every case runs on both engines (conftest.engine), senders and receivers alike
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("engine")]
 
 
 def _reads(n=700, rl=102):

@@ -10,16 +10,8 @@ import pytest
 import kbin
 import oracle
 
-pytestmark = pytest.mark.gpu
-
-
-@pytest.fixture(params=["table", "binned"], autouse=True)
-def engine(request, monkeypatch):
-    """every parity case runs on both engines (KB_ENGINE; the binned engine
-    applies to K <= 31 without first-occurrence tracking, else the table
-    engine runs -- test_binned_engine_selected checks which ran)"""
-    monkeypatch.setenv("KB_ENGINE", request.param)
-    return request.param
+# every case runs on both engines (conftest.engine)
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("engine")]
 
 
 def gpu_result(bases, lens, K, M, cutoff=1, prune=True, ids=None, batches=1, max_read_len=1024):
