@@ -107,19 +107,25 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
 // stages 256 reads in LDS rows and each lane walks its own read's sticky
 // chain serially.  The wave-per-read kernel above keeps 64 lanes busy on a
 // window of only K-M+1 positions; one lane per read does the same argmax
-// with no cross-lane reduction and no idle lanes.
+// with no cross-lane reduction and no idle lanes.  The window of mmer scores
+// is walked with a 2-bit shift per position (two LDS reads per segment).
+// The write pass stages each record as one u64 in LDS and the block then
+// writes its (contiguous) record range with coalesced stores.
 constexpr int SK_THREAD_RW = 16;
+constexpr uint32_t SK_STAGE = 4096;  // staged records per block (8 B each)
 
 template <bool WRITE>
 __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const int RW = A.RW, K = A.K, M = A.M;
-    const int W = K - M + 1;
-    const int RS = RW + 2;  // row stride: two zero words past the read
+    const int W = K - M + 1;  // <= 31 (K <= 31): one 64-base window pair covers it
+    const int RS = RW + 2;    // row stride: two zero words past the read
     const int sh = 64 - 2 * M;
     const uint32_t maskM = (1u << (2 * M)) - 1u;
     const uint32_t halfM = 1u << (2 * M - 1);
     const uint32_t tid = threadIdx.x;
+    uint64_t* stg = smem + 256 * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
+    __shared__ uint32_t span_end;
     uint64_t kmers = 0;
     for (uint64_t r0 = (uint64_t)blockIdx.x * 256; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * 256) {
         const uint32_t nrows = (uint32_t)min<uint64_t>(256, A.n_reads - r0);
@@ -132,46 +138,76 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
             smem[tid * RS + RW] = 0;
             smem[tid * RS + RW + 1] = 0;
         }
+        if (tid == 0) span_end = 0;
         __syncthreads();
-        if (tid >= nrows) continue;
-        const uint64_t r = r0 + tid;
-        const uint64_t* sw = smem + tid * RS;
-        const int nK = (int)A.lens[r] - K + 1;
-        if (nK > 0) kmers += (uint64_t)nK;
-        uint32_t nseg = 0;
-        const uint64_t rbase = WRITE ? A.rec_base[r] : 0;
-        const uint64_t ordv = (uint64_t)(A.ord_base + (uint32_t)r);
-        int lo = 0;
-        while (lo < nK) {
-            // leftmost strict argmax of the canonical score over the window
-            int best = -1, sig = lo;
-            for (int p = lo; p < lo + W; p++) {
-                const uint32_t sm = (uint32_t)(window64(sw, p) >> sh);
-                const int c = (int)(sm >= halfM ? sm : maskM - sm);
-                if (c > best) {
-                    best = c;
-                    sig = p;
+        const uint64_t bfirst = WRITE ? A.rec_base[r0] : 0;
+        if (tid < nrows) {
+            const uint64_t r = r0 + tid;
+            const uint64_t* sw = smem + tid * RS;
+            const int nK = (int)A.lens[r] - K + 1;
+            if (nK > 0) kmers += (uint64_t)nK;
+            uint32_t nseg = 0;
+            const uint64_t rbase = WRITE ? A.rec_base[r] : 0;
+            int lo = 0;
+            while (lo < nK) {
+                // leftmost strict argmax of the canonical score over the window
+                uint64_t x = window64(sw, lo), y = window64(sw, lo + 32);
+                int best = -1, sig = lo;
+                uint32_t bsm = 0;
+                for (int p = lo; p < lo + W; p++) {
+                    const uint32_t sm = (uint32_t)(x >> sh);
+                    const int c = (int)(sm >= halfM ? sm : maskM - sm);
+                    if (c > best) {
+                        best = c;
+                        sig = p;
+                        bsm = sm;
+                    }
+                    x = (x << 2) | (y >> 62);
+                    y <<= 2;
                 }
+                if (WRITE) {
+                    const uint64_t n = (uint64_t)(min(sig, nK - 1) - lo + 1);
+                    const uint64_t rev = bsm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
+                    const uint64_t e = (uint64_t)lo | (n << 16) | ((uint64_t)(sig - lo) << 22) | (rev << 28) |
+                                       ((uint64_t)tid << 29) | ((uint64_t)(uint32_t)best << 37);
+                    const uint64_t loc = rbase + nseg - bfirst;
+                    if (loc < SK_STAGE) {
+                        stg[loc] = e;
+                    } else {  // beyond the staging area: direct (scattered) stores
+                        const uint64_t t = rbase + nseg;
+                        A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)r) | (n << 32) |
+                                           ((uint64_t)(sig - lo) << 38) | (rev << 44) | ((uint64_t)lo << 45);
+                        A.pay[3 * t + 1] = window64(sw, lo);
+                        A.pay[3 * t + 2] = window64(sw, lo + 32);
+                        A.keys[t] = ((uint64_t)(uint32_t)best << 38) | ((63ull - n) << 32) | (uint32_t)t;
+                    }
+                }
+                nseg++;
+                lo = sig + 1;
             }
-            if (WRITE) {
-                const uint64_t t = rbase + nseg;
-                const int n = min(sig, nK - 1) - lo + 1;
-                const uint32_t sm = (uint32_t)(window64(sw, sig) >> sh);
-                const uint64_t rev = sm < halfM ? 1ull : 0ull;
-                A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44) |
-                                   ((uint64_t)lo << 45);
-                A.pay[3 * t + 1] = window64(sw, lo);
-                A.pay[3 * t + 2] = window64(sw, lo + 32);
-                A.keys[t] = ((uint64_t)(uint32_t)best << 38) | ((uint64_t)(63 - n) << 32) | (uint32_t)t;
-            }
-            nseg++;
-            lo = sig + 1;
+            if (!WRITE) A.seg_count[r] = nseg;
+            if (WRITE && nseg) atomicMax(&span_end, (uint32_t)min<uint64_t>(rbase + nseg - bfirst, SK_STAGE));
         }
-        if (!WRITE) A.seg_count[r] = nseg;
+        if (WRITE) {
+            __syncthreads();
+            const uint32_t span = span_end;
+            for (uint32_t i = tid; i < span; i += 256) {
+                const uint64_t e = stg[i];
+                const uint32_t lo = (uint32_t)(e & 0xFFFFu), row = (uint32_t)((e >> 29) & 0xFFu);
+                const uint64_t n = (e >> 16) & 63u, so = (e >> 22) & 63u, rev = (e >> 28) & 1u;
+                const uint64_t* sw = smem + row * RS;
+                const uint64_t t = bfirst + i;
+                A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)(r0 + row)) | (n << 32) | (so << 38) |
+                                   (rev << 44) | ((uint64_t)lo << 45);
+                A.pay[3 * t + 1] = window64(sw, (int)lo);
+                A.pay[3 * t + 2] = window64(sw, (int)lo + 32);
+                A.keys[t] = ((e >> 37) << 38) | ((63ull - n) << 32) | (uint32_t)t;
+            }
+        }
     }
     if (!WRITE) {  // per-block partial sum (summed by sk_kmers_total_kernel)
-        __shared__ uint64_t sh[4];
-        const uint64_t tot = block_sum256(kmers, sh);
+        __shared__ uint64_t shs[4];
+        const uint64_t tot = block_sum256(kmers, shs);
         if (tid == 0) A.n_kmers[blockIdx.x] = tot;
     }
 }
@@ -201,7 +237,7 @@ hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s) {
     if (!a.n_reads) return hipSuccess;
     const uint64_t blocks = sk_blocks(a.n_reads, a.RW);
     if (a.RW <= SK_THREAD_RW) {
-        const size_t lds = (size_t)256 * (a.RW + 2) * sizeof(uint64_t);
+        const size_t lds = (size_t)256 * (a.RW + 2) * sizeof(uint64_t) + (write ? SK_STAGE * sizeof(uint64_t) : 0);
         if (write)
             hipLaunchKernelGGL(sk_thread_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);
         else
