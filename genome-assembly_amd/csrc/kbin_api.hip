@@ -442,7 +442,7 @@ static int read_id_map(kb_ctx* c, bool& affine, int64_t& id_c) {
     return KB_OK;
 }
 
-static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N);
+static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered);
 
 // routing through the binned engine's record pass: records in read order,
 // destination = owner(mmer); counts now, a stable sort by destination and
@@ -450,7 +450,7 @@ static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N);
 static int route_plan_binned(kb_ctx* c, uint32_t G, uint64_t* h_counts) {
     HIPCHK(c->totals.ensure(16));
     uint64_t R = 0, N = 0;
-    int rc = binned_read_records(c, R, N);
+    int rc = binned_read_records(c, R, N, true);  // routed records keep read order
     if (rc) return rc;
     rc = read_id_map(c, c->route_affine, c->route_id_c);
     if (rc) return rc;
@@ -659,9 +659,56 @@ static int log2u(uint64_t x) {
 // ---- phase A (reads): one record per super-k-mer of every unrouted read
 // batch -- pay[3t..3t+2] and keys[t] in occ_a, t in read order; returns the
 // record count R and the k-mer count N (one host sync)
-static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N) {
+static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered) {
     const int M = c->p.M;
     const uint64_t nr = c->n_reads;
+    // one pass (records allocated per block, any order) when every batch takes
+    // the thread-per-read kernel and the buffers sized by the k-mer bound fit
+    uint64_t nb = 0;
+    bool one_pass = !ordered;
+    for (auto& b : c->batches) {
+        if (b.routed || b.superkmers) continue;
+        if (b.RW > 16) one_pass = false;
+        nb += b.n_reads * (uint64_t)std::max(0, b.RW * 32 - c->p.K + 1);
+    }
+    if (one_pass && nb < 0xFFFFFFFFull && nb * 40 <= (32ull << 30)) {
+        HIPCHK(c->pay.ensure(3 * nb + 3));
+        HIPCHK(c->occ_a.ensure(nb + 4));
+        HIPCHK(c->occ_b.ensure(nb + 4));  // radix ping-pong (R <= nb) and ids by ordinal
+        HIPCHK(hipMemsetAsync(c->totals.p + 8, 0, 2 * sizeof(uint64_t), c->s));
+        uint64_t kp = 1;
+        for (auto& b : c->batches) kp = std::max(kp, sk_blocks(b.n_reads, b.RW));
+        HIPCHK(c->kpart.ensure(kp));
+        for (auto& b : c->batches) {
+            if (b.routed || b.superkmers) continue;
+            SkScanArgs a{};
+            a.words = b.words;
+            a.lens = b.lens;
+            a.n_reads = b.n_reads;
+            a.rec_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 9);
+            a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p);
+            a.pay = c->pay.p;
+            a.keys = c->occ_a.p;
+            a.ord_base = (uint32_t)b.ord_base;
+            a.RW = b.RW;
+            a.K = c->p.K;
+            a.M = M;
+            HIPCHK(launch_sk(a, true, c->s));
+            HIPCHK(launch_sk_kmers_total(reinterpret_cast<unsigned long long*>(c->kpart.p),
+                                         sk_blocks(b.n_reads, b.RW),
+                                         reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
+            c->tm.scan_insert_launches++;
+        }
+        HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync: R and N size the rest
+        N = c->h_totals[8];
+        R = c->h_totals[9];
+        if (R > N || N > nb)
+            return fail(KB_EDEVICE, "internal: %llu super-k-mers, %llu k-mers, bound %llu", (unsigned long long)R,
+                        (unsigned long long)N, (unsigned long long)nb);
+        HIPCHK(c->srec.ensure(3 * R));
+        return KB_OK;
+    }
     HIPCHK(c->seg.ensure(nr + 1));
     HIPCHK(hipMemsetAsync(c->seg.p, 0, (nr + 1) * sizeof(uint32_t), c->s));
     HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(nr + 1), c->scratch.cap)));
@@ -761,7 +808,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     REC(1);
     c->tm.scan_insert_launches = 0;
     uint64_t R = 0, N = 0;
-    int rc = received ? binned_sk_records(c, R, N) : binned_read_records(c, R, N);
+    int rc = received ? binned_sk_records(c, R, N) : binned_read_records(c, R, N, false);
     if (rc) return rc;
     c->n_occ = N;
     REC(2);

@@ -126,6 +126,8 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     const uint32_t tid = threadIdx.x;
     uint64_t* stg = smem + 256 * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
     __shared__ uint32_t span_end;
+    __shared__ unsigned long long s_base;
+    const bool alloc = WRITE && A.rec_ctr;  // records placed by block allocation, any order
     uint64_t kmers = 0;
     for (uint64_t r0 = (uint64_t)blockIdx.x * 256; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * 256) {
         const uint32_t nrows = (uint32_t)min<uint64_t>(256, A.n_reads - r0);
@@ -140,14 +142,14 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
         }
         if (tid == 0) span_end = 0;
         __syncthreads();
-        const uint64_t bfirst = WRITE ? A.rec_base[r0] : 0;
+        const uint64_t bfirst = WRITE && !alloc ? A.rec_base[r0] : 0;
         if (tid < nrows) {
             const uint64_t r = r0 + tid;
             const uint64_t* sw = smem + tid * RS;
             const int nK = (int)A.lens[r] - K + 1;
             if (nK > 0) kmers += (uint64_t)nK;
             uint32_t nseg = 0;
-            const uint64_t rbase = WRITE ? A.rec_base[r] : 0;
+            const uint64_t rbase = WRITE && !alloc ? A.rec_base[r] : 0;
             int lo = 0;
             while (lo < nK) {
                 // leftmost strict argmax of the canonical score over the window
@@ -170,11 +172,11 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     const uint64_t rev = bsm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
                     const uint64_t e = (uint64_t)lo | (n << 16) | ((uint64_t)(sig - lo) << 22) | (rev << 28) |
                                        ((uint64_t)tid << 29) | ((uint64_t)(uint32_t)best << 37);
-                    const uint64_t loc = rbase + nseg - bfirst;
+                    const uint64_t loc = alloc ? (uint64_t)atomicAdd(&span_end, 1u) : rbase + nseg - bfirst;
                     if (loc < SK_STAGE) {
                         stg[loc] = e;
                     } else {  // beyond the staging area: direct (scattered) stores
-                        const uint64_t t = rbase + nseg;
+                        const uint64_t t = alloc ? (uint64_t)atomicAdd(A.rec_ctr, 1ull) : rbase + nseg;
                         A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)r) | (n << 32) |
                                            ((uint64_t)(sig - lo) << 38) | (rev << 44) | ((uint64_t)lo << 45);
                         A.pay[3 * t + 1] = window64(sw, lo);
@@ -186,17 +188,23 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                 lo = sig + 1;
             }
             if (!WRITE) A.seg_count[r] = nseg;
-            if (WRITE && nseg) atomicMax(&span_end, (uint32_t)min<uint64_t>(rbase + nseg - bfirst, SK_STAGE));
+            if (WRITE && !alloc && nseg)
+                atomicMax(&span_end, (uint32_t)min<uint64_t>(rbase + nseg - bfirst, SK_STAGE));
         }
         if (WRITE) {
             __syncthreads();
-            const uint32_t span = span_end;
+            const uint32_t span = min(span_end, SK_STAGE);
+            if (alloc) {  // the block's staged records get one contiguous range
+                if (tid == 0) s_base = span ? atomicAdd(A.rec_ctr, (unsigned long long)span) : 0ull;
+                __syncthreads();
+            }
+            const uint64_t tbase = alloc ? (uint64_t)s_base : bfirst;
             for (uint32_t i = tid; i < span; i += 256) {
                 const uint64_t e = stg[i];
                 const uint32_t lo = (uint32_t)(e & 0xFFFFu), row = (uint32_t)((e >> 29) & 0xFFu);
                 const uint64_t n = (e >> 16) & 63u, so = (e >> 22) & 63u, rev = (e >> 28) & 1u;
                 const uint64_t* sw = smem + row * RS;
-                const uint64_t t = bfirst + i;
+                const uint64_t t = tbase + i;
                 A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)(r0 + row)) | (n << 32) | (so << 38) |
                                    (rev << 44) | ((uint64_t)lo << 45);
                 A.pay[3 * t + 1] = window64(sw, (int)lo);
@@ -205,7 +213,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
             }
         }
     }
-    if (!WRITE) {  // per-block partial sum (summed by sk_kmers_total_kernel)
+    if (!WRITE || alloc) {  // per-block partial sum (summed by sk_kmers_total_kernel)
         __shared__ uint64_t shs[4];
         const uint64_t tot = block_sum256(kmers, shs);
         if (tid == 0) A.n_kmers[blockIdx.x] = tot;

@@ -82,6 +82,9 @@ struct SkScanArgs {
     uint32_t* seg_count;       // count pass: segments per read
     unsigned long long* n_kmers;  // count pass: [sk_blocks()] per-block k-mer sums
     const uint32_t* rec_base;  // write pass: exclusive scan of seg_count
+    unsigned long long* rec_ctr;  // write pass without count pass (thread kernel): records
+                                  // allocated per block from this counter, any order; the
+                                  // k-mer sums go to n_kmers as in the count pass
     uint64_t* pay;             // [3R] {ord | n << 32 | sig_off << 38 | rev << 44, span w0, w1}
     uint64_t* keys;            // [R] canonical mmer << 38 | (63 - n) << 32 | record index:
                                // bins in mmer order, records of a bin longest first
