@@ -129,7 +129,6 @@ struct kb_ctx {
     DevBuf<uint32_t> seg;      // super-k-mers per read -> exclusive scan
     DevBuf<uint64_t> pay;      // super-k-mer records, call order (3 words each)
     DevBuf<uint64_t> srec;     // the same, bin order, structure of arrays
-    DevBuf<uint32_t> kbase;    // first occurrence index of each bin-ordered record
     DevBuf<uint64_t> stage;    // per-occurrence (slot, ordinal) staging
     DevBuf<uint32_t> border;   // bin processing order
     DevBuf<uint64_t> kpart;    // per-block k-mer sums of the count pass
@@ -225,7 +224,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->kbase.release(); c->stage.release(); c->border.release(); c->kpart.release(); c->rcount.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->border.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
@@ -830,14 +829,12 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     HIPCHK(c->scratch.ensure(std::max(runs_scratch_elems(R, max_bins), c->scratch.cap)));
     HIPCHK(launch_heads(c->sorted, R, c->starts.p, max_bins, c->scratch.p, c->scratch.cap,
                         c->totals.p, c->s, 38));
-    HIPCHK(c->kbase.ensure(R + 1));
+
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
-    HIPCHK(launch_sk_gather(c->sorted, c->pay.p, R, c->srec.p, c->kbase.p, c->s));
-    HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(R + 1), c->scratch.cap)));
-    HIPCHK(launch_scan_u32(c->kbase.p, R, c->scratch.p, c->scratch.cap, c->s));
-    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(c->kbase.p + R), (int)(uint32_t)N, 1, c->s));
+    HIPCHK(launch_sk_gather(c->sorted, c->pay.p, R, c->srec.p, c->s));
+
     HIPCHK(c->border.ensure(max_bins));
-    HIPCHK(launch_bins_order(c->starts.p, c->kbase.p, c->totals.p, c->border.p, c->s));
+    HIPCHK(launch_bins_order(c->starts.p, c->totals.p, c->border.p, c->s));
     REC(3);
     // ---- one workgroup per bin
     const uint64_t ecap = N + 1;
@@ -855,7 +852,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     a.w0 = c->srec.p + R;
     a.w1 = c->srec.p + 2 * R;
     a.bstart = c->starts.p;
-    a.kbase = c->kbase.p;
+    a.stage_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 10);
     a.order = c->border.p;
     a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
     a.stage = c->stage.p;

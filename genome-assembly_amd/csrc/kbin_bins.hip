@@ -263,22 +263,21 @@ hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s) {
 // records into bin order, structure of arrays (the bin kernel streams them)
 __global__ __launch_bounds__(256) void sk_gather_kernel(const uint64_t* __restrict__ keys,
                                                         const uint64_t* __restrict__ pay, uint64_t R,
-                                                        uint64_t* __restrict__ srec, uint32_t* __restrict__ nk) {
+                                                        uint64_t* __restrict__ srec) {
     for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < R; k += (uint64_t)gridDim.x * 256) {
         const uint64_t t = (uint32_t)keys[k];
         const uint64_t hd = pay[3 * t];
         srec[k] = hd;
-        nk[k] = (uint32_t)(hd >> 32) & 63u;
         srec[R + k] = pay[3 * t + 1];
         srec[2 * R + k] = pay[3 * t + 2];
     }
 }
 
 hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
-                            uint32_t* nk, hipStream_t s) {
+                            hipStream_t s) {
     if (!R) return hipSuccess;
     const uint64_t blocks = std::min<uint64_t>((R + 255) / 256, 8192);
-    hipLaunchKernelGGL(sk_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, s, keys, pay, R, srec, nk);
+    hipLaunchKernelGGL(sk_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, s, keys, pay, R, srec);
     return hipGetLastError();
 }
 
@@ -443,7 +442,7 @@ DEV int lds_find(const uint64_t* claim, uint32_t mask, uint64_t key, uint32_t h)
 
 struct alignas(16) BinShared {
     uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, pad0;
-    unsigned long long e0, i0;
+    unsigned long long e0, i0, stage_base, pad1;
     uint32_t stack_p[BIN_STACK], stack_l[BIN_STACK];
     uint64_t red[BIN_THREADS / 64];
 };
@@ -572,13 +571,17 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
         const uint32_t b = A.order[S.item];
         const uint32_t lo = A.bstart[b], hi = A.bstart[b + 1];
         const uint32_t mmer = (uint32_t)(A.keys[lo] >> 38);
-        uint64_t* stage = A.stage + A.kbase[lo];  // the bin's k-mer range, reused per partition
+
         // occurrences of the bin -> first partition depth
         uint64_t occ = 0;
         for (uint32_t rec = lo + tid; rec < hi; rec += BIN_THREADS)
             occ += (A.hdr[rec] >> 32) & 63u;
         uint64_t occ_tot;
         (void)block_excl_scan_u64(occ, S.red, occ_tot);
+        // the bin's stage range (one slot per occurrence, reused per partition)
+        if (tid == 0) S.stage_base = atomicAdd(A.stage_ctr, (unsigned long long)occ_tot);
+        __syncthreads();
+        uint64_t* stage = A.stage + S.stage_base;
         PROF_CNT(11, 1);
         PROF_CNT(14, occ_tot);
         uint32_t l0 = 0;  // uniform: initial partition depth from the expected distinct keys
@@ -1177,20 +1180,18 @@ hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s) 
     return hipGetLastError();
 }
 
-// Bin processing order: descending log2(occurrences) (longest-processing-time
-// first for the persistent blocks).  One block; counting sort over 33 classes.
+// Bin processing order: descending log2(records) (longest-processing-time
+// first for the persistent blocks; a bin's cost follows its super-k-mers).
+// One block; counting sort over 33 classes.
 __global__ __launch_bounds__(1024) void bins_order_kernel(const uint32_t* __restrict__ bstart,
-                                                          const uint32_t* __restrict__ kbase,
                                                           const uint64_t* __restrict__ totals,
                                                           uint32_t* __restrict__ order) {
     __shared__ uint32_t hist[64];
     const uint32_t nbins = (uint32_t)totals[2];
     if (threadIdx.x < 64) hist[threadIdx.x] = 0;
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
-        const uint32_t occ = kbase[bstart[b + 1]] - kbase[bstart[b]];
-        atomicAdd(&hist[32 - __clz(occ)], 1u);
-    }
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024)
+        atomicAdd(&hist[32 - __clz(bstart[b + 1] - bstart[b])], 1u);
     __syncthreads();
     if (threadIdx.x == 0) {  // exclusive offsets, class 32 first
         uint32_t acc = 0;
@@ -1201,15 +1202,12 @@ __global__ __launch_bounds__(1024) void bins_order_kernel(const uint32_t* __rest
         }
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
-        const uint32_t occ = kbase[bstart[b + 1]] - kbase[bstart[b]];
-        order[atomicAdd(&hist[32 - __clz(occ)], 1u)] = b;
-    }
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024)
+        order[atomicAdd(&hist[32 - __clz(bstart[b + 1] - bstart[b])], 1u)] = b;
 }
 
-hipError_t launch_bins_order(const uint32_t* bstart, const uint32_t* kbase, const uint64_t* totals,
-                             uint32_t* order, hipStream_t s) {
-    hipLaunchKernelGGL(bins_order_kernel, dim3(1), dim3(1024), 0, s, bstart, kbase, totals, order);
+hipError_t launch_bins_order(const uint32_t* bstart, const uint64_t* totals, uint32_t* order, hipStream_t s) {
+    hipLaunchKernelGGL(bins_order_kernel, dim3(1), dim3(1024), 0, s, bstart, totals, order);
     return hipGetLastError();
 }
 

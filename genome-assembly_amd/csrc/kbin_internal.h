@@ -99,7 +99,7 @@ struct BinArgs {
     const uint64_t* w0;        // [R] span bases 0..31
     const uint64_t* w1;        // [R] span bases 32..63
     const uint32_t* bstart;    // [nbins + 1]
-    const uint32_t* kbase;     // [R + 1] first k-mer (occurrence) index of each bin-ordered record
+    unsigned long long* stage_ctr;  // stage allocation (zeroed): each bin takes its occurrences
     const uint32_t* order;     // [nbins] processing order (largest bins first)
     unsigned long long* work;  // work counter (zeroed)
     uint64_t* stage;           // [N] (LDS slot << 32 | ordinal) per occurrence, bin-local ranges
@@ -150,10 +150,9 @@ uint64_t sk_blocks(uint64_t n_reads, int RW);
 hipError_t launch_sk_kmers_total(const unsigned long long* part, uint64_t n, unsigned long long* out,
                                  hipStream_t s);
 hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
-                            uint32_t* nk, hipStream_t s);
+                            hipStream_t s);
 hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s);
-hipError_t launch_bins_order(const uint32_t* bstart, const uint32_t* kbase, const uint64_t* totals,
-                             uint32_t* order, hipStream_t s);
+hipError_t launch_bins_order(const uint32_t* bstart, const uint64_t* totals, uint32_t* order, hipStream_t s);
 size_t bins_lds_bytes(uint32_t ts_log2);
 #ifdef KB_BIN_PROF
 void bins_prof_report(hipStream_t s);
