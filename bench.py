@@ -93,6 +93,9 @@ def main():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=300_000,
                     help="reads timed on the CPU oracle (0 = skip)")
+    ap.add_argument("--routed", action="store_true",
+                    help="N=1 through the multi-GPU path (route, all-to-all over a 1-rank group, "
+                         "receive): measures the routing overhead on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,7 +109,16 @@ def main():
     local = local % ndev if backend == "gloo" else local
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if args.routed and world == 1:
+        import socket
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or args.routed:
         import torch.distributed as tdist
         if backend == "nccl":
             tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -125,7 +137,7 @@ def main():
                                args.err_ppm, args.seed * 1000003 + rank, device=local)
     torch.cuda.synchronize()
 
-    if world > 1:
+    if world > 1 or args.routed:
         from kbin import dist as kdist
         runner = kdist.ShardedBinner(K, M, args.cutoff, L, device=local, group=None)
         step = lambda: runner.step(words, lens, n, wpr, first_id=rank * n)  # noqa: E731
@@ -151,10 +163,13 @@ def main():
     tim = []
     barrier()
     t0 = time.perf_counter()
+    route_t = []
     for _ in range(args.steps):
         step()
         t = eng.timing()
         tim.append(t)
+        if world > 1 or args.routed:
+            route_t.append(runner.last_times)
         scan_ms.append(t["scan_insert_ms"] / max(1, t["scan_insert_launches"]))
     barrier()
     elapsed = time.perf_counter() - t0
@@ -201,9 +216,12 @@ def main():
                                f"K={K} M={M}, prune cutoff {args.cutoff}",
                    "reads_per_gpu": n, "read_len": L, "K": K, "M": M, "cutoff": args.cutoff,
                    "genome_len": args.genome, "err_ppm": args.err_ppm,
-                   "parallelism": f"mmer-sharded x{world}" if world > 1 else "single GPU"},
+                   "parallelism": f"mmer-sharded x{world}" if world > 1 else
+                                  ("single GPU, routed path" if args.routed else "single GPU")},
         "roofline": roof,
         "phases_ms": phases,
+        **({"route_ms": {k: round(float(np.mean([r[k] for r in route_t])), 4) for k in route_t[0]}}
+           if route_t else {}),
         "result": {"entries": int(dev["n_entries"]), "ids": int(dev["n_ids"]),
                    "distinct": int(dev["n_distinct"]), "kmers_owned": n_kmers,
                    "table_slots": int(tim[-1]["table_slots"]),

@@ -560,6 +560,58 @@ extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
     return KB_OK;
 }
 
+extern "C" int kb_route_scatter(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions, uint64_t region_cap,
+                                uint64_t* h_counts) {
+    if (!c || !h_counts) return fail(KB_EINVAL, "null argument");
+    if (n_dest < 1 || n_dest > 64) return fail(KB_EINVAL, "n_dest=%u outside [1,64]", n_dest);
+    if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
+    if (!binned_applies(c)) return fail(KB_EINVAL, "kb_route_scatter needs the binned engine (use plan/pack)");
+    for (auto& b : c->batches)
+        if (!b.routed && !b.superkmers && b.RW > 16)
+            return fail(KB_EINVAL, "kb_route_scatter serves reads of <= 512 bp (use plan/pack)");
+    if (region_cap && !d_regions) return fail(KB_EINVAL, "null regions");
+    int rc = set_device(c);
+    if (rc) return rc;
+    bool affine = false;
+    int64_t id_c = 0;
+    rc = read_id_map(c, affine, id_c);
+    if (rc) return rc;
+    HIPCHK(c->rcount.ensure(64));
+    HIPCHK(hipMemsetAsync(c->rcount.p, 0, 64 * sizeof(unsigned long long), c->s));
+    for (auto& b : c->batches) {
+        if (b.routed || b.superkmers || !b.n_reads) continue;
+        SkScanArgs a{};
+        a.words = b.words;
+        a.lens = b.lens;
+        a.n_reads = b.n_reads;
+        a.ord_base = (uint32_t)b.ord_base;
+        a.RW = b.RW;
+        a.K = c->p.K;
+        a.M = c->p.M;
+        a.regions = d_regions;
+        a.region_cap = region_cap;
+        a.dest_ctr = c->rcount.p;
+        a.read_ids = affine ? nullptr : c->read_ids.p;
+        a.id_off = (uint32_t)(affine ? id_c : 0);
+        a.G = n_dest;
+        a.rw = rec_words(c);
+        HIPCHK(launch_sk(a, true, c->s));
+    }
+    std::vector<unsigned long long> cnt(n_dest);
+    HIPCHK(hipMemcpyAsync(cnt.data(), c->rcount.p, n_dest * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    bool over = false;
+    for (uint32_t d = 0; d < n_dest; d++) {
+        h_counts[d] = cnt[d];
+        over |= cnt[d] > region_cap;
+    }
+    if (over) return fail(KB_EOVERFLOW, "a destination needs more than %llu records (see counts)",
+                          (unsigned long long)region_cap);
+    for (auto& b : c->batches)
+        if (!b.superkmers) b.routed = true;
+    return KB_OK;
+}
+
 extern "C" int kb_route_pack(kb_ctx* c, uint64_t* d_send) {
     if (!c) return fail(KB_EINVAL, "null ctx");
     if (!c->route_G) return fail(KB_ESTATE, "kb_route_pack before kb_route_plan");
@@ -628,18 +680,22 @@ extern "C" int kb_submit_superkmers_device(kb_ctx* c, const uint64_t* d_recs, ui
     b.superkmers = true;
     b.recs = d_recs;
     b.n_reads = n_rec;
-    HIPCHK(hipMalloc((void**)&b.rec_base, n_rec * sizeof(uint32_t)));
-    HIPCHK(launch_sk_counts(d_recs, n_rec, rec_words(c), b.rec_base, c->s));
-    HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(n_rec), c->scratch.cap)));
-    HIPCHK(launch_scan_u32(b.rec_base, n_rec, c->scratch.p, c->scratch.cap, c->s));
+    c->batches.push_back(b);  // occurrence offsets are computed by the engine that bins them
+    return KB_OK;
+}
+
+// the table engine's per-record occurrence offsets of a received batch
+static int sk_batch_offsets(kb_ctx* c, Batch& b) {
+    HIPCHK(hipMalloc((void**)&b.rec_base, std::max<uint64_t>(b.n_reads, 1) * sizeof(uint32_t)));
+    HIPCHK(launch_sk_counts(b.recs, b.n_reads, rec_words(c), b.rec_base, c->s));
+    HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(b.n_reads), c->scratch.cap)));
+    HIPCHK(launch_scan_u32(b.rec_base, b.n_reads, c->scratch.p, c->scratch.cap, c->s));
     uint64_t tot = 0;
-    const uint64_t nb = scan_u32_scratch_elems(n_rec) - 2;
+    const uint64_t nb = scan_u32_scratch_elems(b.n_reads) - 2;
     HIPCHK(hipMemcpyAsync(&tot, c->scratch.p + nb, 8, hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     b.n_occ = tot;
     b.have_occ = true;
-    c->n_occ += tot;
-    c->batches.push_back(b);
     return KB_OK;
 }
 
@@ -773,26 +829,38 @@ static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered
 // record's read id is its ordinal (ids increase with the global call order)
 static int binned_sk_records(kb_ctx* c, uint64_t& R, uint64_t& N) {
     R = 0;
-    N = 0;
     for (auto& b : c->batches)
-        if (b.superkmers) {
-            R += b.n_reads;
-            N += b.n_occ;
-        }
-    if (N >= 0xFFFFFFFFull)
-        return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
-                    (unsigned long long)N);
+        if (b.superkmers) R += b.n_reads;
+    if (R > 0xFFFFFFFFull) return fail(KB_EOVERFLOW, "more than 2^32 received records");
+    // N <= 63 R; buffers that scale with N are sized after the count
     HIPCHK(c->pay.ensure(3 * R));
     HIPCHK(c->srec.ensure(3 * R));
-    HIPCHK(c->occ_a.ensure(std::max<uint64_t>(R, N / 2 + 4)));
-    HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));
+    HIPCHK(c->occ_a.ensure(std::max<uint64_t>(R, 4)));
+    HIPCHK(hipMemsetAsync(c->totals.p + 8, 0, sizeof(uint64_t), c->s));
     uint64_t off = 0;
     for (auto& b : c->batches) {
         if (!b.superkmers) continue;
         HIPCHK(launch_sk_convert(b.recs, b.n_reads, rec_words(c), off, c->p.M, c->pay.p, c->occ_a.p,
-                                 c->misc.p, c->s));
+                                 c->misc.p, reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
         off += b.n_reads;
         c->tm.scan_insert_launches++;
+    }
+    HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    N = c->h_totals[8];
+    if (N >= 0xFFFFFFFFull)
+        return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
+                    (unsigned long long)N);
+    HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));
+    if (c->occ_a.cap < N / 2 + 4) {  // grow, keeping the R keys
+        DevBuf<uint64_t> t;
+        HIPCHK(t.ensure(std::max<uint64_t>(R, N / 2 + 4)));
+        HIPCHK(hipMemcpyAsync(t.p, c->occ_a.p, R * sizeof(uint64_t), hipMemcpyDeviceToDevice, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));
+        c->occ_a.release();
+        c->occ_a = t;
+        t.p = nullptr;
+        t.cap = 0;
     }
     return KB_OK;
 }
@@ -960,8 +1028,8 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     uint64_t N = 0;
     for (auto& b : c->batches) {
         if (b.routed) continue;
-        if (!b.superkmers && !b.have_occ) {
-            rc = batch_offsets(c, b);
+        if (!b.have_occ) {
+            rc = b.superkmers ? sk_batch_offsets(c, b) : batch_offsets(c, b);
             if (rc) return rc;
         }
         b.occ_base = N;

@@ -103,6 +103,15 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
     }
 }
 
+// map a call ordinal to the caller's read id
+DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
+    return read_ids ? read_ids[ord] : (int32_t)(ord + id_off);
+}
+
+DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) {  // = owner_of() in kbin_kernels.hip
+    return (uint32_t)((mix64((uint64_t)mmer + 0x5851F42D4C957F2Dull) >> 32) % G);
+}
+
 // Thread-per-read variant for short reads (RW <= SK_THREAD_RW): a block
 // stages 256 reads in LDS rows and each lane walks its own read's sticky
 // chain serially.  The wave-per-read kernel above keeps 64 lanes busy on a
@@ -127,7 +136,10 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     uint64_t* stg = smem + 256 * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
     __shared__ uint32_t span_end;
     __shared__ unsigned long long s_base;
-    const bool alloc = WRITE && A.rec_ctr;  // records placed by block allocation, any order
+    __shared__ uint32_t dcnt[64];
+    __shared__ unsigned long long dbase[64];
+    const bool route = WRITE && A.regions;          // records to destination regions, any order
+    const bool alloc = WRITE && (A.rec_ctr || route);  // records placed by block allocation
     uint64_t kmers = 0;
     for (uint64_t r0 = (uint64_t)blockIdx.x * 256; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * 256) {
         const uint32_t nrows = (uint32_t)min<uint64_t>(256, A.n_reads - r0);
@@ -175,6 +187,16 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     const uint64_t loc = alloc ? (uint64_t)atomicAdd(&span_end, 1u) : rbase + nseg - bfirst;
                     if (loc < SK_STAGE) {
                         stg[loc] = e;
+                    } else if (route) {  // beyond the staging area: one record, its own slot
+                        const uint32_t d = owner_of_mmer((uint32_t)best, A.G);
+                        const uint64_t i = atomicAdd(&A.dest_ctr[d], 1ull);
+                        if (i < A.region_cap) {
+                            uint64_t* o = A.regions + (d * A.region_cap + i) * (uint64_t)A.rw;
+                            const uint32_t id = (uint32_t)id_of(A.ord_base + (uint32_t)r, A.read_ids, A.id_off);
+                            o[0] = (uint64_t)id | ((uint64_t)lo << 32) | (n << 48) | ((uint64_t)(sig - lo) << 54);
+                            o[1] = window64(sw, lo);
+                            if (A.rw >= 3) o[2] = window64(sw, lo + 32);
+                        }
                     } else {  // beyond the staging area: direct (scattered) stores
                         const uint64_t t = alloc ? (uint64_t)atomicAdd(A.rec_ctr, 1ull) : rbase + nseg;
                         A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)r) | (n << 32) |
@@ -194,6 +216,35 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
         if (WRITE) {
             __syncthreads();
             const uint32_t span = min(span_end, SK_STAGE);
+            if (route) {
+                // per destination: count, reserve a range, place (LDS cursors)
+                if (tid < 64) dcnt[tid] = 0;
+                __syncthreads();
+                for (uint32_t i = tid; i < span; i += 256)
+                    atomicAdd(&dcnt[owner_of_mmer((uint32_t)(stg[i] >> 37), A.G)], 1u);
+                __syncthreads();
+                if (tid < A.G) {
+                    dbase[tid] = dcnt[tid] ? atomicAdd(&A.dest_ctr[tid], (unsigned long long)dcnt[tid]) : 0ull;
+                    dcnt[tid] = 0;
+                }
+                __syncthreads();
+                for (uint32_t i = tid; i < span; i += 256) {
+                    const uint64_t e = stg[i];
+                    const uint32_t d = owner_of_mmer((uint32_t)(e >> 37), A.G);
+                    const uint64_t slot = dbase[d] + atomicAdd(&dcnt[d], 1u);
+                    if (slot >= A.region_cap) continue;  // counted: the caller retries bigger
+                    const uint32_t lo = (uint32_t)(e & 0xFFFFu), row = (uint32_t)((e >> 29) & 0xFFu);
+                    const uint64_t n = (e >> 16) & 63u, so = (e >> 22) & 63u;
+                    const uint64_t* sw = smem + row * RS;
+                    const uint32_t id =
+                        (uint32_t)id_of(A.ord_base + (uint32_t)(r0 + row), A.read_ids, A.id_off);
+                    uint64_t* o = A.regions + (d * A.region_cap + slot) * (uint64_t)A.rw;
+                    o[0] = (uint64_t)id | ((uint64_t)lo << 32) | (n << 48) | (so << 54);
+                    o[1] = window64(sw, (int)lo);
+                    if (A.rw >= 3) o[2] = window64(sw, (int)lo + 32);
+                }
+                continue;  // (the loop-top barrier protects stg and the read rows)
+            }
             if (alloc) {  // the block's staged records get one contiguous range
                 if (tid == 0) s_base = span ? atomicAdd(A.rec_ctr, (unsigned long long)span) : 0ull;
                 __syncthreads();
@@ -213,7 +264,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
             }
         }
     }
-    if (!WRITE || alloc) {  // per-block partial sum (summed by sk_kmers_total_kernel)
+    if (!WRITE || (alloc && !route)) {  // per-block partial sum (summed by sk_kmers_total_kernel)
         __shared__ uint64_t shs[4];
         const uint64_t tot = block_sum256(kmers, shs);
         if (tid == 0) A.n_kmers[blockIdx.x] = tot;
@@ -288,14 +339,7 @@ hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t 
 // destination-major, read order within a destination; the receiver turns
 // them back into binned records.
 // ---------------------------------------------------------------------------
-// map a call ordinal to the caller's read id
-DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
-    return read_ids ? read_ids[ord] : (int32_t)(ord + id_off);
-}
 
-DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) {  // = owner_of() in kbin_kernels.hip
-    return (uint32_t)((mix64((uint64_t)mmer + 0x5851F42D4C957F2Dull) >> 32) % G);
-}
 
 __global__ __launch_bounds__(256) void route_dest_kernel(const uint64_t* __restrict__ keys, uint64_t R,
                                                          uint32_t G, uint64_t* __restrict__ dkeys,
@@ -350,9 +394,11 @@ hipError_t launch_route_pack_binned(const uint64_t* sorted, const uint64_t* pay,
 
 __global__ __launch_bounds__(256) void sk_convert_kernel(const uint64_t* __restrict__ recs, uint64_t n_rec,
                                                          int rw, uint64_t off, int M, uint64_t* __restrict__ pay,
-                                                         uint64_t* __restrict__ keys, uint32_t* status) {
+                                                         uint64_t* __restrict__ keys, uint32_t* status,
+                                                         unsigned long long* n_kmers) {
     const uint32_t maskM = (1u << (2 * M)) - 1u, halfM = 1u << (2 * M - 1);
     bool neg = false;
+    uint64_t kmers = 0;
     for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < n_rec; k += (uint64_t)gridDim.x * 256) {
         const uint64_t* r = recs + k * (uint64_t)rw;
         const uint64_t h = r[0];
@@ -368,16 +414,21 @@ __global__ __launch_bounds__(256) void sk_convert_kernel(const uint64_t* __restr
         pay[3 * t + 1] = w0;
         pay[3 * t + 2] = w1;
         keys[t] = ((uint64_t)canon << 38) | ((63ull - n) << 32) | (uint32_t)t;
+        kmers += n;
     }
     if (neg) atomicOr(status, ST_NEG_ID);
+    __shared__ uint64_t sh[4];
+    kmers = block_sum256(kmers, sh);
+    if (threadIdx.x == 0 && kmers) atomicAdd(n_kmers, (unsigned long long)kmers);
 }
 
 hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint64_t off, int M,
-                             uint64_t* pay, uint64_t* keys, uint32_t* status, hipStream_t s) {
+                             uint64_t* pay, uint64_t* keys, uint32_t* status, unsigned long long* n_kmers,
+                             hipStream_t s) {
     if (!n_rec) return hipSuccess;
     const uint64_t blocks = std::min<uint64_t>((n_rec + 255) / 256, 8192);
     hipLaunchKernelGGL(sk_convert_kernel, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, off, M, pay,
-                       keys, status);
+                       keys, status, n_kmers);
     return hipGetLastError();
 }
 

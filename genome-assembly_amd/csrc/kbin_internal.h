@@ -91,6 +91,15 @@ struct SkScanArgs {
                                // (a wavefront's 64 records have near-equal k-mer counts)
     uint32_t ord_base;
     int RW, K, M;
+    // route mode (thread kernel, with rec_ctr == nullptr): records go to
+    // regions + (dest * region_cap + i) * rw in the routed format
+    uint64_t* regions;
+    uint64_t region_cap;
+    unsigned long long* dest_ctr;  // [G] records per destination (zeroed)
+    const int32_t* read_ids;       // ordinal -> id (null: affine, id = ordinal + id_off)
+    uint32_t id_off;
+    uint32_t G;
+    int rw;
 };
 
 struct BinArgs {
@@ -138,7 +147,8 @@ hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s);
 // received routed records (rw words: {id | i0 << 32 | n << 48 | sig_off << 54}, span words)
 // -> binned records at t = off + k; ids < 0 set ST_NEG_ID in *status
 hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint64_t off, int M,
-                             uint64_t* pay, uint64_t* keys, uint32_t* status, hipStream_t s);
+                             uint64_t* pay, uint64_t* keys, uint32_t* status, unsigned long long* n_kmers,
+                             hipStream_t s);
 // sender: destination of every record (owner of its mmer) -> dkeys = dest << 32 | t, counts[dest]
 hipError_t launch_route_dest(const uint64_t* keys, uint64_t R, uint32_t G, uint64_t* dkeys,
                              unsigned long long* counts, hipStream_t s);

@@ -35,7 +35,7 @@ EXPORTED = [
     "kb_finalize", "kb_export", "kb_export_device", "kb_reset", "kb_set_timing",
     "kb_get_timing", "kb_generate_reads_device", "kb_unpack_reads_to_host", "kb_stream",
     "kb_last_error", "kb_abi_version", "kb_record_words", "kb_route_plan", "kb_route_pack",
-    "kb_submit_superkmers_device",
+    "kb_submit_superkmers_device", "kb_route_scatter",
 ]
 
 
@@ -114,6 +114,7 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_route_plan.argtypes = [vp, u32, C.POINTER(u64)]
     lib.kb_route_pack.argtypes = [vp, vp]
     lib.kb_submit_superkmers_device.argtypes = [vp, vp, u64]
+    lib.kb_route_scatter.argtypes = [vp, C.c_uint32, vp, u64, C.POINTER(C.c_uint64)]
     lib.kb_stream.argtypes = [vp]
     lib.kb_stream.restype = vp
     lib.kb_last_error.argtypes = []
@@ -265,6 +266,18 @@ class Engine:
 
     def route_pack(self, send_ptr: int) -> None:
         _check(self.lib, self.lib.kb_route_pack(self._h, C.c_void_p(send_ptr)))
+
+    def route_scatter(self, n_dest: int, regions_ptr: int, region_cap: int):
+        """one-pass sender: records into per-destination regions of region_cap
+        records each; returns (ok, counts) -- ok False means a destination
+        needs more room (counts say how much; nothing was shipped)"""
+        cnt = np.zeros(n_dest, dtype=np.uint64)
+        rc = self.lib.kb_route_scatter(self._h, n_dest, C.c_void_p(regions_ptr), int(region_cap),
+                                       cnt.ctypes.data_as(C.POINTER(C.c_uint64)))
+        if rc == KB_EOVERFLOW:
+            return False, cnt
+        _check(self.lib, rc)
+        return True, cnt
 
     def submit_superkmers_device(self, recs_ptr: int, n_records: int) -> None:
         _check(self.lib, self.lib.kb_submit_superkmers_device(self._h, C.c_void_p(recs_ptr),

@@ -10,15 +10,21 @@ records (a run of consecutive k-mers of a read that share one signature,
 ~10 per 150-bp read at k31/m7 -- about 2 B per k-mer on the wire instead of
 a 12-16 B per-k-mer record) over RCCL (torch.distributed "nccl") / xGMI.
 
-Per step on every rank:
+Per step on every rank (binned engine, K <= 31):
+  kb_route_scatter (one pass: records straight into per-destination regions)
+  ->  all_to_all_single of the counts, all_to_all of the region slices  ->
+  kb_submit_superkmers_device (one batch per source rank)  ->  kb_finalize.
+Otherwise (table engine: K > 31 or first-occurrence tracking):
   kb_route_plan (counts per destination)  ->  kb_route_pack (dest-major send
-  buffer)  ->  all_to_all_single (counts, then records)  ->
+  buffer, read order)  ->  all_to_all_single (counts, then records)  ->
   kb_submit_superkmers_device (received, concatenated by source rank)  ->
-  kb_finalize (table insert, radix sort, prune, CSR).
+  kb_finalize.
 Read ids must increase with the global call order (rank r's ids below rank
 r+1's): they are the reverse-call-order key of every id list.
 """
 from __future__ import annotations
+
+import time
 
 import torch
 import torch.distributed as dist
@@ -67,6 +73,32 @@ def exchange_records(send: torch.Tensor, counts, rec_words: int, group=None):
     return recv, rc
 
 
+def exchange_regions(regions: torch.Tensor, counts, cap: int, rec_words: int, group=None):
+    """All-to-all of per-destination record regions (destination d's records
+    at regions[d*cap*rec_words:], counts[d] of them; kb_route_scatter's
+    layout).  Returns (one received tensor per source rank, per-source
+    counts).  RCCL moves each region slice directly (no packing pass); the
+    gloo rehearsal of cuda tensors stages through the host."""
+    dev = regions.device
+    G = len(counts)
+    sends = [regions[d * cap * rec_words:(d * cap + int(counts[d])) * rec_words] for d in range(G)]
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        flat = torch.cat(sends).cpu()
+        recv, rc = exchange_records(flat, [int(c) for c in counts], rec_words, group)
+        recv = recv.to(dev)
+        edges = [0]
+        for c in rc:
+            edges.append(edges[-1] + c * rec_words)
+        return [recv[edges[i]:edges[i + 1]] for i in range(G)], rc
+    cnt = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    rc = [int(x) for x in rcnt.cpu().tolist()]
+    recvs = [torch.empty(c * rec_words, dtype=torch.int64, device=dev) for c in rc]
+    dist.all_to_all(recvs, sends, group=group)
+    return recvs, rc
+
+
 class ShardedBinner:
     """One rank's share of a mmer-sharded binning job."""
 
@@ -82,6 +114,33 @@ class ShardedBinner:
         self._send = torch.empty(0, dtype=torch.int64, device=self.device)
         self._recv = None
         self.last_counts = None
+        self.last_times = {}
+        self._regions = torch.empty(0, dtype=torch.int64, device=self.device)
+        self._cap = 0
+        self.scatter = True  # one-pass sender while the engine accepts it
+
+    def _scatter(self, n_reads: int):
+        """kb_route_scatter with a learned region capacity; None when the
+        engine cannot take this path (the caller plans and packs instead)"""
+        from . import KB_EINVAL, KbError
+        if self._cap == 0:  # ~10 records per 150-bp read, spread over the ranks
+            self._cap = int(n_reads * 12 / self.world * 1.25) + 4096
+        for _ in range(2):
+            need = self.world * self._cap * self.rec_words
+            if self._regions.numel() < need:
+                self._regions = torch.empty(need, dtype=torch.int64, device=self.device)
+            try:
+                ok, counts = self.engine.route_scatter(self.world, self._regions.data_ptr(), self._cap)
+            except KbError as e:
+                if e.code != KB_EINVAL:
+                    raise
+                self.scatter = False
+                return None
+            if ok:
+                self._cap = max(self._cap, int(int(counts.max()) * 1.1) + 1024)
+                return counts
+            self._cap = int(int(counts.max()) * 1.2) + 1024  # retry once with room for all
+        raise RuntimeError("kb_route_scatter: region capacity not converging")
 
     def _send_buffer(self, words: int) -> torch.Tensor:
         if self._send.numel() < words:
@@ -94,16 +153,34 @@ class ShardedBinner:
         together with every other rank's; the result this rank owns stays in
         self.engine (export / export_device)."""
         eng = self.engine
+        t = [time.perf_counter()]
         eng.reset()
         eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n_reads, words_per_read,
                                  first_id)
-        counts = eng.route_plan(self.world)
-        total = int(counts.sum())
-        send = self._send_buffer(total * self.rec_words)
-        eng.route_pack(send.data_ptr())  # synchronises the engine stream
-        recv, rc = exchange_records(send, counts.tolist(), self.rec_words, self.group)
+        counts = self._scatter(n_reads) if self.scatter else None
+        if counts is not None:  # one pass: records straight into destination regions
+            t.append(time.perf_counter())
+            t.append(t[-1])
+            recvs, rc = exchange_regions(self._regions, counts.tolist(), self._cap, self.rec_words,
+                                         self.group)
+        else:  # plan / pack: destination-major, read order (any engine)
+            counts = eng.route_plan(self.world)  # synchronises the engine stream
+            t.append(time.perf_counter())
+            total = int(counts.sum())
+            send = self._send_buffer(total * self.rec_words)
+            eng.route_pack(send.data_ptr())  # synchronises the engine stream
+            t.append(time.perf_counter())
+            recv, rc = exchange_records(send, counts.tolist(), self.rec_words, self.group)
+            recvs = [recv]
         torch.cuda.current_stream(self.device).synchronize()
-        self._recv = recv  # referenced by the engine until the next reset
+        t.append(time.perf_counter())
+        self._recv = recvs  # referenced by the engine until the next reset
         self.last_counts = (counts.tolist(), rc)
-        eng.submit_superkmers_device(recv.data_ptr(), recv.numel() // self.rec_words)
+        for r in recvs:
+            if r.numel():
+                eng.submit_superkmers_device(r.data_ptr(), r.numel() // self.rec_words)
         eng.finalize(prune=prune)
+        t.append(time.perf_counter())
+        # host wall time per stage (each ends in a stream synchronisation)
+        self.last_times = {k: (t[i + 1] - t[i]) * 1e3
+                           for i, k in enumerate(("plan_ms", "pack_ms", "exchange_ms", "receive_ms"))}

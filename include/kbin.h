@@ -189,6 +189,18 @@ int kb_route_plan(kb_ctx *ctx, uint32_t n_dest, uint64_t *h_counts);
 int kb_route_pack(kb_ctx *ctx, uint64_t *d_send);
 int kb_submit_superkmers_device(kb_ctx *ctx, const uint64_t *d_records, uint64_t n_records);
 
+/* One-pass sender (binned engine only: K <= 31, reads of <= 512 bp, no
+ * KB_TRACK_FIRST on any rank).  Writes every record of the read batches
+ * submitted so far into d_regions: destination d's records at
+ * d_regions + d * region_cap * kb_record_words, h_counts[d] of them, in no
+ * particular order (the binned receiver orders lists by read id, not by
+ * arrival).  Returns KB_EOVERFLOW, with h_counts holding the counts needed
+ * and the batches left unshipped, when a destination gets more than
+ * region_cap records: call again with a larger region_cap.  Returns
+ * KB_EINVAL when the binned engine does not apply (use plan/pack). */
+int kb_route_scatter(kb_ctx *ctx, uint32_t n_dest, uint64_t *d_regions,
+                     uint64_t region_cap, uint64_t *h_counts);
+
 /* Stream used by the context (hipStream_t as void*), for callers that want
  * to order their own work against the engine. */
 void *kb_stream(kb_ctx *ctx);

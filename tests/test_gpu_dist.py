@@ -70,6 +70,51 @@ def test_virtual_shards(K, M, G):
     assert union == ora
 
 
+@pytest.mark.parametrize("K,M,G", [(31, 7, 1), (31, 7, 3), (21, 5, 8), (15, 7, 4)])
+def test_route_scatter(K, M, G, engine):
+    """one-pass sender: per destination the same multiset of records as
+    plan/pack (order is free), a too-small region reports KB_EOVERFLOW and
+    ships nothing, and the receivers' union equals the oracle"""
+    reads = _reads()
+    bases, lens = kbin.pack_reads(reads)
+    ids = np.arange(len(reads), dtype=np.int32) * 2 + 5
+    rw = skmer_ref.rec_words(K, M)
+    want, wcounts = skmer_ref.encode(reads, ids.tolist(), K, M, G)
+    want = np.asarray(want, dtype=np.uint64).reshape(-1, rw)
+    with kbin.Engine(K, M, cutoff=1, max_read_len=300) as eng:
+        eng.submit(bases=bases, lens=lens, ids=ids)
+        if engine == "table":  # the one-pass sender is the binned engine's
+            with pytest.raises(kbin.KbError) as ei:
+                eng.route_scatter(G, 0, 0)
+            assert ei.value.code == kbin.KB_EINVAL
+            return
+        small = torch.zeros(G * 8 * rw, dtype=torch.int64, device="cuda")
+        ok, need = eng.route_scatter(G, small.data_ptr(), 8)
+        assert not ok and need.tolist() == wcounts
+        cap = int(need.max())
+        regions = torch.zeros(G * cap * rw, dtype=torch.int64, device="cuda")
+        ok, counts = eng.route_scatter(G, regions.data_ptr(), cap)
+        assert ok and counts.tolist() == wcounts
+        torch.cuda.synchronize()
+    got = regions.cpu().numpy().view(np.uint64).reshape(G, cap, rw)
+    edges = np.concatenate([[0], np.cumsum(np.asarray(wcounts, dtype=np.int64))])
+    ora = skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, True, ids=ids))
+    union = {}
+    for d in range(G):
+        mine = got[d, :wcounts[d]]
+        ref = want[edges[d]:edges[d + 1]]
+        order = lambda a: a[np.lexsort(a.T[::-1])]  # noqa: E731
+        np.testing.assert_array_equal(order(mine), order(ref))
+        with kbin.Engine(K, M, cutoff=1, max_read_len=300) as shard:
+            seg = regions[d * cap * rw:]
+            shard.submit_superkmers_device(seg.data_ptr(), int(wcounts[d]))
+            shard.finalize(prune=True)
+            part = _result_dict(shard.export())
+        assert not (set(part) & set(union))
+        union.update(part)
+    assert union == ora
+
+
 def test_track_first_through_routing():
     """first occurrence (id << 16 | position) survives the exchange"""
     reads = _reads(300)
