@@ -834,8 +834,8 @@ void bins_prof_report(hipStream_t s) {
 // whole block (LDS bitonic up to LIST_CAP, else chunks + merge passes).
 // ---------------------------------------------------------------------------
 constexpr int LIST_THREADS = 256;
-constexpr uint32_t LIST_CAP = 8192;   // longest list sorted in LDS in one piece
-constexpr uint32_t LIST_SPAN = 8192;  // ids of 256 entries staged in LDS at once
+constexpr uint32_t LIST_CAP = 4096;   // longest list sorted in LDS in one piece (power of two)
+constexpr uint32_t LIST_SPAN = 7168;  // ids of 256 entries staged in LDS at once (28 KiB: 5 blocks per CU)
 
 // descending bitonic sort of Pw (power of two) values in LDS by a group of G
 // lanes (G = 64: one wavefront, wave barriers; else the block)
