@@ -131,8 +131,14 @@ struct kb_ctx {
     DevBuf<uint64_t> srec;     // the same, bin order, structure of arrays
     DevBuf<uint64_t> stage;    // per-occurrence (slot, ordinal) staging
     DevBuf<uint32_t> border;   // bin processing order
+    DevBuf<uint32_t> bcount, bmmer;  // bin descriptors (with starts)
+    DevBuf<uint64_t> regions;  // local bucket regions (pay layout)
+    DevBuf<unsigned long long> bfill;  // records per bucket
+    uint64_t bucket_cap = 0;   // learned region capacity (records per bucket)
+    uint64_t bucket_cap_used = 0;  // the capacity (region stride) the regions were written with
     DevBuf<uint64_t> kpart;    // per-block k-mer sums of the count pass
     float rho = 0.f;           // learned distinct / occurrences
+    bool bucket_failed = false;  // a bucket overflowed its mmer map: radix path from now on
     uint64_t n_occ_entries_hint = 0;  // entries of the last finalize (lists grid)
     uint64_t* h_totals = nullptr;
     uint32_t* h_misc = nullptr;
@@ -224,7 +230,8 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->border.release(); c->kpart.release(); c->rcount.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->border.release(); c->bcount.release(); c->bmmer.release();
+    c->regions.release(); c->bfill.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
@@ -594,6 +601,7 @@ extern "C" int kb_route_scatter(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions,
         a.read_ids = affine ? nullptr : c->read_ids.p;
         a.id_off = (uint32_t)(affine ? id_c : 0);
         a.G = n_dest;
+        a.dest_salt = 0x5851F42D4C957F2Dull;  // owner_of (kbin_kernels.hip)
         a.rw = rec_words(c);
         HIPCHK(launch_sk(a, true, c->s));
     }
@@ -824,6 +832,87 @@ static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered
     return KB_OK;
 }
 
+// ---- phase A, bucketed: records straight into NB local bucket regions
+// (hash of the mmer); the learned capacity grows (and the pass reruns) when a
+// bucket overflows.  Reads: the one-pass super-k-mer kernel in region mode;
+// received: the block-aggregated converter.  Returns R and N (one sync per try).
+static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, uint64_t& N) {
+    const int M = c->p.M;
+    uint64_t nrec = 0;
+    for (auto& b : c->batches)
+        if (!b.routed) nrec += b.superkmers ? b.n_reads : b.n_reads * 16;
+    for (int attempt = 0; attempt < 3; attempt++) {
+        const uint64_t cap = c->bucket_cap ? c->bucket_cap : nrec / NB + 1024;
+        HIPCHK(c->regions.ensure(NB * cap * 3));
+        HIPCHK(c->bfill.ensure(NB));
+        HIPCHK(hipMemsetAsync(c->bfill.p, 0, NB * sizeof(unsigned long long), c->s));
+        HIPCHK(hipMemsetAsync(c->totals.p + 8, 0, sizeof(uint64_t), c->s));
+        HIPCHK(hipMemsetAsync(c->misc.p, 0, sizeof(uint32_t), c->s));
+        uint64_t kp = 1;
+        for (auto& b : c->batches) kp = std::max(kp, sk_blocks(b.n_reads, b.RW));
+        HIPCHK(c->kpart.ensure(kp));
+        for (auto& b : c->batches) {
+            if (b.routed || !b.n_reads) continue;
+            if (received) {
+                if (!b.superkmers) continue;
+                HIPCHK(launch_sk_convert_buckets(b.recs, b.n_reads, rec_words(c), M, NB, c->regions.p, cap,
+                                                 c->bfill.p, c->misc.p,
+                                                 reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
+            } else {
+                if (b.superkmers) continue;
+                SkScanArgs a{};
+                a.words = b.words;
+                a.lens = b.lens;
+                a.n_reads = b.n_reads;
+                a.ord_base = (uint32_t)b.ord_base;
+                a.RW = b.RW;
+                a.K = c->p.K;
+                a.M = M;
+                a.regions = c->regions.p;
+                a.region_cap = cap;
+                a.dest_ctr = c->bfill.p;
+                a.G = NB;
+                a.dest_salt = sk_bucket_salt();
+                a.rw = 3;
+                a.binned_fmt = 1;
+                a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p);
+                HIPCHK(launch_sk(a, true, c->s));
+                HIPCHK(launch_sk_kmers_total(reinterpret_cast<unsigned long long*>(c->kpart.p),
+                                             sk_blocks(b.n_reads, b.RW),
+                                             reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
+            }
+            c->tm.scan_insert_launches++;
+        }
+        std::vector<unsigned long long> fill(NB);
+        HIPCHK(hipMemcpyAsync(fill.data(), c->bfill.p, NB * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync: R and N size the rest
+        if (c->h_misc[0] & ST_NEG_ID)
+            return fail(KB_EINVAL, "routed read ids must be non-negative (they order the id lists)");
+        R = 0;
+        uint64_t mx = 0;
+        for (uint32_t d = 0; d < NB; d++) {
+            R += fill[d];
+            mx = std::max<uint64_t>(mx, fill[d]);
+        }
+        N = c->h_totals[8];
+        if (mx <= cap) {
+            c->bucket_cap_used = cap;  // the region stride of this pass
+            c->bucket_cap = std::max<uint64_t>(c->bucket_cap, mx + mx / 8 + 1024);  // next passes
+            if (N >= 0xFFFFFFFFull)
+                return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
+                            (unsigned long long)N);
+            if (R > N)
+                return fail(KB_EDEVICE, "internal: %llu super-k-mers > %llu k-mers", (unsigned long long)R,
+                            (unsigned long long)N);
+            return KB_OK;
+        }
+        c->bucket_cap = mx + mx / 4 + 1024;  // grow and rerun the pass
+    }
+    return fail(KB_EDEVICE, "internal: bucket capacity did not converge");
+}
+
 // ---- phase A (received): the routed super-k-mer records of every
 // kb_submit_superkmers_device batch, converted in place of phase A; the
 // record's read id is its ordinal (ids increase with the global call order)
@@ -875,34 +964,66 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     REC(1);
     c->tm.scan_insert_launches = 0;
     uint64_t R = 0, N = 0;
-    int rc = received ? binned_sk_records(c, R, N) : binned_read_records(c, R, N, false);
+    // bucketed (default): records into local bucket regions, one workgroup
+    // orders each bucket; radix: flat records, a global sort by (mmer, n)
+    bool all_short = true;
+    for (auto& b : c->batches)
+        if (!b.routed && !b.superkmers && b.RW > 16) all_short = false;
+    const bool bucketed = all_short && env_int("KB_BIN_RADIX", 0) == 0 && !c->bucket_failed;
+    const uint32_t NB = 512;
+    int rc = bucketed ? binned_buckets(c, NB, received, R, N)
+                      : (received ? binned_sk_records(c, R, N) : binned_read_records(c, R, N, false));
     if (rc) return rc;
     c->n_occ = N;
     REC(2);
-    // ---- stable sort of the records by canonical mmer, bin boundaries
-    const int key_bits = 2 * M + 6;  // (mmer, 63 - n)
-    const uint64_t nflags = onesweep_flag_elems(R);
-    if (c->os_flags.cap < nflags || c->os_epoch > (1u << 24) - 8) {
-        HIPCHK(c->os_flags.ensure(nflags));
-        HIPCHK(hipMemsetAsync(c->os_flags.p, 0, c->os_flags.cap * sizeof(uint64_t), c->s));
-        c->os_epoch = 0;
-    }
-    HIPCHK(c->os_aux.ensure(4 * 256 + 8));
-    HIPCHK(hipMemsetAsync(c->os_aux.p + 1028, 0, sizeof(uint32_t), c->s));
-    HIPCHK(launch_onesweep(c->occ_a.p, c->occ_b.p, R, key_bits, c->os_flags.p, c->os_aux.p,
-                           &c->os_epoch, &c->sorted, c->s));
-    c->tm.sort_passes = (uint32_t)((key_bits + 7) / 8);
     const uint64_t max_bins = std::max<uint64_t>(1, std::min<uint64_t>(R, 1ull << (2 * M - 1)));
     HIPCHK(c->starts.ensure(max_bins + 1));
-    HIPCHK(c->scratch.ensure(std::max(runs_scratch_elems(R, max_bins), c->scratch.cap)));
-    HIPCHK(launch_heads(c->sorted, R, c->starts.p, max_bins, c->scratch.p, c->scratch.cap,
-                        c->totals.p, c->s, 38));
-
+    HIPCHK(c->bcount.ensure(max_bins));
+    HIPCHK(c->bmmer.ensure(max_bins));
+    HIPCHK(c->srec.ensure(3 * R));
+    HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));  // ids by ordinal (+ radix ping-pong)
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
-    HIPCHK(launch_sk_gather(c->sorted, c->pay.p, R, c->srec.p, c->s));
-
+    if (bucketed) {
+        BucketArgs ba{};
+        ba.regions = c->regions.p;
+        ba.cap = c->bucket_cap_used;
+        ba.bfill = c->bfill.p;
+        ba.M = M;
+        ba.hdr = c->srec.p;
+        ba.w0 = c->srec.p + R;
+        ba.w1 = c->srec.p + 2 * R;
+        ba.rec_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 11);
+        ba.bin_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 2);
+        ba.bstart = c->starts.p;
+        ba.bcount = c->bcount.p;
+        ba.bmmer = c->bmmer.p;
+        ba.max_bins = max_bins;
+        ba.status = c->misc.p;
+        HIPCHK(launch_bucket_sort(ba, NB, c->s));
+        c->tm.sort_passes = 0;
+    } else {
+        // ---- stable sort of the records by (mmer, 63 - n), bin boundaries
+        const int key_bits = 2 * M + 6;
+        const uint64_t nflags = onesweep_flag_elems(R);
+        if (c->os_flags.cap < nflags || c->os_epoch > (1u << 24) - 8) {
+            HIPCHK(c->os_flags.ensure(nflags));
+            HIPCHK(hipMemsetAsync(c->os_flags.p, 0, c->os_flags.cap * sizeof(uint64_t), c->s));
+            c->os_epoch = 0;
+        }
+        HIPCHK(c->os_aux.ensure(4 * 256 + 8));
+        HIPCHK(hipMemsetAsync(c->os_aux.p + 1028, 0, sizeof(uint32_t), c->s));
+        HIPCHK(launch_onesweep(c->occ_a.p, c->occ_b.p, R, key_bits, c->os_flags.p, c->os_aux.p,
+                               &c->os_epoch, &c->sorted, c->s));
+        c->tm.sort_passes = (uint32_t)((key_bits + 7) / 8);
+        HIPCHK(c->scratch.ensure(std::max(runs_scratch_elems(R, max_bins), c->scratch.cap)));
+        HIPCHK(launch_heads(c->sorted, R, c->starts.p, max_bins, c->scratch.p, c->scratch.cap,
+                            c->totals.p, c->s, 38));
+        HIPCHK(launch_bins_describe(c->sorted, c->starts.p, c->totals.p, c->bcount.p, c->bmmer.p, max_bins,
+                                    c->s));
+        HIPCHK(launch_sk_gather(c->sorted, c->pay.p, R, c->srec.p, c->s));
+    }
     HIPCHK(c->border.ensure(max_bins));
-    HIPCHK(launch_bins_order(c->starts.p, c->totals.p, c->border.p, c->s));
+    HIPCHK(launch_bins_order(c->bcount.p, c->totals.p, c->border.p, max_bins, c->s));
     REC(3);
     // ---- one workgroup per bin
     const uint64_t ecap = N + 1;
@@ -915,11 +1036,13 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     // >= 10: the sort phase carves 8 wave windows of 256 ids out of the table
     const int ts_log2 = std::min(13, std::max(10, env_int("KB_BIN_TS_LOG2", 13)));
     BinArgs a{};
-    a.keys = c->sorted;
     a.hdr = c->srec.p;
     a.w0 = c->srec.p + R;
     a.w1 = c->srec.p + 2 * R;
     a.bstart = c->starts.p;
+    a.bcount = c->bcount.p;
+    a.bmmer = c->bmmer.p;
+    a.max_bins = max_bins;
     a.stage_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 10);
     a.order = c->border.p;
     a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
@@ -938,7 +1061,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     a.e_lo = c->e_lo.p;
     a.e_cnt = c->e_cnt.p;
     a.e_off = c->e_off.p;
-    a.ids_ord = reinterpret_cast<uint32_t*>(c->sorted == c->occ_a.p ? c->occ_b.p : c->occ_a.p);
+    a.ids_ord = reinterpret_cast<uint32_t*>(bucketed || c->sorted == c->occ_a.p ? c->occ_b.p : c->occ_a.p);
     a.ids_out = c->ids_out.p;
     a.read_ids = affine ? nullptr : c->read_ids.p;
     a.id_off = (uint32_t)(affine ? id_c : 0);
@@ -965,9 +1088,15 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     REC(5);
     HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
-    if (R) HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    if (R && !bucketed)
+        HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
     else c->h_misc[8] = 0;
     HIPCHK(hipStreamSynchronize(c->s));
+    if (c->h_misc[0] & ST_BUCKET_FULL) {  // a bucket held too many mmers: redo with the radix path
+        c->bucket_failed = true;
+        c->finalized = false;
+        return finalize_binned(c, prune, affine, id_c, received);
+    }
     if (c->h_misc[8]) return fail(KB_EDEVICE, "radix look-back timed out (device error word %u)", c->h_misc[8]);
     if (c->h_totals[3]) return fail(KB_EDEVICE, "internal: %llu bins > %llu", (unsigned long long)c->h_totals[3],
                                     (unsigned long long)max_bins);

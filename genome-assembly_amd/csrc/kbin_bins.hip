@@ -108,8 +108,29 @@ DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
     return read_ids ? read_ids[ord] : (int32_t)(ord + id_off);
 }
 
-DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) {  // = owner_of() in kbin_kernels.hip
-    return (uint32_t)((mix64((uint64_t)mmer + 0x5851F42D4C957F2Dull) >> 32) % G);
+constexpr uint64_t OWNER_SALT = 0x5851F42D4C957F2Dull;   // rank of a mmer (= owner_of(), kbin_kernels.hip)
+constexpr uint64_t BUCKET_SALT = 0x2545F4914F6CDD1Dull;  // bucket of a mmer inside one rank (independent)
+uint64_t sk_bucket_salt() { return BUCKET_SALT; }
+
+DEV uint32_t dest_of(uint32_t mmer, uint32_t G, uint64_t salt) {
+    return (uint32_t)((mix64((uint64_t)mmer + salt) >> 32) % G);
+}
+DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) { return dest_of(mmer, G, OWNER_SALT); }
+
+// one record into a destination region: the binned layout (ordinal) or the
+// routed one (read id), see SkScanArgs
+DEV void put_record(const SkScanArgs& A, uint64_t* o, uint32_t ord, uint64_t lo, uint64_t n, uint64_t so,
+                    uint64_t rev, const uint64_t* sw) {
+    if (A.binned_fmt) {
+        o[0] = (uint64_t)ord | (n << 32) | (so << 38) | (rev << 44) | (lo << 45);
+        o[1] = window64(sw, (int)lo);
+        o[2] = window64(sw, (int)lo + 32);
+    } else {
+        const uint32_t id = (uint32_t)id_of(ord, A.read_ids, A.id_off);
+        o[0] = (uint64_t)id | (lo << 32) | (n << 48) | (so << 54);
+        o[1] = window64(sw, (int)lo);
+        if (A.rw >= 3) o[2] = window64(sw, (int)lo + 32);
+    }
 }
 
 // Thread-per-read variant for short reads (RW <= SK_THREAD_RW): a block
@@ -122,6 +143,7 @@ DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) {  // = owner_of() in kbin
 // writes its (contiguous) record range with coalesced stores.
 constexpr int SK_THREAD_RW = 16;
 constexpr uint32_t SK_STAGE = 4096;  // staged records per block (8 B each)
+constexpr uint32_t SK_MAX_DEST = 1024;  // destination regions (ranks or buckets)
 
 template <bool WRITE>
 __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
@@ -136,8 +158,8 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     uint64_t* stg = smem + 256 * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
     __shared__ uint32_t span_end;
     __shared__ unsigned long long s_base;
-    __shared__ uint32_t dcnt[64];
-    __shared__ unsigned long long dbase[64];
+    __shared__ uint32_t dcnt[SK_MAX_DEST];
+    __shared__ unsigned long long dbase[SK_MAX_DEST];
     const bool route = WRITE && A.regions;          // records to destination regions, any order
     const bool alloc = WRITE && (A.rec_ctr || route);  // records placed by block allocation
     uint64_t kmers = 0;
@@ -188,15 +210,11 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     if (loc < SK_STAGE) {
                         stg[loc] = e;
                     } else if (route) {  // beyond the staging area: one record, its own slot
-                        const uint32_t d = owner_of_mmer((uint32_t)best, A.G);
+                        const uint32_t d = dest_of((uint32_t)best, A.G, A.dest_salt);
                         const uint64_t i = atomicAdd(&A.dest_ctr[d], 1ull);
-                        if (i < A.region_cap) {
-                            uint64_t* o = A.regions + (d * A.region_cap + i) * (uint64_t)A.rw;
-                            const uint32_t id = (uint32_t)id_of(A.ord_base + (uint32_t)r, A.read_ids, A.id_off);
-                            o[0] = (uint64_t)id | ((uint64_t)lo << 32) | (n << 48) | ((uint64_t)(sig - lo) << 54);
-                            o[1] = window64(sw, lo);
-                            if (A.rw >= 3) o[2] = window64(sw, lo + 32);
-                        }
+                        if (i < A.region_cap)
+                            put_record(A, A.regions + (d * A.region_cap + i) * (uint64_t)A.rw,
+                                       A.ord_base + (uint32_t)r, (uint64_t)lo, n, (uint64_t)(sig - lo), rev, sw);
                     } else {  // beyond the staging area: direct (scattered) stores
                         const uint64_t t = alloc ? (uint64_t)atomicAdd(A.rec_ctr, 1ull) : rbase + nseg;
                         A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)r) | (n << 32) |
@@ -218,30 +236,25 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
             const uint32_t span = min(span_end, SK_STAGE);
             if (route) {
                 // per destination: count, reserve a range, place (LDS cursors)
-                if (tid < 64) dcnt[tid] = 0;
+                for (uint32_t d = tid; d < A.G; d += 256) dcnt[d] = 0;
                 __syncthreads();
                 for (uint32_t i = tid; i < span; i += 256)
-                    atomicAdd(&dcnt[owner_of_mmer((uint32_t)(stg[i] >> 37), A.G)], 1u);
+                    atomicAdd(&dcnt[dest_of((uint32_t)(stg[i] >> 37), A.G, A.dest_salt)], 1u);
                 __syncthreads();
-                if (tid < A.G) {
-                    dbase[tid] = dcnt[tid] ? atomicAdd(&A.dest_ctr[tid], (unsigned long long)dcnt[tid]) : 0ull;
-                    dcnt[tid] = 0;
+                for (uint32_t d = tid; d < A.G; d += 256) {
+                    dbase[d] = dcnt[d] ? atomicAdd(&A.dest_ctr[d], (unsigned long long)dcnt[d]) : 0ull;
+                    dcnt[d] = 0;
                 }
                 __syncthreads();
                 for (uint32_t i = tid; i < span; i += 256) {
                     const uint64_t e = stg[i];
-                    const uint32_t d = owner_of_mmer((uint32_t)(e >> 37), A.G);
+                    const uint32_t d = dest_of((uint32_t)(e >> 37), A.G, A.dest_salt);
                     const uint64_t slot = dbase[d] + atomicAdd(&dcnt[d], 1u);
                     if (slot >= A.region_cap) continue;  // counted: the caller retries bigger
-                    const uint32_t lo = (uint32_t)(e & 0xFFFFu), row = (uint32_t)((e >> 29) & 0xFFu);
-                    const uint64_t n = (e >> 16) & 63u, so = (e >> 22) & 63u;
-                    const uint64_t* sw = smem + row * RS;
-                    const uint32_t id =
-                        (uint32_t)id_of(A.ord_base + (uint32_t)(r0 + row), A.read_ids, A.id_off);
-                    uint64_t* o = A.regions + (d * A.region_cap + slot) * (uint64_t)A.rw;
-                    o[0] = (uint64_t)id | ((uint64_t)lo << 32) | (n << 48) | (so << 54);
-                    o[1] = window64(sw, (int)lo);
-                    if (A.rw >= 3) o[2] = window64(sw, (int)lo + 32);
+                    const uint32_t row = (uint32_t)((e >> 29) & 0xFFu);
+                    put_record(A, A.regions + (d * A.region_cap + slot) * (uint64_t)A.rw,
+                               A.ord_base + (uint32_t)(r0 + row), e & 0xFFFFu, (e >> 16) & 63u, (e >> 22) & 63u,
+                               (e >> 28) & 1u, smem + row * RS);
                 }
                 continue;  // (the loop-top barrier protects stg and the read rows)
             }
@@ -264,7 +277,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
             }
         }
     }
-    if (!WRITE || (alloc && !route)) {  // per-block partial sum (summed by sk_kmers_total_kernel)
+    if (!WRITE || (alloc && (!route || A.binned_fmt))) {  // per-block k-mer sums (sk_kmers_total_kernel)
         __shared__ uint64_t shs[4];
         const uint64_t tot = block_sum256(kmers, shs);
         if (tid == 0) A.n_kmers[blockIdx.x] = tot;
@@ -606,7 +619,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
     uint32_t* qo = reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(cnt + TS) + BIN_WAVES * BIN_Q) +
                    (threadIdx.x >> 6) * BIN_Q;
     const uint32_t limit = TS - TS / 4;
-    const uint64_t nbins = A.totals[2];
+    const uint64_t nbins = min(A.totals[2], A.max_bins);
     const uint32_t tid = threadIdx.x;
 #ifdef KB_BIN_PROF
     unsigned long long pacc[16] = {};
@@ -620,8 +633,8 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
         __syncthreads();
         if (S.item >= nbins) break;  // uniform
         const uint32_t b = A.order[S.item];
-        const uint32_t lo = A.bstart[b], hi = A.bstart[b + 1];
-        const uint32_t mmer = (uint32_t)(A.keys[lo] >> 38);
+        const uint32_t lo = A.bstart[b], hi = lo + A.bcount[b];
+        const uint32_t mmer = A.bmmer[b];
 
         // occurrences of the bin -> first partition depth
         uint64_t occ = 0;
@@ -1234,15 +1247,14 @@ hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s) 
 // Bin processing order: descending log2(records) (longest-processing-time
 // first for the persistent blocks; a bin's cost follows its super-k-mers).
 // One block; counting sort over 33 classes.
-__global__ __launch_bounds__(1024) void bins_order_kernel(const uint32_t* __restrict__ bstart,
+__global__ __launch_bounds__(1024) void bins_order_kernel(const uint32_t* __restrict__ bcount,
                                                           const uint64_t* __restrict__ totals,
-                                                          uint32_t* __restrict__ order) {
+                                                          uint32_t* __restrict__ order, uint64_t max_bins) {
     __shared__ uint32_t hist[64];
-    const uint32_t nbins = (uint32_t)totals[2];
+    const uint32_t nbins = (uint32_t)min(totals[2], max_bins);
     if (threadIdx.x < 64) hist[threadIdx.x] = 0;
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbins; b += 1024)
-        atomicAdd(&hist[32 - __clz(bstart[b + 1] - bstart[b])], 1u);
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) atomicAdd(&hist[32 - __clz(bcount[b])], 1u);
     __syncthreads();
     if (threadIdx.x == 0) {  // exclusive offsets, class 32 first
         uint32_t acc = 0;
@@ -1253,12 +1265,238 @@ __global__ __launch_bounds__(1024) void bins_order_kernel(const uint32_t* __rest
         }
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbins; b += 1024)
-        order[atomicAdd(&hist[32 - __clz(bstart[b + 1] - bstart[b])], 1u)] = b;
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) order[atomicAdd(&hist[32 - __clz(bcount[b])], 1u)] = b;
 }
 
-hipError_t launch_bins_order(const uint32_t* bstart, const uint64_t* totals, uint32_t* order, hipStream_t s) {
-    hipLaunchKernelGGL(bins_order_kernel, dim3(1), dim3(1024), 0, s, bstart, totals, order);
+hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uint32_t* order, uint64_t max_bins,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(bins_order_kernel, dim3(1), dim3(1024), 0, s, bcount, totals, order, max_bins);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void bins_describe_kernel(const uint64_t* __restrict__ keys,
+                                                            const uint32_t* __restrict__ starts,
+                                                            const uint64_t* __restrict__ totals,
+                                                            uint32_t* __restrict__ bcount,
+                                                            uint32_t* __restrict__ bmmer, uint64_t max_bins) {
+    const uint64_t nbins = min(totals[2], max_bins);
+    for (uint64_t b = blockIdx.x * 256ull + threadIdx.x; b < nbins; b += (uint64_t)gridDim.x * 256) {
+        bcount[b] = starts[b + 1] - starts[b];
+        bmmer[b] = (uint32_t)(keys[starts[b]] >> 38);
+    }
+}
+
+hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, const uint64_t* totals,
+                                uint32_t* bcount, uint32_t* bmmer, uint64_t max_bins, hipStream_t s) {
+    const uint64_t blocks = std::min<uint64_t>((max_bins + 255) / 256, 1024);
+    hipLaunchKernelGGL(bins_describe_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, s, keys,
+                       starts, totals, bcount, bmmer, max_bins);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// bucket_kernel: one workgroup per local bucket.  The bucket's records (pay
+// layout, contiguous) are read twice: pass 1 maps each record's mmer to a
+// slot of a small LDS table and counts (slot, 63 - n); a block scan turns the
+// counts into positions; pass 2 places every record (SoA) so that each bin is
+// contiguous with its longest records first.  Bins are appended to the bin
+// descriptors.  Replaces a global radix sort + gather: no random reads, one
+// bucket per workgroup.
+// ---------------------------------------------------------------------------
+constexpr int BK_THREADS = 512;
+constexpr uint32_t BK_SLOTS = 256;  // mmers per bucket (a bucket with more is reported)
+constexpr uint32_t BK_ROWS = 32;    // k-mers per record: n <= K - M + 1 <= 31 (row 32 - n: longest first)
+
+DEV int bk_slot(uint32_t* keys, uint32_t mmer, bool insert) {
+    const uint32_t k = mmer + 1u;
+    uint32_t i = (uint32_t)((mix64((uint64_t)mmer) >> 32) & (BK_SLOTS - 1));
+    for (uint32_t p = 0; p < BK_SLOTS; p++) {
+        const uint32_t v = keys[i];
+        if (v == k) return (int)i;
+        if (v == 0) {
+            if (!insert) return -1;
+            const uint32_t old = atomicCAS(&keys[i], 0u, k);
+            if (old == 0 || old == k) return (int)i;
+        }
+        i = (i + 1) & (BK_SLOTS - 1);
+    }
+    return -1;
+}
+
+DEV void bk_record(const uint64_t* r, int M, uint64_t& h, uint64_t& a, uint64_t& b, uint32_t& canon, uint32_t& row) {
+    h = r[0];
+    a = r[1];
+    b = r[2];
+    const uint32_t maskM = (1u << (2 * M)) - 1u;
+    const int so = (int)((h >> 38) & 63u);
+    const uint32_t sm = (uint32_t)(span_window(a, b, 0ull, 0ull, so) >> (64 - 2 * M));
+    canon = ((h >> 44) & 1u) ? maskM - sm : sm;
+    row = 32u - (uint32_t)((h >> 32) & 63u);
+}
+
+__global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
+    __shared__ uint32_t keys[BK_SLOTS];
+    __shared__ uint32_t hist[BK_SLOTS * BK_ROWS];  // (slot, 32 - n) counts, then cursors
+    __shared__ uint64_t red[BK_THREADS / 64];
+    __shared__ unsigned long long s_base, s_bin;
+    __shared__ uint32_t s_nb, s_full;
+    const uint32_t tid = threadIdx.x, bk = blockIdx.x;
+    const uint64_t cnt = min<uint64_t>(A.bfill[bk], A.cap);
+    const uint64_t* src = A.regions + (uint64_t)bk * A.cap * 3;
+    for (uint32_t i = tid; i < BK_SLOTS; i += BK_THREADS) keys[i] = 0;
+    for (uint32_t i = tid; i < BK_SLOTS * BK_ROWS; i += BK_THREADS) hist[i] = 0;
+    if (tid == 0) {
+        s_nb = 0;
+        s_full = 0;
+    }
+    __syncthreads();
+    for (uint64_t i = tid; i < cnt; i += BK_THREADS) {
+        uint64_t h, a, b;
+        uint32_t canon, row;
+        bk_record(src + 3 * i, A.M, h, a, b, canon, row);
+        const int sl = bk_slot(keys, canon, true);
+        if (sl < 0) s_full = 1;
+        else atomicAdd(&hist[sl * BK_ROWS + row], 1u);
+    }
+    __syncthreads();
+    if (s_full) {  // uniform
+        if (tid == 0) atomicOr(A.status, ST_BUCKET_FULL);
+        return;
+    }
+    // exclusive scan of the counters in (slot, row) order
+    constexpr uint32_t PER = BK_SLOTS * BK_ROWS / BK_THREADS;
+    uint32_t loc[PER];
+    uint64_t mine = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        loc[k] = hist[tid * PER + k];
+        mine += loc[k];
+    }
+    const int lane = tid & 63, wid = tid >> 6;
+    const uint64_t inc = wave_incl_scan(mine, lane);
+    if (lane == 63) red[wid] = inc;
+    __syncthreads();
+    uint64_t wp = 0;
+    for (int w = 0; w < wid; w++) wp += red[w];
+    uint32_t run = (uint32_t)(wp + inc - mine);
+    if (tid == 0) s_base = cnt ? atomicAdd(A.rec_ctr, (unsigned long long)cnt) : 0ull;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        const uint32_t c = loc[k];
+        hist[tid * PER + k] = run;
+        run += c;
+    }
+    __syncthreads();
+    // count non-empty slots, reserve bin descriptors
+    const bool has = tid < BK_SLOTS && keys[tid] != 0;
+    if (has) atomicAdd(&s_nb, 1u);
+    __syncthreads();
+    if (tid == 0) s_bin = s_nb ? atomicAdd(A.bin_ctr, (unsigned long long)s_nb) : 0ull;
+    __syncthreads();
+    if (has) {
+        // dense index of this slot among non-empty ones: count set slots below
+        uint32_t below = 0;
+        for (uint32_t j = 0; j < tid; j++) below += keys[j] != 0;
+        const uint64_t bi = s_bin + below;
+        const uint32_t first = hist[tid * BK_ROWS];
+        const uint32_t last = tid + 1 < BK_SLOTS ? hist[(tid + 1) * BK_ROWS] : (uint32_t)cnt;
+        if (bi < A.max_bins) {
+            A.bstart[bi] = (uint32_t)s_base + first;
+            A.bcount[bi] = last - first;
+            A.bmmer[bi] = keys[tid] - 1u;
+        }
+    }
+    __syncthreads();
+    const uint64_t base = s_base;
+    for (uint64_t i = tid; i < cnt; i += BK_THREADS) {
+        uint64_t h, a, b;
+        uint32_t canon, row;
+        bk_record(src + 3 * i, A.M, h, a, b, canon, row);
+        const int sl = bk_slot(keys, canon, false);
+        const uint64_t pos = base + atomicAdd(&hist[sl * BK_ROWS + row], 1u);
+        A.hdr[pos] = h;
+        A.w0[pos] = a;
+        A.w1[pos] = b;
+    }
+}
+
+hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s) {
+    if (!NB) return hipSuccess;
+    hipLaunchKernelGGL(bucket_kernel, dim3(NB), dim3(BK_THREADS), 0, s, a);
+    return hipGetLastError();
+}
+
+// received routed records -> local bucket regions (pay layout, ordinal = id);
+// a block reserves one range per bucket for its 256 x 8 records
+__global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t* __restrict__ recs, uint64_t n_rec,
+                                                                 int rw, int M, uint32_t NB,
+                                                                 uint64_t* __restrict__ regions, uint64_t cap,
+                                                                 unsigned long long* bfill, uint32_t* status,
+                                                                 unsigned long long* n_kmers) {
+    constexpr int PERT = 8;
+    __shared__ uint32_t cnt[SK_MAX_DEST];
+    __shared__ unsigned long long base[SK_MAX_DEST];
+    const uint32_t maskM = (1u << (2 * M)) - 1u, halfM = 1u << (2 * M - 1);
+    bool neg = false;
+    uint64_t kmers = 0;
+    for (uint64_t k0 = (uint64_t)blockIdx.x * 256 * PERT; k0 < n_rec; k0 += (uint64_t)gridDim.x * 256 * PERT) {
+        for (uint32_t d = threadIdx.x; d < NB; d += 256) cnt[d] = 0;
+        __syncthreads();
+        uint32_t dst[PERT];
+        uint64_t pay0[PERT], pa[PERT], pb[PERT];
+#pragma unroll
+        for (int j = 0; j < PERT; j++) {
+            const uint64_t k = k0 + (uint64_t)j * 256 + threadIdx.x;
+            dst[j] = 0xFFFFFFFFu;
+            if (k >= n_rec) continue;
+            const uint64_t* r = recs + k * (uint64_t)rw;
+            const uint64_t h = r[0];
+            const uint64_t w0 = r[1], w1 = rw >= 3 ? r[2] : 0ull;
+            const uint32_t id = (uint32_t)h;
+            const uint64_t lo = (h >> 32) & 0xFFFFu, n = (h >> 48) & 63u, so = (h >> 54) & 63u;
+            const uint32_t sm = (uint32_t)(span_window(w0, w1, 0ull, 0ull, (int)so) >> (64 - 2 * M));
+            const bool rev = sm < halfM;  // complement wins (binning.c:1029-1040)
+            const uint32_t canon = rev ? maskM - sm : sm;
+            neg |= (int32_t)id < 0;
+            kmers += n;
+            pay0[j] = (uint64_t)id | (n << 32) | (so << 38) | ((uint64_t)rev << 44) | (lo << 45);
+            pa[j] = w0;
+            pb[j] = w1;
+            dst[j] = dest_of(canon, NB, BUCKET_SALT);
+            atomicAdd(&cnt[dst[j]], 1u);
+        }
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d < NB; d += 256) {
+            base[d] = cnt[d] ? atomicAdd(&bfill[d], (unsigned long long)cnt[d]) : 0ull;
+            cnt[d] = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PERT; j++) {
+            if (dst[j] == 0xFFFFFFFFu) continue;
+            const uint64_t slot = base[dst[j]] + atomicAdd(&cnt[dst[j]], 1u);
+            if (slot >= cap) continue;  // counted: the caller retries bigger
+            uint64_t* o = regions + ((uint64_t)dst[j] * cap + slot) * 3;
+            o[0] = pay0[j];
+            o[1] = pa[j];
+            o[2] = pb[j];
+        }
+        __syncthreads();
+    }
+    if (neg) atomicOr(status, ST_NEG_ID);
+    __shared__ uint64_t sh[4];
+    kmers = block_sum256(kmers, sh);
+    if (threadIdx.x == 0 && kmers) atomicAdd(n_kmers, (unsigned long long)kmers);
+}
+
+hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int M, uint32_t NB,
+                                     uint64_t* regions, uint64_t cap, unsigned long long* bfill,
+                                     uint32_t* status, unsigned long long* n_kmers, hipStream_t s) {
+    if (!n_rec) return hipSuccess;
+    if (NB < 1 || NB > SK_MAX_DEST) return hipErrorInvalidValue;
+    const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
+    hipLaunchKernelGGL(sk_convert_buckets_kernel, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M, NB,
+                       regions, cap, bfill, status, n_kmers);
     return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ constexpr uint32_t ST_TABLE_FULL = 1u;   // distinct keys exceeded the load limi
 constexpr uint32_t ST_PROBE_LIMIT = 2u;  // a probe sequence exceeded max_probe
 constexpr uint32_t ST_ALPHABET = 4u;     // byte outside ACGT in packed input
 constexpr uint32_t ST_NEG_ID = 8u;       // a routed read id < 0 (the binned receiver orders lists by id)
+constexpr uint32_t ST_BUCKET_FULL = 16u; // a local bucket holds more mmers than bucket_kernel maps
 
 struct ScanArgs {
     const uint64_t* words;     // packed reads, RW words per read
@@ -91,23 +92,48 @@ struct SkScanArgs {
                                // (a wavefront's 64 records have near-equal k-mer counts)
     uint32_t ord_base;
     int RW, K, M;
-    // route mode (thread kernel, with rec_ctr == nullptr): records go to
-    // regions + (dest * region_cap + i) * rw in the routed format
+    // region mode (thread kernel, with rec_ctr == nullptr): records go to
+    // regions + (dest * region_cap + i) * rw, dest = hash(mmer + dest_salt) % G:
+    // routing (ranks, routed format with the read id) or local buckets
+    // (binned_fmt: the pay layout with the ordinal, rw = 3)
     uint64_t* regions;
     uint64_t region_cap;
     unsigned long long* dest_ctr;  // [G] records per destination (zeroed)
     const int32_t* read_ids;       // ordinal -> id (null: affine, id = ordinal + id_off)
     uint32_t id_off;
-    uint32_t G;
+    uint32_t G;                    // <= 1024
+    uint64_t dest_salt;
     int rw;
+    int binned_fmt;
+};
+
+// local buckets: every record of a bin lands in bucket dest_of(mmer, NB, BUCKET_SALT);
+// bucket_kernel then orders each bucket's records by (mmer, 63 - n)
+struct BucketArgs {
+    const uint64_t* regions;   // NB regions of cap records, pay layout (3 words)
+    uint64_t cap;
+    const unsigned long long* bfill;  // [NB] records per bucket
+    int M;
+    uint64_t* hdr;             // [R] SoA output, bins contiguous, longest records first
+    uint64_t* w0;
+    uint64_t* w1;
+    unsigned long long* rec_ctr;   // output allocation (zeroed)
+    unsigned long long* bin_ctr;   // bins (zeroed; = totals[2])
+    uint32_t* bstart;          // [max_bins] first record of bin
+    uint32_t* bcount;          // [max_bins] records of bin
+    uint32_t* bmmer;           // [max_bins] the bin's canonical mmer
+    uint64_t max_bins;
+    uint32_t* status;          // ST_BUCKET_FULL: a bucket holds too many mmers
 };
 
 struct BinArgs {
-    const uint64_t* keys;      // sorted by (mmer, 63 - n); mmer = key >> 38
     const uint64_t* hdr;       // [R] bin-ordered record headers (see SkScanArgs::pay)
     const uint64_t* w0;        // [R] span bases 0..31
     const uint64_t* w1;        // [R] span bases 32..63
-    const uint32_t* bstart;    // [nbins + 1]
+    const uint32_t* bstart;    // [nbins] first record of bin
+    const uint32_t* bcount;    // [nbins] records of bin
+    const uint32_t* bmmer;     // [nbins] canonical mmer of bin
+    uint64_t max_bins;         // capacity of the descriptors (nbins never exceeds it)
     unsigned long long* stage_ctr;  // stage allocation (zeroed): each bin takes its occurrences
     const uint32_t* order;     // [nbins] processing order (largest bins first)
     unsigned long long* work;  // work counter (zeroed)
@@ -162,7 +188,17 @@ hipError_t launch_sk_kmers_total(const unsigned long long* part, uint64_t n, uns
 hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
                             hipStream_t s);
 hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s);
-hipError_t launch_bins_order(const uint32_t* bstart, const uint64_t* totals, uint32_t* order, hipStream_t s);
+hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uint32_t* order, uint64_t max_bins,
+                             hipStream_t s);
+hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s);
+uint64_t sk_bucket_salt();
+// radix path: bin descriptors from run starts of the sorted keys
+hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, const uint64_t* totals,
+                                uint32_t* bcount, uint32_t* bmmer, uint64_t max_bins, hipStream_t s);
+// received records into local bucket regions (block-aggregated reservations)
+hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int M, uint32_t NB,
+                                     uint64_t* regions, uint64_t cap, unsigned long long* bfill,
+                                     uint32_t* status, unsigned long long* n_kmers, hipStream_t s);
 size_t bins_lds_bytes(uint32_t ts_log2);
 #ifdef KB_BIN_PROF
 void bins_prof_report(hipStream_t s);

@@ -105,6 +105,23 @@ def test_binned_engine_selected(engine):
         assert t["n_superkmers"] > 0 and t["n_bins"] > 0
 
 
+@pytest.mark.parametrize("K,M", [(31, 7), (6, 3), (21, 5), (2, 1)])
+def test_binned_radix_path(K, M, engine, monkeypatch):
+    """the binned engine's radix-sort record path (the fallback when a local
+    bucket holds too many mmers, and the path for reads > 512 bp) matches the
+    oracle as the default bucketed path does"""
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    monkeypatch.setenv("KB_BIN_RADIX", "1")
+    rng = np.random.default_rng(K * 100 + M)
+    reads = [rng.choice(np.frombuffer(b"ACGT", np.uint8), int(rng.integers(K, 300))).tobytes()
+             for _ in range(400)]
+    bases, lens = kbin.pack_reads(reads)
+    ora = oracle.bin_reads(bases, lens, K, M, 1, True)
+    res = gpu_result(bases, lens, K, M, 1, True)
+    assert_same(res, ora)
+
+
 def test_explicit_ids_nonmonotone():
     """ids are caller-supplied (process_read's read_id): lists keep REVERSE CALL
     order, not id order (binning.c:1065-1068)."""
