@@ -970,7 +970,9 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     for (auto& b : c->batches)
         if (!b.routed && !b.superkmers && b.RW > 16) all_short = false;
     const bool bucketed = all_short && env_int("KB_BIN_RADIX", 0) == 0 && !c->bucket_failed;
-    const uint32_t NB = 512;
+    // local buckets (power of two, <= 1024): more buckets, more workgroups in flight
+    uint32_t NB = 1;
+    while (NB < (uint32_t)std::min(1024, std::max(64, env_int("KB_BIN_NB", 1024)))) NB <<= 1;
     int rc = bucketed ? binned_buckets(c, NB, received, R, N)
                       : (received ? binned_sk_records(c, R, N) : binned_read_records(c, R, N, false));
     if (rc) return rc;

@@ -1323,10 +1323,7 @@ DEV int bk_slot(uint32_t* keys, uint32_t mmer, bool insert) {
     return -1;
 }
 
-DEV void bk_record(const uint64_t* r, int M, uint64_t& h, uint64_t& a, uint64_t& b, uint32_t& canon, uint32_t& row) {
-    h = r[0];
-    a = r[1];
-    b = r[2];
+DEV void bk_decode(uint64_t h, uint64_t a, uint64_t b, int M, uint32_t& canon, uint32_t& row) {
     const uint32_t maskM = (1u << (2 * M)) - 1u;
     const int so = (int)((h >> 38) & 63u);
     const uint32_t sm = (uint32_t)(span_window(a, b, 0ull, 0ull, so) >> (64 - 2 * M));
@@ -1350,13 +1347,27 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
         s_full = 0;
     }
     __syncthreads();
-    for (uint64_t i = tid; i < cnt; i += BK_THREADS) {
-        uint64_t h, a, b;
-        uint32_t canon, row;
-        bk_record(src + 3 * i, A.M, h, a, b, canon, row);
-        const int sl = bk_slot(keys, canon, true);
-        if (sl < 0) s_full = 1;
-        else atomicAdd(&hist[sl * BK_ROWS + row], 1u);
+    constexpr int U = 4;  // records in flight per thread
+    for (uint64_t i0 = tid; i0 < cnt; i0 += U * BK_THREADS) {
+        uint64_t h[U], a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t i = i0 + (uint64_t)u * BK_THREADS;
+            if (i < cnt) {
+                h[u] = src[3 * i];
+                a[u] = src[3 * i + 1];
+                b[u] = src[3 * i + 2];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (i0 + (uint64_t)u * BK_THREADS >= cnt) break;
+            uint32_t canon, row;
+            bk_decode(h[u], a[u], b[u], A.M, canon, row);
+            const int sl = bk_slot(keys, canon, true);
+            if (sl < 0) s_full = 1;
+            else atomicAdd(&hist[sl * BK_ROWS + row], 1u);
+        }
     }
     __syncthreads();
     if (s_full) {  // uniform
@@ -1408,15 +1419,28 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     }
     __syncthreads();
     const uint64_t base = s_base;
-    for (uint64_t i = tid; i < cnt; i += BK_THREADS) {
-        uint64_t h, a, b;
-        uint32_t canon, row;
-        bk_record(src + 3 * i, A.M, h, a, b, canon, row);
-        const int sl = bk_slot(keys, canon, false);
-        const uint64_t pos = base + atomicAdd(&hist[sl * BK_ROWS + row], 1u);
-        A.hdr[pos] = h;
-        A.w0[pos] = a;
-        A.w1[pos] = b;
+    for (uint64_t i0 = tid; i0 < cnt; i0 += U * BK_THREADS) {
+        uint64_t h[U], a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t i = i0 + (uint64_t)u * BK_THREADS;
+            if (i < cnt) {
+                h[u] = src[3 * i];
+                a[u] = src[3 * i + 1];
+                b[u] = src[3 * i + 2];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (i0 + (uint64_t)u * BK_THREADS >= cnt) break;
+            uint32_t canon, row;
+            bk_decode(h[u], a[u], b[u], A.M, canon, row);
+            const int sl = bk_slot(keys, canon, false);
+            const uint64_t pos = base + atomicAdd(&hist[sl * BK_ROWS + row], 1u);
+            A.hdr[pos] = h[u];
+            A.w0[pos] = a[u];
+            A.w1[pos] = b[u];
+        }
     }
 }
 
