@@ -245,3 +245,28 @@ def test_full_scale_engines_agree(engine):
     assert a.n_entries == b.n_entries
     for f in ("mmer", "kmer_hi", "kmer_lo", "count", "offset", "ids"):
         np.testing.assert_array_equal(getattr(a, f), getattr(b, f))
+
+
+def test_edge_inputs_and_context_reuse(engine):
+    """empty input, reads shorter than K, one read, then a context reused
+    across very different sizes (the binned engine's learned bucket capacity
+    is exceeded and the record pass reruns)"""
+    rng = np.random.default_rng(11)
+    K, M = 31, 7
+    with kbin.Engine(K, M, cutoff=1, max_read_len=300) as eng:
+        eng.finalize(prune=True)  # nothing submitted
+        assert eng.export().n_entries == 0
+        eng.reset()
+        eng.submit([b"ACGT" * 5, b"A" * 30])  # all shorter than K
+        eng.finalize(prune=False)
+        r = eng.export()
+        assert r.n_entries == 0 and len(r.ids) == 0
+        for n in (1, 40, 5000, 300):  # small -> large -> small
+            reads = [rng.choice(np.frombuffer(b"ACGT", np.uint8), int(rng.integers(K, 300))).tobytes()
+                     for _ in range(n)]
+            reads += reads[: n // 3]  # repeats -> counts > 1 survive the prune
+            bases, lens = kbin.pack_reads(reads)
+            eng.reset()
+            eng.submit(bases=bases, lens=lens, first_id=0)
+            eng.finalize(prune=True)
+            assert_same(eng.export(), oracle.bin_reads(bases, lens, K, M, 1, True))
