@@ -412,10 +412,10 @@ static int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
-// the binned engine (kbin_bins.hip) serves K <= 31 without first-occurrence
-// tracking unless the table engine is forced (flag, or KB_ENGINE=table)
+// the binned engine (kbin_bins.hip) serves K <= 31 unless the table engine is
+// forced (flag, or KB_ENGINE=table)
 static bool binned_applies(const kb_ctx* c) {
-    if (c->KW != 1 || (c->p.flags & KB_TRACK_FIRST)) return false;
+    if (c->KW != 1) return false;
     if (c->p.flags & KB_ENGINE_BINNED) return true;
     if (c->p.flags & KB_ENGINE_TABLE) return false;
     const char* e = getenv("KB_ENGINE");
@@ -1063,6 +1063,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     a.e_lo = c->e_lo.p;
     a.e_cnt = c->e_cnt.p;
     a.e_off = c->e_off.p;
+    a.e_first = nullptr;
+    if (c->p.flags & KB_TRACK_FIRST) {
+        HIPCHK(c->e_first.ensure(ecap));
+        a.e_first = c->e_first.p;
+    }
     a.ids_ord = reinterpret_cast<uint32_t*>(bucketed || c->sorted == c->occ_a.p ? c->occ_b.p : c->occ_a.p);
     a.ids_out = c->ids_out.p;
     a.read_ids = affine ? nullptr : c->read_ids.p;

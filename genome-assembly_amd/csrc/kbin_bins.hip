@@ -550,7 +550,7 @@ DEV uint32_t part_of(uint64_t code) { return (uint32_t)((code * 0x9E3779B97F4A7C
 
 template <typename F>
 DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, uint32_t l,
-                       uint64_t* qk, uint32_t* qo, uint32_t* ctr, F&& f) {
+                       uint64_t* qk, uint32_t* qo, uint16_t* qp, uint32_t* ctr, F&& f) {
     const int K = A.K;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t kmask = (1ull << (2 * K)) - 1ull;
@@ -563,7 +563,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
         b = (uint32_t)__shfl((int)b, 0, 64);
         const uint32_t i0 = (head + lane) & (BIN_Q - 1), i1 = (head + 64 + lane) & (BIN_Q - 1);
         const bool v0 = (uint32_t)lane < cnt, v1 = (uint32_t)lane + 64 < cnt;
-        f(qk[i0], qo[i0], b + lane, v0, qk[i1], qo[i1], b + 64 + lane, v1);
+        f(qk[i0], qo[i0], qp[i0], b + lane, v0, qk[i1], qo[i1], qp[i1], b + 64 + lane, v1);
         head = (head + cnt) & (BIN_Q - 1);
         fill -= cnt;
         wave_sync();
@@ -586,6 +586,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
         }
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
+        const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);  // the record's first k-mer in its read
         const uint64_t flip = ((hd >> 44) & 1ull) ? kmask : 0ull;
         // records of a bin are sorted longest first: lane 0 holds the chunk's max
         int nmax = rfl(n);
@@ -601,6 +602,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
                 const uint32_t pos = (head + fill + lanes_below(m)) & (BIN_Q - 1);
                 qk[pos] = code + 1ull;
                 qo[pos] = ord;
+                qp[pos] = (uint16_t)(rlo + (uint32_t)j);
             }
             fill += (uint32_t)__popcll(m);
             if (fill >= 128) flush(128);
@@ -617,6 +619,10 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
     uint32_t* cnt = reinterpret_cast<uint32_t*>(claim + TS);  // [TS] count, then cursor
     uint64_t* qk = reinterpret_cast<uint64_t*>(cnt + TS) + (threadIdx.x >> 6) * BIN_Q;
     uint32_t* qo = reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(cnt + TS) + BIN_WAVES * BIN_Q) +
+                   (threadIdx.x >> 6) * BIN_Q;
+    uint16_t* qp = reinterpret_cast<uint16_t*>(reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(cnt + TS) +
+                                                                           BIN_WAVES * BIN_Q) +
+                                               BIN_WAVES * BIN_Q) +
                    (threadIdx.x >> 6) * BIN_Q;
     const uint32_t limit = TS - TS / 4;
     const uint64_t nbins = min(A.totals[2], A.max_bins);
@@ -684,9 +690,10 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             PROF_CNT(8, 1);
             // ---- sweep 1: insert + count (binning.c:1042-1069 semantics per key)
             // each occurrence is staged as (slot, ordinal) for sweep 2
-            for_each_kmer(A, lo, hi, P, Lv, qk, qo, &S.n_stage,
-                          [&](uint64_t k0, uint32_t o0, uint32_t s0, bool v0, uint64_t k1, uint32_t o1,
-                              uint32_t s1, bool v1) {
+            // stage entry: LDS slot << 48 | position in the read << 32 | call ordinal
+            for_each_kmer(A, lo, hi, P, Lv, qk, qo, qp, &S.n_stage,
+                          [&](uint64_t k0, uint32_t o0, uint16_t p0, uint32_t s0, bool v0, uint64_t k1, uint32_t o1,
+                              uint16_t p1, uint32_t s1, bool v1) {
 #ifdef KB_BIN_PROF
                 if (A.ablate == 1) return;  // expansion only
 #endif
@@ -707,7 +714,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
 #ifdef KB_BIN_PROF
                         if (A.ablate != 2)
 #endif
-                        stage[s0] = ((uint64_t)l0 << 32) | o0;
+                        stage[s0] = ((uint64_t)l0 << 48) | ((uint64_t)p0 << 32) | o0;
                     }
                 }
                 if (v1) {
@@ -718,7 +725,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
 #ifdef KB_BIN_PROF
                         if (A.ablate != 2)
 #endif
-                        stage[s1] = ((uint64_t)l1 << 32) | o1;
+                        stage[s1] = ((uint64_t)l1 << 48) | ((uint64_t)p1 << 32) | o1;
                     }
                 }
             });
@@ -779,6 +786,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                             A.e_cnt[ge] = c;
                             A.e_off[ge] = i0 + off;
                         }
+                        if (A.e_first) claim[i] = ~0ull;  // first occurrence (min) from sweep 2 on
                         cnt[i] = off;  // cursor (relative to i0)
                         e++;
                         off += c;
@@ -800,11 +808,24 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
 #endif
                 for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
                     const uint64_t v = stage[i];
-                    const uint32_t ls = (uint32_t)(v >> 32);
+                    const uint32_t ls = (uint32_t)(v >> 48);
                     if (cnt[ls] != NONE) {
                         const uint32_t pos = atomicAdd(&cnt[ls], 1u);
                         A.ids_ord[i0 + pos] = (uint32_t)v;
+                        // (ordinal << 16 | position): binning.c inserts a key at its first
+                        // occurrence (1045-1057); KB_TRACK_FIRST keeps it for the zhash layout
+                        if (A.e_first)
+                            atomicMin((unsigned long long*)&claim[ls],
+                                      (unsigned long long)(((v & 0xFFFFFFFFull) << 16) | ((v >> 32) & 0xFFFFull)));
                     }
+                }
+            }
+            if (A.e_first) {
+                __syncthreads();
+                uint32_t e = (uint32_t)ex;
+                for (uint32_t k = 0; k < per; k++) {
+                    const uint32_t i = tid * per + k;
+                    if (cnt[i] != NONE) A.e_first[e0 + e++] = claim[i];
                 }
             }
             __threadfence_block();
@@ -1527,7 +1548,7 @@ hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int r
 size_t bins_lds_bytes(uint32_t ts_log2) {
     const size_t TS = (size_t)1 << ts_log2;
     return sizeof(BinShared) + TS * (sizeof(uint64_t) + sizeof(uint32_t)) +
-           (size_t)BIN_WAVES * BIN_Q * (sizeof(uint64_t) + sizeof(uint32_t));
+           (size_t)BIN_WAVES * BIN_Q * (sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint16_t));
 }
 
 hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s) {

@@ -137,7 +137,7 @@ struct BinArgs {
     unsigned long long* stage_ctr;  // stage allocation (zeroed): each bin takes its occurrences
     const uint32_t* order;     // [nbins] processing order (largest bins first)
     unsigned long long* work;  // work counter (zeroed)
-    uint64_t* stage;           // [N] (LDS slot << 32 | ordinal) per occurrence, bin-local ranges
+    uint64_t* stage;           // [N] (LDS slot << 48 | position << 32 | ordinal) per occurrence
     const uint64_t* totals;    // totals[2] = nbins
     int K, M;
     uint32_t keep_gt;
@@ -151,6 +151,7 @@ struct BinArgs {
     uint64_t* e_lo;
     uint32_t* e_cnt;
     uint64_t* e_off;
+    uint64_t* e_first;         // KB_TRACK_FIRST: (ordinal << 16 | position) of each key's first occurrence
     uint32_t* ids_ord;
     int32_t* ids_out;
     const int32_t* read_ids;
