@@ -656,7 +656,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
         PROF_CNT(14, occ_tot);
         uint32_t l0 = 0;  // uniform: initial partition depth from the expected distinct keys
         {
-            const double want = (double)occ_tot * A.rho / (0.6 * TS);
+            const double want = (double)occ_tot * A.rho / ((double)A.fill * TS);
             while ((double)(1u << l0) < want && l0 < 16) l0++;
         }
         for (uint32_t p0 = 0; p0 < (1u << l0); p0++) {

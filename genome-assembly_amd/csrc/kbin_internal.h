@@ -143,6 +143,7 @@ struct BinArgs {
     uint32_t keep_gt;
     uint32_t ts_log2;
     float rho;                 // expected distinct keys per occurrence
+    float fill;                // target table load when choosing the partition depth
     int ablate;                // diagnostic build (KB_BIN_PROF) only: 1 expansion only, 2 no staging
     unsigned long long* gcount;  // [0] entries << 32 | ids  [2] distinct keys before prune
     uint32_t* status;
