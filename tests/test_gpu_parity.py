@@ -214,14 +214,14 @@ def test_dropin_reference_program(golden_dir):
         pytest.skip("drop-in binaries not built (needs the reference at build time)")
 
 
-def test_full_scale_engines_agree(engine):
-    """BASELINE C2 size (1M x 150 bp, K31 M7, cutoff 1): both engines produce
-    the same canonical result; CSR contract, prune, list order by property
-    (affine ids: every list strictly non-increasing)"""
+@pytest.mark.parametrize("n,L,K,M", [(1_000_000, 150, 31, 7), (400_000, 250, 27, 6)])
+def test_full_scale_engines_agree(engine, n, L, K, M):
+    """BASELINE C2 size (1M x 150 bp, K31 M7, cutoff 1) and a longer-read
+    variant: both engines produce the same canonical result; CSR contract,
+    prune, list order by property (affine ids: every list non-increasing)"""
     if engine == "binned":
         pytest.skip("runs both engines itself")
     import torch
-    n, L = 1_000_000, 150
     wpr = (L + 31) // 32
     words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
     lens = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -229,7 +229,7 @@ def test_full_scale_engines_agree(engine):
     torch.cuda.synchronize()
     out = {}
     for flag in (kbin.KB_ENGINE_TABLE, kbin.KB_ENGINE_BINNED):
-        with kbin.Engine(31, 7, cutoff=1, max_read_len=L, flags=flag) as eng:
+        with kbin.Engine(K, M, cutoff=1, max_read_len=L, flags=flag) as eng:
             eng.set_timing(True)
             eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
             eng.finalize(True)
