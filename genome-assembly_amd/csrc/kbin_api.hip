@@ -140,6 +140,7 @@ struct kb_ctx {
     float rho = 0.f;           // learned distinct / occurrences
     bool bucket_failed = false;  // a bucket overflowed its mmer map: radix path from now on
     uint64_t n_occ_entries_hint = 0;  // entries of the last finalize (lists grid)
+    uint64_t ecap_hint = 0;    // entry capacity for the next binned finalize
     uint64_t* h_totals = nullptr;
     uint32_t* h_misc = nullptr;
 
@@ -960,7 +961,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     REC(0);
     HIPCHK(c->totals.ensure(16));
     HIPCHK(hipMemsetAsync(c->totals.p, 0, 16 * sizeof(uint64_t), c->s));
-    HIPCHK(hipMemsetAsync(c->misc.p, 0, 2 * sizeof(uint32_t), c->s));
+    HIPCHK(hipMemsetAsync(c->misc.p, 0, 3 * sizeof(uint32_t), c->s));
     REC(1);
     c->tm.scan_insert_launches = 0;
     uint64_t R = 0, N = 0;
@@ -1027,95 +1028,110 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     HIPCHK(c->border.ensure(max_bins));
     HIPCHK(launch_bins_order(c->bcount.p, c->totals.p, c->border.p, max_bins, c->s));
     REC(3);
-    // ---- one workgroup per bin
-    const uint64_t ecap = N + 1;
-    HIPCHK(c->e_mmer.ensure(ecap));
-    HIPCHK(c->e_cnt.ensure(ecap));
-    HIPCHK(c->e_hi.ensure(ecap));
-    HIPCHK(c->e_lo.ensure(ecap));
-    HIPCHK(c->e_off.ensure(ecap));
+    // ---- one workgroup per bin.  Entry capacity: learned (or N/8), rerun once
+    // with the exact need when the packed counter says it was exceeded.
     HIPCHK(c->ids_out.ensure(std::max<uint64_t>(N, 1)));
-    // >= 10: the sort phase carves 8 wave windows of 256 ids out of the table
     const int ts_log2 = std::min(13, std::max(10, env_int("KB_BIN_TS_LOG2", 13)));
+    uint64_t ecap = std::min<uint64_t>(N + 1, c->ecap_hint ? c->ecap_hint : N / 8 + 1024);
+    if (const int forced = env_int("KB_BIN_ECAP0", 0)) ecap = (uint64_t)forced;  // tests: force the rerun
     BinArgs a{};
-    a.hdr = c->srec.p;
-    a.w0 = c->srec.p + R;
-    a.w1 = c->srec.p + 2 * R;
-    a.bstart = c->starts.p;
-    a.bcount = c->bcount.p;
-    a.bmmer = c->bmmer.p;
-    a.max_bins = max_bins;
-    a.stage_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 10);
-    a.order = c->border.p;
-    a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
-    a.stage = c->stage.p;
-    a.totals = c->totals.p;
-    a.K = c->p.K;
-    a.M = M;
-    a.keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
-    a.ts_log2 = (uint32_t)ts_log2;
-    a.rho = c->rho > 0.f ? c->rho : 0.25f;
-    a.fill = (float)std::min(0.74, std::max(0.3, env_int("KB_BIN_FILL_PCT", 60) / 100.0));
-    a.ablate = env_int("KB_BIN_ABLATE", 0);
-    a.gcount = reinterpret_cast<unsigned long long*>(c->totals.p + 4);
-    a.status = c->misc.p;
-    a.e_mmer = c->e_mmer.p;
-    a.e_hi = c->e_hi.p;
-    a.e_lo = c->e_lo.p;
-    a.e_cnt = c->e_cnt.p;
-    a.e_off = c->e_off.p;
-    a.e_first = nullptr;
-    if (c->p.flags & KB_TRACK_FIRST) {
-        HIPCHK(c->e_first.ensure(ecap));
-        a.e_first = c->e_first.p;
-    }
-    a.ids_ord = reinterpret_cast<uint32_t*>(bucketed || c->sorted == c->occ_a.p ? c->occ_b.p : c->occ_a.p);
-    a.ids_out = c->ids_out.p;
-    a.read_ids = affine ? nullptr : c->read_ids.p;
-    a.id_off = (uint32_t)(affine ? id_c : 0);
-    a.max_entries = N;
-    a.max_ids = N;
-    HIPCHK(launch_bins(a, max_bins, c->s));
+    for (int attempt = 0;; attempt++) {
+        HIPCHK(c->e_mmer.ensure(ecap));
+        HIPCHK(c->e_cnt.ensure(ecap));
+        HIPCHK(c->e_hi.ensure(ecap));
+        HIPCHK(c->e_lo.ensure(ecap));
+        HIPCHK(c->e_off.ensure(ecap));
+        if (attempt) {  // the bin kernel's counters and status start again
+            HIPCHK(hipMemsetAsync(c->totals.p + 4, 0, 4 * sizeof(uint64_t), c->s));
+            HIPCHK(hipMemsetAsync(c->totals.p + 10, 0, sizeof(uint64_t), c->s));
+            HIPCHK(hipMemsetAsync(c->misc.p + 2, 0, sizeof(uint32_t), c->s));
+            REC(3);
+        }
+        a = BinArgs{};
+        a.hdr = c->srec.p;
+        a.w0 = c->srec.p + R;
+        a.w1 = c->srec.p + 2 * R;
+        a.bstart = c->starts.p;
+        a.bcount = c->bcount.p;
+        a.bmmer = c->bmmer.p;
+        a.max_bins = max_bins;
+        a.stage_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 10);
+        a.order = c->border.p;
+        a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
+        a.stage = c->stage.p;
+        a.totals = c->totals.p;
+        a.K = c->p.K;
+        a.M = M;
+        a.keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
+        a.ts_log2 = (uint32_t)ts_log2;
+        a.rho = c->rho > 0.f ? c->rho : 0.25f;
+        a.fill = (float)std::min(0.74, std::max(0.3, env_int("KB_BIN_FILL_PCT", 60) / 100.0));
+        a.ablate = env_int("KB_BIN_ABLATE", 0);
+        a.gcount = reinterpret_cast<unsigned long long*>(c->totals.p + 4);
+        a.status = c->misc.p + 2;  // the bin kernel's own status word
+        a.e_mmer = c->e_mmer.p;
+        a.e_hi = c->e_hi.p;
+        a.e_lo = c->e_lo.p;
+        a.e_cnt = c->e_cnt.p;
+        a.e_off = c->e_off.p;
+        a.e_first = nullptr;
+        if (c->p.flags & KB_TRACK_FIRST) {
+            HIPCHK(c->e_first.ensure(ecap));
+            a.e_first = c->e_first.p;
+        }
+        a.ids_ord = reinterpret_cast<uint32_t*>(bucketed || c->sorted == c->occ_a.p ? c->occ_b.p : c->occ_a.p);
+        a.ids_out = c->ids_out.p;
+        a.read_ids = affine ? nullptr : c->read_ids.p;
+        a.id_off = (uint32_t)(affine ? id_c : 0);
+        a.max_entries = ecap - 1;
+        a.max_ids = N;
+        HIPCHK(launch_bins(a, max_bins, c->s));
 #ifdef KB_BIN_PROF
-    bins_prof_report(c->s);
+        bins_prof_report(c->s);
 #endif
-    HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries, c->s));
-    REC(4);
-    ListArgs la{};
-    la.totals = c->totals.p;
-    la.e_cnt = c->e_cnt.p;
-    la.e_off = c->e_off.p;
-    la.ids_ord = a.ids_ord;
-    la.ids_out = c->ids_out.p;
-    la.read_ids = a.read_ids;
-    la.id_off = a.id_off;
-    HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : N / 8 + 1, c->s));
-#ifdef KB_BIN_PROF
-    lists_prof_report(c->s);
-#endif
-    REC(5);
-    HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
-    if (R && !bucketed)
-        HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
-    else c->h_misc[8] = 0;
-    HIPCHK(hipStreamSynchronize(c->s));
-    if (c->h_misc[0] & ST_BUCKET_FULL) {  // a bucket held too many mmers: redo with the radix path
-        c->bucket_failed = true;
-        c->finalized = false;
-        return finalize_binned(c, prune, affine, id_c, received);
+        HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries, c->s));
+        REC(4);
+        ListArgs la{};
+        la.totals = c->totals.p;
+        la.e_cnt = c->e_cnt.p;
+        la.e_off = c->e_off.p;
+        la.ids_ord = a.ids_ord;
+        la.ids_out = c->ids_out.p;
+        la.read_ids = a.read_ids;
+        la.id_off = a.id_off;
+        HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : ecap, c->s));
+        REC(5);
+        HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        if (R && !bucketed)
+            HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        else c->h_misc[8] = 0;
+        HIPCHK(hipStreamSynchronize(c->s));
+        if (c->h_misc[0] & ST_BUCKET_FULL) {  // a bucket held too many mmers: redo with the radix path
+            c->bucket_failed = true;
+            c->finalized = false;
+            return finalize_binned(c, prune, affine, id_c, received);
+        }
+        const uint64_t need = (c->h_totals[4] >> 32) + 1;  // entries asked of the packed counter
+        if ((c->h_misc[2] & ST_TABLE_FULL) && attempt == 0 && need > ecap) {
+            ecap = need + need / 16 + 1024;
+            continue;
+        }
+        break;
     }
+    const uint32_t bst = c->h_misc[2];
     if (c->h_misc[8]) return fail(KB_EDEVICE, "radix look-back timed out (device error word %u)", c->h_misc[8]);
     if (c->h_totals[3]) return fail(KB_EDEVICE, "internal: %llu bins > %llu", (unsigned long long)c->h_totals[3],
                                     (unsigned long long)max_bins);
-    if (c->h_misc[0] & ST_TABLE_FULL) return fail(KB_EDEVICE, "internal: CSR capacity exceeded");
+    if (bst & ST_TABLE_FULL) return fail(KB_EDEVICE, "internal: CSR capacity exceeded");
     if (c->h_misc[0] & ST_NEG_ID)
         return fail(KB_EINVAL, "routed read ids must be non-negative (they order the id lists)");
-    if (c->h_misc[0] & ST_PROBE_LIMIT) return fail(KB_ENOMEM, "a bin exceeded the partition depth");
+    if (bst & ST_PROBE_LIMIT) return fail(KB_ENOMEM, "a bin exceeded the partition depth");
     c->n_entries = c->h_totals[0];
     c->n_ids = c->h_totals[1];
     c->n_distinct = c->h_totals[6];
     c->n_occ_entries_hint = c->n_entries;
+    c->ecap_hint = c->n_entries + c->n_entries / 4 + 1024;
     if (N) c->rho = (float)((double)c->n_distinct / (double)N);
     if (c->timing) {
         HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));

@@ -1568,9 +1568,11 @@ hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s) {
 
 __global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                                   uint64_t max_entries) {
-    // on overflow the counters ran past the capacity (status says so): clamp
+    // on overflow the counters ran past the capacity (status says so) and the
+    // bins past it wrote nothing, so no entry range is whole: publish none (the
+    // lists kernel then has no work and the host reruns at the exact need)
     const uint64_t ne0 = gcount[0] >> 32, ni = gcount[0] & 0xFFFFFFFFull;
-    const uint64_t ne = ne0 < max_entries ? ne0 : max_entries;
+    const uint64_t ne = ne0 <= max_entries ? ne0 : 0;
     totals[0] = ne;
     totals[1] = ni;
     e_off[ne] = ni;

@@ -122,6 +122,25 @@ def test_binned_radix_path(K, M, engine, monkeypatch):
     assert_same(res, ora)
 
 
+@pytest.mark.parametrize("prune", [False, True])
+def test_binned_entry_capacity_rerun(prune, engine, monkeypatch):
+    """the binned engine sizes its entry arrays from a learned estimate; when
+    the estimate is too small the bin phase reruns at the exact need (forced
+    here with a 64-entry first attempt)"""
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    monkeypatch.setenv("KB_BIN_ECAP0", "64")
+    rng = np.random.default_rng(11)
+    reads = [rng.choice(np.frombuffer(b"ACGT", np.uint8), int(rng.integers(31, 200))).tobytes()
+             for _ in range(600)]
+    reads += reads[:200]  # repeats survive the prune
+    bases, lens = kbin.pack_reads(reads)
+    ora = oracle.bin_reads(bases, lens, 21, 6, 1, prune)
+    assert len(ora.count) > 64
+    res = gpu_result(bases, lens, 21, 6, 1, prune)
+    assert_same(res, ora)
+
+
 def test_explicit_ids_nonmonotone():
     """ids are caller-supplied (process_read's read_id): lists keep REVERSE CALL
     order, not id order (binning.c:1065-1068)."""
