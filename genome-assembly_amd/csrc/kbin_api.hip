@@ -141,6 +141,7 @@ struct kb_ctx {
     bool bucket_failed = false;  // a bucket overflowed its mmer map: radix path from now on
     uint64_t n_occ_entries_hint = 0;  // entries of the last finalize (lists grid)
     uint64_t ecap_hint = 0;    // entry capacity for the next binned finalize
+    uint32_t part = 0, part_n = 1;  // kb_set_partition: this pass's mmer partition
     uint64_t* h_totals = nullptr;
     uint32_t* h_misc = nullptr;
 
@@ -252,6 +253,40 @@ extern "C" int kb_reset(kb_ctx* c) {
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->s));
     free_batches(c);
+    c->finalized = false;
+    c->exported = false;
+    c->n_entries = c->n_ids = c->n_distinct = 0;
+    c->part = 0;  // back to one full pass
+    c->part_n = 1;
+    return KB_OK;
+}
+
+static bool binned_applies(const kb_ctx* c);
+
+// Partitioned passes: the next finalize (or route) covers only the mmers of
+// one partition.  Received records and the result are dropped; read batches
+// are kept and re-armed (a shipped batch can be routed again for this pass).
+extern "C" int kb_set_partition(kb_ctx* c, uint32_t part, uint32_t n_parts) {
+    if (!c) return fail(KB_EINVAL, "null ctx");
+    if (n_parts == 0 || part >= n_parts) return fail(KB_EINVAL, "partition %u of %u", part, n_parts);
+    if (n_parts > 1 && !binned_applies(c))
+        return fail(KB_EINVAL, "partitioned passes need the binned engine (K <= 31)");
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->s));
+    std::vector<Batch> keep;
+    for (auto& b : c->batches) {
+        if (b.superkmers) {
+            if (b.rec_base) (void)hipFree(b.rec_base);
+            continue;
+        }
+        b.routed = false;
+        keep.push_back(b);
+    }
+    c->batches.swap(keep);
+    c->route_G = 0;
+    c->part = part;
+    c->part_n = n_parts;
     c->finalized = false;
     c->exported = false;
     c->n_entries = c->n_ids = c->n_distinct = 0;
@@ -589,6 +624,8 @@ extern "C" int kb_route_scatter(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions,
     for (auto& b : c->batches) {
         if (b.routed || b.superkmers || !b.n_reads) continue;
         SkScanArgs a{};
+        a.part = c->part;
+        a.part_n = c->part_n;
         a.words = b.words;
         a.lens = b.lens;
         a.n_reads = b.n_reads;
@@ -746,6 +783,8 @@ static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered
         for (auto& b : c->batches) {
             if (b.routed || b.superkmers) continue;
             SkScanArgs a{};
+            a.part = c->part;
+            a.part_n = c->part_n;
             a.words = b.words;
             a.lens = b.lens;
             a.n_reads = b.n_reads;
@@ -785,6 +824,8 @@ static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered
     for (auto& b : c->batches) {
         if (b.routed || b.superkmers) continue;
         SkScanArgs a{};
+        a.part = c->part;
+        a.part_n = c->part_n;
         a.words = b.words;
         a.lens = b.lens;
         a.n_reads = b.n_reads;
@@ -817,6 +858,8 @@ static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered
     for (auto& b : c->batches) {
         if (b.routed || b.superkmers) continue;
         SkScanArgs a{};
+        a.part = c->part;
+        a.part_n = c->part_n;
         a.words = b.words;
         a.lens = b.lens;
         a.n_reads = b.n_reads;
@@ -862,6 +905,8 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
             } else {
                 if (b.superkmers) continue;
                 SkScanArgs a{};
+                a.part = c->part;
+                a.part_n = c->part_n;
                 a.words = b.words;
                 a.lens = b.lens;
                 a.n_reads = b.n_reads;
@@ -1176,6 +1221,7 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
         if (any_sk) return finalize_binned(c, prune, true, 0, true);  // ordinal = read id
         return finalize_binned(c, prune, affine, id_c, false);
     }
+    if (c->part_n > 1) return fail(KB_EINVAL, "partitioned passes need the binned engine (K <= 31)");
     c->tm.engine = KB_ENG_TABLE;
     // per-read occurrence offsets (the table engine's record slots)
     uint64_t N = 0;

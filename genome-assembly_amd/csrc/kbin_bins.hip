@@ -48,6 +48,20 @@ DEV void segment_at(const uint64_t* sw, int lo, int lane, int W, int M, uint32_t
     canon = (uint32_t)rfl((int)(key >> 16));
 }
 
+constexpr uint64_t OWNER_SALT = 0x5851F42D4C957F2Dull;   // rank of a mmer (= owner_of(), kbin_kernels.hip)
+constexpr uint64_t BUCKET_SALT = 0x2545F4914F6CDD1Dull;  // bucket of a mmer inside one rank (independent)
+constexpr uint64_t PART_SALT = 0x9E3779B97F4A7C15ull;    // pass of a mmer (kb_set_partition; independent)
+uint64_t sk_bucket_salt() { return BUCKET_SALT; }
+
+DEV uint32_t dest_of(uint32_t mmer, uint32_t G, uint64_t salt) {
+    return (uint32_t)((mix64((uint64_t)mmer + salt) >> 32) % G);
+}
+DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) { return dest_of(mmer, G, OWNER_SALT); }
+// a pass keeps the super-k-mers of its own mmer partition
+DEV bool in_part(uint32_t mmer, uint32_t part, uint32_t part_n) {
+    return part_n <= 1 || dest_of(mmer, part_n, PART_SALT) == part;
+}
+
 template <bool WRITE>
 __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -63,7 +77,6 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
     for (uint64_t r = (uint64_t)blockIdx.x * 4 + wid; r < A.n_reads; r += nwaves) {
         const int L = rfl((int)A.lens[r]);
         const int nK = L - K + 1;
-        if (nK > 0) kmers += (uint64_t)nK;
         uint32_t nseg = 0;
         if (nK > 0) {
             wave_sync();
@@ -76,6 +89,11 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
                 int sig;
                 uint32_t canon;
                 segment_at(sw, lo, lane, W, M, maskM, halfM, sig, canon);
+                if (!in_part(canon, A.part, A.part_n)) {  // another pass's super-k-mer
+                    lo = sig + 1;
+                    continue;
+                }
+                kmers += (uint64_t)(min(sig, nK - 1) - lo + 1);
                 if (WRITE && lane == 0) {
                     // one super-k-mer: k-mers lo..min(sig, nK-1) share the
                     // signature at sig (binning.c:1004-1040 with the sticky
@@ -108,14 +126,6 @@ DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
     return read_ids ? read_ids[ord] : (int32_t)(ord + id_off);
 }
 
-constexpr uint64_t OWNER_SALT = 0x5851F42D4C957F2Dull;   // rank of a mmer (= owner_of(), kbin_kernels.hip)
-constexpr uint64_t BUCKET_SALT = 0x2545F4914F6CDD1Dull;  // bucket of a mmer inside one rank (independent)
-uint64_t sk_bucket_salt() { return BUCKET_SALT; }
-
-DEV uint32_t dest_of(uint32_t mmer, uint32_t G, uint64_t salt) {
-    return (uint32_t)((mix64((uint64_t)mmer + salt) >> 32) % G);
-}
-DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) { return dest_of(mmer, G, OWNER_SALT); }
 
 // one record into a destination region: the binned layout (ordinal) or the
 // routed one (read id), see SkScanArgs
@@ -181,7 +191,6 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
             const uint64_t r = r0 + tid;
             const uint64_t* sw = smem + tid * RS;
             const int nK = (int)A.lens[r] - K + 1;
-            if (nK > 0) kmers += (uint64_t)nK;
             uint32_t nseg = 0;
             const uint64_t rbase = WRITE && !alloc ? A.rec_base[r] : 0;
             int lo = 0;
@@ -201,8 +210,13 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     x = (x << 2) | (y >> 62);
                     y <<= 2;
                 }
+                const uint64_t n = (uint64_t)(min(sig, nK - 1) - lo + 1);
+                if (!in_part((uint32_t)best, A.part, A.part_n)) {  // another pass's super-k-mer
+                    lo = sig + 1;
+                    continue;
+                }
+                kmers += n;
                 if (WRITE) {
-                    const uint64_t n = (uint64_t)(min(sig, nK - 1) - lo + 1);
                     const uint64_t rev = bsm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
                     const uint64_t e = (uint64_t)lo | (n << 16) | ((uint64_t)(sig - lo) << 22) | (rev << 28) |
                                        ((uint64_t)tid << 29) | ((uint64_t)(uint32_t)best << 37);

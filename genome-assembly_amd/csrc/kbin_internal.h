@@ -105,6 +105,9 @@ struct SkScanArgs {
     uint64_t dest_salt;
     int rw;
     int binned_fmt;
+    // partitioned passes (kb_set_partition): only super-k-mers whose mmer is in
+    // partition part of part_n are emitted and counted (part_n <= 1: all)
+    uint32_t part, part_n;
 };
 
 // local buckets: every record of a bin lands in bucket dest_of(mmer, NB, BUCKET_SALT);

@@ -35,7 +35,7 @@ EXPORTED = [
     "kb_finalize", "kb_export", "kb_export_device", "kb_reset", "kb_set_timing",
     "kb_get_timing", "kb_generate_reads_device", "kb_unpack_reads_to_host", "kb_stream",
     "kb_last_error", "kb_abi_version", "kb_record_words", "kb_route_plan", "kb_route_pack",
-    "kb_submit_superkmers_device", "kb_route_scatter",
+    "kb_submit_superkmers_device", "kb_route_scatter", "kb_set_partition",
 ]
 
 
@@ -115,6 +115,7 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_route_pack.argtypes = [vp, vp]
     lib.kb_submit_superkmers_device.argtypes = [vp, vp, u64]
     lib.kb_route_scatter.argtypes = [vp, C.c_uint32, vp, u64, C.POINTER(C.c_uint64)]
+    lib.kb_set_partition.argtypes = [vp, u32, u32]
     lib.kb_stream.argtypes = [vp]
     lib.kb_stream.restype = vp
     lib.kb_last_error.argtypes = []
@@ -168,6 +169,21 @@ class Result:
         return Result(self.mmer[order], self.kmer_hi[order], self.kmer_lo[order], cnt, off, ids,
                       self.n_kmers, self.n_distinct,
                       None if self.first is None else self.first[order])
+
+
+    @staticmethod
+    def concat(parts) -> "Result":
+        """union of disjoint results (the passes of kb_set_partition): entries
+        concatenated, each part's offsets shifted past the ids before it"""
+        parts = list(parts)
+        base = np.cumsum([0] + [len(r.ids) for r in parts])
+        off = [np.zeros(1, dtype=np.uint64)] + [r.offset[1:].astype(np.uint64) + np.uint64(b)
+                                                 for r, b in zip(parts, base[:-1])]
+        cat = lambda f, dt: np.concatenate([getattr(r, f) for r in parts]).astype(dt)  # noqa: E731
+        first = None if any(r.first is None for r in parts) else cat("first", np.uint64)
+        return Result(cat("mmer", np.uint32), cat("kmer_hi", np.uint64), cat("kmer_lo", np.uint64),
+                      cat("count", np.uint32), np.concatenate(off), cat("ids", np.int32),
+                      sum(r.n_kmers for r in parts), sum(r.n_distinct for r in parts), first)
 
 
 _BP = np.frombuffer(b"TGCA", dtype=np.uint8)  # getbp (binning.c:69-88)
@@ -288,6 +304,11 @@ class Engine:
 
     def reset(self) -> None:
         _check(self.lib, self.lib.kb_reset(self._h))
+
+    def set_partition(self, part: int, n_parts: int) -> None:
+        """next finalize/route covers mmer partition `part` of `n_parts` only
+        (kbin.h: partitioned passes; the read batches are kept)"""
+        _check(self.lib, self.lib.kb_set_partition(self._h, int(part), int(n_parts)))
 
     def set_timing(self, on: bool = True) -> None:
         _check(self.lib, self.lib.kb_set_timing(self._h, 1 if on else 0))

@@ -148,15 +148,19 @@ class ShardedBinner:
         return self._send
 
     def step(self, words: torch.Tensor, lens: torch.Tensor, n_reads: int, words_per_read: int,
-             first_id: int, prune: bool = True) -> None:
+             first_id: int, prune: bool = True, part: int = 0, n_parts: int = 1) -> None:
         """Bin this rank's resident packed reads (ids first_id..first_id+n-1)
         together with every other rank's; the result this rank owns stays in
-        self.engine (export / export_device)."""
+        self.engine (export / export_device).  n_parts > 1: only the keys of
+        mmer partition `part` (kb_set_partition) -- every rank passes the same
+        (part, n_parts), and the n_parts steps together bin everything."""
         eng = self.engine
         t = [time.perf_counter()]
         eng.reset()
         eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n_reads, words_per_read,
                                  first_id)
+        if n_parts > 1:
+            eng.set_partition(part, n_parts)
         counts = self._scatter(n_reads) if self.scatter else None
         if counts is not None:  # one pass: records straight into destination regions
             t.append(time.perf_counter())

@@ -199,6 +199,21 @@ int kb_submit_superkmers_device(kb_ctx *ctx, const uint64_t *d_records, uint64_t
 int kb_route_scatter(kb_ctx *ctx, uint32_t n_dest, uint64_t *d_regions,
                      uint64_t region_cap, uint64_t *h_counts);
 
+/* ---- partitioned passes (capacity) -------------
+ * One context holds at most 2^32 - 1 k-mer occurrences per finalize.  Larger
+ * inputs are binned in passes over disjoint slices of the canonical-mmer
+ * space: after kb_set_partition(ctx, p, P) the next kb_finalize (and
+ * kb_route_plan / kb_route_pack / kb_route_scatter) covers only the k-mers
+ * whose signature mmer falls in partition p of P (a fixed hash of the mmer,
+ * independent of the rank owner hash).  A key belongs to exactly one
+ * partition (its mmer is part of the key), so the P results are disjoint and
+ * their union is the single-pass result, entry for entry and list for list;
+ * kb_csr.n_kmers counts the pass's occurrences.  The call drops received
+ * super-k-mer batches and the last result, keeps the submitted read batches
+ * (and re-arms shipped ones), and may be called any number of times;
+ * kb_reset returns to one full pass.  Binned engine only (KB_EINVAL for
+ * K > 31 or a forced table engine). */
+int kb_set_partition(kb_ctx *ctx, uint32_t part, uint32_t n_parts);
 /* Stream used by the context (hipStream_t as void*), for callers that want
  * to order their own work against the engine. */
 void *kb_stream(kb_ctx *ctx);

@@ -115,6 +115,54 @@ def test_route_scatter(K, M, G, engine):
     assert union == ora
 
 
+@pytest.mark.parametrize("P", [2, 5])
+def test_partitioned_routing(P, engine):
+    """kb_set_partition on the sender: each pass routes (ordered plan/pack on
+    even passes, one-pass scatter on odd ones) only its mmer slice; the
+    per-destination counts add up to the single pass and the union over
+    passes and shards equals the oracle"""
+    if engine != "binned":
+        pytest.skip("partitioned passes are the binned engine's")
+    K, M, G = 31, 7, 3
+    reads = _reads()
+    bases, lens = kbin.pack_reads(reads)
+    ids = np.arange(len(reads), dtype=np.int32) * 2 + 5
+    rw = skmer_ref.rec_words(K, M)
+    _, wcounts = skmer_ref.encode(reads, ids.tolist(), K, M, G)
+    ora = skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, True, ids=ids))
+    union = {}
+    tot = np.zeros(G, dtype=np.int64)
+    with kbin.Engine(K, M, cutoff=1, max_read_len=300) as eng:
+        eng.submit(bases=bases, lens=lens, ids=ids)
+        for p in range(P):
+            eng.set_partition(p, P)
+            if p % 2 == 0:
+                counts = eng.route_plan(G)
+                send = torch.zeros(max(1, int(counts.sum()) * rw), dtype=torch.int64, device="cuda")
+                eng.route_pack(send.data_ptr())
+                edges = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+                segs = [(send, int(edges[d]) * rw) for d in range(G)]
+            else:
+                cap = int(max(wcounts)) + 16
+                regions = torch.zeros(G * cap * rw, dtype=torch.int64, device="cuda")
+                ok, counts = eng.route_scatter(G, regions.data_ptr(), cap)
+                assert ok
+                segs = [(regions, d * cap * rw) for d in range(G)]
+            torch.cuda.synchronize()
+            tot += counts.astype(np.int64)
+            for d in range(G):
+                buf, o = segs[d]
+                with kbin.Engine(K, M, cutoff=1, max_read_len=300) as shard:
+                    if counts[d]:
+                        shard.submit_superkmers_device(buf[o:].data_ptr(), int(counts[d]))
+                    shard.finalize(prune=True)
+                    part = _result_dict(shard.export())
+                assert not (set(part) & set(union))
+                union.update(part)
+    assert tot.tolist() == list(wcounts)
+    assert union == ora
+
+
 def test_track_first_through_routing():
     """first occurrence (id << 16 | position) survives the exchange"""
     reads = _reads(300)

@@ -141,6 +141,48 @@ def test_binned_entry_capacity_rerun(prune, engine, monkeypatch):
     assert_same(res, ora)
 
 
+@pytest.mark.parametrize("P,radix,long_reads", [(1, False, False), (3, False, False), (8, False, False),
+                                                 (4, True, False), (3, False, True)])
+def test_partitioned_passes(P, radix, long_reads, engine, monkeypatch):
+    """kb_set_partition: P passes over the same submitted reads bin disjoint
+    mmer slices whose union is the single-pass result, list for list"""
+    bases, lens = oracle.read_fgets(kbin.REPO_ROOT / "tests/golden/reads.txt", 101)
+    rng = np.random.default_rng(P * 10 + radix)
+    extra = [rng.choice(np.frombuffer(b"ACGT", np.uint8), int(rng.integers(0, 300))).tobytes()
+             for _ in range(300)]
+    if long_reads:  # > 512 bp: the wave-per-read scan and the radix record path
+        extra += [rng.choice(np.frombuffer(b"ACGT", np.uint8), 700).tobytes() for _ in range(20)]
+    off = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    reads = [bases[off[i]:off[i + 1]] for i in range(3000)] + extra
+    bases, lens = kbin.pack_reads(reads)
+    K, M = 21, 5
+    ora = oracle.bin_reads(bases, lens, K, M, 1, True)
+    if radix:
+        monkeypatch.setenv("KB_BIN_RADIX", "1")
+    with kbin.Engine(K, M, cutoff=1, max_read_len=1024) as eng:
+        eng.submit(bases=bases, lens=lens, first_id=0)
+        if engine != "binned":
+            with pytest.raises(kbin.KbError, match="KB_EINVAL"):
+                eng.set_partition(0, 2)
+            eng.set_partition(0, 1)
+            return
+        parts = []
+        for p in range(P):
+            eng.set_partition(p, P)
+            eng.finalize(prune=True)
+            parts.append(eng.export())
+    seen = [set(np.unique(r.mmer).tolist()) for r in parts]
+    for a in range(P):
+        for b in range(a + 1, P):
+            assert not seen[a] & seen[b], "a mmer in two partitions"
+    if P > 1:
+        assert sum(1 for r in parts if r.n_entries) > 1, "all keys in one partition"
+    for r in parts:
+        assert_csr(r)
+    assert sum(r.n_kmers for r in parts) == ora.n_kmers
+    assert_same(kbin.Result.concat(parts), ora)
+
+
 def test_explicit_ids_nonmonotone():
     """ids are caller-supplied (process_read's read_id): lists keep REVERSE CALL
     order, not id order (binning.c:1065-1068)."""
