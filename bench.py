@@ -37,6 +37,15 @@ METRIC = "canonical k-mers binned/sec, 150bp k=31, at 1/2/4/8 MI355X; % HBM roof
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+# SURVEY.md §8(d) configurations a single GPU runs
+WORKLOADS = {
+    "c2": {"reads": 1_000_000, "genome": 5_000_000, "seed": 2, "parts": 1, "name": "C2"},
+    # 12G occurrences: the 32-bit occurrence index of one finalize caps a pass
+    # at 2^32, so the step bins four disjoint mmer partitions in turn
+    "c3": {"reads": 100_000_000, "genome": 5_000_000, "seed": 3, "parts": 4, "name": "C3"},
+}
+
+
 def algorithmic_bytes_per_read(L: int, K: int) -> float:
     """ceil(L/4) (2-bit read) + n_k * (Kb + 12) per read, Kb = 8 B
     (K<=32) or 16 B: per k-mer a slot-key read, a 4-B count read + 4-B write,
@@ -83,20 +92,31 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
+                    help="SURVEY §8(d) configuration (c2: the headline 1M x 150 bp; c3: "
+                         "100M x 150 bp on one GPU in mmer-partitioned passes)")
+    ap.add_argument("--reads", type=int, default=None, help="reads per GPU")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--K", type=int, default=31)
     ap.add_argument("--M", type=int, default=7)
     ap.add_argument("--cutoff", type=int, default=1)
-    ap.add_argument("--genome", type=int, default=5_000_000)
+    ap.add_argument("--genome", type=int, default=None)
     ap.add_argument("--err-ppm", type=int, default=1000)
-    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--parts", type=int, default=None,
+                    help="mmer partitions (kb_set_partition passes) per step")
+    ap.add_argument("--digest", action="store_true",
+                    help="after timing, one more step reporting kb_digest summed over the passes")
     ap.add_argument("--cpu-sample", type=int, default=300_000,
                     help="reads timed on the CPU oracle (0 = skip)")
     ap.add_argument("--routed", action="store_true",
                     help="N=1 through the multi-GPU path (route, all-to-all over a 1-rank group, "
                          "receive): measures the routing overhead on one GPU")
     args = ap.parse_args()
+    wl = WORKLOADS[args.workload]
+    for k in ("reads", "genome", "seed", "parts"):
+        if getattr(args, k) is None:
+            setattr(args, k, wl[k])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -137,18 +157,38 @@ def main():
                                args.err_ppm, args.seed * 1000003 + rank, device=local)
     torch.cuda.synchronize()
 
+    P = args.parts
+    pass_log = []  # (export_device, timing[, route times]) of every pass of the last step
     if world > 1 or args.routed:
         from kbin import dist as kdist
         runner = kdist.ShardedBinner(K, M, args.cutoff, L, device=local, group=None)
-        step = lambda: runner.step(words, lens, n, wpr, first_id=rank * n)  # noqa: E731
         eng = runner.engine
+
+        def step(digest=False):
+            pass_log.clear()
+            dig = [0, 0, 0, 0]
+            for p in range(P):
+                runner.step(words, lens, n, wpr, first_id=rank * n, part=p, n_parts=P)
+                pass_log.append((eng.export_device(), eng.timing(), runner.last_times))
+                if digest:
+                    dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
+            return dig
     else:
         eng = kbin.Engine(K, M, cutoff=args.cutoff, max_read_len=L, device=local)
 
-        def step():
-            eng.reset()
-            eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, first_id=0)
-            eng.finalize(prune=True)
+        def step(digest=False):
+            pass_log.clear()
+            dig = [0, 0, 0, 0]
+            for p in range(P):
+                eng.reset()
+                eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, first_id=0)
+                if P > 1:
+                    eng.set_partition(p, P)
+                eng.finalize(prune=True)
+                pass_log.append((eng.export_device(), eng.timing(), None))
+                if digest:
+                    dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
+            return dig
 
     eng.set_timing(True)
     for _ in range(args.warmup):
@@ -159,18 +199,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    scan_ms = []
-    tim = []
+    steps_log = []  # per step: [(export_device, timing)] of each finalize (pass)
     barrier()
     t0 = time.perf_counter()
     route_t = []
     for _ in range(args.steps):
         step()
-        t = eng.timing()
-        tim.append(t)
+        steps_log.append([(d, t) for d, t, _ in pass_log])
         if world > 1 or args.routed:
-            route_t.append(runner.last_times)
-        scan_ms.append(t["scan_insert_ms"] / max(1, t["scan_insert_launches"]))
+            rts = [r for _, _, r in pass_log]
+            route_t.append({k: sum(r[k] for r in rts) for k in rts[0]})
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -179,8 +217,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    dev = eng.export_device()
-    n_kmers = int(dev["n_kmers"])          # occurrences this rank inserted (owned)
+    last = steps_log[-1]  # the passes of the last step, added up
+    dev = {k: sum(int(d[k]) for d, _ in last) for k in ("n_kmers", "n_entries", "n_ids", "n_distinct")}
+    n_kmers = dev["n_kmers"]               # occurrences this rank inserted (owned)
     scanned = n * max(0, L - K + 1)         # occurrences this rank scanned
     total_scanned = scanned * world
     value = total_scanned * args.steps / elapsed
@@ -188,41 +227,54 @@ def main():
     # roofline of the dominant kernel: SURVEY.md 8(d)'s algorithmic bytes per
     # k-mer occurrence x the occurrences one launch processes / the launch's
     # device time (HIP events on the engine stream, inside the timed loop)
+    passes = [pt for st in steps_log for pt in st]
+    tim = [t for _, t in passes]
     bpr = algorithmic_bytes_per_read(L, K)
+    bpk = bpr / max(1, L - K + 1)
     binned = int(tim[-1]["engine"]) == kbin.KB_ENG_BINNED
     kname = "bin_kernel" if binned else ("scan_insert_kernel<1>" if K <= 31 else "scan_insert_kernel<2>")
-    avg_kernel_ms = float(np.mean([t["runs_ms"] for t in tim])) if binned else float(np.mean(scan_ms))
-    achieved = (bpr * n) / (avg_kernel_ms * 1e-3) / 1e9  # GB/s, per launch
-    tag = f"n{n}_L{L}_K{K}_M{M}"
+    launch_ms = [t["runs_ms"] if binned else t["scan_insert_ms"] / max(1, t["scan_insert_launches"])
+                 for t in tim]
+    avg_kernel_ms = float(np.mean(launch_ms))
+    kmers_per_launch = float(np.mean([int(d["n_kmers"]) for d, _ in passes]))
+    achieved = kmers_per_launch * bpk / (avg_kernel_ms * 1e-3) / 1e9  # GB/s, per launch
+    tag = f"n{n}_L{L}_K{K}_M{M}" + (f"_P{args.parts}" if args.parts > 1 else "")
     traffic = load_traffic(tag, kname)
     roof = {"bound": "hbm", "kernel": kname,
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
             "kernel_ms": round(avg_kernel_ms, 4),
-            "bytes_per_kmer": round(bpr / max(1, L - K + 1), 3),
-            "path_frac": round(total_scanned * args.steps / elapsed * bpr / max(1, L - K + 1)
+            "kmers_per_launch": int(kmers_per_launch),
+            "bytes_per_kmer": round(bpk, 3),
+            "path_frac": round(total_scanned * args.steps / elapsed * bpk
                                / (world * HBM_PEAK_GBS * 1e9), 4)}
-    phases = {k: round(float(np.mean([t[k] for t in tim])), 4)
+    # device time per step (all passes of a step added up)
+    phases = {k: round(float(np.mean([sum(t[k] for _, t in st) for st in steps_log])), 4)
               for k in ("scan_insert_ms", "sort_ms", "runs_ms", "emit_ms", "total_ms")}
+    digest = None
+    if args.digest:  # this rank's share (ranks own disjoint mmers: shares add up)
+        digest = [hex(x) for x in step(digest=True)]
 
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-        "config": {"workload": f"C2: {n} x {L}bp reads per GPU, genome {args.genome} bp, "
+        "config": {"workload": f"{WORKLOADS[args.workload]['name']}: {n} x {L}bp reads per GPU, genome {args.genome} bp, "
                                f"{args.err_ppm / 1e4:.2f}% substitutions, seed {args.seed}, "
                                f"K={K} M={M}, prune cutoff {args.cutoff}",
                    "reads_per_gpu": n, "read_len": L, "K": K, "M": M, "cutoff": args.cutoff,
                    "genome_len": args.genome, "err_ppm": args.err_ppm,
+                   **({"mmer_partitions": args.parts} if args.parts > 1 else {}),
                    "parallelism": f"mmer-sharded x{world}" if world > 1 else
                                   ("single GPU, routed path" if args.routed else "single GPU")},
         "roofline": roof,
         "phases_ms": phases,
         **({"route_ms": {k: round(float(np.mean([r[k] for r in route_t])), 4) for k in route_t[0]}}
            if route_t else {}),
-        "result": {"entries": int(dev["n_entries"]), "ids": int(dev["n_ids"]),
+        "result": {**({"digest": digest} if digest else {}),
+                   "entries": int(dev["n_entries"]), "ids": int(dev["n_ids"]),
                    "distinct": int(dev["n_distinct"]), "kmers_owned": n_kmers,
                    "table_slots": int(tim[-1]["table_slots"]),
                    "engine": {1: "table", 2: "binned"}.get(int(tim[-1]["engine"]), "?"),

@@ -130,6 +130,8 @@ struct kb_ctx {
     DevBuf<uint64_t> pay;      // super-k-mer records, call order (3 words each)
     DevBuf<uint64_t> srec;     // the same, bin order, structure of arrays
     DevBuf<uint64_t> stage;    // per-occurrence (slot, ordinal) staging
+    DevBuf<uint64_t> kstage;   // heavy bins: per-occurrence k-mer code + 1
+    DevBuf<uint32_t> long_q;   // entries with 257..4096 ids (lists_long_kernel)
     DevBuf<uint32_t> border;   // bin processing order
     DevBuf<uint32_t> bcount, bmmer;  // bin descriptors (with starts)
     DevBuf<uint64_t> regions;  // local bucket regions (pay layout)
@@ -232,7 +234,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->border.release(); c->bcount.release(); c->bmmer.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bcount.release(); c->bmmer.release();
     c->regions.release(); c->bfill.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
@@ -1031,6 +1033,9 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     HIPCHK(c->srec.ensure(3 * R));
     HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));  // ids by ordinal (+ radix ping-pong)
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
+    // heavy bins' flat k-mer lists (touched only when a bin needs many tables)
+    const uint32_t flat_l = (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", 3));
+    if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(N, 1)));
     if (bucketed) {
         BucketArgs ba{};
         ba.regions = c->regions.p;
@@ -1104,6 +1109,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.order = c->border.p;
         a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
         a.stage = c->stage.p;
+        a.kstage = flat_l ? c->kstage.p : nullptr;
+        a.flat_l = flat_l;
         a.totals = c->totals.p;
         a.K = c->p.K;
         a.M = M;
@@ -1144,6 +1151,10 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         la.ids_out = c->ids_out.p;
         la.read_ids = a.read_ids;
         la.id_off = a.id_off;
+        la.long_cap = N / 256 + 2;  // lists of > 256 ids
+        HIPCHK(c->long_q.ensure(2 * la.long_cap));
+        la.long_q = c->long_q.p;
+        la.long_n = c->misc.p + 4;
         HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : ecap, c->s));
         REC(5);
         HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
@@ -1382,6 +1393,24 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     c->tm.table_slots = slots;
     c->finalized = true;
     c->exported = false;
+    return KB_OK;
+}
+
+extern "C" int kb_digest(kb_ctx* c, uint64_t* out) {
+    if (!c || !out) return fail(KB_EINVAL, "null argument");
+    if (!c->finalized) return fail(KB_ESTATE, "digest before finalize");
+    int rc = set_device(c);
+    if (rc) return rc;
+    // totals[12..13] are free after the finalize
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(c->totals.p + 12);
+    HIPCHK(launch_digest(c->e_mmer.p, c->e_hi.p, c->e_lo.p, c->e_cnt.p, c->e_off.p, c->ids_out.p, c->n_entries, d,
+                         c->s));
+    HIPCHK(hipMemcpyAsync(c->h_totals + 12, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    out[0] = c->n_entries;
+    out[1] = c->n_ids;
+    out[2] = c->h_totals[12];
+    out[3] = c->h_totals[13];
     return KB_OK;
 }
 

@@ -625,6 +625,37 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
     if (fill) flush(fill);
 }
 
+// Every k-mer of the bin's records, once, to g(code, ordinal, position) on
+// its own lane (no ring, no filter): the two expansions of a heavy bin.
+template <typename G>
+DEV void expand_bin(const BinArgs& A, uint32_t lo, uint32_t hi, G&& g) {
+    const int K = A.K;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t kmask = (1ull << (2 * K)) - 1ull;
+    for (uint32_t base = lo + wid * 64; base < hi; base += BIN_THREADS) {
+        const uint32_t r = base + lane;
+        const uint64_t hd = r < hi ? A.hdr[r] : 0ull;
+        uint64_t w = r < hi ? A.w0[r] : 0ull, x = r < hi ? A.w1[r] : 0ull;
+        const int n = (int)((hd >> 32) & 63u);
+        const uint32_t ord = (uint32_t)hd;
+        const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);
+        const uint64_t flip = ((hd >> 44) & 1ull) ? kmask : 0ull;
+        for (int j = 0; j < n; j++) {
+            g((w >> (64 - 2 * K)) ^ flip, ord, (uint32_t)(rlo + (uint32_t)j));
+            w = (w << 2) | (x >> 62);
+            x <<= 2;
+        }
+    }
+}
+
+// Heavy bins (more distinct keys than several LDS tables hold): rather than
+// re-expanding every record once per hash partition, the bin is expanded
+// twice -- count per partition, then scatter (k-mer code, position, ordinal)
+// into flat per-partition lists -- and each partition is then swept from its
+// list.  Up to FLAT_MAX partitions; deeper splits filter the flat lists.
+constexpr uint32_t FLAT_MAX = 4096;
+constexpr uint64_t M48 = (1ull << 48) - 1ull;
+
 __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     BinShared& S = *reinterpret_cast<BinShared*>(smem);      // all LDS in one dynamic array
@@ -665,13 +696,55 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
         // the bin's stage range (one slot per occurrence, reused per partition)
         if (tid == 0) S.stage_base = atomicAdd(A.stage_ctr, (unsigned long long)occ_tot);
         __syncthreads();
-        uint64_t* stage = A.stage + S.stage_base;
+        uint64_t* stage = A.stage + S.stage_base;  // (flat: moved to each partition's list)
         PROF_CNT(11, 1);
         PROF_CNT(14, occ_tot);
         uint32_t l0 = 0;  // uniform: initial partition depth from the expected distinct keys
         {
             const double want = (double)occ_tot * A.rho / ((double)A.fill * TS);
             while ((double)(1u << l0) < want && l0 < 16) l0++;
+        }
+        // heavy bin: flat per-partition lists (the ring area holds the cursors)
+        const bool flat = A.flat_l && l0 >= A.flat_l;
+        uint32_t* fl_cur = reinterpret_cast<uint32_t*>(cnt + TS);  // [FLAT_MAX]
+        uint32_t* fl_off = fl_cur + FLAT_MAX;                       // [FLAT_MAX + 1]
+        uint64_t* kst = A.kstage + S.stage_base;
+        if (flat) {
+            if (l0 > 12) l0 = 12;  // FLAT_MAX partitions; deeper splits filter
+            const uint32_t np = 1u << l0, pm = np - 1u;
+            for (uint32_t i = tid; i < np; i += BIN_THREADS) fl_cur[i] = 0;
+            __syncthreads();
+            expand_bin(A, lo, hi, [&](uint64_t code, uint32_t, uint32_t) {
+                atomicAdd(&fl_cur[part_of(code) & pm], 1u);
+            });
+            __syncthreads();
+            // exclusive offsets: thread t owns partitions [t*q, t*q + q)
+            const uint32_t q = (np + BIN_THREADS - 1) / BIN_THREADS;
+            uint64_t mine = 0;
+            for (uint32_t k = 0; k < q; k++) {
+                const uint32_t i = tid * q + k;
+                if (i < np) mine += fl_cur[i];
+            }
+            uint64_t tot_f;
+            uint64_t run = block_excl_scan_u64(mine, S.red, tot_f);
+            for (uint32_t k = 0; k < q; k++) {
+                const uint32_t i = tid * q + k;
+                if (i < np) {
+                    const uint32_t c = fl_cur[i];
+                    fl_off[i] = (uint32_t)run;
+                    fl_cur[i] = (uint32_t)run;
+                    run += c;
+                }
+            }
+            if (tid == 0) fl_off[np] = (uint32_t)tot_f;
+            __syncthreads();
+            expand_bin(A, lo, hi, [&](uint64_t code, uint32_t ord, uint32_t pos) {
+                const uint32_t i = atomicAdd(&fl_cur[part_of(code) & pm], 1u);
+                kst[i] = code + 1ull;
+                stage[i] = ((uint64_t)pos << 32) | ord;
+            });
+            __threadfence_block();
+            __syncthreads();
         }
         for (uint32_t p0 = 0; p0 < (1u << l0); p0++) {
         if (tid == 0) {
@@ -680,6 +753,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             S.stack_l[0] = l0;
         }
         __syncthreads();
+        // flat: this partition's list is [fa, fb) of the bin's stage range
+        const uint32_t fa = flat ? fl_off[p0] : 0u, fb = flat ? fl_off[p0 + 1] : 0u;
+        stage = A.stage + S.stage_base + fa;
         while (true) {
             if (tid == 0) {
                 if (S.sp == 0) {
@@ -705,8 +781,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             // ---- sweep 1: insert + count (binning.c:1042-1069 semantics per key)
             // each occurrence is staged as (slot, ordinal) for sweep 2
             // stage entry: LDS slot << 48 | position in the read << 32 | call ordinal
-            for_each_kmer(A, lo, hi, P, Lv, qk, qo, qp, &S.n_stage,
-                          [&](uint64_t k0, uint32_t o0, uint16_t p0, uint32_t s0, bool v0, uint64_t k1, uint32_t o1,
+            auto insert2 = [&](uint64_t k0, uint32_t o0, uint16_t p0, uint32_t s0, bool v0, uint64_t k1, uint32_t o1,
                               uint16_t p1, uint32_t s1, bool v1) {
 #ifdef KB_BIN_PROF
                 if (A.ablate == 1) return;  // expansion only
@@ -742,7 +817,27 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                         stage[s1] = ((uint64_t)l1 << 48) | ((uint64_t)p1 << 32) | o1;
                     }
                 }
-            });
+            };
+            if (!flat) {
+                for_each_kmer(A, lo, hi, P, Lv, qk, qo, qp, &S.n_stage, insert2);
+            } else {
+                // the partition's flat list, two entries per lane; a deeper split
+                // (Lv > l0) filters it, entries keep their index (sweep 2 filters too)
+                const uint32_t nf = fb - fa, pmask = (1u << Lv) - 1u;
+                for (uint32_t c0 = (uint32_t)(tid >> 6) * 128u; c0 < nf; c0 += BIN_THREADS * 2) {
+                    const uint32_t lane = tid & 63u, i0 = c0 + lane, i1 = c0 + 64u + lane;
+                    bool v0 = i0 < nf, v1 = i1 < nf;
+                    const uint64_t k0 = v0 ? kst[fa + i0] : 0ull, k1 = v1 ? kst[fa + i1] : 0ull;
+                    const uint64_t e0 = v0 ? stage[i0] & M48 : 0ull, e1 = v1 ? stage[i1] & M48 : 0ull;
+                    if (Lv > l0) {
+                        v0 = v0 && (part_of(k0 - 1ull) & pmask) == P;
+                        v1 = v1 && (part_of(k1 - 1ull) & pmask) == P;
+                    }
+                    insert2(k0, (uint32_t)e0, (uint16_t)(e0 >> 32), i0, v0, k1, (uint32_t)e1, (uint16_t)(e1 >> 32),
+                            i1, v1);
+                }
+                if (tid == 0) S.n_stage = nf;
+            }
             __syncthreads();
             PROF_MARK(2);
             if (S.overflow) {  // uniform: split this partition in two and redo both
@@ -820,7 +915,10 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
 #else
                 const uint32_t ns = S.n_stage;
 #endif
+                const bool filt = flat && Lv > l0;
+                const uint32_t pmask = (1u << Lv) - 1u;
                 for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
+                    if (filt && (part_of(kst[fa + i] - 1ull) & pmask) != P) continue;
                     const uint64_t v = stage[i];
                     const uint32_t ls = (uint32_t)(v >> 48);
                     if (cnt[ls] != NONE) {
@@ -884,6 +982,7 @@ void bins_prof_report(hipStream_t s) {
 constexpr int LIST_THREADS = 256;
 constexpr uint32_t LIST_CAP = 4096;   // longest list sorted in LDS in one piece (power of two)
 constexpr uint32_t LIST_SPAN = 7168;  // ids of 256 entries staged in LDS at once (28 KiB: 5 blocks per CU)
+constexpr uint32_t WAVE_LIST_MAX = 4096;  // longest list one wavefront sorts in its registers (64 x 64)
 
 // descending bitonic sort of Pw (power of two) values in LDS by a group of G
 // lanes (G = 64: one wavefront, wave barriers; else the block)
@@ -911,14 +1010,12 @@ DEV void bitonic_desc(uint32_t* a, uint32_t Pw, uint32_t r) {
 // up to 256 values sorted descending by one wavefront, in registers: element
 // i = r * 64 + lane lives in v[r]; partners across lanes meet by xor-shuffle,
 // partners 64 or 128 apart are in the same lane.  In place in LDS.
+// Bitonic sort, descending, of R*64 values held by one wavefront in
+// registers, striped (value i = v[i / 64] of lane i % 64): partner distances
+// below 64 are lane shuffles, 64 and up are register pairs.  No LDS, no
+// barriers -- a wavefront sorts a list of up to 64 R ids on its own.
 template <int R>
-DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane) {
-    uint32_t v[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        const uint32_t i = (uint32_t)(r * 64 + lane);
-        v[r] = i < n ? p[i] : 0u;
-    }
+DEV void wave_bitonic(uint32_t (&v)[R], int lane) {
 #pragma unroll
     for (int kk = 2; kk <= R * 64; kk <<= 1) {
 #pragma unroll
@@ -950,10 +1047,103 @@ DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane) {
             }
         }
     }
+}
+
+// The same network for long lists with the stage loops left rolled: the
+// register-pair stages are unrolled per distance (RJ), so the code and the
+// register file stay at O(R), not O(R log^2 R).
+template <int R, int RJ>
+DEV void reg_stage(uint32_t (&v)[R], int lane, uint32_t kk) {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int r2 = r ^ RJ;
+        if (r2 > r) {
+            const bool desc = ((uint32_t)(r * 64 + lane) & kk) == 0;
+            const uint32_t x = v[r], y = v[r2];
+            const uint32_t hi = x > y ? x : y, lo = x > y ? y : x;
+            v[r] = desc ? hi : lo;
+            v[r2] = desc ? lo : hi;
+        }
+    }
+}
+
+template <int R>
+DEV void wave_bitonic_rolled(uint32_t (&v)[R], int lane) {
+    for (uint32_t kk = 2; kk <= R * 64; kk <<= 1) {
+        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+            if (jj >= 64) {
+                switch (jj >> 6) {
+                    case 1: if constexpr (R > 1) reg_stage<R, 1>(v, lane, kk); break;
+                    case 2: if constexpr (R > 2) reg_stage<R, 2>(v, lane, kk); break;
+                    case 4: if constexpr (R > 4) reg_stage<R, 4>(v, lane, kk); break;
+                    case 8: if constexpr (R > 8) reg_stage<R, 8>(v, lane, kk); break;
+                    case 16: if constexpr (R > 16) reg_stage<R, 16>(v, lane, kk); break;
+                    case 32: if constexpr (R > 32) reg_stage<R, 32>(v, lane, kk); break;
+                    default: break;
+                }
+            } else {
+                const bool lower = (lane & jj) == 0;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const uint32_t y = (uint32_t)__shfl_xor((int)v[r], (int)jj, 64);
+                    const bool desc = ((uint32_t)(r * 64 + lane) & kk) == 0;
+                    const uint32_t hi = v[r] > y ? v[r] : y, lo = v[r] > y ? y : v[r];
+                    v[r] = (lower == desc) ? hi : lo;
+                }
+            }
+        }
+    }
+}
+
+template <int R>
+DEV void wave_sort_list_long(const uint32_t* __restrict__ src, int32_t* __restrict__ dst, uint32_t n, int lane,
+                             const int32_t* read_ids, uint32_t id_off) {
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t i = (uint32_t)(r * 64 + lane);
+        v[r] = i < n ? src[i] + 1u : 0u;
+    }
+    wave_bitonic_rolled<R>(v, lane);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t i = (uint32_t)(r * 64 + lane);
+        if (i < n) dst[i] = id_of(v[r] - 1u, read_ids, id_off);
+    }
+}
+
+// n <= 64 R values (ordinal + 1) in LDS, sorted descending in place
+template <int R>
+DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane) {
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t i = (uint32_t)(r * 64 + lane);
+        v[r] = i < n ? p[i] : 0u;
+    }
+    wave_bitonic<R>(v, lane);
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const uint32_t i = (uint32_t)(r * 64 + lane);
         if (i < n) p[i] = v[r];
+    }
+}
+
+// one list of n <= 64 R call ordinals from HBM to its ids, reverse call order
+template <int R>
+DEV void wave_sort_list(const uint32_t* __restrict__ src, int32_t* __restrict__ dst, uint32_t n, int lane,
+                        const int32_t* read_ids, uint32_t id_off) {
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t i = (uint32_t)(r * 64 + lane);
+        v[r] = i < n ? src[i] + 1u : 0u;
+    }
+    wave_bitonic<R>(v, lane);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t i = (uint32_t)(r * 64 + lane);
+        if (i < n) dst[i] = id_of(v[r] - 1u, read_ids, id_off);
     }
 }
 
@@ -1122,47 +1312,27 @@ __global__ __launch_bounds__(LIST_THREADS) void lists_kernel(ListArgs A) {
                 if ((uint32_t)j < n) A.ids_out[o + j] = id_of(v[j] - 1u, A.read_ids, A.id_off);
         }
         __syncthreads();
-        // longer lists.  33..256: one wavefront per list, LDS bitonic in a
-        // private 256-entry window, no block barriers.  Longer: the whole block.
+        // longer lists.  33..WAVE_LIST_MAX: one wavefront per list, sorted in its
+        // registers (no LDS, no block barriers).  Longer: the whole block.
         const uint32_t nbig = n_big;
-        {
-            const int lane = tid & 63, wid = tid >> 6;
-            uint32_t* wb = buf + wid * 256;
-            for (uint32_t q = wid; q < nbig; q += LIST_THREADS / 64) {
-                const uint64_t ge = e0 + big[q];
-                const uint32_t n = A.e_cnt[ge];
-                if (n > 256) continue;
-                const uint64_t o = A.e_off[ge];
-                uint32_t Pw = 64;
-                while (Pw < n) Pw <<= 1;
-                for (uint32_t j = lane; j < Pw; j += 64) wb[j] = j < n ? A.ids_ord[o + j] + 1u : 0u;
-                wave_sync();
-                for (uint32_t kk = 2; kk <= Pw; kk <<= 1) {
-                    for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-                        for (uint32_t i = lane; i < Pw; i += 64) {
-                            const uint32_t l2 = i ^ jj;
-                            if (l2 > i) {
-                                const uint32_t x = wb[i], y = wb[l2];
-                                const bool desc = (i & kk) == 0;
-                                if (desc ? (x < y) : (x > y)) {
-                                    wb[i] = y;
-                                    wb[l2] = x;
-                                }
-                            }
-                        }
-                        wave_sync();
-                    }
-                }
-                for (uint32_t j = lane; j < n; j += 64) A.ids_out[o + j] = id_of(wb[j] - 1u, A.read_ids, A.id_off);
-                wave_sync();
-            }
+        for (uint32_t q = wid; q < nbig; q += LIST_THREADS / 64) {
+            const uint64_t ge = e0 + big[q];
+            const uint32_t n = A.e_cnt[ge];
+            if (n > WAVE_LIST_MAX) continue;  // wave-uniform
+            const uint64_t o = A.e_off[ge];
+            const uint32_t* src = A.ids_ord + o;
+            int32_t* dst = A.ids_out + o;
+            if (n <= 64) wave_sort_list<1>(src, dst, n, lane, A.read_ids, A.id_off);
+            else if (n <= 128) wave_sort_list<2>(src, dst, n, lane, A.read_ids, A.id_off);
+            else if (n <= 256) wave_sort_list<4>(src, dst, n, lane, A.read_ids, A.id_off);
+            else if (lane == 0) A.long_q[atomicAdd(A.long_n, 1u)] = (uint32_t)ge;  // lists_long_kernel
         }
         __syncthreads();
         for (uint32_t q = 0; q < nbig; q++) {
             const uint64_t ge = e0 + big[q];
             const uint32_t n = A.e_cnt[ge];
             const uint64_t o = A.e_off[ge];
-            if (n <= 256) continue;  // uniform
+            if (n <= WAVE_LIST_MAX) continue;  // uniform
             if (n <= (uint32_t)LIST_CAP) {
                 uint32_t Pw = 64;
                 while (Pw < n) Pw <<= 1;
@@ -1273,9 +1443,148 @@ void lists_prof_report(hipStream_t s) {
 }
 #endif
 
+// lists of 257..WAVE_LIST_MAX ids that lists_bucket_kernel passed on: one
+// wavefront per list, a full bitonic network in its registers (kept out of the
+// other list kernels, whose occupancy its 64-register lists would cap)
+__global__ __launch_bounds__(256) void lists_long_kernel(ListArgs A) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nq = A.long_n[1];
+    for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < nq; q += gridDim.x * 4) {
+        const uint32_t e = A.long_q[A.long_cap + q];
+        const uint32_t n = A.e_cnt[e];
+        const uint64_t o = A.e_off[e];
+        const uint32_t* src = A.ids_ord + o;
+        int32_t* dst = A.ids_out + o;
+        if (n <= 512) wave_sort_list_long<8>(src, dst, n, lane, A.read_ids, A.id_off);
+        else if (n <= 1024) wave_sort_list_long<16>(src, dst, n, lane, A.read_ids, A.id_off);
+        else if (n <= 2048) wave_sort_list_long<32>(src, dst, n, lane, A.read_ids, A.id_off);
+        else wave_sort_list_long<64>(src, dst, n, lane, A.read_ids, A.id_off);
+    }
+}
+
+// Lists of 257..WAVE_LIST_MAX ids (high coverage: every true k-mer's list
+// is this long) by bucketing rather than a full sorting network.  One
+// wavefront per list: min/max of its ordinals, NB order-preserving buckets
+// over that range (an LDS histogram, a wave scan, an LDS scatter), then every
+// lane sorts its own bucket(s) of <= 64 ids in registers and writes them
+// straight to their place in the list.  About n (log2(64) + 3) wave steps
+// against the network's n log2^2(n) / 2; a list with a bucket past 64 ids
+// (clustered ordinals) is queued for the network (lists_long_kernel).
+constexpr uint32_t LB_WAVES = 4;
+constexpr uint32_t LB_SPAN = WAVE_LIST_MAX;  // ids per wave in LDS
+
+// n <= 64 values in registers, sorted descending (0 pads last)
+template <int W>
+DEV void lane_sort_desc(uint32_t (&v)[W]) {
+#pragma unroll
+    for (int kk = 2; kk <= W; kk <<= 1) {
+#pragma unroll
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+#pragma unroll
+            for (int i = 0; i < W; i++) {
+                const int l2 = i ^ jj;
+                if (l2 > i) {
+                    const uint32_t x = v[i], y = v[l2];
+                    const bool desc = (i & kk) == 0;
+                    const bool sw = desc ? (x < y) : (x > y);
+                    v[i] = sw ? y : x;
+                    v[l2] = sw ? x : y;
+                }
+            }
+        }
+    }
+}
+
+template <int W>
+DEV void lane_bucket_out(const uint32_t* buf, uint32_t off, uint32_t c, int32_t* dst, uint32_t out,
+                         const int32_t* read_ids, uint32_t id_off) {
+    uint32_t v[W];
+#pragma unroll
+    for (int j = 0; j < W; j++) v[j] = (uint32_t)j < c ? buf[off + j] : 0u;
+    lane_sort_desc<W>(v);
+#pragma unroll
+    for (int j = 0; j < W; j++)
+        if ((uint32_t)j < c) dst[out + j] = id_of(v[j] - 1u, read_ids, id_off);
+}
+
+__global__ __launch_bounds__(LB_WAVES * 64) void lists_bucket_kernel(ListArgs A) {
+    __shared__ uint32_t sbuf[LB_WAVES][LB_SPAN];
+    __shared__ uint32_t scnt[LB_WAVES][128], scur[LB_WAVES][128];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t* buf = sbuf[wid];
+    uint32_t* cnt = scnt[wid];
+    uint32_t* cur = scur[wid];
+    const uint32_t nq = *A.long_n;
+    for (uint32_t q = blockIdx.x * LB_WAVES + wid; q < nq; q += gridDim.x * LB_WAVES) {
+        const uint32_t e = A.long_q[q];
+        const uint32_t n = A.e_cnt[e];
+        const uint64_t o = A.e_off[e];
+        const uint32_t* src = A.ids_ord + o;
+        int32_t* dst = A.ids_out + o;
+        uint32_t mn = 0xFFFFFFFFu, mx = 0;
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t x = src[i];
+            mn = min(mn, x);
+            mx = max(mx, x);
+        }
+        mx = wave_max_u32(mx);
+        mn = ~wave_max_u32(~mn);
+        const uint32_t nb = n <= 2048 ? 64u : 128u;
+        // order-preserving bucket of an ordinal: floor((x - mn) * nb / range)
+        const float scale = (float)nb / ((float)(mx - mn) + 1.0f);
+        for (uint32_t b = lane; b < nb; b += 64) cnt[b] = 0;
+        wave_sync();
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t b = min(nb - 1u, (uint32_t)((float)(src[i] - mn) * scale));
+            atomicAdd(&cnt[b], 1u);
+        }
+        wave_sync();
+        // lane l owns buckets ba, ba + 1 (nb = 128: ba = 2 l) or ba = l (nb = 64):
+        // adjacent buckets, so one wave scan of the per-lane totals places both
+        const uint32_t ba = nb > 64 ? 2u * (uint32_t)lane : (uint32_t)lane;
+        const uint32_t c0 = cnt[ba], c1 = nb > 64 ? cnt[ba + 1] : 0u;
+        const uint32_t big = wave_max_u32(max(c0, c1));
+        if (big > 64) {  // clustered ordinals: the sorting network takes the list
+            if (lane == 0) A.long_q[A.long_cap + atomicAdd(A.long_n + 1, 1u)] = e;
+            continue;
+        }
+        const uint32_t base = wave_incl_scan(c0 + c1, lane) - (c0 + c1);  // ascending offsets
+        wave_sync();
+        cur[ba] = base;
+        if (nb > 64) cur[ba + 1] = base + c0;
+        wave_sync();
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t x = src[i];
+            const uint32_t b = min(nb - 1u, (uint32_t)((float)(x - mn) * scale));
+            buf[atomicAdd(&cur[b], 1u)] = x + 1u;
+        }
+        wave_sync();
+        // descending list: bucket at ascending offset a with c ids starts at n - a - c
+        if (big <= 16) {
+            lane_bucket_out<16>(buf, base, c0, dst, n - base - c0, A.read_ids, A.id_off);
+            if (nb > 64) lane_bucket_out<16>(buf, base + c0, c1, dst, n - base - c0 - c1, A.read_ids, A.id_off);
+        } else if (big <= 32) {
+            lane_bucket_out<32>(buf, base, c0, dst, n - base - c0, A.read_ids, A.id_off);
+            if (nb > 64) lane_bucket_out<32>(buf, base + c0, c1, dst, n - base - c0 - c1, A.read_ids, A.id_off);
+        } else {
+            lane_bucket_out<64>(buf, base, c0, dst, n - base - c0, A.read_ids, A.id_off);
+            if (nb > 64) lane_bucket_out<64>(buf, base + c0, c1, dst, n - base - c0 - c1, A.read_ids, A.id_off);
+        }
+        wave_sync();
+    }
+}
+
 hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s) {
     const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>(1, (max_entries + LIST_THREADS - 1) / LIST_THREADS), 16384);
+    hipError_t e = hipMemsetAsync(a.long_n, 0, 2 * sizeof(unsigned int), s);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(lists_kernel, dim3((unsigned)blocks), dim3(LIST_THREADS), 0, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lists_bucket_kernel, dim3(4096), dim3(LB_WAVES * 64), 0, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lists_long_kernel, dim3(1024), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

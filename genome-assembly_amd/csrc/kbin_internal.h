@@ -141,6 +141,8 @@ struct BinArgs {
     const uint32_t* order;     // [nbins] processing order (largest bins first)
     unsigned long long* work;  // work counter (zeroed)
     uint64_t* stage;           // [N] (LDS slot << 48 | position << 32 | ordinal) per occurrence
+    uint64_t* kstage;          // [N] heavy bins: k-mer code + 1 per occurrence, parallel to stage
+    uint32_t flat_l;           // heavy bin: initial partition depth >= flat_l (0 = never)
     const uint64_t* totals;    // totals[2] = nbins
     int K, M;
     uint32_t keep_gt;
@@ -171,6 +173,10 @@ struct ListArgs {
     int32_t* ids_out;
     const int32_t* read_ids;
     uint32_t id_off;
+    uint32_t* long_q;          // [2 long_cap] entries with 257..4096 ids: [0, long_cap) for
+                               // lists_bucket_kernel, [long_cap, 2 long_cap) passed on to lists_long_kernel
+    uint64_t long_cap;
+    unsigned int* long_n;      // [2] (zeroed) queue lengths
 };
 
 hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s);
@@ -209,6 +215,9 @@ size_t bins_lds_bytes(uint32_t ts_log2);
 void bins_prof_report(hipStream_t s);
 void lists_prof_report(hipStream_t s);
 #endif
+hipError_t launch_digest(const uint32_t* mmer, const uint64_t* hi, const uint64_t* lo, const uint32_t* cnt,
+                         const uint64_t* off, const int32_t* ids, uint64_t n_entries, unsigned long long* out,
+                         hipStream_t s);
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                              uint64_t max_entries, hipStream_t s);
 

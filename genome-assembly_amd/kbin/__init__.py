@@ -35,7 +35,7 @@ EXPORTED = [
     "kb_finalize", "kb_export", "kb_export_device", "kb_reset", "kb_set_timing",
     "kb_get_timing", "kb_generate_reads_device", "kb_unpack_reads_to_host", "kb_stream",
     "kb_last_error", "kb_abi_version", "kb_record_words", "kb_route_plan", "kb_route_pack",
-    "kb_submit_superkmers_device", "kb_route_scatter", "kb_set_partition",
+    "kb_submit_superkmers_device", "kb_route_scatter", "kb_set_partition", "kb_digest",
 ]
 
 
@@ -116,6 +116,7 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_submit_superkmers_device.argtypes = [vp, vp, u64]
     lib.kb_route_scatter.argtypes = [vp, C.c_uint32, vp, u64, C.POINTER(C.c_uint64)]
     lib.kb_set_partition.argtypes = [vp, u32, u32]
+    lib.kb_digest.argtypes = [vp, C.POINTER(u64)]
     lib.kb_stream.argtypes = [vp]
     lib.kb_stream.restype = vp
     lib.kb_last_error.argtypes = []
@@ -184,6 +185,36 @@ class Result:
         return Result(cat("mmer", np.uint32), cat("kmer_hi", np.uint64), cat("kmer_lo", np.uint64),
                       cat("count", np.uint32), np.concatenate(off), cat("ids", np.int32),
                       sum(r.n_kmers for r in parts), sum(r.n_distinct for r in parts), first)
+
+
+def _mix64_np(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser, uint64 wrap-around (kbin_device.h mix64)"""
+    x = x.astype(np.uint64, copy=True)
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+    return x
+
+
+def result_digest(res: "Result") -> tuple:
+    """kb_digest (kbin.h) of a host result: (entries, ids, key sum, list sum)"""
+    key = _mix64_np(_mix64_np(_mix64_np(res.mmer.astype(np.uint64)) ^ res.kmer_hi.astype(np.uint64))
+                    ^ res.kmer_lo.astype(np.uint64))
+    cnt = res.count.astype(np.uint64)
+    dk = int(_mix64_np(key ^ (cnt << np.uint64(1))).sum(dtype=np.uint64))
+    n = len(res.ids)
+    if n:
+        e_of = np.repeat(np.arange(res.n_entries), res.count.astype(np.int64))
+        j = np.arange(n, dtype=np.int64) - res.offset[:-1].astype(np.int64)[e_of] + 1
+        ids = res.ids.astype(np.int64) & 0xFFFFFFFF
+        t = key[e_of] ^ ((j.astype(np.uint64) << np.uint64(32)) | ids.astype(np.uint64))
+        dl = int(_mix64_np(t).sum(dtype=np.uint64))
+    else:
+        dl = 0
+    return res.n_entries, n, dk, dl
 
 
 _BP = np.frombuffer(b"TGCA", dtype=np.uint8)  # getbp (binning.c:69-88)
@@ -304,6 +335,12 @@ class Engine:
 
     def reset(self) -> None:
         _check(self.lib, self.lib.kb_reset(self._h))
+
+    def digest(self) -> tuple:
+        """kb_digest of the last result: (entries, ids, key sum, list sum)"""
+        out = (C.c_uint64 * 4)()
+        _check(self.lib, self.lib.kb_digest(self._h, out))
+        return tuple(int(x) for x in out)
 
     def set_partition(self, part: int, n_parts: int) -> None:
         """next finalize/route covers mmer partition `part` of `n_parts` only

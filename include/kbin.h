@@ -149,6 +149,14 @@ int kb_export(kb_ctx *ctx, kb_csr *out);
 /* Device pointers of the same result (no copy). */
 int kb_export_device(kb_ctx *ctx, kb_csr *out);
 
+/* Order-independent digest of the last result, for comparing results too
+ * large to dump: out[0] entries, out[1] ids,
+ * out[2] = sum_e mix(key_e ^ count_e << 1), out[3] = sum over every list
+ * position j of mix(key_e ^ ((j + 1) << 32 | id)), sums mod 2^64, key_e =
+ * mix(mix(mix(mmer) ^ kmer_hi) ^ kmer_lo), mix = the splitmix64 finaliser.
+ * Independent of entry order, sensitive to list order; digests of disjoint
+ * results (partitioned passes, ranks) add up to the digest of their union. */
+int kb_digest(kb_ctx *ctx, uint64_t out[4]);
 /* Drop all submitted reads and results; keeps allocations for reuse. */
 int kb_reset(kb_ctx *ctx);
 

@@ -166,11 +166,14 @@ def test_partitioned_passes(P, radix, long_reads, engine, monkeypatch):
                 eng.set_partition(0, 2)
             eng.set_partition(0, 1)
             return
-        parts = []
+        parts, dig = [], [0, 0, 0, 0]
         for p in range(P):
             eng.set_partition(p, P)
             eng.finalize(prune=True)
             parts.append(eng.export())
+            d = eng.digest()
+            assert d == kbin.result_digest(parts[-1])
+            dig = [(a + b) % (1 << 64) for a, b in zip(dig, d)]
     seen = [set(np.unique(r.mmer).tolist()) for r in parts]
     for a in range(P):
         for b in range(a + 1, P):
@@ -181,6 +184,7 @@ def test_partitioned_passes(P, radix, long_reads, engine, monkeypatch):
         assert_csr(r)
     assert sum(r.n_kmers for r in parts) == ora.n_kmers
     assert_same(kbin.Result.concat(parts), ora)
+    assert tuple(dig) == kbin.result_digest(ora)  # digests add over partitions
 
 
 def test_explicit_ids_nonmonotone():
@@ -202,6 +206,23 @@ def test_large_lists():
     ora = oracle.bin_reads(bases, lens, 9, 3, 1, True)
     res = gpu_result(bases, lens, 9, 3, 1, True)
     assert int(res.count.max()) > 4096 * 4
+    assert_same(res, ora)
+
+
+def test_clustered_long_lists():
+    """lists of 257..4096 ids are bucketed by ordinal range; ordinals that
+    cluster (300 copies of one read, then one far away) overflow a bucket and
+    take the full sorting network instead"""
+    rng = np.random.default_rng(5)
+    a = rng.choice(np.frombuffer(b"ACGT", np.uint8), 120).tobytes()
+    mid = [rng.choice(np.frombuffer(b"ACGT", np.uint8), 120).tobytes() for _ in range(3000)]
+    spread = [a if i % 7 == 0 else m for i, m in enumerate(mid)]  # uniform: bucketed
+    b = rng.choice(np.frombuffer(b"ACGT", np.uint8), 90).tobytes()
+    reads = [b] * 300 + spread + [b] + [a] * 5
+    bases, lens = kbin.pack_reads(reads)
+    ora = oracle.bin_reads(bases, lens, 25, 6, 1, True)
+    assert int(ora.count.max()) > 256
+    res = gpu_result(bases, lens, 25, 6, 1, True)
     assert_same(res, ora)
 
 
@@ -229,6 +250,41 @@ def test_device_generator_roundtrip():
         eng.finalize(True)
         res = eng.export()
     assert_same(res, ora)
+
+
+@pytest.mark.parametrize("ts_log2,flat_l,fill", [(13, 2, 60), (10, 1, 60), (10, 1, 30), (10, 0, 60)])
+def test_heavy_bins_flat_lists(ts_log2, flat_l, fill, engine, monkeypatch):
+    """high coverage (40K reads of a 3 kbp genome, 2000x): bins with far more
+    distinct keys than one LDS table holds take the flat per-partition lists
+    (KB_BIN_FLAT_L; small tables force it, low fill forces deeper first
+    splits) -- and, with flat_l 0, the re-expansion path; lists run to
+    thousands of ids"""
+    import torch
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    monkeypatch.setenv("KB_BIN_TS_LOG2", str(ts_log2))
+    monkeypatch.setenv("KB_BIN_FLAT_L", str(flat_l))
+    monkeypatch.setenv("KB_BIN_FILL_PCT", str(fill))
+    n, L = 40000, 150
+    wpr = (L + 31) // 32
+    words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, 3000, 5000, 9)
+    torch.cuda.synchronize()
+    bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n, wpr, n * L)
+    ora = oracle.bin_reads(bases, hl, 31, 7, 1, True)
+    assert int(ora.count.max()) > 1000
+    with kbin.Engine(31, 7, cutoff=1, max_read_len=L, flags=kbin.KB_TRACK_FIRST) as eng:
+        for _ in range(2):  # the second pass runs with the learned density
+            eng.reset()
+            eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
+            eng.finalize(True)
+            res = eng.export()
+            assert_same(res, ora)
+            # first occurrence: its call ordinal is the list's oldest id
+            last = res.ids[res.offset[1:].astype(np.int64) - 1]
+            np.testing.assert_array_equal(res.first >> np.uint64(16), last.astype(np.uint64))
+            assert int((res.first & np.uint64(0xFFFF)).max()) <= L - 31
 
 
 def test_alphabet_rejected():

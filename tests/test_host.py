@@ -87,3 +87,31 @@ def test_zhash_growth_and_lookup(host):
     assert C.cast(t, C.POINTER(C.c_size_t))[0] < 6  # shrank below 1/8
     assert host.zhash_get(t, keys[-1]) == 3000
     host.zfree_hash_table(t)
+
+
+def test_result_digest_properties():
+    """kb_digest's numpy restatement: entry order free, list order counts,
+    additive over disjoint parts (kbin.Result.concat of the two halves)"""
+    bases, lens = oracle.read_fgets(kbin.REPO_ROOT / "tests/golden/reads.txt", 101)
+    o = oracle.bin_reads(bases, lens, 6, 3, 1, True)
+    r = kbin.Result(o.mmer, o.kmer_hi, o.kmer_lo, o.count, o.offset, o.ids, o.n_kmers, 0)
+    d = kbin.result_digest(r)
+    assert d[:2] == (r.n_entries, len(r.ids))
+    perm = np.random.default_rng(1).permutation(r.n_entries)
+    sub = lambda idx: kbin.Result(  # noqa: E731
+        r.mmer[idx], r.kmer_hi[idx], r.kmer_lo[idx], r.count[idx],
+        np.concatenate([[0], np.cumsum(r.count[idx].astype(np.uint64))]).astype(np.uint64),
+        np.concatenate([r.ids[int(r.offset[e]):int(r.offset[e + 1])] for e in idx]).astype(np.int32),
+        0, 0)
+    assert kbin.result_digest(sub(perm)) == d
+    half = r.n_entries // 2
+    a, b = kbin.result_digest(sub(perm[:half])), kbin.result_digest(sub(perm[half:]))
+    assert tuple((x + y) % (1 << 64) for x, y in zip(a, b)) == d
+    assert kbin.result_digest(kbin.Result.concat([sub(perm[:half]), sub(perm[half:])])) == d
+    e = int(np.argmax(r.count))  # a list in another order changes the list sum
+    ids = r.ids.copy()
+    s0, s1 = int(r.offset[e]), int(r.offset[e + 1])
+    ids[s0:s1] = ids[s0:s1][::-1]
+    assert np.any(ids != r.ids)
+    swapped = kbin.Result(r.mmer, r.kmer_hi, r.kmer_lo, r.count, r.offset, ids, 0, 0)
+    assert kbin.result_digest(swapped)[3] != d[3]
