@@ -37,12 +37,21 @@ METRIC = "canonical k-mers binned/sec, 150bp k=31, at 1/2/4/8 MI355X; % HBM roof
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-# SURVEY.md §8(d) configurations a single GPU runs
+# SURVEY.md §8(d) configurations (per GPU: C4/C5 are the per-rank shares of
+# the 8-GPU runs; at N>1 every rank bins its own share, routed by mmer owner)
 WORKLOADS = {
-    "c2": {"reads": 1_000_000, "genome": 5_000_000, "seed": 2, "parts": 1, "name": "C2"},
+    "c2": {"reads": 1_000_000, "read_len": 150, "K": 31, "M": 7, "err_ppm": 1000,
+           "genome": 5_000_000, "seed": 2, "parts": 1, "name": "C2"},
     # 12G occurrences: the 32-bit occurrence index of one finalize caps a pass
-    # at 2^32, so the step bins four disjoint mmer partitions in turn
-    "c3": {"reads": 100_000_000, "genome": 5_000_000, "seed": 3, "parts": 4, "name": "C3"},
+    # at 2^32, so the step bins disjoint mmer partitions in turn
+    "c3": {"reads": 100_000_000, "read_len": 150, "K": 31, "M": 7, "err_ppm": 1000,
+           "genome": 5_000_000, "seed": 3, "parts": 4, "name": "C3"},
+    # 1B x 150 bp over 8 GPUs: 125M reads (15G occurrences) per GPU
+    "c4": {"reads": 125_000_000, "read_len": 150, "K": 31, "M": 7, "err_ppm": 1000,
+           "genome": 3_100_000_000, "seed": 4, "parts": 5, "name": "C4 (per-GPU share)"},
+    # 500M x 250 bp, K63 two-word k-mers, 1% errors, over 8 GPUs: 62.5M reads per GPU
+    "c5": {"reads": 62_500_000, "read_len": 250, "K": 63, "M": 7, "err_ppm": 10000,
+           "genome": 3_100_000_000, "seed": 5, "parts": 4, "name": "C5 (per-GPU share)"},
 }
 
 
@@ -55,19 +64,52 @@ def algorithmic_bytes_per_read(L: int, K: int) -> float:
     return (L + 3) // 4 + nk * (kb + 12)
 
 
-def cpu_baseline(words, lens, n_sample, wpr, L, K, M, cutoff):
-    """CPU oracle (oracle/liboracle.so, single thread) on the first n_sample
-    reads of the same workload."""
+def cpu_baseline(words, lens, n_sample, wpr, L, K, M, cutoff, ref_sample):
+    """CPU baseline on the host cores of this box, single thread.
+
+    kind "reference": the reference's own binning.c/zhash.c/llist.c, compiled
+    in the build container by oracle/build_ref.sh into oracle/_ref/ (the binary
+    travels with the tree), timed over its fgets + process_read loop and
+    prune_data (BASELINE.md's timed region) on the first ref_sample reads of
+    the workload, written as one line per read (READ_LENGTH = L + 2, no split).
+    The clean-room C port (oracle/kb_oracle.c) on n_sample reads is reported
+    beside it ("port"), and is the baseline when the reference binary is absent.
+    """
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # test-infrastructure checker, used here only as the CPU baseline leg
+    import subprocess
+    import tempfile
     bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n_sample, wpr,
                                           n_sample * L)
     t0 = time.perf_counter()
     r = oracle.bin_reads(bases, hl, K, M, cutoff, True)
     dt = time.perf_counter() - t0
-    return {"value": r.n_kmers / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+    port = {"value": r.n_kmers / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
             "sample": f"first {n_sample} reads of the bench workload ({r.n_kmers} k-mers), "
                       f"oracle/kb_oracle.c single-threaded, {dt:.2f} s, host nproc={os.cpu_count()}"}
+    ref = REPO / "oracle" / "_ref" / f"ref_k{K}_m{M}_c{cutoff}"
+    if not (ref_sample > 0 and ref.is_file() and os.access(ref, os.X_OK)):
+        return port
+    m = min(ref_sample, n_sample)
+    offs = np.concatenate([[0], np.cumsum(hl[:m].astype(np.int64))])
+    buf = np.frombuffer(bases, dtype=np.uint8) if not isinstance(bases, np.ndarray) else bases
+    lines = b"".join(buf[offs[i]:offs[i + 1]].tobytes() + b"\n" for i in range(m))
+    with tempfile.NamedTemporaryFile(suffix=".txt") as f:
+        f.write(lines)
+        f.flush()
+        try:
+            out = subprocess.run([str(ref), f.name, str(L + 2), "1", "time"], capture_output=True,
+                                 text=True, timeout=180, check=True).stdout
+        except (subprocess.SubprocessError, OSError) as e:
+            port["note"] = f"reference binary failed ({type(e).__name__}); port reported"
+            return port
+    kv = dict(t.split("=") for t in out.split())
+    kmers, secs = int(kv["kmers"]), float(kv["bin_s"]) + float(kv["prune_s"])
+    return {"value": kmers / secs, "unit": "k-mers/s", "cores": 1, "kind": "reference",
+            "sample": f"first {m} reads of the bench workload ({kmers} k-mers): reference "
+                      f"binning.c process_read loop {float(kv['bin_s']):.2f} s + prune_data "
+                      f"{float(kv['prune_s']):.2f} s, gcc -O2, single-threaded, host nproc={os.cpu_count()}",
+            "port": port}
 
 
 def load_traffic(tag: str, kernel: str):
@@ -94,14 +136,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
                     help="SURVEY §8(d) configuration (c2: the headline 1M x 150 bp; c3: "
-                         "100M x 150 bp on one GPU in mmer-partitioned passes)")
+                         "100M x 150 bp on one GPU in mmer-partitioned passes; c4/c5: the "
+                         "per-GPU shares of the 8-GPU configurations)")
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU")
-    ap.add_argument("--read-len", type=int, default=150)
-    ap.add_argument("--K", type=int, default=31)
-    ap.add_argument("--M", type=int, default=7)
+    ap.add_argument("--read-len", type=int, default=None)
+    ap.add_argument("--K", type=int, default=None)
+    ap.add_argument("--M", type=int, default=None)
     ap.add_argument("--cutoff", type=int, default=1)
     ap.add_argument("--genome", type=int, default=None)
-    ap.add_argument("--err-ppm", type=int, default=1000)
+    ap.add_argument("--err-ppm", type=int, default=None)
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--parts", type=int, default=None,
                     help="mmer partitions (kb_set_partition passes) per step")
@@ -109,12 +152,14 @@ def main():
                     help="after timing, one more step reporting kb_digest summed over the passes")
     ap.add_argument("--cpu-sample", type=int, default=300_000,
                     help="reads timed on the CPU oracle (0 = skip)")
+    ap.add_argument("--ref-sample", type=int, default=120_000,
+                    help="reads timed on the compiled reference (oracle/_ref; 0 = port only)")
     ap.add_argument("--routed", action="store_true",
                     help="N=1 through the multi-GPU path (route, all-to-all over a 1-rank group, "
                          "receive): measures the routing overhead on one GPU")
     args = ap.parse_args()
     wl = WORKLOADS[args.workload]
-    for k in ("reads", "genome", "seed", "parts"):
+    for k in ("reads", "genome", "seed", "parts", "read_len", "K", "M", "err_ppm"):
         if getattr(args, k) is None:
             setattr(args, k, wl[k])
 
@@ -282,7 +327,7 @@ def main():
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(words, lens, min(args.cpu_sample, n), wpr, L, K, M,
-                                           args.cutoff)
+                                           args.cutoff, args.ref_sample)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -272,7 +272,7 @@ extern "C" int kb_set_partition(kb_ctx* c, uint32_t part, uint32_t n_parts) {
     if (!c) return fail(KB_EINVAL, "null ctx");
     if (n_parts == 0 || part >= n_parts) return fail(KB_EINVAL, "partition %u of %u", part, n_parts);
     if (n_parts > 1 && !binned_applies(c))
-        return fail(KB_EINVAL, "partitioned passes need the binned engine (K <= 31)");
+        return fail(KB_EINVAL, "partitioned passes need the binned engine (K <= 63, reads <= 512 bp)");
     int rc = set_device(c);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->s));
@@ -450,14 +450,22 @@ static int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
-// the binned engine (kbin_bins.hip) serves K <= 31 unless the table engine is
-// forced (flag, or KB_ENGINE=table)
+// the binned engine (kbin_bins.hip) serves K <= 63 unless the table engine is
+// forced (flag, or KB_ENGINE=table).  Two-word k-mers (K > 31) take only its
+// bucketed record path: reads of <= 512 bp (or received super-k-mers), no
+// forced radix path, and no bucket overflow so far -- elsewhere the table
+// engine bins them.
 static bool binned_applies(const kb_ctx* c) {
-    if (c->KW != 1) return false;
-    if (c->p.flags & KB_ENGINE_BINNED) return true;
     if (c->p.flags & KB_ENGINE_TABLE) return false;
-    const char* e = getenv("KB_ENGINE");
-    return !(e && strcmp(e, "table") == 0);
+    if (!(c->p.flags & KB_ENGINE_BINNED)) {
+        const char* e = getenv("KB_ENGINE");
+        if (e && strcmp(e, "table") == 0) return false;
+    }
+    if (c->KW == 1) return true;
+    if (c->bucket_failed || env_int("KB_BIN_RADIX", 0)) return false;
+    for (auto& b : c->batches)
+        if (!b.routed && !b.superkmers && b.RW > 16) return false;
+    return true;
 }
 
 // ordinal -> read id over the unrouted read batches: one affine map (id =
@@ -559,7 +567,7 @@ extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
     if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
     int rc = set_device(c);
     if (rc) return rc;
-    if (binned_applies(c)) return route_plan_binned(c, n_dest, h_counts);
+    if (binned_applies(c) && c->KW == 1) return route_plan_binned(c, n_dest, h_counts);
     c->route_binned = false;
     std::vector<uint64_t> tot(n_dest, 0);
     for (auto& b : c->batches) {
@@ -889,7 +897,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
         if (!b.routed) nrec += b.superkmers ? b.n_reads : b.n_reads * 16;
     for (int attempt = 0; attempt < 3; attempt++) {
         const uint64_t cap = c->bucket_cap ? c->bucket_cap : nrec / NB + 1024;
-        HIPCHK(c->regions.ensure(NB * cap * 3));
+        HIPCHK(c->regions.ensure(NB * cap * (1 + 2 * c->KW)));
         HIPCHK(c->bfill.ensure(NB));
         HIPCHK(hipMemsetAsync(c->bfill.p, 0, NB * sizeof(unsigned long long), c->s));
         HIPCHK(hipMemsetAsync(c->totals.p + 8, 0, sizeof(uint64_t), c->s));
@@ -901,7 +909,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
             if (b.routed || !b.n_reads) continue;
             if (received) {
                 if (!b.superkmers) continue;
-                HIPCHK(launch_sk_convert_buckets(b.recs, b.n_reads, rec_words(c), M, NB, c->regions.p, cap,
+                HIPCHK(launch_sk_convert_buckets(b.recs, b.n_reads, rec_words(c), 2 * c->KW, M, NB, c->regions.p, cap,
                                                  c->bfill.p, c->misc.p,
                                                  reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
             } else {
@@ -921,7 +929,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
                 a.dest_ctr = c->bfill.p;
                 a.G = NB;
                 a.dest_salt = sk_bucket_salt();
-                a.rw = 3;
+                a.rw = 1 + 2 * c->KW;  // header + span words
                 a.binned_fmt = 1;
                 a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p);
                 HIPCHK(launch_sk(a, true, c->s));
@@ -1018,6 +1026,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     for (auto& b : c->batches)
         if (!b.routed && !b.superkmers && b.RW > 16) all_short = false;
     const bool bucketed = all_short && env_int("KB_BIN_RADIX", 0) == 0 && !c->bucket_failed;
+    const int KW = c->KW, RWD = 1 + 2 * KW;  // record words: header + span words
+    if (KW != 1 && !bucketed) return fail(KB_EDEVICE, "internal: two-word k-mers off the bucketed path");
     // local buckets (power of two, <= 1024): more buckets, more workgroups in flight
     uint32_t NB = 1;
     while (NB < (uint32_t)std::min(1024, std::max(64, env_int("KB_BIN_NB", 1024)))) NB <<= 1;
@@ -1030,12 +1040,12 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     HIPCHK(c->starts.ensure(max_bins + 1));
     HIPCHK(c->bcount.ensure(max_bins));
     HIPCHK(c->bmmer.ensure(max_bins));
-    HIPCHK(c->srec.ensure(3 * R));
+    HIPCHK(c->srec.ensure(RWD * R));
     HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));  // ids by ordinal (+ radix ping-pong)
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
     // heavy bins' flat k-mer lists (touched only when a bin needs many tables)
     const uint32_t flat_l = (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", 3));
-    if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(N, 1)));
+    if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(KW * N, 1)));
     if (bucketed) {
         BucketArgs ba{};
         ba.regions = c->regions.p;
@@ -1045,6 +1055,9 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         ba.hdr = c->srec.p;
         ba.w0 = c->srec.p + R;
         ba.w1 = c->srec.p + 2 * R;
+        ba.w2 = KW == 2 ? c->srec.p + 3 * R : nullptr;
+        ba.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
+        ba.spw = 2 * KW;
         ba.rec_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 11);
         ba.bin_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 2);
         ba.bstart = c->starts.p;
@@ -1081,7 +1094,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     // ---- one workgroup per bin.  Entry capacity: learned (or N/8), rerun once
     // with the exact need when the packed counter says it was exceeded.
     HIPCHK(c->ids_out.ensure(std::max<uint64_t>(N, 1)));
-    const int ts_log2 = std::min(13, std::max(10, env_int("KB_BIN_TS_LOG2", 13)));
+    // LDS table slots: 8192 one-word keys, 4096 two-word keys (bins_lds_bytes <= 160 KiB)
+    const int ts_log2 = std::min(KW == 1 ? 13 : 12, std::max(10, env_int("KB_BIN_TS_LOG2", KW == 1 ? 13 : 12)));
     uint64_t ecap = std::min<uint64_t>(N + 1, c->ecap_hint ? c->ecap_hint : N / 8 + 1024);
     if (const int forced = env_int("KB_BIN_ECAP0", 0)) ecap = (uint64_t)forced;  // tests: force the rerun
     BinArgs a{};
@@ -1101,6 +1115,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.hdr = c->srec.p;
         a.w0 = c->srec.p + R;
         a.w1 = c->srec.p + 2 * R;
+        a.w2 = KW == 2 ? c->srec.p + 3 * R : nullptr;
+        a.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
         a.bstart = c->starts.p;
         a.bcount = c->bcount.p;
         a.bmmer = c->bmmer.p;
@@ -1137,7 +1153,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.id_off = (uint32_t)(affine ? id_c : 0);
         a.max_entries = ecap - 1;
         a.max_ids = N;
-        HIPCHK(launch_bins(a, max_bins, c->s));
+        HIPCHK(launch_bins(a, max_bins, KW, c->s));
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
 #endif
@@ -1163,10 +1179,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         else c->h_misc[8] = 0;
         HIPCHK(hipStreamSynchronize(c->s));
-        if (c->h_misc[0] & ST_BUCKET_FULL) {  // a bucket held too many mmers: redo with the radix path
-            c->bucket_failed = true;
+        if (c->h_misc[0] & ST_BUCKET_FULL) {  // a bucket held too many mmers: redo with the radix
+            c->bucket_failed = true;              // path (K <= 31) or the table engine (K > 31)
             c->finalized = false;
-            return finalize_binned(c, prune, affine, id_c, received);
+            if (KW == 1) return finalize_binned(c, prune, affine, id_c, received);
+            return kb_finalize(c, prune);
         }
         const uint64_t need = (c->h_totals[4] >> 32) + 1;  // entries asked of the packed counter
         if ((c->h_misc[2] & ST_TABLE_FULL) && attempt == 0 && need > ecap) {
@@ -1232,7 +1249,7 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
         if (any_sk) return finalize_binned(c, prune, true, 0, true);  // ordinal = read id
         return finalize_binned(c, prune, affine, id_c, false);
     }
-    if (c->part_n > 1) return fail(KB_EINVAL, "partitioned passes need the binned engine (K <= 31)");
+    if (c->part_n > 1) return fail(KB_EINVAL, "partitioned passes need the binned engine (K <= 63, reads <= 512 bp)");
     c->tm.engine = KB_ENG_TABLE;
     // per-read occurrence offsets (the table engine's record slots)
     uint64_t N = 0;
@@ -1292,7 +1309,7 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
                 a.n_distinct = c->misc.p + 1;
                 a.status = c->misc.p;
                 a.max_distinct = (uint32_t)std::min<uint64_t>(slots - slots / 8, 0xFFFFFFFFull);
-                a.max_probe = (uint32_t)std::min<uint64_t>(slots, 1u << 20);
+                a.max_probe = (uint32_t)std::min<uint64_t>(slots, 1u << 14);  // past it: rerun bigger
                 a.K = c->p.K;
                 a.M = c->p.M;
                 HIPCHK(launch_insert_sk(a, c->KW, c->s));
@@ -1314,7 +1331,7 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
             a.n_distinct = c->misc.p + 1;
             a.status = c->misc.p;
             a.max_distinct = (uint32_t)std::min<uint64_t>(slots - slots / 8, 0xFFFFFFFFull);
-            a.max_probe = (uint32_t)std::min<uint64_t>(slots, 1u << 20);
+            a.max_probe = (uint32_t)std::min<uint64_t>(slots, 1u << 14);  // past it: rerun bigger
             a.RW = b.RW;
             a.K = c->p.K;
             a.M = c->p.M;

@@ -128,20 +128,22 @@ DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
 
 
 // one record into a destination region: the binned layout (ordinal) or the
-// routed one (read id), see SkScanArgs
+// routed one (read id), see SkScanArgs; then rw - 1 span words from base lo
+// (n + K - 1 <= 2K - M bases: 2 words for K <= 31, 4 for K <= 63)
 DEV void put_record(const SkScanArgs& A, uint64_t* o, uint32_t ord, uint64_t lo, uint64_t n, uint64_t so,
                     uint64_t rev, const uint64_t* sw) {
     if (A.binned_fmt) {
         o[0] = (uint64_t)ord | (n << 32) | (so << 38) | (rev << 44) | (lo << 45);
-        o[1] = window64(sw, (int)lo);
-        o[2] = window64(sw, (int)lo + 32);
     } else {
         const uint32_t id = (uint32_t)id_of(ord, A.read_ids, A.id_off);
         o[0] = (uint64_t)id | (lo << 32) | (n << 48) | (so << 54);
-        o[1] = window64(sw, (int)lo);
-        if (A.rw >= 3) o[2] = window64(sw, (int)lo + 32);
     }
+    for (int w = 1; w < A.rw; w++) o[w] = window64(sw, (int)lo + 32 * (w - 1));
 }
+
+// LDS row of one read in sk_thread_kernel: the read's words, then zero words
+// so that every span window (up to 4 words past the first base) stays inside
+__device__ __host__ inline int sk_row_words(int RW, int rw) { return RW + (rw > 3 ? rw - 1 : 2); }
 
 // Thread-per-read variant for short reads (RW <= SK_THREAD_RW): a block
 // stages 256 reads in LDS rows and each lane walks its own read's sticky
@@ -159,8 +161,8 @@ template <bool WRITE>
 __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const int RW = A.RW, K = A.K, M = A.M;
-    const int W = K - M + 1;  // <= 31 (K <= 31): one 64-base window pair covers it
-    const int RS = RW + 2;    // row stride: two zero words past the read
+    const int W = K - M + 1;  // <= 57 (K <= 63): mmer starts lo..lo+W-1 end inside one 64-base window pair
+    const int RS = sk_row_words(RW, A.rw);  // row stride: zero words past the read
     const int sh = 64 - 2 * M;
     const uint32_t maskM = (1u << (2 * M)) - 1u;
     const uint32_t halfM = 1u << (2 * M - 1);
@@ -180,10 +182,8 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
             const uint32_t row = i / (uint32_t)RW, col = i - row * (uint32_t)RW;
             smem[row * RS + col] = A.words[r0 * RW + i];
         }
-        if (tid < nrows) {
-            smem[tid * RS + RW] = 0;
-            smem[tid * RS + RW + 1] = 0;
-        }
+        if (tid < nrows)
+            for (int w = RW; w < RS; w++) smem[tid * RS + w] = 0;
         if (tid == 0) span_end = 0;
         __syncthreads();
         const uint64_t bfirst = WRITE && !alloc ? A.rec_base[r0] : 0;
@@ -323,7 +323,8 @@ hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s) {
     if (!a.n_reads) return hipSuccess;
     const uint64_t blocks = sk_blocks(a.n_reads, a.RW);
     if (a.RW <= SK_THREAD_RW) {
-        const size_t lds = (size_t)256 * (a.RW + 2) * sizeof(uint64_t) + (write ? SK_STAGE * sizeof(uint64_t) : 0);
+        const size_t lds = (size_t)256 * sk_row_words(a.RW, a.rw) * sizeof(uint64_t) +
+                           (write ? SK_STAGE * sizeof(uint64_t) : 0);
         if (write)
             hipLaunchKernelGGL(sk_thread_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);
         else
@@ -486,38 +487,6 @@ DEV uint64_t lds_load_u64(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// find-or-insert a k-mer (stored as code + 1) in the bin's LDS table
-DEV int lds_insert(uint64_t* claim, uint32_t mask, uint64_t key, uint32_t h, uint32_t* n_keys,
-                   uint32_t limit) {
-    uint32_t idx = h & mask;
-    for (uint32_t probe = 0; probe <= mask; probe++) {
-        const uint64_t v = lds_load_u64(&claim[idx]);
-        if (v == key) return (int)idx;
-        if (v == 0) {
-            const uint64_t old = atomicCAS((unsigned long long*)&claim[idx], 0ull, (unsigned long long)key);
-            if (old == 0) {
-                if (atomicAdd(n_keys, 1u) >= limit) return -2;
-                return (int)idx;
-            }
-            if (old == key) return (int)idx;
-        }
-        idx = (idx + 1) & mask;
-    }
-    return -1;
-}
-
-DEV int lds_find(const uint64_t* claim, uint32_t mask, uint64_t key, uint32_t h) {
-    uint32_t idx = h & mask;
-    for (uint32_t probe = 0; probe <= mask; probe++) {
-        const uint64_t v = claim[idx];
-        if (v == key) return (int)idx;
-        if (v == 0) return -1;
-        idx = (idx + 1) & mask;
-    }
-    return -1;
-}
-
-
 struct alignas(16) BinShared {
     uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, pad0;
     unsigned long long e0, i0, stage_base, pad1;
@@ -546,129 +515,275 @@ DEV uint64_t block_excl_scan_u64(uint64_t v, uint64_t* red, uint64_t& total) {
 }
 
 constexpr int BIN_WAVES = BIN_THREADS / 64;
-constexpr uint32_t BIN_Q = 256;  // per-wave k-mer ring (flushes of 128 = 2 per lane)
+// per-wave k-mer ring: flushes of 128 k-mers (2 per lane) for one-word keys,
+// 64 (1 per lane) for two-word keys, whose table and ring take twice the LDS
+template <int KW>
+constexpr uint32_t bin_q() { return KW == 1 ? 256u : 128u; }
 
 DEV uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// partition of a k-mer inside its bin (independent of the table hash)
+DEV uint32_t part_of(uint64_t code) { return (uint32_t)((code * 0x9E3779B97F4A7C15ull) >> 40); }
+
+// ---- the bin table's key of a k-mer (the mmer is implied by the bin)
+//   KW = 1 (K <= 31): a = 2K-bit code + 1 (0 = empty slot)
+//   KW = 2 (K <= 63): the 2K-bit code split at bit 63 as in the table engine
+//                     (kbin_internal.h): a = (code >> 63) + 1 claims the slot,
+//                     b = (code & (2^63 - 1)) | PUB is published after it
+template <int KW>
+struct TKey;
+template <>
+struct TKey<1> {
+    uint64_t a;
+    DEV uint32_t hash() const { return (uint32_t)mix64(a - 1ull); }
+    DEV uint32_t part() const { return part_of(a - 1ull); }
+    DEV void code(uint64_t& hi, uint64_t& lo) const {
+        hi = 0;
+        lo = a - 1ull;
+    }
+};
+template <>
+struct TKey<2> {
+    uint64_t a, b;
+    DEV uint64_t h64() const { return mix64(a ^ (b * 0xD6E8FEB86659FD93ull)); }
+    DEV uint32_t hash() const { return (uint32_t)h64(); }
+    DEV uint32_t part() const { return (uint32_t)(h64() >> 40); }
+    DEV void code(uint64_t& hi, uint64_t& lo) const {
+        hi = (a - 1ull) >> 1;
+        lo = ((a - 1ull) << 63) | (b & ~PUB);
+    }
+};
+
+// a record's span bases in registers, advanced one base per k-mer
+template <int KW>
+struct Span;
+template <>
+struct Span<1> {
+    uint64_t w, x;
+    DEV void load(const BinArgs& A, uint32_t r) {
+        w = A.w0[r];
+        x = A.w1[r];
+    }
+    DEV TKey<1> key(int K, bool rev) const {
+        const uint64_t kmask = (1ull << (2 * K)) - 1ull;
+        return TKey<1>{((w >> (64 - 2 * K)) ^ (rev ? kmask : 0ull)) + 1ull};
+    }
+    DEV void step() {
+        w = (w << 2) | (x >> 62);
+        x <<= 2;
+    }
+};
+template <>
+struct Span<2> {
+    uint64_t s0, s1, s2, s3;
+    DEV void load(const BinArgs& A, uint32_t r) {
+        s0 = A.w0[r];
+        s1 = A.w1[r];
+        s2 = A.w2[r];
+        s3 = A.w3[r];
+    }
+    // complement without reversal (binning.c:1029-1040) = every code bit flipped
+    DEV TKey<2> key(int K, bool rev) const {
+        const int kh = K - 32;  // bases above the low 64-bit word (0..31)
+        uint64_t hi = kh ? s0 >> (64 - 2 * kh) : 0ull;
+        uint64_t lo = kh ? (s0 << (2 * kh)) | (s1 >> (64 - 2 * kh)) : s0;
+        if (rev) {
+            hi ^= kh ? (1ull << (2 * kh)) - 1ull : 0ull;
+            lo = ~lo;
+        }
+        return TKey<2>{((hi << 1) | (lo >> 63)) + 1ull, lo | PUB};
+    }
+    DEV void step() {
+        s0 = (s0 << 2) | (s1 >> 62);
+        s1 = (s1 << 2) | (s2 >> 62);
+        s2 = (s2 << 2) | (s3 >> 62);
+        s3 <<= 2;
+    }
+};
+
+// ---- the bin's LDS table: claim words (a), for KW = 2 the published low
+// words (b), and a u32 count (then cursor) per slot
+template <int KW>
+struct BinTable {
+    uint64_t* ca;
+    uint64_t* cb;
+    DEV bool hit(uint32_t i, const TKey<KW>& k) const {
+        if constexpr (KW == 1) return lds_load_u64(&ca[i]) == k.a;
+        else return lds_load_u64(&ca[i]) == k.a && lds_load_u64(&cb[i]) == k.b;
+    }
+    // find-or-insert; -2 past the key limit, -1 table full
+    DEV int insert(uint32_t mask, const TKey<KW>& k, uint32_t h, uint32_t* n_keys, uint32_t limit) const {
+        uint32_t idx = h & mask;
+        for (uint32_t probe = 0; probe <= mask;) {
+            uint64_t v = lds_load_u64(&ca[idx]);
+            if (v == 0) {
+                const uint64_t old = atomicCAS((unsigned long long*)&ca[idx], 0ull, (unsigned long long)k.a);
+                if (old == 0) {
+                    if constexpr (KW == 2)
+                        __hip_atomic_store(&cb[idx], k.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (atomicAdd(n_keys, 1u) >= limit) return -2;
+                    return (int)idx;
+                }
+                v = old;
+            }
+            if (v == k.a) {
+                if constexpr (KW == 1) {
+                    return (int)idx;
+                } else {
+                    // claimed by another lane: its low word may not be published yet --
+                    // re-read this slot on the next trip (no lane waits inside a branch)
+                    const uint64_t w = lds_load_u64(&cb[idx]);
+                    if (w == 0) continue;
+                    if (w == k.b) return (int)idx;
+                }
+            }
+            idx = (idx + 1) & mask;
+            probe++;
+        }
+        return -1;
+    }
+};
+
 // Expand the k-mers of the bin's records that fall in partition (p, l) and
 // hand them to f.  Records are the bin's super-k-mers, streamed from the
 // bin-ordered SoA arrays, one record per lane, the next chunk's loads issued
 // before the current chunk is expanded.  Matching k-mers are compacted into a
-// per-wave LDS ring; every 128 of them f(k0, o0, s0, k1, o1, s1, v1) runs with
-// two k-mers per lane (independent LDS chains interleave), s = block-unique
-// index from *ctr (0 .. k-mers of the partition - 1).  The partition filter is
-// one multiply; the table hash (mix64) is computed by f on compacted k-mers.
-DEV uint32_t part_of(uint64_t code) { return (uint32_t)((code * 0x9E3779B97F4A7C15ull) >> 40); }
-
-template <typename F>
-DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, uint32_t l,
-                       uint64_t* qk, uint32_t* qo, uint16_t* qp, uint32_t* ctr, F&& f) {
+// per-wave LDS ring; every Q/2 of them f(k0, o0, s0, k1, o1, s1, v1) runs with
+// up to two k-mers per lane (independent LDS chains interleave), s =
+// block-unique index from *ctr (0 .. k-mers of the partition - 1).  The
+// partition filter is one multiply (KW = 1); the table hash is computed by f
+// on compacted k-mers.
+template <int KW, typename F>
+DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, uint32_t l, uint64_t* qa,
+                       uint64_t* qb, uint32_t* qo, uint16_t* qp, uint32_t* ctr, F&& f) {
+    constexpr uint32_t Q = bin_q<KW>(), FL = Q / 2;
     const int K = A.K;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t kmask = (1ull << (2 * K)) - 1ull;
     const uint32_t pmask = (1u << l) - 1u;
     uint32_t head = 0, fill = 0;  // wave-uniform ring state
-    auto flush = [&](uint32_t cnt) {  // cnt <= 128 entries from head
+    auto ring = [&](uint32_t i) {
+        if constexpr (KW == 1) return TKey<1>{qa[i]};
+        else return TKey<2>{qa[i], qb[i]};
+    };
+    auto flush = [&](uint32_t cnt) {  // cnt <= FL entries from head
         wave_sync();
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(ctr, cnt);
         b = (uint32_t)__shfl((int)b, 0, 64);
-        const uint32_t i0 = (head + lane) & (BIN_Q - 1), i1 = (head + 64 + lane) & (BIN_Q - 1);
-        const bool v0 = (uint32_t)lane < cnt, v1 = (uint32_t)lane + 64 < cnt;
-        f(qk[i0], qo[i0], qp[i0], b + lane, v0, qk[i1], qo[i1], qp[i1], b + 64 + lane, v1);
-        head = (head + cnt) & (BIN_Q - 1);
+        const uint32_t i0 = (head + lane) & (Q - 1), i1 = (head + 64 + lane) & (Q - 1);
+        const bool v0 = (uint32_t)lane < cnt, v1 = FL > 64 && (uint32_t)lane + 64 < cnt;
+        f(ring(i0), qo[i0], qp[i0], b + lane, v0, ring(i1), qo[i1], qp[i1], b + 64 + lane, v1);
+        head = (head + cnt) & (Q - 1);
         fill -= cnt;
         wave_sync();
     };
     uint32_t base = lo + wid * 64;
-    uint64_t nhd = 0, ns0 = 0, ns1 = 0;
+    uint64_t nhd = 0;
+    Span<KW> nsp{};
     if (base + lane < hi) {
         nhd = A.hdr[base + lane];
-        ns0 = A.w0[base + lane];
-        ns1 = A.w1[base + lane];
+        nsp.load(A, base + lane);
     }
     for (; base < hi; base += BIN_THREADS) {
-        const uint64_t hd = nhd, s0 = ns0, s1 = ns1;
+        const uint64_t hd = nhd;
+        Span<KW> sp = nsp;
         const uint32_t nxt = base + BIN_THREADS + lane;
         nhd = 0;
         if (nxt < hi) {  // prefetch the next chunk
             nhd = A.hdr[nxt];
-            ns0 = A.w0[nxt];
-            ns1 = A.w1[nxt];
+            nsp.load(A, nxt);
         }
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
         const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);  // the record's first k-mer in its read
-        const uint64_t flip = ((hd >> 44) & 1ull) ? kmask : 0ull;
+        const bool rev = ((hd >> 44) & 1ull) != 0;
         // records of a bin are sorted longest first: lane 0 holds the chunk's max
         int nmax = rfl(n);
         if (__ballot(n > nmax)) nmax = rfl((int)wave_max_u32((uint32_t)n));
-        uint64_t w = s0, x = s1;  // 64-base window at k-mer j, bases past it
         for (int j = 0; j < nmax; j++) {
-            const uint64_t code = (w >> (64 - 2 * K)) ^ flip;
-            w = (w << 2) | (x >> 62);
-            x <<= 2;
-            const bool take = j < n && (l == 0 || (part_of(code) & pmask) == p);
+            const TKey<KW> key = sp.key(K, rev);
+            sp.step();
+            const bool take = j < n && (l == 0 || (key.part() & pmask) == p);
             const uint64_t m = __ballot(take);
             if (take) {
-                const uint32_t pos = (head + fill + lanes_below(m)) & (BIN_Q - 1);
-                qk[pos] = code + 1ull;
+                const uint32_t pos = (head + fill + lanes_below(m)) & (Q - 1);
+                qa[pos] = key.a;
+                if constexpr (KW == 2) qb[pos] = key.b;
                 qo[pos] = ord;
                 qp[pos] = (uint16_t)(rlo + (uint32_t)j);
             }
             fill += (uint32_t)__popcll(m);
-            if (fill >= 128) flush(128);
+            if (fill >= FL) flush(FL);
         }
     }
     if (fill) flush(fill);
 }
 
-// Every k-mer of the bin's records, once, to g(code, ordinal, position) on
+// Every k-mer of the bin's records, once, to g(key, ordinal, position) on
 // its own lane (no ring, no filter): the two expansions of a heavy bin.
-template <typename G>
+template <int KW, typename G>
 DEV void expand_bin(const BinArgs& A, uint32_t lo, uint32_t hi, G&& g) {
     const int K = A.K;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t kmask = (1ull << (2 * K)) - 1ull;
     for (uint32_t base = lo + wid * 64; base < hi; base += BIN_THREADS) {
         const uint32_t r = base + lane;
         const uint64_t hd = r < hi ? A.hdr[r] : 0ull;
-        uint64_t w = r < hi ? A.w0[r] : 0ull, x = r < hi ? A.w1[r] : 0ull;
+        Span<KW> sp{};
+        if (r < hi) sp.load(A, r);
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
         const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);
-        const uint64_t flip = ((hd >> 44) & 1ull) ? kmask : 0ull;
+        const bool rev = ((hd >> 44) & 1ull) != 0;
         for (int j = 0; j < n; j++) {
-            g((w >> (64 - 2 * K)) ^ flip, ord, (uint32_t)(rlo + (uint32_t)j));
-            w = (w << 2) | (x >> 62);
-            x <<= 2;
+            g(sp.key(K, rev), ord, (uint32_t)(rlo + (uint32_t)j));
+            sp.step();
         }
+    }
+}
+
+// heavy bins' flat k-mer lists: KW words per occurrence
+template <int KW>
+DEV TKey<KW> kst_load(const uint64_t* kst, uint32_t i) {
+    if constexpr (KW == 1) return TKey<1>{kst[i]};
+    else return TKey<2>{kst[2 * (uint64_t)i], kst[2 * (uint64_t)i + 1]};
+}
+template <int KW>
+DEV void kst_store(uint64_t* kst, uint32_t i, const TKey<KW>& k) {
+    if constexpr (KW == 1) {
+        kst[i] = k.a;
+    } else {
+        kst[2 * (uint64_t)i] = k.a;
+        kst[2 * (uint64_t)i + 1] = k.b;
     }
 }
 
 // Heavy bins (more distinct keys than several LDS tables hold): rather than
 // re-expanding every record once per hash partition, the bin is expanded
-// twice -- count per partition, then scatter (k-mer code, position, ordinal)
+// twice -- count per partition, then scatter (table key, position, ordinal)
 // into flat per-partition lists -- and each partition is then swept from its
 // list.  Up to FLAT_MAX partitions; deeper splits filter the flat lists.
 constexpr uint32_t FLAT_MAX = 4096;
 constexpr uint64_t M48 = (1ull << 48) - 1ull;
 
+template <int KW>
 __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
+    constexpr uint32_t Q = bin_q<KW>();
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     BinShared& S = *reinterpret_cast<BinShared*>(smem);      // all LDS in one dynamic array
     const uint32_t TS = 1u << A.ts_log2, tmask = TS - 1;
-    uint64_t* claim = smem + sizeof(BinShared) / 8;          // [TS] k-mer code + 1
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(claim + TS);  // [TS] count, then cursor
-    uint64_t* qk = reinterpret_cast<uint64_t*>(cnt + TS) + (threadIdx.x >> 6) * BIN_Q;
-    uint32_t* qo = reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(cnt + TS) + BIN_WAVES * BIN_Q) +
-                   (threadIdx.x >> 6) * BIN_Q;
-    uint16_t* qp = reinterpret_cast<uint16_t*>(reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(cnt + TS) +
-                                                                           BIN_WAVES * BIN_Q) +
-                                               BIN_WAVES * BIN_Q) +
-                   (threadIdx.x >> 6) * BIN_Q;
+    BinTable<KW> T;
+    T.ca = smem + sizeof(BinShared) / 8;                     // [TS] claim words
+    T.cb = KW == 2 ? T.ca + TS : nullptr;                    // [TS] published low words
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(T.ca + KW * TS);  // [TS] count, then cursor
+    uint64_t* ring0 = reinterpret_cast<uint64_t*>(cnt + TS);
+    const uint32_t wq = (threadIdx.x >> 6) * Q;
+    uint64_t* qa = ring0 + wq;
+    uint64_t* qb = KW == 2 ? ring0 + BIN_WAVES * Q + wq : nullptr;
+    uint32_t* qo = reinterpret_cast<uint32_t*>(ring0 + KW * BIN_WAVES * Q) + wq;
+    uint16_t* qp = reinterpret_cast<uint16_t*>(reinterpret_cast<uint32_t*>(ring0 + KW * BIN_WAVES * Q) +
+                                               BIN_WAVES * Q) + wq;
     const uint32_t limit = TS - TS / 4;
     const uint64_t nbins = min(A.totals[2], A.max_bins);
     const uint32_t tid = threadIdx.x;
@@ -706,16 +821,16 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
         }
         // heavy bin: flat per-partition lists (the ring area holds the cursors)
         const bool flat = A.flat_l && l0 >= A.flat_l;
-        uint32_t* fl_cur = reinterpret_cast<uint32_t*>(cnt + TS);  // [FLAT_MAX]
-        uint32_t* fl_off = fl_cur + FLAT_MAX;                       // [FLAT_MAX + 1]
-        uint64_t* kst = A.kstage + S.stage_base;
+        uint32_t* fl_cur = reinterpret_cast<uint32_t*>(ring0);  // [FLAT_MAX]
+        uint32_t* fl_off = fl_cur + FLAT_MAX;                    // [FLAT_MAX + 1]
+        uint64_t* kst = A.kstage + KW * S.stage_base;
         if (flat) {
             if (l0 > 12) l0 = 12;  // FLAT_MAX partitions; deeper splits filter
             const uint32_t np = 1u << l0, pm = np - 1u;
             for (uint32_t i = tid; i < np; i += BIN_THREADS) fl_cur[i] = 0;
             __syncthreads();
-            expand_bin(A, lo, hi, [&](uint64_t code, uint32_t, uint32_t) {
-                atomicAdd(&fl_cur[part_of(code) & pm], 1u);
+            expand_bin<KW>(A, lo, hi, [&](const TKey<KW>& key, uint32_t, uint32_t) {
+                atomicAdd(&fl_cur[key.part() & pm], 1u);
             });
             __syncthreads();
             // exclusive offsets: thread t owns partitions [t*q, t*q + q)
@@ -738,9 +853,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             }
             if (tid == 0) fl_off[np] = (uint32_t)tot_f;
             __syncthreads();
-            expand_bin(A, lo, hi, [&](uint64_t code, uint32_t ord, uint32_t pos) {
-                const uint32_t i = atomicAdd(&fl_cur[part_of(code) & pm], 1u);
-                kst[i] = code + 1ull;
+            expand_bin<KW>(A, lo, hi, [&](const TKey<KW>& key, uint32_t ord, uint32_t pos) {
+                const uint32_t i = atomicAdd(&fl_cur[key.part() & pm], 1u);
+                kst_store<KW>(kst, i, key);
                 stage[i] = ((uint64_t)pos << 32) | ord;
             });
             __threadfence_block();
@@ -770,7 +885,8 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 S.n_stage = 0;
             }
             for (uint32_t i = tid; i < TS; i += BIN_THREADS) {
-                claim[i] = 0;
+                T.ca[i] = 0;
+                if constexpr (KW == 2) T.cb[i] = 0;
                 cnt[i] = 0;
             }
             __syncthreads();
@@ -781,20 +897,18 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             // ---- sweep 1: insert + count (binning.c:1042-1069 semantics per key)
             // each occurrence is staged as (slot, ordinal) for sweep 2
             // stage entry: LDS slot << 48 | position in the read << 32 | call ordinal
-            auto insert2 = [&](uint64_t k0, uint32_t o0, uint16_t p0, uint32_t s0, bool v0, uint64_t k1, uint32_t o1,
-                              uint16_t p1, uint32_t s1, bool v1) {
+            auto insert2 = [&](const TKey<KW>& k0, uint32_t o0, uint16_t p0, uint32_t s0, bool v0,
+                               const TKey<KW>& k1, uint32_t o1, uint16_t p1, uint32_t s1, bool v1) {
 #ifdef KB_BIN_PROF
                 if (A.ablate == 1) return;  // expansion only
 #endif
-                const uint32_t h0 = (uint32_t)mix64(k0 - 1ull), h1 = (uint32_t)mix64(k1 - 1ull);
+                const uint32_t h0 = k0.hash(), h1 = k1.hash();
                 // first probes of both k-mers in flight together; the rest
                 // (empty slot, collision chain) takes the full insert path
-                const uint64_t c0 = v0 ? lds_load_u64(&claim[h0 & tmask]) : 0ull;
-                const uint64_t c1 = v1 ? lds_load_u64(&claim[h1 & tmask]) : 0ull;
-                int l0 = c0 == k0 ? (int)(h0 & tmask) : -3;
-                int l1 = c1 == k1 ? (int)(h1 & tmask) : -3;
-                if (v0 && l0 == -3) l0 = lds_insert(claim, tmask, k0, h0, &S.n_keys, limit);
-                if (v1 && l1 == -3) l1 = lds_insert(claim, tmask, k1, h1, &S.n_keys, limit);
+                int l0 = v0 && T.hit(h0 & tmask, k0) ? (int)(h0 & tmask) : -3;
+                int l1 = v1 && T.hit(h1 & tmask, k1) ? (int)(h1 & tmask) : -3;
+                if (v0 && l0 == -3) l0 = T.insert(tmask, k0, h0, &S.n_keys, limit);
+                if (v1 && l1 == -3) l1 = T.insert(tmask, k1, h1, &S.n_keys, limit);
                 if (v0) {
                     if (l0 < 0) {
                         S.overflow = 1;
@@ -819,7 +933,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 }
             };
             if (!flat) {
-                for_each_kmer(A, lo, hi, P, Lv, qk, qo, qp, &S.n_stage, insert2);
+                for_each_kmer<KW>(A, lo, hi, P, Lv, qa, qb, qo, qp, &S.n_stage, insert2);
             } else {
                 // the partition's flat list, two entries per lane; a deeper split
                 // (Lv > l0) filters it, entries keep their index (sweep 2 filters too)
@@ -827,11 +941,12 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 for (uint32_t c0 = (uint32_t)(tid >> 6) * 128u; c0 < nf; c0 += BIN_THREADS * 2) {
                     const uint32_t lane = tid & 63u, i0 = c0 + lane, i1 = c0 + 64u + lane;
                     bool v0 = i0 < nf, v1 = i1 < nf;
-                    const uint64_t k0 = v0 ? kst[fa + i0] : 0ull, k1 = v1 ? kst[fa + i1] : 0ull;
+                    const TKey<KW> k0 = v0 ? kst_load<KW>(kst, fa + i0) : TKey<KW>{};
+                    const TKey<KW> k1 = v1 ? kst_load<KW>(kst, fa + i1) : TKey<KW>{};
                     const uint64_t e0 = v0 ? stage[i0] & M48 : 0ull, e1 = v1 ? stage[i1] & M48 : 0ull;
                     if (Lv > l0) {
-                        v0 = v0 && (part_of(k0 - 1ull) & pmask) == P;
-                        v1 = v1 && (part_of(k1 - 1ull) & pmask) == P;
+                        v0 = v0 && (k0.part() & pmask) == P;
+                        v1 = v1 && (k1.part() & pmask) == P;
                     }
                     insert2(k0, (uint32_t)e0, (uint16_t)(e0 >> 32), i0, v0, k1, (uint32_t)e1, (uint16_t)(e1 >> 32),
                             i1, v1);
@@ -862,7 +977,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             for (uint32_t k = 0; k < per; k++) {
                 const uint32_t i = tid * per + k;
                 const uint32_t c = cnt[i];
-                if (claim[i] && c > A.keep_gt) mine += ((uint64_t)c << 32) + 1ull;
+                if (T.ca[i] && c > A.keep_gt) mine += ((uint64_t)c << 32) + 1ull;
             }
             uint64_t tot;
             uint64_t ex = block_excl_scan_u64(mine, S.red, tot);
@@ -886,16 +1001,21 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 for (uint32_t k = 0; k < per; k++) {
                     const uint32_t i = tid * per + k;
                     const uint32_t c = cnt[i];
-                    if (claim[i] && c > A.keep_gt) {
+                    if (T.ca[i] && c > A.keep_gt) {
                         if (room) {
                             const uint64_t ge = e0 + e;
+                            TKey<KW> key;
+                            key.a = T.ca[i];
+                            if constexpr (KW == 2) key.b = T.cb[i];
+                            uint64_t khi, klo;
+                            key.code(khi, klo);
                             A.e_mmer[ge] = mmer;
-                            A.e_hi[ge] = 0;
-                            A.e_lo[ge] = claim[i] - 1ull;
+                            A.e_hi[ge] = khi;
+                            A.e_lo[ge] = klo;
                             A.e_cnt[ge] = c;
                             A.e_off[ge] = i0 + off;
                         }
-                        if (A.e_first) claim[i] = ~0ull;  // first occurrence (min) from sweep 2 on
+                        if (A.e_first) T.ca[i] = ~0ull;  // first occurrence (min) from sweep 2 on
                         cnt[i] = off;  // cursor (relative to i0)
                         e++;
                         off += c;
@@ -918,7 +1038,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 const bool filt = flat && Lv > l0;
                 const uint32_t pmask = (1u << Lv) - 1u;
                 for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
-                    if (filt && (part_of(kst[fa + i] - 1ull) & pmask) != P) continue;
+                    if (filt && (kst_load<KW>(kst, fa + i).part() & pmask) != P) continue;
                     const uint64_t v = stage[i];
                     const uint32_t ls = (uint32_t)(v >> 48);
                     if (cnt[ls] != NONE) {
@@ -927,7 +1047,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                         // (ordinal << 16 | position): binning.c inserts a key at its first
                         // occurrence (1045-1057); KB_TRACK_FIRST keeps it for the zhash layout
                         if (A.e_first)
-                            atomicMin((unsigned long long*)&claim[ls],
+                            atomicMin((unsigned long long*)&T.ca[ls],
                                       (unsigned long long)(((v & 0xFFFFFFFFull) << 16) | ((v >> 32) & 0xFFFFull)));
                     }
                 }
@@ -937,7 +1057,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 uint32_t e = (uint32_t)ex;
                 for (uint32_t k = 0; k < per; k++) {
                     const uint32_t i = tid * per + k;
-                    if (cnt[i] != NONE) A.e_first[e0 + e++] = claim[i];
+                    if (cnt[i] != NONE) A.e_first[e0 + e++] = T.ca[i];
                 }
             }
             __threadfence_block();
@@ -1649,7 +1769,6 @@ hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, co
 // ---------------------------------------------------------------------------
 constexpr int BK_THREADS = 512;
 constexpr uint32_t BK_SLOTS = 256;  // mmers per bucket (a bucket with more is reported)
-constexpr uint32_t BK_ROWS = 32;    // k-mers per record: n <= K - M + 1 <= 31 (row 32 - n: longest first)
 
 DEV int bk_slot(uint32_t* keys, uint32_t mmer, bool insert) {
     const uint32_t k = mmer + 1u;
@@ -1667,50 +1786,57 @@ DEV int bk_slot(uint32_t* keys, uint32_t mmer, bool insert) {
     return -1;
 }
 
+// ROWS = k-mers per record rounded up to a power of two: n <= K - M + 1
+// (<= 31 for K <= 31, <= 57 for K <= 63); row ROWS - n puts longest first
+template <int ROWS>
 DEV void bk_decode(uint64_t h, uint64_t a, uint64_t b, int M, uint32_t& canon, uint32_t& row) {
     const uint32_t maskM = (1u << (2 * M)) - 1u;
     const int so = (int)((h >> 38) & 63u);
     const uint32_t sm = (uint32_t)(span_window(a, b, 0ull, 0ull, so) >> (64 - 2 * M));
     canon = ((h >> 44) & 1u) ? maskM - sm : sm;
-    row = 32u - (uint32_t)((h >> 32) & 63u);
+    row = (uint32_t)ROWS - (uint32_t)((h >> 32) & 63u);
 }
 
+// SPW span words per record (2: K <= 31, 4: K <= 63)
+template <int SPW>
 __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
+    constexpr uint32_t ROWS = SPW == 2 ? 32 : 64;
     __shared__ uint32_t keys[BK_SLOTS];
-    __shared__ uint32_t hist[BK_SLOTS * BK_ROWS];  // (slot, 32 - n) counts, then cursors
+    __shared__ uint32_t hist[BK_SLOTS * ROWS];  // (slot, ROWS - n) counts, then cursors
     __shared__ uint64_t red[BK_THREADS / 64];
     __shared__ unsigned long long s_base, s_bin;
     __shared__ uint32_t s_nb, s_full;
     const uint32_t tid = threadIdx.x, bk = blockIdx.x;
     const uint64_t cnt = min<uint64_t>(A.bfill[bk], A.cap);
-    const uint64_t* src = A.regions + (uint64_t)bk * A.cap * 3;
+    constexpr int RWD = 1 + SPW;  // record words
+    const uint64_t* src = A.regions + (uint64_t)bk * A.cap * RWD;
     for (uint32_t i = tid; i < BK_SLOTS; i += BK_THREADS) keys[i] = 0;
-    for (uint32_t i = tid; i < BK_SLOTS * BK_ROWS; i += BK_THREADS) hist[i] = 0;
+    for (uint32_t i = tid; i < BK_SLOTS * ROWS; i += BK_THREADS) hist[i] = 0;
     if (tid == 0) {
         s_nb = 0;
         s_full = 0;
     }
     __syncthreads();
-    constexpr int U = 4;  // records in flight per thread
+    constexpr int U = SPW == 2 ? 4 : 2;  // records in flight per thread
     for (uint64_t i0 = tid; i0 < cnt; i0 += U * BK_THREADS) {
         uint64_t h[U], a[U], b[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint64_t i = i0 + (uint64_t)u * BK_THREADS;
             if (i < cnt) {
-                h[u] = src[3 * i];
-                a[u] = src[3 * i + 1];
-                b[u] = src[3 * i + 2];
+                h[u] = src[RWD * i];
+                a[u] = src[RWD * i + 1];
+                b[u] = src[RWD * i + 2];
             }
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (i0 + (uint64_t)u * BK_THREADS >= cnt) break;
             uint32_t canon, row;
-            bk_decode(h[u], a[u], b[u], A.M, canon, row);
+            bk_decode<ROWS>(h[u], a[u], b[u], A.M, canon, row);
             const int sl = bk_slot(keys, canon, true);
             if (sl < 0) s_full = 1;
-            else atomicAdd(&hist[sl * BK_ROWS + row], 1u);
+            else atomicAdd(&hist[sl * ROWS + row], 1u);
         }
     }
     __syncthreads();
@@ -1719,7 +1845,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
         return;
     }
     // exclusive scan of the counters in (slot, row) order
-    constexpr uint32_t PER = BK_SLOTS * BK_ROWS / BK_THREADS;
+    constexpr uint32_t PER = BK_SLOTS * ROWS / BK_THREADS;
     uint32_t loc[PER];
     uint64_t mine = 0;
 #pragma unroll
@@ -1753,8 +1879,8 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
         uint32_t below = 0;
         for (uint32_t j = 0; j < tid; j++) below += keys[j] != 0;
         const uint64_t bi = s_bin + below;
-        const uint32_t first = hist[tid * BK_ROWS];
-        const uint32_t last = tid + 1 < BK_SLOTS ? hist[(tid + 1) * BK_ROWS] : (uint32_t)cnt;
+        const uint32_t first = hist[tid * ROWS];
+        const uint32_t last = tid + 1 < BK_SLOTS ? hist[(tid + 1) * ROWS] : (uint32_t)cnt;
         if (bi < A.max_bins) {
             A.bstart[bi] = (uint32_t)s_base + first;
             A.bcount[bi] = last - first;
@@ -1764,38 +1890,52 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     __syncthreads();
     const uint64_t base = s_base;
     for (uint64_t i0 = tid; i0 < cnt; i0 += U * BK_THREADS) {
-        uint64_t h[U], a[U], b[U];
+        uint64_t h[U], a[U], b[U], c[U], d[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint64_t i = i0 + (uint64_t)u * BK_THREADS;
             if (i < cnt) {
-                h[u] = src[3 * i];
-                a[u] = src[3 * i + 1];
-                b[u] = src[3 * i + 2];
+                h[u] = src[RWD * i];
+                a[u] = src[RWD * i + 1];
+                b[u] = src[RWD * i + 2];
+                if constexpr (SPW == 4) {
+                    c[u] = src[RWD * i + 3];
+                    d[u] = src[RWD * i + 4];
+                }
             }
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (i0 + (uint64_t)u * BK_THREADS >= cnt) break;
             uint32_t canon, row;
-            bk_decode(h[u], a[u], b[u], A.M, canon, row);
+            bk_decode<ROWS>(h[u], a[u], b[u], A.M, canon, row);
             const int sl = bk_slot(keys, canon, false);
-            const uint64_t pos = base + atomicAdd(&hist[sl * BK_ROWS + row], 1u);
+            const uint64_t pos = base + atomicAdd(&hist[sl * ROWS + row], 1u);
             A.hdr[pos] = h[u];
             A.w0[pos] = a[u];
             A.w1[pos] = b[u];
+            if constexpr (SPW == 4) {
+                A.w2[pos] = c[u];
+                A.w3[pos] = d[u];
+            }
         }
     }
 }
 
 hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s) {
     if (!NB) return hipSuccess;
-    hipLaunchKernelGGL(bucket_kernel, dim3(NB), dim3(BK_THREADS), 0, s, a);
+    if (a.spw == 2)
+        hipLaunchKernelGGL(bucket_kernel<2>, dim3(NB), dim3(BK_THREADS), 0, s, a);
+    else if (a.spw == 4)
+        hipLaunchKernelGGL(bucket_kernel<4>, dim3(NB), dim3(BK_THREADS), 0, s, a);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
-// received routed records -> local bucket regions (pay layout, ordinal = id);
-// a block reserves one range per bucket for its 256 x 8 records
+// received routed records -> local bucket regions (pay layout, ordinal = id,
+// 1 + spw words); a block reserves one range per bucket for its 256 x 8 records
+template <int SPW>
 __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t* __restrict__ recs, uint64_t n_rec,
                                                                  int rw, int M, uint32_t NB,
                                                                  uint64_t* __restrict__ regions, uint64_t cap,
@@ -1811,7 +1951,7 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
         for (uint32_t d = threadIdx.x; d < NB; d += 256) cnt[d] = 0;
         __syncthreads();
         uint32_t dst[PERT];
-        uint64_t pay0[PERT], pa[PERT], pb[PERT];
+        uint64_t pay0[PERT], ps[PERT][SPW];
 #pragma unroll
         for (int j = 0; j < PERT; j++) {
             const uint64_t k = k0 + (uint64_t)j * 256 + threadIdx.x;
@@ -1819,17 +1959,17 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
             if (k >= n_rec) continue;
             const uint64_t* r = recs + k * (uint64_t)rw;
             const uint64_t h = r[0];
-            const uint64_t w0 = r[1], w1 = rw >= 3 ? r[2] : 0ull;
+#pragma unroll
+            for (int w = 0; w < SPW; w++) ps[j][w] = w + 1 < rw ? r[w + 1] : 0ull;
             const uint32_t id = (uint32_t)h;
             const uint64_t lo = (h >> 32) & 0xFFFFu, n = (h >> 48) & 63u, so = (h >> 54) & 63u;
-            const uint32_t sm = (uint32_t)(span_window(w0, w1, 0ull, 0ull, (int)so) >> (64 - 2 * M));
+            // the signature (so <= 56) ends inside the first two span words
+            const uint32_t sm = (uint32_t)(span_window(ps[j][0], ps[j][1], 0ull, 0ull, (int)so) >> (64 - 2 * M));
             const bool rev = sm < halfM;  // complement wins (binning.c:1029-1040)
             const uint32_t canon = rev ? maskM - sm : sm;
             neg |= (int32_t)id < 0;
             kmers += n;
             pay0[j] = (uint64_t)id | (n << 32) | (so << 38) | ((uint64_t)rev << 44) | (lo << 45);
-            pa[j] = w0;
-            pb[j] = w1;
             dst[j] = dest_of(canon, NB, BUCKET_SALT);
             atomicAdd(&cnt[dst[j]], 1u);
         }
@@ -1844,10 +1984,10 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
             if (dst[j] == 0xFFFFFFFFu) continue;
             const uint64_t slot = base[dst[j]] + atomicAdd(&cnt[dst[j]], 1u);
             if (slot >= cap) continue;  // counted: the caller retries bigger
-            uint64_t* o = regions + ((uint64_t)dst[j] * cap + slot) * 3;
+            uint64_t* o = regions + ((uint64_t)dst[j] * cap + slot) * (1 + SPW);
             o[0] = pay0[j];
-            o[1] = pa[j];
-            o[2] = pb[j];
+#pragma unroll
+            for (int w = 0; w < SPW; w++) o[1 + w] = ps[j][w];
         }
         __syncthreads();
     }
@@ -1857,36 +1997,49 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
     if (threadIdx.x == 0 && kmers) atomicAdd(n_kmers, (unsigned long long)kmers);
 }
 
-hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int M, uint32_t NB,
+hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
                                      uint64_t* regions, uint64_t cap, unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s) {
     if (!n_rec) return hipSuccess;
-    if (NB < 1 || NB > SK_MAX_DEST) return hipErrorInvalidValue;
+    if (NB < 1 || NB > SK_MAX_DEST || (spw != 2 && spw != 4)) return hipErrorInvalidValue;
     const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
-    hipLaunchKernelGGL(sk_convert_buckets_kernel, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M, NB,
-                       regions, cap, bfill, status, n_kmers);
+    if (spw == 2)
+        hipLaunchKernelGGL(sk_convert_buckets_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
+                           NB, regions, cap, bfill, status, n_kmers);
+    else
+        hipLaunchKernelGGL(sk_convert_buckets_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
+                           NB, regions, cap, bfill, status, n_kmers);
     return hipGetLastError();
 }
 
-size_t bins_lds_bytes(uint32_t ts_log2) {
+size_t bins_lds_bytes(uint32_t ts_log2, int KW) {
     const size_t TS = (size_t)1 << ts_log2;
-    return sizeof(BinShared) + TS * (sizeof(uint64_t) + sizeof(uint32_t)) +
-           (size_t)BIN_WAVES * BIN_Q * (sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint16_t));
+    const size_t Q = KW == 1 ? bin_q<1>() : bin_q<2>();
+    return sizeof(BinShared) + TS * (KW * sizeof(uint64_t) + sizeof(uint32_t)) +
+           (size_t)BIN_WAVES * Q * (KW * sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint16_t));
 }
 
-hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s) {
-    if (!max_bins) return hipSuccess;
+template <int KW>
+static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_t s) {
     const uint32_t TS = 1u << a.ts_log2;
-    if (TS < 1024 || bins_lds_bytes(a.ts_log2) > 160 * 1024) return hipErrorInvalidValue;  // wave sort windows: 8 x 256 u32 in the 2*TS u32 table space
-    const size_t lds = bins_lds_bytes(a.ts_log2);
+    const size_t lds = bins_lds_bytes(a.ts_log2, KW);
+    // TS >= BIN_THREADS (the prune loop); the ring area holds the flat-list cursors
+    const size_t ring = (size_t)BIN_WAVES * bin_q<KW>() * (KW * sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint16_t));
+    if (TS < (uint32_t)BIN_THREADS || lds > 160 * 1024 || ring < (2 * FLAT_MAX + 1) * sizeof(uint32_t))
+        return hipErrorInvalidValue;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel, BIN_THREADS, lds);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel<KW>, BIN_THREADS, lds);
     if (e != hipSuccess) return e;
     const uint64_t blocks = std::min<uint64_t>(max_bins, (uint64_t)std::max(1, cus) * std::max(1, per_cu));
-    hipLaunchKernelGGL(bin_kernel, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a);
+    hipLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a);
     return hipGetLastError();
+}
+
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s) {
+    if (!max_bins) return hipSuccess;
+    return KW == 1 ? launch_bins_kw<1>(a, max_bins, s) : launch_bins_kw<2>(a, max_bins, s);
 }
 
 __global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,

@@ -95,7 +95,8 @@ struct SkScanArgs {
     // region mode (thread kernel, with rec_ctr == nullptr): records go to
     // regions + (dest * region_cap + i) * rw, dest = hash(mmer + dest_salt) % G:
     // routing (ranks, routed format with the read id) or local buckets
-    // (binned_fmt: the pay layout with the ordinal, rw = 3)
+    // (binned_fmt: the pay layout with the ordinal, rw = 1 + span words:
+    // 3 for K <= 31, 5 for K <= 63)
     uint64_t* regions;
     uint64_t region_cap;
     unsigned long long* dest_ctr;  // [G] records per destination (zeroed)
@@ -113,13 +114,16 @@ struct SkScanArgs {
 // local buckets: every record of a bin lands in bucket dest_of(mmer, NB, BUCKET_SALT);
 // bucket_kernel then orders each bucket's records by (mmer, 63 - n)
 struct BucketArgs {
-    const uint64_t* regions;   // NB regions of cap records, pay layout (3 words)
+    const uint64_t* regions;   // NB regions of cap records, pay layout (1 + spw words)
     uint64_t cap;
     const unsigned long long* bfill;  // [NB] records per bucket
     int M;
     uint64_t* hdr;             // [R] SoA output, bins contiguous, longest records first
     uint64_t* w0;
     uint64_t* w1;
+    uint64_t* w2;              // K > 31 (spw = 4): span bases 64..127
+    uint64_t* w3;
+    int spw;                   // span words per record: 2 (K <= 31) or 4 (K <= 63)
     unsigned long long* rec_ctr;   // output allocation (zeroed)
     unsigned long long* bin_ctr;   // bins (zeroed; = totals[2])
     uint32_t* bstart;          // [max_bins] first record of bin
@@ -133,6 +137,8 @@ struct BinArgs {
     const uint64_t* hdr;       // [R] bin-ordered record headers (see SkScanArgs::pay)
     const uint64_t* w0;        // [R] span bases 0..31
     const uint64_t* w1;        // [R] span bases 32..63
+    const uint64_t* w2;        // [R] span bases 64..95   (K > 31: two-word k-mers)
+    const uint64_t* w3;        // [R] span bases 96..127
     const uint32_t* bstart;    // [nbins] first record of bin
     const uint32_t* bcount;    // [nbins] records of bin
     const uint32_t* bmmer;     // [nbins] canonical mmer of bin
@@ -141,7 +147,7 @@ struct BinArgs {
     const uint32_t* order;     // [nbins] processing order (largest bins first)
     unsigned long long* work;  // work counter (zeroed)
     uint64_t* stage;           // [N] (LDS slot << 48 | position << 32 | ordinal) per occurrence
-    uint64_t* kstage;          // [N] heavy bins: k-mer code + 1 per occurrence, parallel to stage
+    uint64_t* kstage;          // [KW N] heavy bins: the k-mer's table key per occurrence, parallel to stage
     uint32_t flat_l;           // heavy bin: initial partition depth >= flat_l (0 = never)
     const uint64_t* totals;    // totals[2] = nbins
     int K, M;
@@ -198,7 +204,7 @@ hipError_t launch_sk_kmers_total(const unsigned long long* part, uint64_t n, uns
                                  hipStream_t s);
 hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
                             hipStream_t s);
-hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, hipStream_t s);
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s);
 hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uint32_t* order, uint64_t max_bins,
                              hipStream_t s);
 hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s);
@@ -207,10 +213,10 @@ uint64_t sk_bucket_salt();
 hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, const uint64_t* totals,
                                 uint32_t* bcount, uint32_t* bmmer, uint64_t max_bins, hipStream_t s);
 // received records into local bucket regions (block-aggregated reservations)
-hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int M, uint32_t NB,
+hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
                                      uint64_t* regions, uint64_t cap, unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s);
-size_t bins_lds_bytes(uint32_t ts_log2);
+size_t bins_lds_bytes(uint32_t ts_log2, int KW);
 #ifdef KB_BIN_PROF
 void bins_prof_report(hipStream_t s);
 void lists_prof_report(hipStream_t s);

@@ -349,6 +349,9 @@ __global__ __launch_bounds__(256) void scan_insert_kernel(ScanArgs A) {
     uint32_t st = 0;
 
     for (uint64_t r = (uint64_t)blockIdx.x * 4 + wid; r < A.n_reads; r += nwaves) {
+        // a full table (or a probe past the limit) anywhere: the host reruns
+        // bigger, so the rest of this attempt is wasted work -- stop now
+        if (rfl((int)atomic_load_u32(A.status)) & (int)(ST_TABLE_FULL | ST_PROBE_LIMIT)) break;
         const int L = rfl((int)A.lens[r]);
         const int nK = L - K + 1;
         if (nK <= 0) continue;
@@ -412,7 +415,10 @@ __global__ __launch_bounds__(256) void scan_insert_kernel(ScanArgs A) {
 #else
                 const uint32_t slot = table_insert<KW>(A.table, A.mask, key, mm + 1u, A.max_probe, is_new);
 #endif
-                if (slot == NONE) st |= ST_PROBE_LIMIT;
+                if (slot == NONE) {
+                    st |= ST_PROBE_LIMIT;
+                    atomicOr(A.status, ST_PROBE_LIMIT);  // now: every wave stops at its next read
+                }
                 local_new += is_new ? 1u : 0u;
                 *(orow - i) = ((uint64_t)slot << 32) | ordv;
                 if (A.first && slot != NONE)  // insertion order of the reference (KB_TRACK_FIRST)
@@ -564,6 +570,7 @@ __global__ __launch_bounds__(256) void insert_sk_kernel(SkArgs A) {
     uint32_t local_new = 0, st = 0;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < A.n_rec;
          t += (uint64_t)gridDim.x * blockDim.x) {
+        if (atomic_load_u32(A.status) & (ST_TABLE_FULL | ST_PROBE_LIMIT)) break;  // rerun bigger
         const uint64_t* rec = A.recs + t * A.rec_words;
         const uint64_t h = rec[0];
         const uint64_t ordv = (uint32_t)h;
@@ -597,7 +604,10 @@ __global__ __launch_bounds__(256) void insert_sk_kernel(SkArgs A) {
             }
             bool is_new;
             const uint32_t slot = table_insert<KW>(A.table, A.mask, key, mm + 1u, A.max_probe, is_new);
-            if (slot == NONE) st |= ST_PROBE_LIMIT;
+            if (slot == NONE) {
+                st |= ST_PROBE_LIMIT;
+                atomicOr(A.status, ST_PROBE_LIMIT);
+            }
             local_new += is_new ? 1u : 0u;
             *(orow - j) = ((uint64_t)slot << 32) | ordv;
             if (A.first && slot != NONE)

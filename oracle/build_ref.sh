@@ -50,7 +50,7 @@ case $MODE in
     gcc -O2 -w -I"$REF" $DEFS -Dmain=binning_main -c "$TMP/binning_guarded.c" -o "$TMP/binning.o"
     gcc -O2 -w -I"$REF" -c "$REF/zhash.c" -o "$TMP/zhash.o"
     gcc -O2 -w -I"$REF" -c "$REF/llist.c" -o "$TMP/llist.o"
-    gcc -O2 -w -I"$REF" -c "$HERE/ref_harness.c" -o "$TMP/harness.o"
+    gcc -O2 -w -I"$REF" $DEFS -c "$HERE/ref_harness.c" -o "$TMP/harness.o"
     gcc -O2 "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/harness.o" -o "$BIN"
     ;;
   full|dropin)

@@ -14,13 +14,17 @@
  * harness owns the buffer.  K, M and the cutoff stay compile-time in the
  * reference, so build_ref.sh builds one binary per (K, M, cutoff).
  *
- * Usage:  ref_kK_mM_cC <reads-file> <READ_LENGTH> <prune 0|1>
+ * Usage:  ref_kK_mM_cC <reads-file> <READ_LENGTH> <prune 0|1> [time]
  * Output is unsorted (hash-bucket order); callers sort bytewise.
+ * With "time" the dump is skipped and one line goes to stdout instead:
+ *     kmers=<n> bin_s=<fgets+process_read loop> prune_s=<prune_data>
+ * (the timed region of BASELINE.md; bench.py's cpu_baseline "reference" leg).
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <stdbool.h>
+#include <time.h>
 
 #include "zhash.h"
 #include "llist.h"
@@ -41,20 +45,34 @@ int main(int argc, char **argv)
     if (!file) { perror(argv[1]); return 2; }
     int rl = atoi(argv[2]);
     int do_prune = atoi(argv[3]);
+    int timing = argc > 4 && strcmp(argv[4], "time") == 0;
+    struct timespec t0, t1, t2;
+    long long kmers = 0;
     char *read = malloc((size_t)rl + 1);
     struct ZHashTable *hash_table = zcreate_hash_table();
     int read_id = 0;
 
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     /* binning.c:1158-1166 */
     while (fgets(read, rl, file) != NULL) {
         int len = strlen(read);
         read[--len] = '\0';
+        if (len >= KMER_SIZE) kmers += len - KMER_SIZE + 1;
         process_read(hash_table, read, read_id++);
     }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
     fclose(file);
 
     if (do_prune)
         prune_data(hash_table); /* binning.c:1169 */
+    clock_gettime(CLOCK_MONOTONIC, &t2);
+    if (timing) {
+        printf("kmers=%lld bin_s=%.6f prune_s=%.6f\n", kmers,
+               (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec),
+               (t2.tv_sec - t1.tv_sec) + 1e-9 * (t2.tv_nsec - t1.tv_nsec));
+        free(read);
+        return 0;
+    }
 
     struct ZHashEntry *me, *ke;
     while ((me = iterate_level_one_hash(hash_table, false, false)) != NULL) {

@@ -36,7 +36,8 @@ def digests():
 
 @pytest.fixture(params=["table", "binned"])
 def engine(request, monkeypatch):
-    """KB_ENGINE for the case: the binned engine applies to K <= 31 without
-    first-occurrence tracking (elsewhere the table engine runs either way)"""
+    """KB_ENGINE for the case: the binned engine applies to K <= 63 (two-word
+    k-mers on its bucketed path: reads <= 512 bp); elsewhere the table engine
+    runs either way"""
     monkeypatch.setenv("KB_ENGINE", request.param)
     return request.param

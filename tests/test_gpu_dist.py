@@ -70,7 +70,7 @@ def test_virtual_shards(K, M, G):
     assert union == ora
 
 
-@pytest.mark.parametrize("K,M,G", [(31, 7, 1), (31, 7, 3), (21, 5, 8), (15, 7, 4)])
+@pytest.mark.parametrize("K,M,G", [(31, 7, 1), (31, 7, 3), (21, 5, 8), (15, 7, 4), (63, 7, 4), (40, 6, 3)])
 def test_route_scatter(K, M, G, engine):
     """one-pass sender: per destination the same multiset of records as
     plan/pack (order is free), a too-small region reports KB_EOVERFLOW and

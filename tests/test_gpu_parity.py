@@ -105,6 +105,48 @@ def test_binned_engine_selected(engine):
         assert t["n_superkmers"] > 0 and t["n_bins"] > 0
 
 
+@pytest.mark.parametrize("K,M", [(63, 7), (33, 7), (32, 8), (45, 1), (63, 1), (40, 6)])
+def test_binned_two_word_kmers(K, M, engine, monkeypatch):
+    """K > 31: the binned engine with two-word table keys (LDS claim word +
+    published low word), 4-word super-k-mer spans and 64 length rows in the
+    bucket ordering -- bit-exact against the oracle, with and without prune,
+    first occurrences tracked; reads > 512 bp (or a forced radix path) hand
+    two-word k-mers to the table engine"""
+    rng = np.random.default_rng(K * 7 + M)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=4000)
+    reads = []
+    for _ in range(1200):
+        L = int(rng.integers(K - 5, 300))
+        s = int(rng.integers(0, 4000 - L))
+        r = genome[s:s + L].copy()
+        m = rng.random(L) < 0.01
+        r[m] = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=int(m.sum()))
+        reads.append(r.tobytes())
+    bases, lens = kbin.pack_reads(reads)
+    for prune in (False, True):
+        ora = oracle.bin_reads(bases, lens, K, M, 1, prune)
+        with kbin.Engine(K, M, cutoff=1, max_read_len=300, flags=kbin.KB_TRACK_FIRST) as eng:
+            eng.set_timing(True)
+            eng.submit(bases=bases, lens=lens, first_id=0)
+            eng.finalize(prune=prune)
+            t = eng.timing()
+            res = eng.export()
+        assert t["engine"] == (kbin.KB_ENG_BINNED if engine == "binned" else kbin.KB_ENG_TABLE)
+        assert_same(res, ora)
+        last = res.ids[res.offset[1:].astype(np.int64) - 1]  # oldest id = first occurrence
+        np.testing.assert_array_equal(res.first >> np.uint64(16), last.astype(np.uint64))
+    if engine != "binned":
+        return
+    monkeypatch.setenv("KB_BIN_RADIX", "1")  # no radix path for two-word keys: table engine
+    ora = oracle.bin_reads(bases, lens, K, M, 1, True)
+    with kbin.Engine(K, M, cutoff=1, max_read_len=300) as eng:
+        eng.set_timing(True)
+        eng.submit(bases=bases, lens=lens, first_id=0)
+        eng.finalize(prune=True)
+        assert eng.timing()["engine"] == kbin.KB_ENG_TABLE
+        assert_same(eng.export(), ora)
+
+
 @pytest.mark.parametrize("K,M", [(31, 7), (6, 3), (21, 5), (2, 1)])
 def test_binned_radix_path(K, M, engine, monkeypatch):
     """the binned engine's radix-sort record path (the fallback when a local
@@ -141,9 +183,10 @@ def test_binned_entry_capacity_rerun(prune, engine, monkeypatch):
     assert_same(res, ora)
 
 
-@pytest.mark.parametrize("P,radix,long_reads", [(1, False, False), (3, False, False), (8, False, False),
-                                                 (4, True, False), (3, False, True)])
-def test_partitioned_passes(P, radix, long_reads, engine, monkeypatch):
+@pytest.mark.parametrize("P,radix,long_reads,K,M", [(1, False, False, 21, 5), (3, False, False, 21, 5),
+                                                     (8, False, False, 21, 5), (4, True, False, 21, 5),
+                                                     (3, False, True, 21, 5), (4, False, False, 63, 7)])
+def test_partitioned_passes(P, radix, long_reads, K, M, engine, monkeypatch):
     """kb_set_partition: P passes over the same submitted reads bin disjoint
     mmer slices whose union is the single-pass result, list for list"""
     bases, lens = oracle.read_fgets(kbin.REPO_ROOT / "tests/golden/reads.txt", 101)
@@ -155,7 +198,6 @@ def test_partitioned_passes(P, radix, long_reads, engine, monkeypatch):
     off = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
     reads = [bases[off[i]:off[i + 1]] for i in range(3000)] + extra
     bases, lens = kbin.pack_reads(reads)
-    K, M = 21, 5
     ora = oracle.bin_reads(bases, lens, K, M, 1, True)
     if radix:
         monkeypatch.setenv("KB_BIN_RADIX", "1")
@@ -252,8 +294,10 @@ def test_device_generator_roundtrip():
     assert_same(res, ora)
 
 
-@pytest.mark.parametrize("ts_log2,flat_l,fill", [(13, 2, 60), (10, 1, 60), (10, 1, 30), (10, 0, 60)])
-def test_heavy_bins_flat_lists(ts_log2, flat_l, fill, engine, monkeypatch):
+@pytest.mark.parametrize("ts_log2,flat_l,fill,K", [(13, 2, 60, 31), (10, 1, 60, 31), (10, 1, 30, 31),
+                                                    (10, 0, 60, 31), (12, 2, 60, 63), (10, 1, 30, 63),
+                                                    (10, 0, 60, 63)])
+def test_heavy_bins_flat_lists(ts_log2, flat_l, fill, K, engine, monkeypatch):
     """high coverage (40K reads of a 3 kbp genome, 2000x): bins with far more
     distinct keys than one LDS table holds take the flat per-partition lists
     (KB_BIN_FLAT_L; small tables force it, low fill forces deeper first
@@ -272,9 +316,9 @@ def test_heavy_bins_flat_lists(ts_log2, flat_l, fill, engine, monkeypatch):
     kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, 3000, 5000, 9)
     torch.cuda.synchronize()
     bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n, wpr, n * L)
-    ora = oracle.bin_reads(bases, hl, 31, 7, 1, True)
-    assert int(ora.count.max()) > 1000
-    with kbin.Engine(31, 7, cutoff=1, max_read_len=L, flags=kbin.KB_TRACK_FIRST) as eng:
+    ora = oracle.bin_reads(bases, hl, K, 7, 1, True)
+    assert int(ora.count.max()) > (1000 if K <= 31 else 500)  # (fewer 63-mers per 150-bp read)
+    with kbin.Engine(K, 7, cutoff=1, max_read_len=L, flags=kbin.KB_TRACK_FIRST) as eng:
         for _ in range(2):  # the second pass runs with the learned density
             eng.reset()
             eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
@@ -284,7 +328,7 @@ def test_heavy_bins_flat_lists(ts_log2, flat_l, fill, engine, monkeypatch):
             # first occurrence: its call ordinal is the list's oldest id
             last = res.ids[res.offset[1:].astype(np.int64) - 1]
             np.testing.assert_array_equal(res.first >> np.uint64(16), last.astype(np.uint64))
-            assert int((res.first & np.uint64(0xFFFF)).max()) <= L - 31
+            assert int((res.first & np.uint64(0xFFFF)).max()) <= L - K
 
 
 def test_alphabet_rejected():
@@ -331,7 +375,7 @@ def test_dropin_reference_program(golden_dir):
         pytest.skip("drop-in binaries not built (needs the reference at build time)")
 
 
-@pytest.mark.parametrize("n,L,K,M", [(1_000_000, 150, 31, 7), (400_000, 250, 27, 6)])
+@pytest.mark.parametrize("n,L,K,M", [(1_000_000, 150, 31, 7), (400_000, 250, 27, 6), (300_000, 250, 63, 7)])
 def test_full_scale_engines_agree(engine, n, L, K, M):
     """BASELINE C2 size (1M x 150 bp, K31 M7, cutoff 1) and a longer-read
     variant: both engines produce the same canonical result; CSR contract,
