@@ -15,7 +15,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <queue>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/kbin.h"
@@ -144,6 +146,18 @@ struct kb_ctx {
     uint64_t n_occ_entries_hint = 0;  // entries of the last finalize (lists grid)
     uint64_t ecap_hint = 0;    // entry capacity for the next binned finalize
     uint32_t part = 0, part_n = 1;  // kb_set_partition: this pass's mmer partition
+    // balanced local buckets: records per canonical mmer seen in earlier passes,
+    // and one device map (mmer -> bucket) per (part, part_n) key
+    std::vector<uint32_t> mmer_w;
+    struct BucketMap {
+        uint64_t key = 0;
+        uint32_t nb = 0;
+        bool stale = false;
+        uint64_t want_max = 0;  // the largest bucket load the packing expects (records)
+        uint64_t want_tot = 0;
+        DevBuf<uint16_t> map;
+    };
+    std::vector<BucketMap> bmaps;
     uint64_t* h_totals = nullptr;
     uint32_t* h_misc = nullptr;
 
@@ -240,6 +254,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
     c->misc.release(); c->totals.release(); c->first.release(); c->e_first.release();
+    for (auto& m : c->bmaps) m.map.release();
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
@@ -886,6 +901,93 @@ static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered
     return KB_OK;
 }
 
+// ---- balanced local buckets.  A bucket's records are ordered by ONE
+// workgroup (bucket_kernel), so the largest bucket sets that kernel's time.
+// The minimizer rule (leftmost max of the complement-canonical score) makes
+// mmer frequencies very uneven: hashed into 1024 buckets the largest holds
+// ~8x the mean.  After a pass the host learns the records per mmer from the
+// bin descriptors and packs the mmers of each (part, part_n) key into buckets
+// longest-processing-time first; later passes route records by that map.
+static uint64_t bmap_key(const kb_ctx* c) { return ((uint64_t)c->part << 32) | c->part_n; }
+
+static kb_ctx::BucketMap* bmap_find(kb_ctx* c, uint32_t NB) {
+    for (auto& m : c->bmaps)
+        if (m.key == bmap_key(c) && m.nb == NB) return &m;
+    return nullptr;
+}
+
+static int bmap_build(kb_ctx* c, uint32_t NB) {
+    const int M = c->p.M;
+    const uint32_t half = 1u << (2 * M - 1);
+    std::vector<std::pair<uint32_t, uint32_t>> items;  // (records, mmer)
+    std::vector<uint16_t> h(half);
+    for (uint32_t i = 0; i < half; i++) {
+        const uint32_t mm = half + i;
+        if (c->part_n > 1 && sk_hash_dest(mm, c->part_n, 0x9E3779B97F4A7C15ull) != c->part) {
+            h[i] = (uint16_t)sk_hash_dest(mm, NB, sk_bucket_salt());  // another pass's mmer: never seen here
+            continue;
+        }
+        if (i < c->mmer_w.size() && c->mmer_w[i]) items.push_back({c->mmer_w[i], mm});
+        else h[i] = (uint16_t)sk_hash_dest(mm, NB, sk_bucket_salt());  // unseen: hash
+    }
+    std::sort(items.begin(), items.end(), [](const std::pair<uint32_t, uint32_t>& a,
+                                             const std::pair<uint32_t, uint32_t>& b) { return a.first > b.first; });
+    // least-loaded bucket first; at most 128 mmers per bucket (bucket_kernel maps 256)
+    using Slot = std::pair<uint64_t, uint32_t>;  // (load, bucket)
+    std::priority_queue<Slot, std::vector<Slot>, std::greater<Slot>> pq;
+    std::vector<uint32_t> nm(NB, 0);
+    for (uint32_t b = 0; b < NB; b++) pq.push({0, b});
+    for (auto& it : items) {
+        Slot sl = pq.top();
+        pq.pop();
+        while (nm[sl.second] >= 128 && !pq.empty()) {  // full: retire it
+            sl = pq.top();
+            pq.pop();
+        }
+        h[it.second - half] = (uint16_t)sl.second;
+        nm[sl.second]++;
+        pq.push({sl.first + it.first, sl.second});
+    }
+    uint64_t want_max = 0, want_tot = 0;
+    while (!pq.empty()) {
+        want_max = std::max(want_max, pq.top().first);
+        want_tot += pq.top().first;
+        pq.pop();
+    }
+    kb_ctx::BucketMap* m = bmap_find(c, NB);
+    if (!m) {
+        c->bmaps.emplace_back();
+        m = &c->bmaps.back();
+        m->key = bmap_key(c);
+        m->nb = NB;
+    }
+    HIPCHK(m->map.ensure(half));
+    HIPCHK(hipMemcpyAsync(m->map.p, h.data(), half * sizeof(uint16_t), hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));  // h is a local
+    m->stale = false;
+    m->want_max = want_max;
+    m->want_tot = want_tot;
+    return KB_OK;
+}
+
+// after a bucketed pass: learn records per mmer from the bin descriptors and
+// (re)build this key's map when it is missing or the pass found it unbalanced
+static int bmap_learn(kb_ctx* c, uint32_t NB, uint64_t R, uint64_t nbins) {
+    if (!env_int("KB_BIN_BALANCE", 1) || R < (uint64_t)std::max(0, env_int("KB_BIN_BALANCE_MIN", 1 << 18)))
+        return KB_OK;
+    kb_ctx::BucketMap* m = bmap_find(c, NB);
+    if (m && !m->stale) return KB_OK;
+    std::vector<uint32_t> mm(nbins), cnt(nbins);
+    HIPCHK(hipMemcpyAsync(mm.data(), c->bmmer.p, nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipMemcpyAsync(cnt.data(), c->bcount.p, nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    const uint32_t half = 1u << (2 * c->p.M - 1);
+    if (c->mmer_w.size() != half) c->mmer_w.assign(half, 0);
+    for (uint64_t b = 0; b < nbins; b++)
+        if (mm[b] >= half && mm[b] < 2 * half) c->mmer_w[mm[b] - half] = std::max(cnt[b], 1u);
+    return bmap_build(c, NB);
+}
+
 // ---- phase A, bucketed: records straight into NB local bucket regions
 // (hash of the mmer); the learned capacity grows (and the pass reruns) when a
 // bucket overflows.  Reads: the one-pass super-k-mer kernel in region mode;
@@ -895,6 +997,8 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
     uint64_t nrec = 0;
     for (auto& b : c->batches)
         if (!b.routed) nrec += b.superkmers ? b.n_reads : b.n_reads * 16;
+    kb_ctx::BucketMap* bm = bmap_find(c, NB);
+    const uint16_t* bmap = bm ? bm->map.p : nullptr;
     for (int attempt = 0; attempt < 3; attempt++) {
         const uint64_t cap = c->bucket_cap ? c->bucket_cap : nrec / NB + 1024;
         HIPCHK(c->regions.ensure(NB * cap * (1 + 2 * c->KW)));
@@ -909,7 +1013,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
             if (b.routed || !b.n_reads) continue;
             if (received) {
                 if (!b.superkmers) continue;
-                HIPCHK(launch_sk_convert_buckets(b.recs, b.n_reads, rec_words(c), 2 * c->KW, M, NB, c->regions.p, cap,
+                HIPCHK(launch_sk_convert_buckets(b.recs, b.n_reads, rec_words(c), 2 * c->KW, M, NB, bmap, c->regions.p, cap,
                                                  c->bfill.p, c->misc.p,
                                                  reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
             } else {
@@ -930,6 +1034,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
                 a.G = NB;
                 a.dest_salt = sk_bucket_salt();
                 a.rw = 1 + 2 * c->KW;  // header + span words
+                a.bucket_map = bmap;
                 a.binned_fmt = 1;
                 a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p);
                 HIPCHK(launch_sk(a, true, c->s));
@@ -939,7 +1044,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
             }
             c->tm.scan_insert_launches++;
         }
-        std::vector<unsigned long long> fill(NB);
+        std::vector<unsigned long long> fill(NB);  // (bmap: see below)
         HIPCHK(hipMemcpyAsync(fill.data(), c->bfill.p, NB * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
@@ -953,6 +1058,11 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
             mx = std::max<uint64_t>(mx, fill[d]);
         }
         N = c->h_totals[8];
+        // a map that no longer fits (largest bucket > 1.5x what the packing
+        // expected, scaled to this pass's records): relearn it after this pass
+        if (bm && R && bm->want_tot &&
+            (double)mx > 1.5 * (double)bm->want_max * (double)R / (double)bm->want_tot + 64.0)
+            bm->stale = true;
         if (mx <= cap) {
             c->bucket_cap_used = cap;  // the region stride of this pass
             c->bucket_cap = std::max<uint64_t>(c->bucket_cap, mx + mx / 8 + 1024);  // next passes
@@ -1203,6 +1313,10 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     c->n_entries = c->h_totals[0];
     c->n_ids = c->h_totals[1];
     c->n_distinct = c->h_totals[6];
+    if (bucketed) {
+        const int rc2 = bmap_learn(c, NB, R, std::min<uint64_t>(c->h_totals[2], max_bins));
+        if (rc2) return rc2;
+    }
     c->n_occ_entries_hint = c->n_entries;
     c->ecap_hint = c->n_entries + c->n_entries / 4 + 1024;
     if (N) c->rho = (float)((double)c->n_distinct / (double)N);

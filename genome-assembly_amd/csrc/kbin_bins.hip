@@ -56,6 +56,15 @@ uint64_t sk_bucket_salt() { return BUCKET_SALT; }
 DEV uint32_t dest_of(uint32_t mmer, uint32_t G, uint64_t salt) {
     return (uint32_t)((mix64((uint64_t)mmer + salt) >> 32) % G);
 }
+uint32_t sk_hash_dest(uint32_t mmer, uint32_t G, uint64_t salt) {
+    uint64_t x = (uint64_t)mmer + salt;  // mix64 (kbin_device.h), host side
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return (uint32_t)((x >> 32) % G);
+}
 DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) { return dest_of(mmer, G, OWNER_SALT); }
 // a pass keeps the super-k-mers of its own mmer partition
 DEV bool in_part(uint32_t mmer, uint32_t part, uint32_t part_n) {
@@ -141,6 +150,12 @@ DEV void put_record(const SkScanArgs& A, uint64_t* o, uint32_t ord, uint64_t lo,
     for (int w = 1; w < A.rw; w++) o[w] = window64(sw, (int)lo + 32 * (w - 1));
 }
 
+// destination region of a super-k-mer: its owner rank (routing) or its local
+// bucket (the balanced map when the host has one, else the hash)
+DEV uint32_t region_of(const SkScanArgs& A, uint32_t mmer) {
+    return A.bucket_map ? (uint32_t)A.bucket_map[mmer - (1u << (2 * A.M - 1))] : dest_of(mmer, A.G, A.dest_salt);
+}
+
 // LDS row of one read in sk_thread_kernel: the read's words, then zero words
 // so that every span window (up to 4 words past the first base) stays inside
 __device__ __host__ inline int sk_row_words(int RW, int rw) { return RW + (rw > 3 ? rw - 1 : 2); }
@@ -224,7 +239,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     if (loc < SK_STAGE) {
                         stg[loc] = e;
                     } else if (route) {  // beyond the staging area: one record, its own slot
-                        const uint32_t d = dest_of((uint32_t)best, A.G, A.dest_salt);
+                        const uint32_t d = region_of(A, (uint32_t)best);
                         const uint64_t i = atomicAdd(&A.dest_ctr[d], 1ull);
                         if (i < A.region_cap)
                             put_record(A, A.regions + (d * A.region_cap + i) * (uint64_t)A.rw,
@@ -253,7 +268,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                 for (uint32_t d = tid; d < A.G; d += 256) dcnt[d] = 0;
                 __syncthreads();
                 for (uint32_t i = tid; i < span; i += 256)
-                    atomicAdd(&dcnt[dest_of((uint32_t)(stg[i] >> 37), A.G, A.dest_salt)], 1u);
+                    atomicAdd(&dcnt[region_of(A, (uint32_t)(stg[i] >> 37))], 1u);
                 __syncthreads();
                 for (uint32_t d = tid; d < A.G; d += 256) {
                     dbase[d] = dcnt[d] ? atomicAdd(&A.dest_ctr[d], (unsigned long long)dcnt[d]) : 0ull;
@@ -262,7 +277,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                 __syncthreads();
                 for (uint32_t i = tid; i < span; i += 256) {
                     const uint64_t e = stg[i];
-                    const uint32_t d = dest_of((uint32_t)(e >> 37), A.G, A.dest_salt);
+                    const uint32_t d = region_of(A, (uint32_t)(e >> 37));
                     const uint64_t slot = dbase[d] + atomicAdd(&dcnt[d], 1u);
                     if (slot >= A.region_cap) continue;  // counted: the caller retries bigger
                     const uint32_t row = (uint32_t)((e >> 29) & 0xFFu);
@@ -566,10 +581,8 @@ struct Span<1> {
         w = A.w0[r];
         x = A.w1[r];
     }
-    DEV TKey<1> key(int K, bool rev) const {
-        const uint64_t kmask = (1ull << (2 * K)) - 1ull;
-        return TKey<1>{((w >> (64 - 2 * K)) ^ (rev ? kmask : 0ull)) + 1ull};
-    }
+    // fl = all ones when the complement wins (binning.c:1029-1040), else 0
+    DEV TKey<1> key(int K, uint64_t fl) const { return TKey<1>{((w ^ fl) >> (64 - 2 * K)) + 1ull}; }
     DEV void step() {
         w = (w << 2) | (x >> 62);
         x <<= 2;
@@ -584,15 +597,12 @@ struct Span<2> {
         s2 = A.w2[r];
         s3 = A.w3[r];
     }
-    // complement without reversal (binning.c:1029-1040) = every code bit flipped
-    DEV TKey<2> key(int K, bool rev) const {
+    // complement without reversal (binning.c:1029-1040) = every code bit
+    // flipped: fl = all ones when the complement wins, else 0
+    DEV TKey<2> key(int K, uint64_t fl) const {
         const int kh = K - 32;  // bases above the low 64-bit word (0..31)
-        uint64_t hi = kh ? s0 >> (64 - 2 * kh) : 0ull;
-        uint64_t lo = kh ? (s0 << (2 * kh)) | (s1 >> (64 - 2 * kh)) : s0;
-        if (rev) {
-            hi ^= kh ? (1ull << (2 * kh)) - 1ull : 0ull;
-            lo = ~lo;
-        }
+        const uint64_t hi = kh ? (s0 ^ fl) >> (64 - 2 * kh) : 0ull;
+        const uint64_t lo = (kh ? (s0 << (2 * kh)) | (s1 >> (64 - 2 * kh)) : s0) ^ fl;
         return TKey<2>{((hi << 1) | (lo >> 63)) + 1ull, lo | PUB};
     }
     DEV void step() {
@@ -698,12 +708,12 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
         const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);  // the record's first k-mer in its read
-        const bool rev = ((hd >> 44) & 1ull) != 0;
+        const uint64_t fl = 0ull - ((hd >> 44) & 1ull);        // complement wins: flip every bit
         // records of a bin are sorted longest first: lane 0 holds the chunk's max
         int nmax = rfl(n);
         if (__ballot(n > nmax)) nmax = rfl((int)wave_max_u32((uint32_t)n));
         for (int j = 0; j < nmax; j++) {
-            const TKey<KW> key = sp.key(K, rev);
+            const TKey<KW> key = sp.key(K, fl);
             sp.step();
             const bool take = j < n && (l == 0 || (key.part() & pmask) == p);
             const uint64_t m = __ballot(take);
@@ -735,9 +745,9 @@ DEV void expand_bin(const BinArgs& A, uint32_t lo, uint32_t hi, G&& g) {
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
         const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);
-        const bool rev = ((hd >> 44) & 1ull) != 0;
+        const uint64_t fl = 0ull - ((hd >> 44) & 1ull);
         for (int j = 0; j < n; j++) {
-            g(sp.key(K, rev), ord, (uint32_t)(rlo + (uint32_t)j));
+            g(sp.key(K, fl), ord, (uint32_t)(rlo + (uint32_t)j));
             sp.step();
         }
     }
@@ -765,6 +775,7 @@ DEV void kst_store(uint64_t* kst, uint32_t i, const TKey<KW>& k) {
 // into flat per-partition lists -- and each partition is then swept from its
 // list.  Up to FLAT_MAX partitions; deeper splits filter the flat lists.
 constexpr uint32_t FLAT_MAX = 4096;
+constexpr uint32_t PRUNED = 0x80000000u;  // cursor of a pruned (or empty) slot in sweep 2
 constexpr uint64_t M48 = (1ull << 48) - 1ull;
 
 template <int KW>
@@ -905,8 +916,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 const uint32_t h0 = k0.hash(), h1 = k1.hash();
                 // first probes of both k-mers in flight together; the rest
                 // (empty slot, collision chain) takes the full insert path
-                int l0 = v0 && T.hit(h0 & tmask, k0) ? (int)(h0 & tmask) : -3;
-                int l1 = v1 && T.hit(h1 & tmask, k1) ? (int)(h1 & tmask) : -3;
+                const bool f0 = T.hit(h0 & tmask, k0), f1 = T.hit(h1 & tmask, k1);
+                int l0 = f0 ? (int)(h0 & tmask) : -3;
+                int l1 = f1 ? (int)(h1 & tmask) : -3;
                 if (v0 && l0 == -3) l0 = T.insert(tmask, k0, h0, &S.n_keys, limit);
                 if (v1 && l1 == -3) l1 = T.insert(tmask, k1, h1, &S.n_keys, limit);
                 if (v0) {
@@ -1020,7 +1032,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                         e++;
                         off += c;
                     } else {
-                        cnt[i] = NONE;
+                        cnt[i] = PRUNED;
                     }
                 }
             }
@@ -1041,8 +1053,10 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                     if (filt && (kst_load<KW>(kst, fa + i).part() & pmask) != P) continue;
                     const uint64_t v = stage[i];
                     const uint32_t ls = (uint32_t)(v >> 48);
-                    if (cnt[ls] != NONE) {
-                        const uint32_t pos = atomicAdd(&cnt[ls], 1u);
+                    // one returning atomic: a pruned key's cursor starts at PRUNED and
+                    // takes at most cutoff adds, so it never reaches a real position
+                    const uint32_t pos = atomicAdd(&cnt[ls], 1u);
+                    if (pos < PRUNED) {
                         A.ids_ord[i0 + pos] = (uint32_t)v;
                         // (ordinal << 16 | position): binning.c inserts a key at its first
                         // occurrence (1045-1057); KB_TRACK_FIRST keeps it for the zhash layout
@@ -1057,7 +1071,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 uint32_t e = (uint32_t)ex;
                 for (uint32_t k = 0; k < per; k++) {
                     const uint32_t i = tid * per + k;
-                    if (cnt[i] != NONE) A.e_first[e0 + e++] = T.ca[i];
+                    if (cnt[i] < PRUNED) A.e_first[e0 + e++] = T.ca[i];
                 }
             }
             __threadfence_block();
@@ -1938,6 +1952,7 @@ hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s) {
 template <int SPW>
 __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t* __restrict__ recs, uint64_t n_rec,
                                                                  int rw, int M, uint32_t NB,
+                                                                 const uint16_t* __restrict__ bucket_map,
                                                                  uint64_t* __restrict__ regions, uint64_t cap,
                                                                  unsigned long long* bfill, uint32_t* status,
                                                                  unsigned long long* n_kmers) {
@@ -1970,7 +1985,7 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
             neg |= (int32_t)id < 0;
             kmers += n;
             pay0[j] = (uint64_t)id | (n << 32) | (so << 38) | ((uint64_t)rev << 44) | (lo << 45);
-            dst[j] = dest_of(canon, NB, BUCKET_SALT);
+            dst[j] = bucket_map ? (uint32_t)bucket_map[canon - halfM] : dest_of(canon, NB, BUCKET_SALT);
             atomicAdd(&cnt[dst[j]], 1u);
         }
         __syncthreads();
@@ -1998,17 +2013,17 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
 }
 
 hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
-                                     uint64_t* regions, uint64_t cap, unsigned long long* bfill,
+                                     const uint16_t* bucket_map, uint64_t* regions, uint64_t cap, unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s) {
     if (!n_rec) return hipSuccess;
     if (NB < 1 || NB > SK_MAX_DEST || (spw != 2 && spw != 4)) return hipErrorInvalidValue;
     const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
     if (spw == 2)
         hipLaunchKernelGGL(sk_convert_buckets_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, regions, cap, bfill, status, n_kmers);
+                           NB, bucket_map, regions, cap, bfill, status, n_kmers);
     else
         hipLaunchKernelGGL(sk_convert_buckets_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, regions, cap, bfill, status, n_kmers);
+                           NB, bucket_map, regions, cap, bfill, status, n_kmers);
     return hipGetLastError();
 }
 

@@ -106,6 +106,9 @@ struct SkScanArgs {
     uint64_t dest_salt;
     int rw;
     int binned_fmt;
+    // local buckets only: canonical mmer - 2^(2M-1) -> bucket, balanced by the
+    // host from the bins of earlier passes (null: hash of the mmer)
+    const uint16_t* bucket_map;
     // partitioned passes (kb_set_partition): only super-k-mers whose mmer is in
     // partition part of part_n are emitted and counted (part_n <= 1: all)
     uint32_t part, part_n;
@@ -209,11 +212,13 @@ hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uin
                              hipStream_t s);
 hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s);
 uint64_t sk_bucket_salt();
+uint32_t sk_hash_dest(uint32_t mmer, uint32_t G, uint64_t salt);  // host twin of dest_of
 // radix path: bin descriptors from run starts of the sorted keys
 hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, const uint64_t* totals,
                                 uint32_t* bcount, uint32_t* bmmer, uint64_t max_bins, hipStream_t s);
 // received records into local bucket regions (block-aggregated reservations)
 hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
+                                     const uint16_t* bucket_map,
                                      uint64_t* regions, uint64_t cap, unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s);
 size_t bins_lds_bytes(uint32_t ts_log2, int KW);

@@ -56,8 +56,9 @@ extern "C" {
                             to rebuild its exact zhash layout */
 #define KB_ENGINE_TABLE 2  /* force the global-table engine                      */
 #define KB_ENGINE_BINNED 4 /* force the binned engine where it applies (the
-                              default): K <= 31.  Elsewhere (K > 31) the table
-                              engine runs.  Neither flag: KB_ENGINE=table|binned from
+                              default): K <= 31 always; K <= 63 on reads of
+                              <= 512 bp (or received super-k-mers).  Elsewhere
+                              the table engine runs.  Neither flag: KB_ENGINE=table|binned from
                               the environment (A/B runs), else binned.
                               Results are identical either way. */
 
@@ -196,7 +197,7 @@ int kb_route_plan(kb_ctx *ctx, uint32_t n_dest, uint64_t *h_counts);
 int kb_route_pack(kb_ctx *ctx, uint64_t *d_send);
 int kb_submit_superkmers_device(kb_ctx *ctx, const uint64_t *d_records, uint64_t n_records);
 
-/* One-pass sender (binned engine only: K <= 31, reads of <= 512 bp).  Writes every record of the read batches
+/* One-pass sender (binned engine only: K <= 63, reads of <= 512 bp).  Writes every record of the read batches
  * submitted so far into d_regions: destination d's records at
  * d_regions + d * region_cap * kb_record_words, h_counts[d] of them, in no
  * particular order (the binned receiver orders lists by read id, not by

@@ -229,6 +229,36 @@ def test_partitioned_passes(P, radix, long_reads, K, M, engine, monkeypatch):
     assert tuple(dig) == kbin.result_digest(ora)  # digests add over partitions
 
 
+@pytest.mark.parametrize("K,M", [(21, 5), (63, 7)])
+def test_balanced_buckets(K, M, engine, monkeypatch):
+    """after a pass the host packs the mmers into local buckets by their
+    record counts (largest first, least-loaded bucket); later passes route
+    records by that map, per partition key -- every pass equals the oracle"""
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    monkeypatch.setenv("KB_BIN_BALANCE_MIN", "0")
+    rng = np.random.default_rng(K)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20000)
+    reads = []
+    for _ in range(3000):
+        L = int(rng.integers(K, 260))
+        s0 = int(rng.integers(0, 20000 - L))
+        reads.append(genome[s0:s0 + L].tobytes())
+    bases, lens = kbin.pack_reads(reads)
+    ora = oracle.bin_reads(bases, lens, K, M, 1, True)
+    with kbin.Engine(K, M, cutoff=1, max_read_len=300) as eng:
+        for P in (1, 3):
+            for _ in range(3):  # the first pass of a key learns its map, the next ones use it
+                parts = []
+                for p in range(P):
+                    eng.reset()
+                    eng.submit(bases=bases, lens=lens, first_id=0)
+                    eng.set_partition(p, P)
+                    eng.finalize(prune=True)
+                    parts.append(eng.export())
+                assert_same(kbin.Result.concat(parts), ora)
+
+
 def test_explicit_ids_nonmonotone():
     """ids are caller-supplied (process_read's read_id): lists keep REVERSE CALL
     order, not id order (binning.c:1065-1068)."""
