@@ -638,6 +638,7 @@ extern "C" int kb_route_scatter(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions,
         if (!b.routed && !b.superkmers && b.RW > 16)
             return fail(KB_EINVAL, "kb_route_scatter serves reads of <= 512 bp (use plan/pack)");
     if (region_cap && !d_regions) return fail(KB_EINVAL, "null regions");
+    if (region_cap >= 0xFFFFFFFFull) return fail(KB_EINVAL, "region_cap must be below 2^32 records");
     int rc = set_device(c);
     if (rc) return rc;
     bool affine = false;

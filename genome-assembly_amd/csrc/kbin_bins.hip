@@ -169,7 +169,10 @@ __device__ __host__ inline int sk_row_words(int RW, int rw) { return RW + (rw > 
 // The write pass stages each record as one u64 in LDS and the block then
 // writes its (contiguous) record range with coalesced stores.
 constexpr int SK_THREAD_RW = 16;
-constexpr uint32_t SK_STAGE = 4096;  // staged records per block (8 B each)
+// staged records per block (8 B each): 256 reads of 150 bp make ~2.5 K; a
+// block past it stores the rest directly.  With the per-destination arrays
+// and the read rows the block fits three to a CU.
+constexpr uint32_t SK_STAGE = 3584;
 constexpr uint32_t SK_MAX_DEST = 1024;  // destination regions (ranks or buckets)
 
 template <bool WRITE>
@@ -186,7 +189,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     __shared__ uint32_t span_end;
     __shared__ unsigned long long s_base;
     __shared__ uint32_t dcnt[SK_MAX_DEST];
-    __shared__ unsigned long long dbase[SK_MAX_DEST];
+    __shared__ uint32_t dbase[SK_MAX_DEST];  // reserved slot in the region (< region_cap < 2^32)
     const bool route = WRITE && A.regions;          // records to destination regions, any order
     const bool alloc = WRITE && (A.rec_ctr || route);  // records placed by block allocation
     uint64_t kmers = 0;
@@ -271,14 +274,16 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     atomicAdd(&dcnt[region_of(A, (uint32_t)(stg[i] >> 37))], 1u);
                 __syncthreads();
                 for (uint32_t d = tid; d < A.G; d += 256) {
-                    dbase[d] = dcnt[d] ? atomicAdd(&A.dest_ctr[d], (unsigned long long)dcnt[d]) : 0ull;
+                    dbase[d] = dcnt[d] ? (uint32_t)min<unsigned long long>(
+                                             atomicAdd(&A.dest_ctr[d], (unsigned long long)dcnt[d]), 0xFFFFFFFFull)
+                                       : 0u;
                     dcnt[d] = 0;
                 }
                 __syncthreads();
                 for (uint32_t i = tid; i < span; i += 256) {
                     const uint64_t e = stg[i];
                     const uint32_t d = region_of(A, (uint32_t)(e >> 37));
-                    const uint64_t slot = dbase[d] + atomicAdd(&dcnt[d], 1u);
+                    const uint64_t slot = (uint64_t)dbase[d] + atomicAdd(&dcnt[d], 1u);
                     if (slot >= A.region_cap) continue;  // counted: the caller retries bigger
                     const uint32_t row = (uint32_t)((e >> 29) & 0xFFu);
                     put_record(A, A.regions + (d * A.region_cap + slot) * (uint64_t)A.rw,
@@ -1722,28 +1727,36 @@ hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s) 
     return hipGetLastError();
 }
 
-// Bin processing order: descending log2(records) (longest-processing-time
-// first for the persistent blocks; a bin's cost follows its super-k-mers).
-// One block; counting sort over 33 classes.
+// Bin processing order: descending records (longest-processing-time first
+// for the persistent blocks; a bin's cost follows its super-k-mers).  One
+// block; counting sort over 8 classes per power of two (class = log2 of the
+// count with 3 fractional bits), largest class first.
+DEV uint32_t order_class(uint32_t c) {
+    if (c < 8) return c;
+    const uint32_t msb = 31u - (uint32_t)__clz(c);
+    return msb * 8u + ((c >> (msb - 3u)) & 7u);  // <= 255
+}
+
 __global__ __launch_bounds__(1024) void bins_order_kernel(const uint32_t* __restrict__ bcount,
                                                           const uint64_t* __restrict__ totals,
                                                           uint32_t* __restrict__ order, uint64_t max_bins) {
-    __shared__ uint32_t hist[64];
+    constexpr uint32_t NC = 256;
+    __shared__ uint32_t hist[NC];
     const uint32_t nbins = (uint32_t)min(totals[2], max_bins);
-    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i < NC; i += 1024) hist[i] = 0;
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) atomicAdd(&hist[32 - __clz(bcount[b])], 1u);
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) atomicAdd(&hist[order_class(bcount[b])], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {  // exclusive offsets, class 32 first
+    if (threadIdx.x == 0) {  // exclusive offsets, largest class first
         uint32_t acc = 0;
-        for (int c = 32; c >= 0; c--) {
+        for (int c = NC - 1; c >= 0; c--) {
             const uint32_t h = hist[c];
             hist[c] = acc;
             acc += h;
         }
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) order[atomicAdd(&hist[32 - __clz(bcount[b])], 1u)] = b;
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) order[atomicAdd(&hist[order_class(bcount[b])], 1u)] = b;
 }
 
 hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uint32_t* order, uint64_t max_bins,
