@@ -171,8 +171,8 @@ __device__ __host__ inline int sk_row_words(int RW, int rw) { return RW + (rw > 
 constexpr int SK_THREAD_RW = 16;
 // staged records per block (8 B each): 256 reads of 150 bp make ~2.5 K; a
 // block past it stores the rest directly.  With the per-destination arrays
-// and the read rows the block fits three to a CU.
-constexpr uint32_t SK_STAGE = 3584;
+// (16-bit counts, two per word) and the read rows the block fits four to a CU.
+constexpr uint32_t SK_STAGE = 2496;
 constexpr uint32_t SK_MAX_DEST = 1024;  // destination regions (ranks or buckets)
 
 template <bool WRITE>
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     uint64_t* stg = smem + 256 * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
     __shared__ uint32_t span_end;
     __shared__ unsigned long long s_base;
-    __shared__ uint32_t dcnt[SK_MAX_DEST];
+    __shared__ uint32_t dcnt2[SK_MAX_DEST / 2];  // per-destination counts, 16 bits each (< SK_STAGE)
     __shared__ uint32_t dbase[SK_MAX_DEST];  // reserved slot in the region (< region_cap < 2^32)
     const bool route = WRITE && A.regions;          // records to destination regions, any order
     const bool alloc = WRITE && (A.rec_ctr || route);  // records placed by block allocation
@@ -268,22 +268,27 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
             const uint32_t span = min(span_end, SK_STAGE);
             if (route) {
                 // per destination: count, reserve a range, place (LDS cursors)
-                for (uint32_t d = tid; d < A.G; d += 256) dcnt[d] = 0;
+                for (uint32_t d = tid; d < (A.G + 1) / 2; d += 256) dcnt2[d] = 0;
                 __syncthreads();
-                for (uint32_t i = tid; i < span; i += 256)
-                    atomicAdd(&dcnt[region_of(A, (uint32_t)(stg[i] >> 37))], 1u);
+                for (uint32_t i = tid; i < span; i += 256) {
+                    const uint32_t d = region_of(A, (uint32_t)(stg[i] >> 37));
+                    atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1)));
+                }
                 __syncthreads();
                 for (uint32_t d = tid; d < A.G; d += 256) {
-                    dbase[d] = dcnt[d] ? (uint32_t)min<unsigned long long>(
-                                             atomicAdd(&A.dest_ctr[d], (unsigned long long)dcnt[d]), 0xFFFFFFFFull)
-                                       : 0u;
-                    dcnt[d] = 0;
+                    const uint32_t nd = (dcnt2[d >> 1] >> (16 * (d & 1))) & 0xFFFFu;
+                    dbase[d] = nd ? (uint32_t)min<unsigned long long>(
+                                        atomicAdd(&A.dest_ctr[d], (unsigned long long)nd), 0xFFFFFFFFull)
+                                  : 0u;
                 }
+                __syncthreads();
+                for (uint32_t d = tid; d < (A.G + 1) / 2; d += 256) dcnt2[d] = 0;
                 __syncthreads();
                 for (uint32_t i = tid; i < span; i += 256) {
                     const uint64_t e = stg[i];
                     const uint32_t d = region_of(A, (uint32_t)(e >> 37));
-                    const uint64_t slot = (uint64_t)dbase[d] + atomicAdd(&dcnt[d], 1u);
+                    const uint64_t slot = (uint64_t)dbase[d] +
+                                          ((atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1))) >> (16 * (d & 1))) & 0xFFFFu);
                     if (slot >= A.region_cap) continue;  // counted: the caller retries bigger
                     const uint32_t row = (uint32_t)((e >> 29) & 0xFFu);
                     put_record(A, A.regions + (d * A.region_cap + slot) * (uint64_t)A.rw,
