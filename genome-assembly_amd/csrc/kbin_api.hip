@@ -1244,7 +1244,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
         a.ts_log2 = (uint32_t)ts_log2;
         a.rho = c->rho > 0.f ? c->rho : 0.25f;
-        a.fill = (float)std::min(0.74, std::max(0.3, env_int("KB_BIN_FILL_PCT", 60) / 100.0));
+        a.fill = (float)std::min(0.85, std::max(0.3, env_int("KB_BIN_FILL_PCT", 60) / 100.0));
         a.ablate = env_int("KB_BIN_ABLATE", 0);
         a.gcount = reinterpret_cast<unsigned long long*>(c->totals.p + 4);
         a.status = c->misc.p + 2;  // the bin kernel's own status word

@@ -624,43 +624,74 @@ struct Span<2> {
 };
 
 // ---- the bin's LDS table: claim words (a), for KW = 2 the published low
-// words (b), and a u32 count (then cursor) per slot
+// words (b), and a u32 count (then cursor) per slot.  Slots come in buckets
+// of four (32 B of claim words): a probe reads a whole bucket at once and
+// compares four keys, so a wavefront's 64 lookups rarely need a second
+// dependent LDS round trip (linear probing one slot at a time left the
+// wave waiting on its longest chain).  Buckets fill in slot order and slots
+// never empty again, so a bucket with an empty slot ends every probe sequence.
 template <int KW>
 struct BinTable {
     uint64_t* ca;
     uint64_t* cb;
-    DEV bool hit(uint32_t i, const TKey<KW>& k) const {
-        if constexpr (KW == 1) return lds_load_u64(&ca[i]) == k.a;
-        else return lds_load_u64(&ca[i]) == k.a && lds_load_u64(&cb[i]) == k.b;
+    // the key's slot in bucket bk, -1 (absent: the bucket has an empty slot),
+    // -2 (not here, bucket full), -3 (a-match whose low word is unpublished)
+    DEV int in_bucket(uint32_t bk, const TKey<KW>& k, int& empty) const {
+        const uint32_t s0 = bk * 4u;
+        uint64_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) w[j] = lds_load_u64(&ca[s0 + j]);
+        empty = -1;
+#pragma unroll
+        for (int j = 3; j >= 0; j--)
+            if (w[j] == 0) empty = j;
+        int hit = -1;
+#pragma unroll
+        for (int j = 3; j >= 0; j--)
+            if (w[j] == k.a) hit = j;
+        if (hit >= 0) {
+            if constexpr (KW == 1) {
+                return (int)s0 + hit;
+            } else {
+                // (two-word keys: an a-match is rare; check the low words of all a-matches)
+                bool pend = false;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (w[j] != k.a) continue;
+                    const uint64_t x = lds_load_u64(&cb[s0 + j]);
+                    if (x == k.b) return (int)s0 + j;
+                    if (x == 0) pend = true;
+                }
+                if (pend) return -3;
+            }
+        }
+        return empty >= 0 ? -1 : -2;
     }
     // find-or-insert; -2 past the key limit, -1 table full
-    DEV int insert(uint32_t mask, const TKey<KW>& k, uint32_t h, uint32_t* n_keys, uint32_t limit) const {
-        uint32_t idx = h & mask;
-        for (uint32_t probe = 0; probe <= mask;) {
-            uint64_t v = lds_load_u64(&ca[idx]);
-            if (v == 0) {
-                const uint64_t old = atomicCAS((unsigned long long*)&ca[idx], 0ull, (unsigned long long)k.a);
-                if (old == 0) {
-                    if constexpr (KW == 2)
-                        __hip_atomic_store(&cb[idx], k.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (atomicAdd(n_keys, 1u) >= limit) return -2;
-                    return (int)idx;
-                }
-                v = old;
+    DEV int insert(uint32_t bmask, const TKey<KW>& k, uint32_t h, uint32_t* n_keys, uint32_t limit) const {
+        uint32_t bk = h & bmask;
+        for (uint32_t probe = 0; probe <= bmask;) {
+            int empty;
+            const int r = in_bucket(bk, k, empty);
+            if (r >= 0) return r;
+            if (r == -3) continue;  // claimed, low word not yet published: re-read
+            if (r == -2) {          // full bucket: the next one
+                bk = (bk + 1) & bmask;
+                probe++;
+                continue;
             }
-            if (v == k.a) {
-                if constexpr (KW == 1) {
-                    return (int)idx;
-                } else {
-                    // claimed by another lane: its low word may not be published yet --
-                    // re-read this slot on the next trip (no lane waits inside a branch)
-                    const uint64_t w = lds_load_u64(&cb[idx]);
-                    if (w == 0) continue;
-                    if (w == k.b) return (int)idx;
-                }
+            const uint32_t sl = bk * 4u + (uint32_t)empty;
+            const uint64_t old = atomicCAS((unsigned long long*)&ca[sl], 0ull, (unsigned long long)k.a);
+            if (old == 0) {
+                if constexpr (KW == 2)
+                    __hip_atomic_store(&cb[sl], k.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (atomicAdd(n_keys, 1u) >= limit) return -2;
+                return (int)sl;
             }
-            idx = (idx + 1) & mask;
-            probe++;
+            if constexpr (KW == 1)
+                if (old == k.a) return (int)sl;
+            // another key (or ours, two-word: its low word decides) took the
+            // slot: re-read the bucket
         }
         return -1;
     }
@@ -793,7 +824,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
     constexpr uint32_t Q = bin_q<KW>();
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     BinShared& S = *reinterpret_cast<BinShared*>(smem);      // all LDS in one dynamic array
-    const uint32_t TS = 1u << A.ts_log2, tmask = TS - 1;
+    const uint32_t TS = 1u << A.ts_log2, bmask = TS / 4 - 1;  // buckets of four slots
     BinTable<KW> T;
     T.ca = smem + sizeof(BinShared) / 8;                     // [TS] claim words
     T.cb = KW == 2 ? T.ca + TS : nullptr;                    // [TS] published low words
@@ -924,13 +955,13 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 if (A.ablate == 1) return;  // expansion only
 #endif
                 const uint32_t h0 = k0.hash(), h1 = k1.hash();
-                // first probes of both k-mers in flight together; the rest
-                // (empty slot, collision chain) takes the full insert path
-                const bool f0 = T.hit(h0 & tmask, k0), f1 = T.hit(h1 & tmask, k1);
-                int l0 = f0 ? (int)(h0 & tmask) : -3;
-                int l1 = f1 ? (int)(h1 & tmask) : -3;
-                if (v0 && l0 == -3) l0 = T.insert(tmask, k0, h0, &S.n_keys, limit);
-                if (v1 && l1 == -3) l1 = T.insert(tmask, k1, h1, &S.n_keys, limit);
+                // home buckets of both k-mers in flight together; the rest
+                // (new key, full bucket) takes the full insert path
+                int e0_, e1_;
+                int l0 = T.in_bucket(h0 & bmask, k0, e0_);
+                int l1 = T.in_bucket(h1 & bmask, k1, e1_);
+                if (v0 && l0 < 0) l0 = T.insert(bmask, k0, h0, &S.n_keys, limit);
+                if (v1 && l1 < 0) l1 = T.insert(bmask, k1, h1, &S.n_keys, limit);
                 if (v0) {
                     if (l0 < 0) {
                         S.overflow = 1;
@@ -1332,7 +1363,7 @@ __device__ unsigned long long g_list_prof[8];
 #define LPROF(ph) do {} while (0)
 #endif
 
-__global__ __launch_bounds__(LIST_THREADS) void lists_kernel(ListArgs A) {
+__global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5, 8))) void lists_kernel(ListArgs A) {
 #ifdef KB_BIN_PROF
     unsigned long long lacc[8] = {};
     unsigned long long lt = clock64();
