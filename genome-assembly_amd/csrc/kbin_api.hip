@@ -51,12 +51,21 @@ struct DevBuf {
     uint64_t cap = 0;
     hipError_t ensure(uint64_t n) {
         if (n <= cap && p) return hipSuccess;
+        // growing an existing buffer: 1/8 headroom, so passes whose sizes
+        // wander by a few percent do not free and map tens of GB each time
+        uint64_t want = std::max<uint64_t>(n, 1);
+        if (p) want += want / 8;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        uint64_t want = std::max<uint64_t>(n, 1);
         hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
+        if (e != hipSuccess && want > n) {  // no room for the headroom: exactly n
+            (void)hipGetLastError();
+            want = std::max<uint64_t>(n, 1);
+            e = hipMalloc((void**)&p, want * sizeof(T));
+        }
         if (e == hipSuccess) cap = want;
+        else p = nullptr;
         return e;
     }
     void release() {
@@ -136,6 +145,8 @@ struct kb_ctx {
     DevBuf<uint32_t> long_q;   // entries with 257..4096 ids (lists_long_kernel)
     DevBuf<uint32_t> border;   // bin processing order
     DevBuf<uint32_t> bcount, bmmer;  // bin descriptors (with starts)
+    DevBuf<uint32_t> flat_list, flat_next, flat_l0, flat_off;  // heavy bins published for phase 1
+    DevBuf<unsigned long long> flat_sbase, flat_obase, flat_n;  // flat_n[0] bins, [1] offset pool
     DevBuf<uint64_t> regions;  // local bucket regions (pay layout)
     DevBuf<unsigned long long> bfill;  // records per bucket
     uint64_t bucket_cap = 0;   // learned region capacity (records per bucket)
@@ -255,6 +266,8 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
     c->misc.release(); c->totals.release(); c->first.release(); c->e_first.release();
     for (auto& m : c->bmaps) m.map.release();
+    c->flat_list.release(); c->flat_next.release(); c->flat_l0.release(); c->flat_off.release();
+    c->flat_sbase.release(); c->flat_obase.release(); c->flat_n.release();
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
@@ -1238,6 +1251,26 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.stage = c->stage.p;
         a.kstage = flat_l ? c->kstage.p : nullptr;
         a.flat_l = flat_l;
+        if (flat_l) {
+            HIPCHK(c->flat_list.ensure(max_bins));
+            HIPCHK(c->flat_next.ensure(max_bins));
+            HIPCHK(c->flat_l0.ensure(max_bins));
+            HIPCHK(c->flat_sbase.ensure(max_bins));
+            HIPCHK(c->flat_obase.ensure(max_bins));
+            // offsets: np + 1 per heavy bin, np < 2 x (expected keys / (fill x TS)) + 1,
+            // expected keys <= occurrences, fill x TS >= 0.3 x 1024
+            HIPCHK(c->flat_off.ensure(N / 150 + 2 * max_bins + KB_FLAT_MAX + 1));
+            HIPCHK(c->flat_n.ensure(2));
+            HIPCHK(hipMemsetAsync(c->flat_n.p, 0, 2 * sizeof(unsigned long long), c->s));
+            a.flat_list = c->flat_list.p;
+            a.flat_next = c->flat_next.p;
+            a.flat_l0 = c->flat_l0.p;
+            a.flat_sbase = c->flat_sbase.p;
+            a.flat_off = c->flat_off.p;
+            a.flat_obase = c->flat_obase.p;
+            a.flat_n = c->flat_n.p;
+            a.flat_octr = c->flat_n.p + 1;
+        }
         a.totals = c->totals.p;
         a.K = c->p.K;
         a.M = M;

@@ -513,8 +513,9 @@ DEV uint64_t lds_load_u64(const uint64_t* p) {
 }
 
 struct alignas(16) BinShared {
-    uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, pad0;
-    unsigned long long e0, i0, stage_base, pad1;
+    uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, part0;
+    unsigned long long e0, i0, stage_base;
+    uint32_t flat_idx, fa, fb, l0;
     uint32_t stack_p[BIN_STACK], stack_l[BIN_STACK];
     uint64_t red[BIN_THREADS / 64];
 };
@@ -815,12 +816,14 @@ DEV void kst_store(uint64_t* kst, uint32_t i, const TKey<KW>& k) {
 // twice -- count per partition, then scatter (table key, position, ordinal)
 // into flat per-partition lists -- and each partition is then swept from its
 // list.  Up to FLAT_MAX partitions; deeper splits filter the flat lists.
-constexpr uint32_t FLAT_MAX = 4096;
+constexpr uint32_t FLAT_LOG2 = 14;
+constexpr uint32_t FLAT_MAX = 1u << FLAT_LOG2;  // (cursors in the table area: 64 KiB)
+static_assert(FLAT_MAX == KB_FLAT_MAX, "host and device agree on the flat list count");
 constexpr uint32_t PRUNED = 0x80000000u;  // cursor of a pruned (or empty) slot in sweep 2
 constexpr uint64_t M48 = (1ull << 48) - 1ull;
 
-template <int KW>
-__global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
+template <int KW, int PHASE>
+DEV void bin_body(const BinArgs& A) {
     constexpr uint32_t Q = bin_q<KW>();
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     BinShared& S = *reinterpret_cast<BinShared*>(smem);      // all LDS in one dynamic array
@@ -844,40 +847,82 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
     unsigned long long pt = clock64();
 #endif
 
+    if (tid == 0) S.flat_idx = 0;
     while (true) {
-        // persistent blocks take bins from a shared counter, largest first
+        // phase 0: persistent blocks take bins from a shared counter, largest
+        // first.  Phase 1: the partitions of the heavy bins phase 0 turned into
+        // flat lists, any block any partition (a giant bin is no longer one
+        // workgroup's serial loop)
         __syncthreads();
-        if (tid == 0) S.item = (uint32_t)atomicAdd(A.work, 1ull);
+        if (tid == 0) {
+            if (PHASE == 0) {
+                S.item = (uint32_t)atomicAdd(A.work, 1ull);
+            } else {
+                S.item = 0xFFFFFFFFu;
+                const uint32_t nf = (uint32_t)min<unsigned long long>(*A.flat_n, A.max_bins);
+                while (S.flat_idx < nf) {
+                    const uint32_t fb0 = A.flat_list[S.flat_idx];
+                    const uint32_t pp = atomicAdd(&A.flat_next[fb0], 1u);
+                    if (pp < (1u << A.flat_l0[fb0])) {
+                        S.item = fb0;
+                        S.part0 = pp;
+                        break;
+                    }
+                    S.flat_idx++;
+                }
+            }
+        }
         __syncthreads();
-        if (S.item >= nbins) break;  // uniform
-        const uint32_t b = A.order[S.item];
+        if (PHASE == 0 ? S.item >= nbins : S.item == 0xFFFFFFFFu) break;  // uniform
+        if (PHASE == 1) {  // one flat partition of bin S.item
+            const uint32_t b = S.item;
+            if (tid == 0) {
+                S.stage_base = A.flat_sbase[b];
+                S.l0 = A.flat_l0[b];
+                S.fa = A.flat_off[A.flat_obase[b] + S.part0];
+                S.fb = A.flat_off[A.flat_obase[b] + S.part0 + 1];
+            }
+            __syncthreads();
+        }
+        const uint32_t b = PHASE == 0 ? A.order[S.item] : S.item;
         const uint32_t lo = A.bstart[b], hi = lo + A.bcount[b];
         const uint32_t mmer = A.bmmer[b];
 
         // occurrences of the bin -> first partition depth
-        uint64_t occ = 0;
-        for (uint32_t rec = lo + tid; rec < hi; rec += BIN_THREADS)
-            occ += (A.hdr[rec] >> 32) & 63u;
-        uint64_t occ_tot;
-        (void)block_excl_scan_u64(occ, S.red, occ_tot);
-        // the bin's stage range (one slot per occurrence, reused per partition)
-        if (tid == 0) S.stage_base = atomicAdd(A.stage_ctr, (unsigned long long)occ_tot);
-        __syncthreads();
+        uint64_t occ_tot = 0;
+        if (PHASE == 0) {
+            uint64_t occ = 0;
+            for (uint32_t rec = lo + tid; rec < hi; rec += BIN_THREADS)
+                occ += (A.hdr[rec] >> 32) & 63u;
+            (void)block_excl_scan_u64(occ, S.red, occ_tot);
+            // the bin's stage range (one slot per occurrence, reused per partition)
+            if (tid == 0) S.stage_base = atomicAdd(A.stage_ctr, (unsigned long long)occ_tot);
+            __syncthreads();
+        }
         uint64_t* stage = A.stage + S.stage_base;  // (flat: moved to each partition's list)
-        PROF_CNT(11, 1);
+        PROF_CNT(11, PHASE == 0);
         PROF_CNT(14, occ_tot);
+#ifdef KB_BIN_PROF
+        const unsigned long long bin_t0 = clock64();
+#endif
         uint32_t l0 = 0;  // uniform: initial partition depth from the expected distinct keys
-        {
+        if (PHASE == 0) {
             const double want = (double)occ_tot * A.rho / ((double)A.fill * TS);
             while ((double)(1u << l0) < want && l0 < 16) l0++;
+        } else {
+            l0 = S.l0;
         }
         // heavy bin: flat per-partition lists (the ring area holds the cursors)
-        const bool flat = A.flat_l && l0 >= A.flat_l;
-        uint32_t* fl_cur = reinterpret_cast<uint32_t*>(ring0);  // [FLAT_MAX]
-        uint32_t* fl_off = fl_cur + FLAT_MAX;                    // [FLAT_MAX + 1]
+        const bool flat = PHASE == 1 || (A.flat_l && l0 >= A.flat_l);
+        // (the table area holds the cursors: no table while the lists are built;
+        // the offsets go straight to the published pool)
+        uint32_t* fl_cur = reinterpret_cast<uint32_t*>(T.ca);  // [FLAT_MAX]
         uint64_t* kst = A.kstage + KW * S.stage_base;
-        if (flat) {
-            if (l0 > 12) l0 = 12;  // FLAT_MAX partitions; deeper splits filter
+        if (flat && PHASE == 0) {
+            // at most FLAT_MAX lists, and as many cursors as the table area holds
+            // (TS x (2 KW + 1) words); deeper splits filter the lists
+            const uint32_t l0_cap = min(FLAT_LOG2, A.ts_log2 + (uint32_t)KW);
+            if (l0 > l0_cap) l0 = l0_cap;
             const uint32_t np = 1u << l0, pm = np - 1u;
             for (uint32_t i = tid; i < np; i += BIN_THREADS) fl_cur[i] = 0;
             __syncthreads();
@@ -894,6 +939,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             }
             uint64_t tot_f;
             uint64_t run = block_excl_scan_u64(mine, S.red, tot_f);
+            if (tid == 0) S.e0 = atomicAdd(A.flat_octr, (unsigned long long)(np + 1));  // this bin's pool range
+            __syncthreads();
+            uint32_t* fl_off = A.flat_off + S.e0;  // [np + 1], read by phase 1
             for (uint32_t k = 0; k < q; k++) {
                 const uint32_t i = tid * q + k;
                 if (i < np) {
@@ -910,10 +958,20 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
                 kst_store<KW>(kst, i, key);
                 stage[i] = ((uint64_t)pos << 32) | ord;
             });
-            __threadfence_block();
-            __syncthreads();
+            // publish the lists: phase 1 sweeps the partitions, any block each
+            if (tid == 0) {
+                A.flat_obase[b] = S.e0;
+                A.flat_sbase[b] = S.stage_base;
+                A.flat_l0[b] = l0;
+                A.flat_next[b] = 0;
+                A.flat_list[atomicAdd(A.flat_n, 1ull)] = b;
+            }
+            PROF_MARK(7);
+            continue;  // (the next kernel launch sees every store)
         }
-        for (uint32_t p0 = 0; p0 < (1u << l0); p0++) {
+        PROF_MARK(7);
+        const uint32_t p_lo = PHASE == 0 ? 0u : S.part0, p_hi = PHASE == 0 ? (1u << l0) : S.part0 + 1u;
+        for (uint32_t p0 = p_lo; p0 < p_hi; p0++) {
         if (tid == 0) {
             S.sp = 1;
             S.stack_p[0] = p0;
@@ -921,7 +979,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
         }
         __syncthreads();
         // flat: this partition's list is [fa, fb) of the bin's stage range
-        const uint32_t fa = flat ? fl_off[p0] : 0u, fb = flat ? fl_off[p0 + 1] : 0u;
+        const uint32_t fa = flat ? S.fa : 0u, fb = flat ? S.fb : 0u;
         stage = A.stage + S.stage_base + fa;
         while (true) {
             if (tid == 0) {
@@ -1123,12 +1181,40 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
             PROF_MARK(6);
         }
         }  // initial partitions
+#ifdef KB_BIN_PROF
+        if (tid == 0) {  // the slowest bin: cycles, and its occurrences
+            const unsigned long long dt = clock64() - bin_t0;
+            if (dt > pacc[13]) {
+                pacc[13] = dt;
+                pacc[12] = occ_tot;
+            }
+        }
+#endif
         __syncthreads();
     }
 #ifdef KB_BIN_PROF
     if (tid == 0)
-        for (int i = 0; i < 16; i++) atomicAdd(&g_bin_prof[i], pacc[i]);
+        for (int i = 0; i < 16; i++) {
+            if (i == 12) continue;
+            if (i == 13) {  // max over blocks (and that bin's occurrences)
+                if (atomicMax(&g_bin_prof[13], pacc[13]) < pacc[13]) g_bin_prof[12] = pacc[12];
+            } else {
+                atomicAdd(&g_bin_prof[i], pacc[i]);
+            }
+        }
 #endif
+}
+
+// phase 0: every light bin, and each heavy bin's flat lists
+template <int KW>
+__global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
+    bin_body<KW, 0>(A);
+}
+
+// phase 1: the heavy bins' partitions, any block any partition
+template <int KW>
+__global__ __launch_bounds__(BIN_THREADS) void bin_parts_kernel(BinArgs A) {
+    bin_body<KW, 1>(A);
 }
 
 #ifdef KB_BIN_PROF
@@ -1136,8 +1222,9 @@ void bins_prof_report(hipStream_t s) {
     unsigned long long h[16];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bin_prof), sizeof(h));
-    static const char* nm[16] = {"occ", "zero", "sweep1", "prune/entries", "sweep2", "small sort", "big sort", "-",
-                                 "partitions", "overflows", "big lists", "bins", "-", "-", "occ", "-"};
+    static const char* nm[16] = {"occ", "zero", "sweep1", "prune/entries", "sweep2", "small sort", "big sort", "flat",
+                                 "partitions", "overflows", "big lists", "bins", "slowest-bin-occ", "slowest-bin-cycles",
+                                 "occ", "-"};
     fprintf(stderr, "[bin_prof]");
     for (int i = 0; i < 16; i++)
         if (h[i]) fprintf(stderr, " %s=%llu", nm[i], h[i]);
@@ -2087,17 +2174,19 @@ template <int KW>
 static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_t s) {
     const uint32_t TS = 1u << a.ts_log2;
     const size_t lds = bins_lds_bytes(a.ts_log2, KW);
-    // TS >= BIN_THREADS (the prune loop); the ring area holds the flat-list cursors
-    const size_t ring = (size_t)BIN_WAVES * bin_q<KW>() * (KW * sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint16_t));
-    if (TS < (uint32_t)BIN_THREADS || lds > 160 * 1024 || ring < (2 * FLAT_MAX + 1) * sizeof(uint32_t))
-        return hipErrorInvalidValue;
+    if (TS < (uint32_t)BIN_THREADS || lds > 160 * 1024) return hipErrorInvalidValue;  // (the prune loop)
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel<KW>, BIN_THREADS, lds);
     if (e != hipSuccess) return e;
-    const uint64_t blocks = std::min<uint64_t>(max_bins, (uint64_t)std::max(1, cus) * std::max(1, per_cu));
-    hipLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a);
+    const uint64_t blocks = (uint64_t)std::max(1, cus) * std::max(1, per_cu);
+    hipLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS), lds, s,
+                       a);
+    e = hipGetLastError();
+    if (e != hipSuccess || !a.flat_l) return e;
+    // the heavy bins' partitions, spread over every CU (exits at once without any)
+    hipLaunchKernelGGL(bin_parts_kernel<KW>, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a);
     return hipGetLastError();
 }
 

@@ -136,6 +136,8 @@ struct BucketArgs {
     uint32_t* status;          // ST_BUCKET_FULL: a bucket holds too many mmers
 };
 
+constexpr uint32_t KB_FLAT_MAX = 16384;  // partitions of one heavy bin's flat lists (kbin_bins.hip FLAT_MAX)
+
 struct BinArgs {
     const uint64_t* hdr;       // [R] bin-ordered record headers (see SkScanArgs::pay)
     const uint64_t* w0;        // [R] span bases 0..31
@@ -152,6 +154,17 @@ struct BinArgs {
     uint64_t* stage;           // [N] (LDS slot << 48 | position << 32 | ordinal) per occurrence
     uint64_t* kstage;          // [KW N] heavy bins: the k-mer's table key per occurrence, parallel to stage
     uint32_t flat_l;           // heavy bin: initial partition depth >= flat_l (0 = never)
+    // heavy bins, two launches: phase 0 bins every light bin and turns each heavy
+    // bin into flat per-partition lists (published below); phase 1 sweeps the
+    // published partitions, any block any partition
+    uint32_t* flat_list;            // [max_bins] published heavy bins
+    unsigned long long* flat_n;     // (zeroed) their number
+    uint32_t* flat_next;            // [max_bins] next partition to claim
+    uint32_t* flat_l0;              // [max_bins] partition depth
+    unsigned long long* flat_sbase; // [max_bins] stage base
+    unsigned long long* flat_obase; // [max_bins] the bin's range of flat_off
+    uint32_t* flat_off;             // pool of list offsets, np + 1 per heavy bin
+    unsigned long long* flat_octr;  // (zeroed) pool allocation
     const uint64_t* totals;    // totals[2] = nbins
     int K, M;
     uint32_t keep_gt;
