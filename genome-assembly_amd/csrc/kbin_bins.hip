@@ -156,6 +156,37 @@ DEV uint32_t region_of(const SkScanArgs& A, uint32_t mmer) {
     return A.bucket_map ? (uint32_t)A.bucket_map[mmer - (1u << (2 * A.M - 1))] : dest_of(mmer, A.G, A.dest_salt);
 }
 
+// Add one record to a packed 16-bit LDS destination count (two per word) and
+// return the count before it, aggregated over the wave: lanes bound for the
+// same destination share one atomic (the lowest lane's) and take their
+// offsets from the ballot.  With few destinations (ranks) every lane of a wave
+// would otherwise hit the same word and the LDS would serialise 64 returning
+// atomics per instruction (1.97 ms vs 0.27 ms for the pass at one rank).
+DEV uint32_t wave_dest_add(uint32_t* cnt2, uint32_t d) {
+    const int lane = (int)(threadIdx.x & 63u);
+    uint32_t off = 0;
+    bool pending = true;
+    for (;;) {
+        const uint64_t rem = __ballot(pending);
+        if (!rem) break;
+        const int leader = __builtin_ctzll(rem);
+        const uint32_t ld = (uint32_t)__shfl((int)d, leader, 64);
+        const bool mine = pending && d == ld;
+        const uint64_t m = __ballot(mine);
+        uint32_t b = 0;
+        if (lane == leader) {
+            const uint32_t sh = 16u * (ld & 1u);
+            b = (atomicAdd(&cnt2[ld >> 1], (uint32_t)__popcll(m) << sh) >> sh) & 0xFFFFu;
+        }
+        b = (uint32_t)__shfl((int)b, leader, 64);
+        if (mine) {
+            off = b + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            pending = false;
+        }
+    }
+    return off;
+}
+
 // LDS row of one read in sk_thread_kernel: the read's words, then zero words
 // so that every span window (up to 4 words past the first base) stays inside
 __device__ __host__ inline int sk_row_words(int RW, int rw) { return RW + (rw > 3 ? rw - 1 : 2); }
@@ -192,6 +223,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     __shared__ uint32_t dbase[SK_MAX_DEST];  // reserved slot in the region (< region_cap < 2^32)
     const bool route = WRITE && A.regions;          // records to destination regions, any order
     const bool alloc = WRITE && (A.rec_ctr || route);  // records placed by block allocation
+    const bool rounds = alloc && !(route && A.G > 64);  // see the walk below
     uint64_t kmers = 0;
     for (uint64_t r0 = (uint64_t)blockIdx.x * 256; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * 256) {
         const uint32_t nrows = (uint32_t)min<uint64_t>(256, A.n_reads - r0);
@@ -205,13 +237,20 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
         if (tid == 0) span_end = 0;
         __syncthreads();
         const uint64_t bfirst = WRITE && !alloc ? A.rec_base[r0] : 0;
-        if (tid < nrows) {
-            const uint64_t r = r0 + tid;
-            const uint64_t* sw = smem + tid * RS;
-            const int nK = (int)A.lens[r] - K + 1;
-            uint32_t nseg = 0;
-            const uint64_t rbase = WRITE && !alloc ? A.rec_base[r] : 0;
-            int lo = 0;
+        // Block allocation onto few counters (ranks, or the one record counter)
+        // runs in rounds: a walk whose record finds the stage full stops there
+        // and resumes after the block has written the stage out.  (Writing such
+        // records one by one took a global atomic per record on a few hot
+        // counters -- 256 reads of 150 bp average ~2.5 K records, so about half
+        // the blocks overflowed: 1.97 ms at one rank.)  With 1024 local buckets
+        // the per-record atomics spread out and are cheaper than a round.
+        const uint64_t r = r0 + tid;
+        const uint64_t* sw = smem + tid * RS;
+        const int nK = tid < nrows ? (int)A.lens[r] - K + 1 : 0;
+        const uint64_t rbase = WRITE && !alloc && tid < nrows ? A.rec_base[r] : 0;
+        uint32_t nseg = 0;
+        int lo = 0;
+        for (;;) {
             while (lo < nK) {
                 // leftmost strict argmax of the canonical score over the window
                 uint64_t x = window64(sw, lo), y = window64(sw, lo + 32);
@@ -233,7 +272,6 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     lo = sig + 1;
                     continue;
                 }
-                kmers += n;
                 if (WRITE) {
                     const uint64_t rev = bsm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
                     const uint64_t e = (uint64_t)lo | (n << 16) | ((uint64_t)(sig - lo) << 22) | (rev << 28) |
@@ -241,14 +279,16 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     const uint64_t loc = alloc ? (uint64_t)atomicAdd(&span_end, 1u) : rbase + nseg - bfirst;
                     if (loc < SK_STAGE) {
                         stg[loc] = e;
-                    } else if (route) {  // beyond the staging area: one record, its own slot
+                    } else if (rounds) {
+                        break;  // stage full: resume at this record in the next round
+                    } else if (route) {  // many destinations: one record, its own slot
                         const uint32_t d = region_of(A, (uint32_t)best);
                         const uint64_t i = atomicAdd(&A.dest_ctr[d], 1ull);
                         if (i < A.region_cap)
                             put_record(A, A.regions + (d * A.region_cap + i) * (uint64_t)A.rw,
                                        A.ord_base + (uint32_t)r, (uint64_t)lo, n, (uint64_t)(sig - lo), rev, sw);
-                    } else {  // beyond the staging area: direct (scattered) stores
-                        const uint64_t t = alloc ? (uint64_t)atomicAdd(A.rec_ctr, 1ull) : rbase + nseg;
+                    } else {  // ordered records beyond the staging area: direct (scattered) stores
+                        const uint64_t t = rbase + nseg;
                         A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)r) | (n << 32) |
                                            ((uint64_t)(sig - lo) << 38) | (rev << 44) | ((uint64_t)lo << 45);
                         A.pay[3 * t + 1] = window64(sw, lo);
@@ -256,23 +296,27 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                         A.keys[t] = ((uint64_t)(uint32_t)best << 38) | ((63ull - n) << 32) | (uint32_t)t;
                     }
                 }
+                kmers += n;
                 nseg++;
                 lo = sig + 1;
             }
-            if (!WRITE) A.seg_count[r] = nseg;
+            if (!WRITE && tid < nrows) A.seg_count[r] = nseg;
             if (WRITE && !alloc && nseg)
                 atomicMax(&span_end, (uint32_t)min<uint64_t>(rbase + nseg - bfirst, SK_STAGE));
-        }
-        if (WRITE) {
+            if (!WRITE) break;
             __syncthreads();
             const uint32_t span = min(span_end, SK_STAGE);
             if (route) {
                 // per destination: count, reserve a range, place (LDS cursors)
                 for (uint32_t d = tid; d < (A.G + 1) / 2; d += 256) dcnt2[d] = 0;
                 __syncthreads();
+                const bool agg = A.G <= 64;  // ranks, not local buckets: aggregate per wave
                 for (uint32_t i = tid; i < span; i += 256) {
                     const uint32_t d = region_of(A, (uint32_t)(stg[i] >> 37));
-                    atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1)));
+                    if (agg)
+                        wave_dest_add(dcnt2, d);
+                    else
+                        atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1)));
                 }
                 __syncthreads();
                 for (uint32_t d = tid; d < A.G; d += 256) {
@@ -287,33 +331,39 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                 for (uint32_t i = tid; i < span; i += 256) {
                     const uint64_t e = stg[i];
                     const uint32_t d = region_of(A, (uint32_t)(e >> 37));
-                    const uint64_t slot = (uint64_t)dbase[d] +
-                                          ((atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1))) >> (16 * (d & 1))) & 0xFFFFu);
+                    const uint64_t slot =
+                        (uint64_t)dbase[d] +
+                        (agg ? wave_dest_add(dcnt2, d)
+                             : ((atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1))) >> (16 * (d & 1))) & 0xFFFFu));
                     if (slot >= A.region_cap) continue;  // counted: the caller retries bigger
                     const uint32_t row = (uint32_t)((e >> 29) & 0xFFu);
                     put_record(A, A.regions + (d * A.region_cap + slot) * (uint64_t)A.rw,
                                A.ord_base + (uint32_t)(r0 + row), e & 0xFFFFu, (e >> 16) & 63u, (e >> 22) & 63u,
                                (e >> 28) & 1u, smem + row * RS);
                 }
-                continue;  // (the loop-top barrier protects stg and the read rows)
+            } else {
+                if (alloc) {  // the block's staged records get one contiguous range
+                    if (tid == 0) s_base = span ? atomicAdd(A.rec_ctr, (unsigned long long)span) : 0ull;
+                    __syncthreads();
+                }
+                const uint64_t tbase = alloc ? (uint64_t)s_base : bfirst;
+                for (uint32_t i = tid; i < span; i += 256) {
+                    const uint64_t e = stg[i];
+                    const uint32_t elo = (uint32_t)(e & 0xFFFFu), row = (uint32_t)((e >> 29) & 0xFFu);
+                    const uint64_t en = (e >> 16) & 63u, so = (e >> 22) & 63u, rev = (e >> 28) & 1u;
+                    const uint64_t* rw_ = smem + row * RS;
+                    const uint64_t t = tbase + i;
+                    A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)(r0 + row)) | (en << 32) | (so << 38) |
+                                       (rev << 44) | ((uint64_t)elo << 45);
+                    A.pay[3 * t + 1] = window64(rw_, (int)elo);
+                    A.pay[3 * t + 2] = window64(rw_, (int)elo + 32);
+                    A.keys[t] = ((e >> 37) << 38) | ((63ull - en) << 32) | (uint32_t)t;
+                }
             }
-            if (alloc) {  // the block's staged records get one contiguous range
-                if (tid == 0) s_base = span ? atomicAdd(A.rec_ctr, (unsigned long long)span) : 0ull;
-                __syncthreads();
-            }
-            const uint64_t tbase = alloc ? (uint64_t)s_base : bfirst;
-            for (uint32_t i = tid; i < span; i += 256) {
-                const uint64_t e = stg[i];
-                const uint32_t lo = (uint32_t)(e & 0xFFFFu), row = (uint32_t)((e >> 29) & 0xFFu);
-                const uint64_t n = (e >> 16) & 63u, so = (e >> 22) & 63u, rev = (e >> 28) & 1u;
-                const uint64_t* sw = smem + row * RS;
-                const uint64_t t = tbase + i;
-                A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)(r0 + row)) | (n << 32) | (so << 38) |
-                                   (rev << 44) | ((uint64_t)lo << 45);
-                A.pay[3 * t + 1] = window64(sw, (int)lo);
-                A.pay[3 * t + 2] = window64(sw, (int)lo + 32);
-                A.keys[t] = ((e >> 37) << 38) | ((63ull - n) << 32) | (uint32_t)t;
-            }
+            // another round while a walk stopped at the full stage
+            if (!rounds || !__syncthreads_or(lo < nK)) break;
+            if (tid == 0) span_end = 0;
+            __syncthreads();
         }
     }
     if (!WRITE || (alloc && (!route || A.binned_fmt))) {  // per-block k-mer sums (sk_kmers_total_kernel)
