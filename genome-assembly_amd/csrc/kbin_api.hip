@@ -230,7 +230,9 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
     e = hipHostMalloc((void**)&c->h_totals, 16 * sizeof(uint64_t), hipHostMallocDefault);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
-    if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(16) != hipSuccess) {
+    if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(16) != hipSuccess ||
+        hipMemsetAsync(c->misc.p, 0, 16 * sizeof(uint32_t), c->s) != hipSuccess ||
+        hipMemsetAsync(c->totals.p, 0, 16 * sizeof(uint64_t), c->s) != hipSuccess) {
         kb_destroy(c);
         return fail(KB_ENOMEM, "device alloc");
     }
@@ -1251,6 +1253,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.stage = c->stage.p;
         a.kstage = flat_l ? c->kstage.p : nullptr;
         a.flat_l = flat_l;
+        a.n_occ = N;
+        a.split_div = (uint32_t)std::max(0, env_int("KB_BIN_SPLIT_DIV", 0));
         if (flat_l) {
             HIPCHK(c->flat_list.ensure(max_bins));
             HIPCHK(c->flat_next.ensure(max_bins));
@@ -1259,7 +1263,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             HIPCHK(c->flat_obase.ensure(max_bins));
             // offsets: np + 1 per heavy bin, np < 2 x (expected keys / (fill x TS)) + 1,
             // expected keys <= occurrences, fill x TS >= 0.3 x 1024
-            HIPCHK(c->flat_off.ensure(N / 150 + 2 * max_bins + KB_FLAT_MAX + 1));
+            HIPCHK(c->flat_off.ensure(N / 150 + 9 * max_bins + KB_FLAT_MAX + 1));
             HIPCHK(c->flat_n.ensure(2));
             HIPCHK(hipMemsetAsync(c->flat_n.p, 0, 2 * sizeof(unsigned long long), c->s));
             a.flat_list = c->flat_list.p;

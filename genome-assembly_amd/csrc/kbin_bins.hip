@@ -869,6 +869,7 @@ DEV void kst_store(uint64_t* kst, uint32_t i, const TKey<KW>& k) {
 constexpr uint32_t FLAT_LOG2 = 14;
 constexpr uint32_t FLAT_MAX = 1u << FLAT_LOG2;  // (cursors in the table area: 64 KiB)
 static_assert(FLAT_MAX == KB_FLAT_MAX, "host and device agree on the flat list count");
+constexpr uint32_t SPLIT_BIT = 0x100u;     // flat_l0: a split bin's partitions (no flat lists)
 constexpr uint32_t PRUNED = 0x80000000u;  // cursor of a pruned (or empty) slot in sweep 2
 constexpr uint64_t M48 = (1ull << 48) - 1ull;
 
@@ -913,7 +914,7 @@ DEV void bin_body(const BinArgs& A) {
                 while (S.flat_idx < nf) {
                     const uint32_t fb0 = A.flat_list[S.flat_idx];
                     const uint32_t pp = atomicAdd(&A.flat_next[fb0], 1u);
-                    if (pp < (1u << A.flat_l0[fb0])) {
+                    if (pp < (1u << (A.flat_l0[fb0] & 0xFFu))) {
                         S.item = fb0;
                         S.part0 = pp;
                         break;
@@ -928,7 +929,7 @@ DEV void bin_body(const BinArgs& A) {
             const uint32_t b = S.item;
             if (tid == 0) {
                 S.stage_base = A.flat_sbase[b];
-                S.l0 = A.flat_l0[b];
+                S.l0 = A.flat_l0[b];  // depth | SPLIT_BIT (split, not flat)
                 S.fa = A.flat_off[A.flat_obase[b] + S.part0];
                 S.fb = A.flat_off[A.flat_obase[b] + S.part0 + 1];
             }
@@ -960,14 +961,50 @@ DEV void bin_body(const BinArgs& A) {
             const double want = (double)occ_tot * A.rho / ((double)A.fill * TS);
             while ((double)(1u << l0) < want && l0 < 16) l0++;
         } else {
-            l0 = S.l0;
+            l0 = S.l0 & 0xFFu;
         }
         // heavy bin: flat per-partition lists (the ring area holds the cursors)
-        const bool flat = PHASE == 1 || (A.flat_l && l0 >= A.flat_l);
+        const bool flat = PHASE == 1 ? !(S.l0 & SPLIT_BIT) : (A.flat_l && l0 >= A.flat_l);
+        // a large light bin (more occurrences than a fair share of one CU) is
+        // split: phase 0 counts its k-mers per hash partition (one expansion,
+        // no probes) and gives each partition its own stage range, phase 1
+        // bins the partitions on any block, each re-expanding the records with
+        // the partition filter -- the light path, in parallel
+        bool split = PHASE == 1 && !flat;
+        if (PHASE == 0 && !flat && A.split_occ && occ_tot > A.split_occ) {
+            const uint32_t lmax = A.flat_l ? A.flat_l - 1u : 3u;
+            while (l0 < lmax && (occ_tot >> l0) > A.split_occ) l0++;
+            split = l0 >= 1;
+        }
         // (the table area holds the cursors: no table while the lists are built;
         // the offsets go straight to the published pool)
         uint32_t* fl_cur = reinterpret_cast<uint32_t*>(T.ca);  // [FLAT_MAX]
         uint64_t* kst = A.kstage + KW * S.stage_base;
+        if (split && PHASE == 0) {
+            const uint32_t np = 1u << l0, pm = np - 1u;
+            if (tid < np) fl_cur[tid] = 0;
+            __syncthreads();
+            expand_bin<KW>(A, lo, hi, [&](const TKey<KW>& key, uint32_t, uint32_t) {
+                atomicAdd(&fl_cur[key.part() & pm], 1u);
+            });
+            __syncthreads();
+            if (tid == 0) {
+                const unsigned long long e0 = atomicAdd(A.flat_octr, (unsigned long long)(np + 1));
+                uint32_t run = 0;
+                for (uint32_t i = 0; i < np; i++) {
+                    A.flat_off[e0 + i] = run;
+                    run += fl_cur[i];
+                }
+                A.flat_off[e0 + np] = run;
+                A.flat_obase[b] = e0;
+                A.flat_sbase[b] = S.stage_base;
+                A.flat_l0[b] = l0 | SPLIT_BIT;
+                A.flat_next[b] = 0;
+                A.flat_list[atomicAdd(A.flat_n, 1ull)] = b;
+            }
+            PROF_MARK(7);
+            continue;  // (the next kernel launch sees every store)
+        }
         if (flat && PHASE == 0) {
             // at most FLAT_MAX lists, and as many cursors as the table area holds
             // (TS x (2 KW + 1) words); deeper splits filter the lists
@@ -1029,7 +1066,7 @@ DEV void bin_body(const BinArgs& A) {
         }
         __syncthreads();
         // flat: this partition's list is [fa, fb) of the bin's stage range
-        const uint32_t fa = flat ? S.fa : 0u, fb = flat ? S.fb : 0u;
+        const uint32_t fa = flat || split ? S.fa : 0u, fb = flat ? S.fb : 0u;
         stage = A.stage + S.stage_base + fa;
         while (true) {
             if (tid == 0) {
@@ -1293,7 +1330,8 @@ void bins_prof_report(hipStream_t s) {
 // ---------------------------------------------------------------------------
 constexpr int LIST_THREADS = 256;
 constexpr uint32_t LIST_CAP = 4096;   // longest list sorted in LDS in one piece (power of two)
-constexpr uint32_t LIST_SPAN = 7168;  // ids of 256 entries staged in LDS at once (28 KiB: 5 blocks per CU)
+constexpr uint32_t LIST_SPAN = 7168;  // ids staged in LDS at once (28 KiB: 5 blocks per CU)
+constexpr uint32_t LIST_WIN = LIST_SPAN - 256 - 8;  // window of list starts: + one list <= 256, + alignment
 constexpr uint32_t WAVE_LIST_MAX = 4096;  // longest list one wavefront sorts in its registers (64 x 64)
 
 // descending bitonic sort of Pw (power of two) values in LDS by a group of G
@@ -1511,8 +1549,8 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
     static_assert(LIST_CAP <= LIST_SPAN, "block sort space aliases the staging area");
     uint32_t* const ibuf = lds;
     uint32_t* const buf = lds;
-    __shared__ uint32_t big[LIST_THREADS];
-    __shared__ uint32_t n_big;
+    __shared__ uint32_t big[LIST_THREADS], mid[LIST_THREADS];
+    __shared__ uint32_t n_big, n_mid, w_lo, w_hi;
     const uint32_t tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     const uint64_t n_entries = A.totals[0];
@@ -1520,43 +1558,76 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
          e0 += (uint64_t)gridDim.x * LIST_THREADS) {
         const uint32_t ne = (uint32_t)min<uint64_t>(LIST_THREADS, n_entries - e0);
         const uint64_t ob = A.e_off[e0], span = A.e_off[e0 + ne] - ob;
-        // staging is 16-B aligned: ibuf[j] holds id base + j, lists start at sh
-        const uint64_t base = ob & ~3ull;
-        const uint32_t sh = (uint32_t)(ob - base);
-        const uint32_t nv = (uint32_t)((sh + span + 3) >> 2);  // uint4 groups
         if (tid == 0) n_big = 0;
-        const bool long_list = tid < ne && A.e_cnt[e0 + tid] > 256;
-        if (!__syncthreads_or(long_list) && sh + span + 3 <= LIST_SPAN) {
-            // staged: coalesced 16-B in, every list sorted in LDS, 16-B out
+        __syncthreads();
+        // this thread's entry; lists > 256 leave the staged windows: up to
+        // WAVE_LIST_MAX to lists_bucket_kernel, longer ones to this block below
+        const uint32_t n_me = tid < ne ? A.e_cnt[e0 + tid] : 0u;
+        const uint32_t rel = tid < ne ? (uint32_t)(A.e_off[e0 + tid] - ob) : 0u;  // < 2^32 ids per finalize
+        const bool short_me = tid < ne && n_me <= 256;
+        if (tid < ne && !short_me) {
+            if (n_me <= WAVE_LIST_MAX) A.long_q[atomicAdd(A.long_n, 1u)] = (uint32_t)(e0 + tid);
+            else big[atomicAdd(&n_big, 1u)] = tid;
+        }
+        // Staged windows: the chunk's id range cut every LIST_WIN ids; a short
+        // list belongs to the window its first id falls in, and a window stages
+        // [first start, last end) of its lists (<= LIST_WIN + 256 ids) with
+        // coalesced 16-B loads, sorts each list in LDS (<= 32: one lane's
+        // registers, 33..256: one wavefront) and writes the range back with 16-B
+        // stores.  (Ids of a long list inside the range are written back
+        // unsorted; its own kernel rewrites them later on the stream.)
+        // (the common case -- every list short, the chunk fits -- is one window)
+        const bool one = !__syncthreads_or(tid < ne && !short_me) && span + 8 <= LIST_SPAN;
+        const uint32_t nw = one ? 1u : (uint32_t)((span + LIST_WIN - 1) / LIST_WIN);
+        const uint32_t wk = rel / LIST_WIN;
+        for (uint32_t k = 0; k < nw; k++) {
+            if (tid == 0) {
+                w_lo = one ? 0u : 0xFFFFFFFFu;
+                w_hi = one ? (uint32_t)span : 0u;
+                n_mid = 0;
+            }
+            __syncthreads();
+            const bool in_w = short_me && (one || wk == k);
+            if (!one) {
+                if (in_w) {
+                    atomicMin(&w_lo, rel);
+                    atomicMax(&w_hi, rel + n_me);
+                }
+                __syncthreads();
+            }
+            const uint32_t lo_w = w_lo, hi_w = w_hi;
+            if (lo_w >= hi_w) continue;  // uniform: no short list starts here
             LPROF(0);
+            const uint64_t base = (ob + lo_w) & ~3ull;   // staging is 16-B aligned
+            const uint32_t sh = (uint32_t)(ob + lo_w - base);  // ibuf[j] holds id base + j
+            const uint32_t nv = (sh + (hi_w - lo_w) + 3) >> 2;  // uint4 groups (<= LIST_SPAN / 4)
             const uint4* src4 = reinterpret_cast<const uint4*>(A.ids_ord + base);
             uint4* ib4 = reinterpret_cast<uint4*>(ibuf);
-            for (uint32_t b = 0; b < nv; b += 4 * LIST_THREADS) {  // 4 x 16 B in flight
+            for (uint32_t g0 = 0; g0 < nv; g0 += 4 * LIST_THREADS) {  // 4 x 16 B in flight
                 uint4 v[4];
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t g = b + k * LIST_THREADS + tid;
-                    if (g < nv) v[k] = src4[g];  // may read up to 3 ids past the span: same allocation
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t g = g0 + q * LIST_THREADS + tid;
+                    if (g < nv) v[q] = src4[g];  // may read up to 3 ids past the range: same allocation
                 }
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t g = b + k * LIST_THREADS + tid;
-                    if (g < nv) ib4[g] = make_uint4(v[k].x + 1u, v[k].y + 1u, v[k].z + 1u, v[k].w + 1u);
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t g = g0 + q * LIST_THREADS + tid;
+                    if (g < nv) ib4[g] = make_uint4(v[q].x + 1u, v[q].y + 1u, v[q].z + 1u, v[q].w + 1u);
                 }
-            }            __syncthreads();
+            }
+            __syncthreads();
             LPROF(1);
-            if (tid < ne) {
-                const uint32_t n = A.e_cnt[e0 + tid];
-                const uint32_t o = (uint32_t)(A.e_off[e0 + tid] - base);
-                if (n <= 32) sort32_inplace(ibuf + o, n);
-                else big[atomicAdd(&n_big, 1u)] = tid;
+            if (in_w) {
+                if (n_me <= 32) sort32_inplace(ibuf + sh + (rel - lo_w), n_me);
+                else mid[atomicAdd(&n_mid, 1u)] = tid;
             }
             __syncthreads();
             LPROF(2);
-            const uint32_t nbig = n_big;
-            for (uint32_t q = wid; q < nbig; q += LIST_THREADS / 64) {
-                const uint32_t n = A.e_cnt[e0 + big[q]];
-                uint32_t* p = ibuf + (uint32_t)(A.e_off[e0 + big[q]] - base);
+            const uint32_t nmid = n_mid;
+            for (uint32_t q = wid; q < nmid; q += LIST_THREADS / 64) {
+                const uint32_t n = A.e_cnt[e0 + mid[q]];
+                uint32_t* p = ibuf + sh + (uint32_t)(A.e_off[e0 + mid[q]] - ob - lo_w);
                 if (n <= 64) wave_sort_desc<1>(p, n, lane);
                 else if (n <= 128) wave_sort_desc<2>(p, n, lane);
                 else wave_sort_desc<4>(p, n, lane);
@@ -1566,7 +1637,7 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
             LPROF(3);
             {
                 // full groups as 16-B stores, the partial first/last group per id
-                const uint32_t end = sh + (uint32_t)span;  // ibuf index past the span
+                const uint32_t end = sh + (hi_w - lo_w);  // ibuf index past the range
                 int4* dst4 = reinterpret_cast<int4*>(A.ids_out + base);
                 for (uint32_t g = tid; g < nv; g += LIST_THREADS) {
                     const uint32_t j0 = g * 4;
@@ -1577,69 +1648,21 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
                     } else {
                         const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                        for (int k = 0; k < 4; k++)
-                            if (j0 + k >= sh && j0 + k < end)
-                                A.ids_out[base + j0 + k] = id_of(vv[k] - 1u, A.read_ids, A.id_off);
+                        for (int q = 0; q < 4; q++)
+                            if (j0 + q >= sh && j0 + q < end)
+                                A.ids_out[base + j0 + q] = id_of(vv[q] - 1u, A.read_ids, A.id_off);
                     }
                 }
             }
             __syncthreads();
             LPROF(4);
 #ifdef KB_BIN_PROF
-            if (tid == 0) lacc[5]++, lacc[6] += nbig;
+            if (tid == 0) lacc[5]++, lacc[6] += nmid;
 #endif
-            continue;
         }
+        __threadfence_block();
         __syncthreads();
-        for (uint32_t e = tid; e < ne; e += LIST_THREADS) {
-            const uint64_t ge = e0 + e;
-            const uint32_t n = A.e_cnt[ge];
-            const uint64_t o = A.e_off[ge];
-            if (n > 32) {
-                big[atomicAdd(&n_big, 1u)] = e;
-                continue;
-            }
-            uint32_t v[32];
-#pragma unroll
-            for (int j = 0; j < 32; j++) v[j] = (uint32_t)j < n ? A.ids_ord[o + j] + 1u : 0u;
-#pragma unroll
-            for (int kk = 2; kk <= 32; kk <<= 1) {
-#pragma unroll
-                for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-#pragma unroll
-                    for (int i = 0; i < 32; i++) {
-                        const int l2 = i ^ jj;
-                        if (l2 > i) {
-                            const uint32_t x = v[i], y = v[l2];
-                            const bool desc = (i & kk) == 0;
-                            const bool sw = desc ? (x < y) : (x > y);
-                            v[i] = sw ? y : x;
-                            v[l2] = sw ? x : y;
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 32; j++)
-                if ((uint32_t)j < n) A.ids_out[o + j] = id_of(v[j] - 1u, A.read_ids, A.id_off);
-        }
-        __syncthreads();
-        // longer lists.  33..WAVE_LIST_MAX: one wavefront per list, sorted in its
-        // registers (no LDS, no block barriers).  Longer: the whole block.
-        const uint32_t nbig = n_big;
-        for (uint32_t q = wid; q < nbig; q += LIST_THREADS / 64) {
-            const uint64_t ge = e0 + big[q];
-            const uint32_t n = A.e_cnt[ge];
-            if (n > WAVE_LIST_MAX) continue;  // wave-uniform
-            const uint64_t o = A.e_off[ge];
-            const uint32_t* src = A.ids_ord + o;
-            int32_t* dst = A.ids_out + o;
-            if (n <= 64) wave_sort_list<1>(src, dst, n, lane, A.read_ids, A.id_off);
-            else if (n <= 128) wave_sort_list<2>(src, dst, n, lane, A.read_ids, A.id_off);
-            else if (n <= 256) wave_sort_list<4>(src, dst, n, lane, A.read_ids, A.id_off);
-            else if (lane == 0) A.long_q[atomicAdd(A.long_n, 1u)] = (uint32_t)ge;  // lists_long_kernel
-        }
-        __syncthreads();
+        const uint32_t nbig = n_big;  // lists > WAVE_LIST_MAX: the whole block
         for (uint32_t q = 0; q < nbig; q++) {
             const uint64_t ge = e0 + big[q];
             const uint32_t n = A.e_cnt[ge];
@@ -2231,12 +2254,15 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel<KW>, BIN_THREADS, lds);
     if (e != hipSuccess) return e;
     const uint64_t blocks = (uint64_t)std::max(1, cus) * std::max(1, per_cu);
+    // split a light bin above 1/split_div of an even per-block share of the occurrences
+    BinArgs a2 = a;
+    a2.split_occ = a.flat_l && a.split_div ? a.n_occ / ((uint64_t)blocks * a.split_div) + 1 : 0;
     hipLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS), lds, s,
-                       a);
+                       a2);
     e = hipGetLastError();
     if (e != hipSuccess || !a.flat_l) return e;
-    // the heavy bins' partitions, spread over every CU (exits at once without any)
-    hipLaunchKernelGGL(bin_parts_kernel<KW>, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a);
+    // the heavy and split bins' partitions, spread over every CU (exits at once without any)
+    hipLaunchKernelGGL(bin_parts_kernel<KW>, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a2);
     return hipGetLastError();
 }
 

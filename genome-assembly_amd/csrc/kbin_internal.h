@@ -163,8 +163,13 @@ struct BinArgs {
     uint32_t* flat_l0;              // [max_bins] partition depth
     unsigned long long* flat_sbase; // [max_bins] stage base
     unsigned long long* flat_obase; // [max_bins] the bin's range of flat_off
-    uint32_t* flat_off;             // pool of list offsets, np + 1 per heavy bin
+    uint32_t* flat_off;             // pool of list offsets, np + 1 per heavy (or split) bin
     unsigned long long* flat_octr;  // (zeroed) pool allocation
+    // split bins (light bins above a fair share of one block): published like
+    // heavy bins (flat_l0 | SPLIT_BIT), their partitions binned from the records
+    uint64_t n_occ;                 // occurrences of this finalize
+    uint32_t split_div;             // split above n_occ / (blocks x split_div) (0 = never)
+    uint64_t split_occ;             // (set at launch)
     const uint64_t* totals;    // totals[2] = nbins
     int K, M;
     uint32_t keep_gt;

@@ -1216,8 +1216,8 @@ hipError_t launch_runs(const uint64_t* S, uint64_t n, const uint64_t* table, int
     const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     const uint64_t nbr = (max_runs + SCAN_TILE - 1) / SCAN_TILE;
     if (scratch_n < std::max(nb + 1, 2 * nbr + 2)) return hipErrorInvalidValue;
-    if (n == 0) {
-        hipError_t e = hipMemsetAsync(d_totals, 0, 3 * sizeof(uint64_t), s);
+    if (n == 0) {  // (totals[3], the run-overflow word, too: the host checks it)
+        hipError_t e = hipMemsetAsync(d_totals, 0, 4 * sizeof(uint64_t), s);
         if (e == hipSuccess) e = hipMemsetAsync(e_off, 0, sizeof(uint64_t), s);
         return e;
     }

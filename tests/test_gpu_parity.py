@@ -361,6 +361,38 @@ def test_heavy_bins_flat_lists(ts_log2, flat_l, fill, K, engine, monkeypatch):
             assert int((res.first & np.uint64(0xFFFF)).max()) <= L - K
 
 
+@pytest.mark.parametrize("genome,flat_l,ts_log2,K", [(3000, 3, 13, 31), (3000, 2, 10, 31), (200000, 3, 13, 31),
+                                                      (200000, 3, 11, 31), (3000, 3, 12, 63), (200000, 3, 11, 63)])
+def test_split_bins(genome, flat_l, ts_log2, K, engine, monkeypatch):
+    """split bins: a light bin above a fair share of one block is counted per
+    hash partition in phase 0 and its partitions are binned by any block in
+    phase 1 (KB_BIN_SPLIT_DIV forces it for nearly every bin); small tables
+    add overflow re-splits inside a partition"""
+    import torch
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    monkeypatch.setenv("KB_BIN_SPLIT_DIV", "1000000")
+    monkeypatch.setenv("KB_BIN_FLAT_L", str(flat_l))
+    monkeypatch.setenv("KB_BIN_TS_LOG2", str(ts_log2))
+    n, L = 40000, 150
+    wpr = (L + 31) // 32
+    words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, genome, 5000, 11)
+    torch.cuda.synchronize()
+    bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n, wpr, n * L)
+    ora = oracle.bin_reads(bases, hl, K, 7, 1, True)
+    with kbin.Engine(K, 7, cutoff=1, max_read_len=L, flags=kbin.KB_TRACK_FIRST) as eng:
+        for _ in range(2):  # the second pass runs with the learned density
+            eng.reset()
+            eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
+            eng.finalize(True)
+            res = eng.export()
+            assert_same(res, ora)
+            last = res.ids[res.offset[1:].astype(np.int64) - 1]
+            np.testing.assert_array_equal(res.first >> np.uint64(16), last.astype(np.uint64))
+
+
 def test_alphabet_rejected():
     """bytes outside ACGT are rejected loudly (alphabet)"""
     with kbin.Engine(11, 4) as eng:
