@@ -145,7 +145,7 @@ struct kb_ctx {
     DevBuf<uint32_t> long_q;   // entries with 257..4096 ids (lists_long_kernel)
     DevBuf<uint32_t> border;   // bin processing order
     DevBuf<uint32_t> bcount, bmmer;  // bin descriptors (with starts)
-    DevBuf<uint32_t> flat_list, flat_next, flat_l0, flat_off;  // heavy bins published for phase 1
+    DevBuf<uint32_t> flat_list, flat_next, flat_l0, flat_off, flat_cur, flat_chunk, pool_bin, chunk_bin;  // heavy bins published for phase 1
     DevBuf<unsigned long long> flat_sbase, flat_obase, flat_n;  // flat_n[0] bins, [1] offset pool
     DevBuf<uint64_t> regions;  // local bucket regions (pay layout)
     DevBuf<unsigned long long> bfill;  // records per bucket
@@ -183,6 +183,7 @@ struct kb_ctx {
     // timing
     bool timing = false;
     kb_timing tm{};
+    uint32_t nbins_hint = 0;  // bins of the last binned finalize (flat-list threshold)
     hipEvent_t ev[8] = {};
 };
 
@@ -269,6 +270,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->misc.release(); c->totals.release(); c->first.release(); c->e_first.release();
     for (auto& m : c->bmaps) m.map.release();
     c->flat_list.release(); c->flat_next.release(); c->flat_l0.release(); c->flat_off.release();
+    c->flat_cur.release(); c->flat_chunk.release(); c->pool_bin.release(); c->chunk_bin.release();
     c->flat_sbase.release(); c->flat_obase.release(); c->flat_n.release();
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -1170,7 +1172,15 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));  // ids by ordinal (+ radix ping-pong)
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
     // heavy bins' flat k-mer lists (touched only when a bin needs many tables)
-    const uint32_t flat_l = (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", 3));
+    // Few, large bins (the last finalize had fewer than two per CU: the
+    // mmer-sharded receivers of N ranks, high coverage): every multi-table bin
+    // takes the flat lists, whose build and partitions spread over the chip
+    // (2.97 vs 3.9 ms per pass on the 8-rank share); otherwise depth >= 3
+    // (many bins keep the CUs busy, and the lists' HBM round trip would cost)
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev));
+    const int fl_auto = c->nbins_hint && c->nbins_hint < 2u * (uint32_t)std::max(1, cus) ? 1 : 3;
+    const uint32_t flat_l = (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", fl_auto));
     if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(KW * N, 1)));
     if (bucketed) {
         BucketArgs ba{};
@@ -1255,6 +1265,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.flat_l = flat_l;
         a.n_occ = N;
         a.split_div = (uint32_t)std::max(0, env_int("KB_BIN_SPLIT_DIV", 0));
+        a.big_div = (uint32_t)std::max(0, env_int("KB_BIN_BIG_DIV", 2));
         if (flat_l) {
             HIPCHK(c->flat_list.ensure(max_bins));
             HIPCHK(c->flat_next.ensure(max_bins));
@@ -1264,13 +1275,21 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             // offsets: np + 1 per heavy bin, np < 2 x (expected keys / (fill x TS)) + 1,
             // expected keys <= occurrences, fill x TS >= 0.3 x 1024
             HIPCHK(c->flat_off.ensure(N / 150 + 9 * max_bins + KB_FLAT_MAX + 1));
-            HIPCHK(c->flat_n.ensure(2));
-            HIPCHK(hipMemsetAsync(c->flat_n.p, 0, 2 * sizeof(unsigned long long), c->s));
+            HIPCHK(c->flat_cur.ensure(c->flat_off.cap));
+            HIPCHK(c->flat_chunk.ensure(max_bins));
+            HIPCHK(c->pool_bin.ensure(c->flat_off.cap));
+            HIPCHK(c->chunk_bin.ensure(R / 1024 + max_bins + 1));
+            HIPCHK(c->flat_n.ensure(8));
+            HIPCHK(hipMemsetAsync(c->flat_n.p, 0, 8 * sizeof(unsigned long long), c->s));
             a.flat_list = c->flat_list.p;
             a.flat_next = c->flat_next.p;
             a.flat_l0 = c->flat_l0.p;
             a.flat_sbase = c->flat_sbase.p;
             a.flat_off = c->flat_off.p;
+            a.flat_cur = c->flat_cur.p;
+            a.flat_chunk = c->flat_chunk.p;
+            a.pool_bin = c->pool_bin.p;
+            a.chunk_bin = c->chunk_bin.p;
             a.flat_obase = c->flat_obase.p;
             a.flat_n = c->flat_n.p;
             a.flat_octr = c->flat_n.p + 1;
@@ -1367,6 +1386,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     }
     c->tm.table_slots = 1ull << ts_log2;
     c->tm.n_bins = (uint32_t)c->h_totals[2];
+    c->nbins_hint = c->tm.n_bins;
     c->tm.n_superkmers = R;
     c->finalized = true;
     c->exported = false;

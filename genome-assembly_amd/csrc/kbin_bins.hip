@@ -825,11 +825,11 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
 
 // Every k-mer of the bin's records, once, to g(key, ordinal, position) on
 // its own lane (no ring, no filter): the two expansions of a heavy bin.
-template <int KW, typename G>
+template <int KW, int NT = BIN_THREADS, typename G>
 DEV void expand_bin(const BinArgs& A, uint32_t lo, uint32_t hi, G&& g) {
     const int K = A.K;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint32_t base = lo + wid * 64; base < hi; base += BIN_THREADS) {
+    for (uint32_t base = lo + wid * 64; base < hi; base += NT) {
         const uint32_t r = base + lane;
         const uint64_t hd = r < hi ? A.hdr[r] : 0ull;
         Span<KW> sp{};
@@ -867,8 +867,10 @@ DEV void kst_store(uint64_t* kst, uint32_t i, const TKey<KW>& k) {
 // into flat per-partition lists -- and each partition is then swept from its
 // list.  Up to FLAT_MAX partitions; deeper splits filter the flat lists.
 constexpr uint32_t FLAT_LOG2 = 14;
-constexpr uint32_t FLAT_MAX = 1u << FLAT_LOG2;  // (cursors in the table area: 64 KiB)
+constexpr uint32_t FLAT_MAX = 1u << FLAT_LOG2;  // (a 64-KiB LDS histogram in the build kernels)
 static_assert(FLAT_MAX == KB_FLAT_MAX, "host and device agree on the flat list count");
+constexpr int FB_THREADS = 256;        // the build kernels' blocks
+constexpr uint32_t FB_CHUNK = 1024;    // records per build item
 constexpr uint32_t SPLIT_BIT = 0x100u;     // flat_l0: a split bin's partitions (no flat lists)
 constexpr uint32_t PRUNED = 0x80000000u;  // cursor of a pruned (or empty) slot in sweep 2
 constexpr uint64_t M48 = (1ull << 48) - 1ull;
@@ -898,7 +900,6 @@ DEV void bin_body(const BinArgs& A) {
     unsigned long long pt = clock64();
 #endif
 
-    if (tid == 0) S.flat_idx = 0;
     while (true) {
         // phase 0: persistent blocks take bins from a shared counter, largest
         // first.  Phase 1: the partitions of the heavy bins phase 0 turned into
@@ -909,17 +910,18 @@ DEV void bin_body(const BinArgs& A) {
             if (PHASE == 0) {
                 S.item = (uint32_t)atomicAdd(A.work, 1ull);
             } else {
+                // items are offset-pool indices: entry e0 + p of a published
+                // bin is its partition p (the bin's last entry is no item)
                 S.item = 0xFFFFFFFFu;
-                const uint32_t nf = (uint32_t)min<unsigned long long>(*A.flat_n, A.max_bins);
-                while (S.flat_idx < nf) {
-                    const uint32_t fb0 = A.flat_list[S.flat_idx];
-                    const uint32_t pp = atomicAdd(&A.flat_next[fb0], 1u);
-                    if (pp < (1u << (A.flat_l0[fb0] & 0xFFu))) {
-                        S.item = fb0;
-                        S.part0 = pp;
-                        break;
-                    }
-                    S.flat_idx++;
+                const unsigned long long npool = A.flat_n[1];
+                for (;;) {
+                    const unsigned long long it = atomicAdd(&A.flat_n[5], 1ull);
+                    if (it >= npool) break;
+                    const uint32_t fb0 = A.pool_bin[it];
+                    if (fb0 == 0xFFFFFFFFu) continue;
+                    S.item = fb0;
+                    S.part0 = (uint32_t)(it - A.flat_obase[fb0]);
+                    break;
                 }
             }
         }
@@ -964,10 +966,14 @@ DEV void bin_body(const BinArgs& A) {
             l0 = S.l0 & 0xFFu;
         }
         // heavy bin: flat per-partition lists (the ring area holds the cursors)
-        const bool flat = PHASE == 1 ? !(S.l0 & SPLIT_BIT) : (A.flat_l && l0 >= A.flat_l);
+        // flat: a heavy bin (l0 >= flat_l), or a multi-table bin above a fair
+        // share of one block's occurrences (few, large bins: N ranks, high
+        // coverage) -- its build and its partitions then spread over the chip
+        const bool flat = PHASE == 1 ? !(S.l0 & SPLIT_BIT)
+                                     : (A.flat_l && (l0 >= A.flat_l || (A.big_occ && l0 >= 1 && occ_tot > A.big_occ)));
         // a large light bin (more occurrences than a fair share of one CU) is
-        // split: phase 0 counts its k-mers per hash partition (one expansion,
-        // no probes) and gives each partition its own stage range, phase 1
+        // split: its k-mers are counted per hash partition (flat_count_kernel,
+        // no probes), each partition gets its own stage range, and phase 1
         // bins the partitions on any block, each re-expanding the records with
         // the partition filter -- the light path, in parallel
         bool split = PHASE == 1 && !flat;
@@ -976,81 +982,32 @@ DEV void bin_body(const BinArgs& A) {
             while (l0 < lmax && (occ_tot >> l0) > A.split_occ) l0++;
             split = l0 >= 1;
         }
-        // (the table area holds the cursors: no table while the lists are built;
-        // the offsets go straight to the published pool)
-        uint32_t* fl_cur = reinterpret_cast<uint32_t*>(T.ca);  // [FLAT_MAX]
         uint64_t* kst = A.kstage + KW * S.stage_base;
-        if (split && PHASE == 0) {
-            const uint32_t np = 1u << l0, pm = np - 1u;
-            if (tid < np) fl_cur[tid] = 0;
-            __syncthreads();
-            expand_bin<KW>(A, lo, hi, [&](const TKey<KW>& key, uint32_t, uint32_t) {
-                atomicAdd(&fl_cur[key.part() & pm], 1u);
-            });
-            __syncthreads();
-            if (tid == 0) {
-                const unsigned long long e0 = atomicAdd(A.flat_octr, (unsigned long long)(np + 1));
-                uint32_t run = 0;
-                for (uint32_t i = 0; i < np; i++) {
-                    A.flat_off[e0 + i] = run;
-                    run += fl_cur[i];
-                }
-                A.flat_off[e0 + np] = run;
-                A.flat_obase[b] = e0;
-                A.flat_sbase[b] = S.stage_base;
-                A.flat_l0[b] = l0 | SPLIT_BIT;
-                A.flat_next[b] = 0;
-                A.flat_list[atomicAdd(A.flat_n, 1ull)] = b;
+        if ((split || flat) && PHASE == 0) {
+            // publish: flat_count_kernel counts the k-mers per partition (any
+            // block, chunks of records), flat_scan_kernel turns the counts into
+            // offsets, flat_scatter_kernel writes a flat bin's lists, and phase 1
+            // bins the partitions (a heavy bin is no longer one block's serial build)
+            if (flat) {  // at most FLAT_MAX lists; deeper splits filter them
+                if (l0 > FLAT_LOG2) l0 = FLAT_LOG2;
             }
-            PROF_MARK(7);
-            continue;  // (the next kernel launch sees every store)
-        }
-        if (flat && PHASE == 0) {
-            // at most FLAT_MAX lists, and as many cursors as the table area holds
-            // (TS x (2 KW + 1) words); deeper splits filter the lists
-            const uint32_t l0_cap = min(FLAT_LOG2, A.ts_log2 + (uint32_t)KW);
-            if (l0 > l0_cap) l0 = l0_cap;
-            const uint32_t np = 1u << l0, pm = np - 1u;
-            for (uint32_t i = tid; i < np; i += BIN_THREADS) fl_cur[i] = 0;
-            __syncthreads();
-            expand_bin<KW>(A, lo, hi, [&](const TKey<KW>& key, uint32_t, uint32_t) {
-                atomicAdd(&fl_cur[key.part() & pm], 1u);
-            });
-            __syncthreads();
-            // exclusive offsets: thread t owns partitions [t*q, t*q + q)
-            const uint32_t q = (np + BIN_THREADS - 1) / BIN_THREADS;
-            uint64_t mine = 0;
-            for (uint32_t k = 0; k < q; k++) {
-                const uint32_t i = tid * q + k;
-                if (i < np) mine += fl_cur[i];
-            }
-            uint64_t tot_f;
-            uint64_t run = block_excl_scan_u64(mine, S.red, tot_f);
+            const uint32_t np = 1u << l0;
             if (tid == 0) S.e0 = atomicAdd(A.flat_octr, (unsigned long long)(np + 1));  // this bin's pool range
             __syncthreads();
-            uint32_t* fl_off = A.flat_off + S.e0;  // [np + 1], read by phase 1
-            for (uint32_t k = 0; k < q; k++) {
-                const uint32_t i = tid * q + k;
-                if (i < np) {
-                    const uint32_t c = fl_cur[i];
-                    fl_off[i] = (uint32_t)run;
-                    fl_cur[i] = (uint32_t)run;
-                    run += c;
-                }
+            for (uint32_t i = tid; i <= np; i += BIN_THREADS) {
+                A.flat_off[S.e0 + i] = 0;  // counts, then offsets
+                A.pool_bin[S.e0 + i] = i < np ? b : 0xFFFFFFFFu;
             }
-            if (tid == 0) fl_off[np] = (uint32_t)tot_f;
+            // the build kernels' items: chunks of FB_CHUNK records
+            const uint32_t nch = (hi - lo + FB_CHUNK - 1) / FB_CHUNK;
+            if (tid == 0) S.i0 = atomicAdd(&A.flat_n[2], (unsigned long long)nch);
             __syncthreads();
-            expand_bin<KW>(A, lo, hi, [&](const TKey<KW>& key, uint32_t ord, uint32_t pos) {
-                const uint32_t i = atomicAdd(&fl_cur[key.part() & pm], 1u);
-                kst_store<KW>(kst, i, key);
-                stage[i] = ((uint64_t)pos << 32) | ord;
-            });
-            // publish the lists: phase 1 sweeps the partitions, any block each
+            for (uint32_t k = tid; k < nch; k += BIN_THREADS) A.chunk_bin[S.i0 + k] = b;
             if (tid == 0) {
                 A.flat_obase[b] = S.e0;
                 A.flat_sbase[b] = S.stage_base;
-                A.flat_l0[b] = l0;
-                A.flat_next[b] = 0;
+                A.flat_l0[b] = l0 | (split ? SPLIT_BIT : 0u);
+                A.flat_chunk[b] = (uint32_t)S.i0;
                 A.flat_list[atomicAdd(A.flat_n, 1ull)] = b;
             }
             PROF_MARK(7);
@@ -1302,6 +1259,208 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
 template <int KW>
 __global__ __launch_bounds__(BIN_THREADS) void bin_parts_kernel(BinArgs A) {
     bin_body<KW, 1>(A);
+}
+
+// ---- the parallel build of published (heavy / split) bins.  Work items are
+// (bin, chunk of FB_CHUNK records), numbered by phase 0 (chunk_bin); block i
+// takes items i, i + grid, ... (near-equal items; a shared claim counter cost
+// ~60 ns per serialised returning atomic, 0.13 ms for an empty launch)
+DEV bool fb_claim(const BinArgs& A, bool flat_only, unsigned long long& it, uint32_t& b, uint32_t& c) {
+    const unsigned long long n = A.flat_n[2];
+    for (; it < n; it += gridDim.x) {
+        b = A.chunk_bin[it];
+        if (flat_only && (A.flat_l0[b] & SPLIT_BIT)) continue;
+        c = (uint32_t)(it - A.flat_chunk[b]);
+        return true;
+    }
+    return false;
+}
+
+// per chunk: an LDS histogram of its k-mers over the bin's partitions, added
+// into the bin's counts (flat_off, zeroed by phase 0)
+template <int KW>
+__global__ __launch_bounds__(FB_THREADS) void flat_count_kernel(BinArgs A) {
+    extern __shared__ uint32_t hist[];  // [np]
+    __shared__ uint32_t s_b, s_c, s_ok;
+    unsigned long long it = blockIdx.x;
+    for (;; it += gridDim.x) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t b = 0, c = 0;
+            s_ok = fb_claim(A, false, it, b, c);
+            s_b = b;
+            s_c = c;
+        }
+        __syncthreads();
+        if (!s_ok) break;
+        const uint32_t b = s_b, l0 = A.flat_l0[b] & 0xFFu, np = 1u << l0, pm = np - 1u;
+        const uint32_t lo = A.bstart[b] + s_c * FB_CHUNK, hi = min(lo + FB_CHUNK, A.bstart[b] + A.bcount[b]);
+        for (uint32_t i = threadIdx.x; i < np; i += FB_THREADS) hist[i] = 0;
+        __syncthreads();
+        // up to 8 partitions: 8-bit counts packed in a lane's register (a lane
+        // expands <= 4 records of <= 63 k-mers), added per wave -- 256 lanes
+        // on 8 LDS words would serialise
+        const bool packed = np <= 8;
+        uint64_t pk = 0;
+        expand_bin<KW, FB_THREADS>(A, lo, hi, [&](const TKey<KW>& key, uint32_t, uint32_t) {
+            const uint32_t pp = key.part() & pm;
+            if (packed)
+                pk += 1ull << (8 * pp);
+            else
+                atomicAdd(&hist[pp], 1u);
+        });
+        if (packed)
+            for (uint32_t pp = 0; pp < np; pp++) {
+                const uint32_t c = wave_incl_scan((uint32_t)((pk >> (8 * pp)) & 0xFFull), (int)(threadIdx.x & 63));
+                if ((threadIdx.x & 63) == 63 && c) atomicAdd(&hist[pp], c);
+            }
+        __syncthreads();
+        uint32_t* cnt = A.flat_off + A.flat_obase[b];
+        for (uint32_t i = threadIdx.x; i < np; i += FB_THREADS)
+            if (hist[i]) atomicAdd(&cnt[i], hist[i]);
+    }
+}
+
+// per published bin: counts -> exclusive offsets (np + 1, relative to the
+// bin's stage range) and, for a flat bin, the scatter cursors
+__global__ __launch_bounds__(1024) void flat_scan_kernel(BinArgs A) {
+    __shared__ uint64_t red[16];
+    const uint32_t nf = (uint32_t)min<unsigned long long>(*A.flat_n, A.max_bins);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t q = blockIdx.x; q < nf; q += gridDim.x) {
+        const uint32_t b = A.flat_list[q];
+        const uint32_t np = 1u << (A.flat_l0[b] & 0xFFu);
+        uint32_t* off = A.flat_off + A.flat_obase[b];
+        uint32_t* cur = A.flat_cur + A.flat_obase[b];
+        const uint32_t per = (np + 1023) / 1024, i0 = threadIdx.x * per;
+        uint64_t mine = 0;
+        for (uint32_t k = 0; k < per; k++)
+            if (i0 + k < np) mine += off[i0 + k];
+        const uint64_t inc = wave_incl_scan(mine, lane);
+        if (lane == 63) red[wid] = inc;
+        __syncthreads();
+        uint64_t run = inc - mine, tot = 0;
+        for (int w = 0; w < 16; w++) {
+            if (w < wid) run += red[w];
+            tot += red[w];
+        }
+        for (uint32_t k = 0; k < per; k++) {
+            if (i0 + k < np) {
+                const uint32_t c = off[i0 + k];
+                off[i0 + k] = (uint32_t)run;
+                cur[i0 + k] = (uint32_t)run;
+                run += c;
+            }
+        }
+        if (threadIdx.x == 0) off[np] = (uint32_t)tot;
+        __syncthreads();
+    }
+}
+
+// per chunk of a flat bin: count per partition in LDS, reserve each
+// partition's range with one global atomic, then scatter (table key,
+// position << 32 | ordinal) into the lists (LDS cursors)
+template <int KW>
+__global__ __launch_bounds__(FB_THREADS) void flat_scatter_kernel(BinArgs A) {
+    extern __shared__ uint32_t hist[];  // [np]: counts, then cursors
+    __shared__ uint32_t s_b, s_c, s_ok;
+    __shared__ uint32_t fb_wtot[FB_THREADS / 64][8];
+    unsigned long long it = blockIdx.x;
+    for (;; it += gridDim.x) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t b = 0, c = 0;
+            s_ok = fb_claim(A, true, it, b, c);
+            s_b = b;
+            s_c = c;
+        }
+        __syncthreads();
+        if (!s_ok) break;
+        const uint32_t b = s_b, l0 = A.flat_l0[b] & 0xFFu, np = 1u << l0, pm = np - 1u;
+        const uint32_t lo = A.bstart[b] + s_c * FB_CHUNK, hi = min(lo + FB_CHUNK, A.bstart[b] + A.bcount[b]);
+        for (uint32_t i = threadIdx.x; i < np; i += FB_THREADS) hist[i] = 0;
+        __syncthreads();
+        // up to 8 partitions: packed per-lane counts (see flat_count_kernel)
+        // give each wave a range per partition; the second expansion steps the
+        // wave's lanes together and ranks them per partition by ballot, so
+        // consecutive lanes of one partition store to consecutive entries
+        const bool packed = np <= 8;
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        uint64_t pk = 0;
+        expand_bin<KW, FB_THREADS>(A, lo, hi, [&](const TKey<KW>& key, uint32_t, uint32_t) {
+            const uint32_t pp = key.part() & pm;
+            if (packed)
+                pk += 1ull << (8 * pp);
+            else
+                atomicAdd(&hist[pp], 1u);
+        });
+        if (packed) {
+#pragma unroll
+            for (uint32_t pp = 0; pp < 8; pp++) {
+                const uint32_t c = pp < np ? (uint32_t)((pk >> (8 * pp)) & 0xFFull) : 0u;
+                const uint32_t inc = wave_incl_scan(c, lane);
+                if (lane == 63) fb_wtot[wid][pp] = inc;
+            }
+        }
+        __syncthreads();
+        if (packed && threadIdx.x < np) {
+            uint32_t t = 0;
+            for (int w = 0; w < FB_THREADS / 64; w++) t += fb_wtot[w][threadIdx.x];
+            hist[threadIdx.x] = t;
+        }
+        __syncthreads();
+        uint32_t* cur = A.flat_cur + A.flat_obase[b];
+        for (uint32_t i = threadIdx.x; i < np; i += FB_THREADS)
+            if (hist[i]) hist[i] = atomicAdd(&cur[i], hist[i]);
+        __syncthreads();
+        const uint64_t sb = A.flat_sbase[b];
+        uint64_t* kst = A.kstage + KW * sb;
+        uint64_t* stage = A.stage + sb;
+        if (packed) {
+            uint32_t wb[8];  // this wave's next entry per partition (wave-uniform)
+#pragma unroll
+            for (uint32_t pp = 0; pp < 8; pp++) {
+                uint32_t w0 = 0;
+                for (int w = 0; w < wid; w++) w0 += fb_wtot[w][pp];
+                wb[pp] = pp < np ? hist[pp] + w0 : 0u;
+            }
+            const uint64_t lt = (1ull << lane) - 1ull;
+            const int K = A.K;
+            for (uint32_t base = lo + (uint32_t)wid * 64u; base < hi; base += FB_THREADS) {
+                const uint32_t r = base + (uint32_t)lane;
+                const uint64_t hd = r < hi ? A.hdr[r] : 0ull;
+                Span<KW> sp{};
+                if (r < hi) sp.load(A, r);
+                const int n = (int)((hd >> 32) & 63u);
+                const uint32_t ord = (uint32_t)hd;
+                const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);
+                const uint64_t fl = 0ull - ((hd >> 44) & 1ull);
+                const int nmax = (int)wave_max_u32((uint32_t)n);
+                for (int j = 0; j < nmax; j++) {
+                    const TKey<KW> key = sp.key(K, fl);
+                    sp.step();
+                    const uint32_t pp = j < n ? key.part() & pm : 0xFFu;
+                    uint32_t i = 0;
+#pragma unroll
+                    for (uint32_t q = 0; q < 8; q++) {
+                        const uint64_t m = __ballot(pp == q);
+                        if (pp == q) i = wb[q] + (uint32_t)__popcll(m & lt);
+                        wb[q] += (uint32_t)__popcll(m);
+                    }
+                    if (j < n) {
+                        kst_store<KW>(kst, i, key);
+                        stage[i] = ((uint64_t)(rlo + (uint32_t)j) << 32) | ord;
+                    }
+                }
+            }
+        } else {
+            expand_bin<KW, FB_THREADS>(A, lo, hi, [&](const TKey<KW>& key, uint32_t ord, uint32_t pos) {
+                const uint32_t i = atomicAdd(&hist[key.part() & pm], 1u);
+                kst_store<KW>(kst, i, key);
+                stage[i] = ((uint64_t)pos << 32) | ord;
+            });
+        }
+    }
 }
 
 #ifdef KB_BIN_PROF
@@ -2257,11 +2416,18 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     // split a light bin above 1/split_div of an even per-block share of the occurrences
     BinArgs a2 = a;
     a2.split_occ = a.flat_l && a.split_div ? a.n_occ / ((uint64_t)blocks * a.split_div) + 1 : 0;
+    a2.big_occ = a.flat_l && a.big_div ? a.n_occ / ((uint64_t)blocks * a.big_div) + 1 : 0;
     hipLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS), lds, s,
                        a2);
     e = hipGetLastError();
     if (e != hipSuccess || !a.flat_l) return e;
-    // the heavy and split bins' partitions, spread over every CU (exits at once without any)
+    // the published bins: counts, offsets, flat lists -- every kernel exits at
+    // once without any -- then their partitions, spread over every CU
+    const size_t fb_lds = (size_t)FLAT_MAX * sizeof(uint32_t);
+    const unsigned fb_blocks = (unsigned)std::max(1, cus) * 8u;
+    hipLaunchKernelGGL(flat_count_kernel<KW>, dim3(fb_blocks), dim3(FB_THREADS), fb_lds, s, a2);
+    hipLaunchKernelGGL(flat_scan_kernel, dim3(1024), dim3(1024), 0, s, a2);
+    hipLaunchKernelGGL(flat_scatter_kernel<KW>, dim3(fb_blocks), dim3(FB_THREADS), fb_lds, s, a2);
     hipLaunchKernelGGL(bin_parts_kernel<KW>, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a2);
     return hipGetLastError();
 }

@@ -158,18 +158,25 @@ struct BinArgs {
     // bin into flat per-partition lists (published below); phase 1 sweeps the
     // published partitions, any block any partition
     uint32_t* flat_list;            // [max_bins] published heavy bins
-    unsigned long long* flat_n;     // (zeroed) their number
+    unsigned long long* flat_n;     // (zeroed) [0] published bins [1] pool [2] build items,
+                                    // claims: [3] count [4] scatter [5] phase 1
     uint32_t* flat_next;            // [max_bins] next partition to claim
     uint32_t* flat_l0;              // [max_bins] partition depth
     unsigned long long* flat_sbase; // [max_bins] stage base
     unsigned long long* flat_obase; // [max_bins] the bin's range of flat_off
     uint32_t* flat_off;             // pool of list offsets, np + 1 per heavy (or split) bin
+    uint32_t* flat_cur;             // the same layout: scatter cursors (flat bins)
+    uint32_t* flat_chunk;           // [max_bins] first build item (record chunk) of the bin
+    uint32_t* pool_bin;             // [flat_off] bin of an offset-pool entry (phase 1 items)
+    uint32_t* chunk_bin;            // [R / 1024 + max_bins] bin of a build item
     unsigned long long* flat_octr;  // (zeroed) pool allocation
     // split bins (light bins above a fair share of one block): published like
     // heavy bins (flat_l0 | SPLIT_BIT), their partitions binned from the records
     uint64_t n_occ;                 // occurrences of this finalize
     uint32_t split_div;             // split above n_occ / (blocks x split_div) (0 = never)
     uint64_t split_occ;             // (set at launch)
+    uint32_t big_div;               // flat lists for a multi-table bin above n_occ / (blocks x big_div)
+    uint64_t big_occ;               // (set at launch; 0 = by depth only)
     const uint64_t* totals;    // totals[2] = nbins
     int K, M;
     uint32_t keep_gt;
