@@ -8,13 +8,15 @@ Inputs are generated on the device before the timed region (seeded, SURVEY
 §8(d) C2 at N=1: 1M x 150 bp, genome 5 Mbp, 0.1% substitutions, seed 2,
 K=31 M=7, cutoff 1); outputs stay device-resident (CSR).
 
-N>1 (torchrun, one rank per GPU): every rank owns its own 1M-read shard
-(weak scaling) and k-mers are routed to the GPU that owns their canonical mmer
-with an RCCL all-to-all (genome-assembly_amd/kbin/dist.py).
+N>1 (torchrun, one rank per GPU): every rank generates its own 1M-read shard
+of its own 5-Mbp genome (weak scaling at constant coverage) and k-mers are
+routed to the GPU that owns their canonical mmer with an RCCL all-to-all
+(genome-assembly_amd/kbin/dist.py).
 
 Prints ONE JSON line on rank 0 (contract in the task statement); extra
-objects: "roofline" for the dominant kernel (scan_insert) and "cpu_baseline"
-(the CPU oracle on a bounded sample of the same workload, rank 0 only).
+objects: "roofline" for the dominant kernel (bin_kernel; scan_insert_kernel
+on the table engine) and "cpu_baseline" (the compiled reference, with the C
+port beside it, on a bounded sample of the same workload, rank 0 only).
 """
 from __future__ import annotations
 
@@ -196,8 +198,10 @@ def main():
     n = args.reads
     words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
     lens = torch.empty(n, dtype=torch.int32, device="cuda")
-    # rank r draws read indices [r*n, (r+1)*n) of one global stream: seed is
-    # per rank-shard so shards are disjoint slices of the same genome
+    # rank r samples its n reads from its own genome (the generator seeds the
+    # genome from the shard seed): the N-rank job bins N x 1M reads of N
+    # genomes of `genome` bp at a constant 30x coverage, each rank owning 1/N of
+    # the canonical mmers (bins N x larger per GPU)
     kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, args.genome,
                                args.err_ppm, args.seed * 1000003 + rank, device=local)
     torch.cuda.synchronize()
