@@ -1172,14 +1172,14 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));  // ids by ordinal (+ radix ping-pong)
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
     // heavy bins' flat k-mer lists (touched only when a bin needs many tables)
-    // Few, large bins (the last finalize had fewer than two per CU: the
+    // Few, large bins (the last finalize had fewer than three per CU: the
     // mmer-sharded receivers of N ranks, high coverage): every multi-table bin
     // takes the flat lists, whose build and partitions spread over the chip
     // (2.97 vs 3.9 ms per pass on the 8-rank share); otherwise depth >= 3
     // (many bins keep the CUs busy, and the lists' HBM round trip would cost)
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev));
-    const int fl_auto = c->nbins_hint && c->nbins_hint < 2u * (uint32_t)std::max(1, cus) ? 1 : 3;
+    const int fl_auto = c->nbins_hint && c->nbins_hint < 3u * (uint32_t)std::max(1, cus) ? 1 : 3;
     const uint32_t flat_l = (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", fl_auto));
     if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(KW * N, 1)));
     if (bucketed) {
