@@ -1173,14 +1173,15 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
     // heavy bins' flat k-mer lists (touched only when a bin needs many tables)
     // Few, large bins (the last finalize had fewer than three per CU: the
-    // mmer-sharded receivers of N ranks, high coverage): every multi-table bin
-    // takes the flat lists, whose build and partitions spread over the chip
-    // (2.97 vs 3.9 ms per pass on the 8-rank share); otherwise depth >= 3
-    // (many bins keep the CUs busy, and the lists' HBM round trip would cost)
+    // mmer-sharded receivers of N ranks, high coverage): bins above 1/32 of a
+    // block's fair share are split (their partitions re-expanded by any block)
+    // up to depth 3, deeper ones take the flat lists -- both spread over the
+    // chip (bins 3.67 -> 2.70 ms per pass on the 8-rank share).  Otherwise
+    // flat lists from depth 3 on and no splits (many bins keep the CUs busy).
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev));
-    const int fl_auto = c->nbins_hint && c->nbins_hint < 3u * (uint32_t)std::max(1, cus) ? 1 : 3;
-    const uint32_t flat_l = (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", fl_auto));
+    const bool few_bins = c->nbins_hint && c->nbins_hint < 3u * (uint32_t)std::max(1, cus);
+    const uint32_t flat_l = (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", few_bins ? 4 : 3));
     if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(KW * N, 1)));
     if (bucketed) {
         BucketArgs ba{};
@@ -1264,7 +1265,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.kstage = flat_l ? c->kstage.p : nullptr;
         a.flat_l = flat_l;
         a.n_occ = N;
-        a.split_div = (uint32_t)std::max(0, env_int("KB_BIN_SPLIT_DIV", 0));
+        a.split_div = (uint32_t)std::max(0, env_int("KB_BIN_SPLIT_DIV", few_bins ? 32 : 0));
         a.big_div = (uint32_t)std::max(0, env_int("KB_BIN_BIG_DIV", 2));
         if (flat_l) {
             HIPCHK(c->flat_list.ensure(max_bins));
