@@ -149,6 +149,7 @@ struct kb_ctx {
     DevBuf<unsigned long long> flat_sbase, flat_obase, flat_n;  // flat_n[0] bins, [1] offset pool
     DevBuf<uint64_t> regions;  // local bucket regions (pay layout)
     DevBuf<unsigned long long> bfill;  // records per bucket
+    DevBuf<uint64_t> bbase;  // [NB + 1] bucket output bases (bucket_bases_kernel)
     uint64_t bucket_cap = 0;   // learned region capacity (records per bucket)
     uint64_t bucket_cap_used = 0;  // the capacity (region stride) the regions were written with
     DevBuf<uint64_t> kpart;    // per-block k-mer sums of the count pass
@@ -164,9 +165,12 @@ struct kb_ctx {
         uint64_t key = 0;
         uint32_t nb = 0;
         bool stale = false;
+        bool spread = false;  // some mmer has a run of buckets
         uint64_t want_max = 0;  // the largest bucket load the packing expects (records)
         uint64_t want_tot = 0;
         DevBuf<uint16_t> map;
+        DevBuf<uint16_t> run;  // [nb] spread runs (bucket_kernel's brun)
+        DevBuf<uint32_t> run_mmer;  // [nb] the mmer of a run's head
     };
     std::vector<BucketMap> bmaps;
     uint64_t* h_totals = nullptr;
@@ -263,12 +267,12 @@ extern "C" void kb_destroy(kb_ctx* c) {
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
     c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bcount.release(); c->bmmer.release();
-    c->regions.release(); c->bfill.release(); c->kpart.release(); c->rcount.release();
+    c->regions.release(); c->bfill.release(); c->bbase.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
     c->misc.release(); c->totals.release(); c->first.release(); c->e_first.release();
-    for (auto& m : c->bmaps) m.map.release();
+    for (auto& m : c->bmaps) { m.map.release(); m.run.release(); m.run_mmer.release(); }
     c->flat_list.release(); c->flat_next.release(); c->flat_l0.release(); c->flat_off.release();
     c->flat_cur.release(); c->flat_chunk.release(); c->pool_bin.release(); c->chunk_bin.release();
     c->flat_sbase.release(); c->flat_obase.release(); c->flat_n.release();
@@ -950,12 +954,41 @@ static int bmap_build(kb_ctx* c, uint32_t NB) {
     }
     std::sort(items.begin(), items.end(), [](const std::pair<uint32_t, uint32_t>& a,
                                              const std::pair<uint32_t, uint32_t>& b) { return a.first > b.first; });
+    // Spread: an mmer above twice the mean bucket load gets a run of k
+    // consecutive buckets of its own (from the front, at most 3/4 of them);
+    // its records pick one by hash and the run's regions are laid out
+    // contiguously, one bin (few mmers per rank: one workgroup ordering a whole
+    // mmer set bucket_kernel's time)
+    uint64_t tot_w = 0;
+    for (auto& it : items) tot_w += it.first;
+    const double mean = (double)tot_w / NB;
+    std::vector<uint16_t> run(NB, 0);
+    std::vector<uint32_t> run_mm(NB, 0);
+    uint32_t next = 0;
+    uint64_t spread_max_load = 0;
+    const uint32_t spread_cap = env_int("KB_BIN_SPREAD", 1) ? NB * 3 / 4 : 0;
+    std::vector<bool> placed(items.size(), false);
+    for (size_t i = 0; i < items.size() && NB <= 1024; i++) {
+        const double w = items[i].first;
+        if (w <= 2.0 * mean || next + 2 > spread_cap) break;  // (sorted: the rest are smaller)
+        uint32_t k = (uint32_t)std::min(63.0, std::ceil(w / mean));
+        k = std::min(k, spread_cap - next);
+        h[items[i].second - half] = (uint16_t)(next | (k << 10));
+        run[next] = (uint16_t)k;
+        run_mm[next] = items[i].second;
+        for (uint32_t j = 1; j < k; j++) run[next + j] = BK_RUN_CONT;
+        spread_max_load = std::max<uint64_t>(spread_max_load, (uint64_t)(w / k) + 1);
+        next += k;
+        placed[i] = true;
+    }
     // least-loaded bucket first; at most 128 mmers per bucket (bucket_kernel maps 256)
     using Slot = std::pair<uint64_t, uint32_t>;  // (load, bucket)
     std::priority_queue<Slot, std::vector<Slot>, std::greater<Slot>> pq;
     std::vector<uint32_t> nm(NB, 0);
-    for (uint32_t b = 0; b < NB; b++) pq.push({0, b});
-    for (auto& it : items) {
+    for (uint32_t b = next; b < NB; b++) pq.push({0, b});
+    for (size_t i = 0; i < items.size(); i++) {
+        if (placed[i]) continue;
+        auto& it = items[i];
         Slot sl = pq.top();
         pq.pop();
         while (nm[sl.second] >= 128 && !pq.empty()) {  // full: retire it
@@ -966,7 +999,9 @@ static int bmap_build(kb_ctx* c, uint32_t NB) {
         nm[sl.second]++;
         pq.push({sl.first + it.first, sl.second});
     }
-    uint64_t want_max = 0, want_tot = 0;
+    uint64_t want_max = spread_max_load, want_tot = 0;
+    for (size_t i = 0; i < items.size(); i++)
+        if (placed[i]) want_tot += items[i].first;
     while (!pq.empty()) {
         want_max = std::max(want_max, pq.top().first);
         want_tot += pq.top().first;
@@ -981,6 +1016,13 @@ static int bmap_build(kb_ctx* c, uint32_t NB) {
     }
     HIPCHK(m->map.ensure(half));
     HIPCHK(hipMemcpyAsync(m->map.p, h.data(), half * sizeof(uint16_t), hipMemcpyHostToDevice, c->s));
+    m->spread = next > 0;
+    if (m->spread) {
+        HIPCHK(m->run.ensure(NB));
+        HIPCHK(m->run_mmer.ensure(NB));
+        HIPCHK(hipMemcpyAsync(m->run.p, run.data(), NB * sizeof(uint16_t), hipMemcpyHostToDevice, c->s));
+        HIPCHK(hipMemcpyAsync(m->run_mmer.p, run_mm.data(), NB * sizeof(uint32_t), hipMemcpyHostToDevice, c->s));
+    }
     HIPCHK(hipStreamSynchronize(c->s));  // h is a local
     m->stale = false;
     m->want_max = want_max;
@@ -1195,7 +1237,13 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         ba.w2 = KW == 2 ? c->srec.p + 3 * R : nullptr;
         ba.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
         ba.spw = 2 * KW;
-        ba.rec_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 11);
+        HIPCHK(c->bbase.ensure(NB + 1));
+        ba.bbase = c->bbase.p;
+        {
+            kb_ctx::BucketMap* bm = bmap_find(c, NB);  // (the map the record pass used)
+            ba.brun = bm && bm->spread ? bm->run.p : nullptr;
+            ba.brun_mmer = bm && bm->spread ? bm->run_mmer.p : nullptr;
+        }
         ba.bin_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 2);
         ba.bstart = c->starts.p;
         ba.bcount = c->bcount.p;

@@ -152,8 +152,8 @@ DEV void put_record(const SkScanArgs& A, uint64_t* o, uint32_t ord, uint64_t lo,
 
 // destination region of a super-k-mer: its owner rank (routing) or its local
 // bucket (the balanced map when the host has one, else the hash)
-DEV uint32_t region_of(const SkScanArgs& A, uint32_t mmer) {
-    return A.bucket_map ? (uint32_t)A.bucket_map[mmer - (1u << (2 * A.M - 1))] : dest_of(mmer, A.G, A.dest_salt);
+DEV uint32_t region_of(const SkScanArgs& A, uint32_t mmer, uint64_t rec) {
+    return A.bucket_map ? bucket_of(A.bucket_map[mmer - (1u << (2 * A.M - 1))], rec) : dest_of(mmer, A.G, A.dest_salt);
 }
 
 // Add one record to a packed 16-bit LDS destination count (two per word) and
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     } else if (rounds) {
                         break;  // stage full: resume at this record in the next round
                     } else if (route) {  // many destinations: one record, its own slot
-                        const uint32_t d = region_of(A, (uint32_t)best);
+                        const uint32_t d = region_of(A, (uint32_t)best, (r << 16) | (uint64_t)lo);
                         const uint64_t i = atomicAdd(&A.dest_ctr[d], 1ull);
                         if (i < A.region_cap)
                             put_record(A, A.regions + (d * A.region_cap + i) * (uint64_t)A.rw,
@@ -312,7 +312,8 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                 __syncthreads();
                 const bool agg = A.G <= 64;  // ranks, not local buckets: aggregate per wave
                 for (uint32_t i = tid; i < span; i += 256) {
-                    const uint32_t d = region_of(A, (uint32_t)(stg[i] >> 37));
+                    const uint64_t e = stg[i];
+                    const uint32_t d = region_of(A, (uint32_t)(e >> 37), ((r0 + ((e >> 29) & 0xFFu)) << 16) | (e & 0xFFFFu));
                     if (agg)
                         wave_dest_add(dcnt2, d);
                     else
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                 __syncthreads();
                 for (uint32_t i = tid; i < span; i += 256) {
                     const uint64_t e = stg[i];
-                    const uint32_t d = region_of(A, (uint32_t)(e >> 37));
+                    const uint32_t d = region_of(A, (uint32_t)(e >> 37), ((r0 + ((e >> 29) & 0xFFu)) << 16) | (e & 0xFFFFu));
                     const uint64_t slot =
                         (uint64_t)dbase[d] +
                         (agg ? wave_dest_add(dcnt2, d)
@@ -2242,7 +2243,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     uint64_t wp = 0;
     for (int w = 0; w < wid; w++) wp += red[w];
     uint32_t run = (uint32_t)(wp + inc - mine);
-    if (tid == 0) s_base = cnt ? atomicAdd(A.rec_ctr, (unsigned long long)cnt) : 0ull;
+    if (tid == 0) s_base = A.bbase[bk];  // exclusive prefix of the fills: a spread run is contiguous
 #pragma unroll
     for (uint32_t k = 0; k < PER; k++) {
         const uint32_t c = loc[k];
@@ -2250,8 +2251,22 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
         run += c;
     }
     __syncthreads();
-    // count non-empty slots, reserve bin descriptors
-    const bool has = tid < BK_SLOTS && keys[tid] != 0;
+    // count non-empty slots, reserve bin descriptors.  A spread mmer's run of
+    // buckets (that mmer only) gets one descriptor, from its first bucket --
+    // which may itself have drawn no record
+    const uint16_t brun = A.brun ? A.brun[bk] : (uint16_t)0;
+    if (brun != 0 && brun != BK_RUN_CONT && tid == 0) {
+        const uint64_t n = A.bbase[bk + brun] - A.bbase[bk];
+        if (n) {
+            const unsigned long long bi = atomicAdd(A.bin_ctr, 1ull);
+            if (bi < A.max_bins) {
+                A.bstart[bi] = (uint32_t)A.bbase[bk];
+                A.bcount[bi] = (uint32_t)n;
+                A.bmmer[bi] = A.brun_mmer[bk];
+            }
+        }
+    }
+    const bool has = brun == 0 && tid < BK_SLOTS && keys[tid] != 0;
     if (has) atomicAdd(&s_nb, 1u);
     __syncthreads();
     if (tid == 0) s_bin = s_nb ? atomicAdd(A.bin_ctr, (unsigned long long)s_nb) : 0ull;
@@ -2304,8 +2319,28 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     }
 }
 
+// exclusive prefix of the bucket fills (clamped to the capacity) -> bbase[NB + 1]
+__global__ __launch_bounds__(1024) void bucket_bases_kernel(const unsigned long long* __restrict__ bfill, uint64_t cap,
+                                                          uint32_t NB, uint64_t* __restrict__ bbase) {
+    __shared__ uint64_t red[16];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t v = threadIdx.x < NB ? min<uint64_t>(bfill[threadIdx.x], cap) : 0ull;
+    const uint64_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) red[wid] = inc;
+    __syncthreads();
+    uint64_t wp = 0, tot = 0;
+    for (int w = 0; w < 16; w++) {
+        if (w < wid) wp += red[w];
+        tot += red[w];
+    }
+    if (threadIdx.x < NB) bbase[threadIdx.x] = wp + inc - v;
+    if (threadIdx.x == 0) bbase[NB] = tot;
+}
+
 hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s) {
     if (!NB) return hipSuccess;
+    if (NB > 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bucket_bases_kernel, dim3(1), dim3(1024), 0, s, a.bfill, a.cap, NB, a.bbase);
     if (a.spw == 2)
         hipLaunchKernelGGL(bucket_kernel<2>, dim3(NB), dim3(BK_THREADS), 0, s, a);
     else if (a.spw == 4)
@@ -2353,7 +2388,8 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
             neg |= (int32_t)id < 0;
             kmers += n;
             pay0[j] = (uint64_t)id | (n << 32) | (so << 38) | ((uint64_t)rev << 44) | (lo << 45);
-            dst[j] = bucket_map ? (uint32_t)bucket_map[canon - halfM] : dest_of(canon, NB, BUCKET_SALT);
+            dst[j] = bucket_map ? bucket_of(bucket_map[canon - halfM], ((uint64_t)id << 16) | lo)
+                                : dest_of(canon, NB, BUCKET_SALT);
             atomicAdd(&cnt[dst[j]], 1u);
         }
         __syncthreads();

@@ -127,7 +127,9 @@ struct BucketArgs {
     uint64_t* w2;              // K > 31 (spw = 4): span bases 64..127
     uint64_t* w3;
     int spw;                   // span words per record: 2 (K <= 31) or 4 (K <= 63)
-    unsigned long long* rec_ctr;   // output allocation (zeroed)
+    uint64_t* bbase;           // [NB + 1] output base of each bucket (bucket_bases_kernel)
+    const uint16_t* brun;      // [NB] or null: spread runs (BK_RUN_CONT, or the run length at its head)
+    const uint32_t* brun_mmer; // [NB] the canonical mmer of a run's head bucket
     unsigned long long* bin_ctr;   // bins (zeroed; = totals[2])
     uint32_t* bstart;          // [max_bins] first record of bin
     uint32_t* bcount;          // [max_bins] records of bin
@@ -135,6 +137,17 @@ struct BucketArgs {
     uint64_t max_bins;
     uint32_t* status;          // ST_BUCKET_FULL: a bucket holds too many mmers
 };
+
+constexpr uint16_t BK_RUN_CONT = 0xFFFF;  // brun: a spread mmer's bucket after the first
+
+// Bucket map entry (u16 per canonical mmer): the bucket, or for a large mmer
+// spread over a run of k >= 2 consecutive buckets (each holding only it),
+// first | k << 10; the record picks one by a hash of (read, first k-mer).
+__device__ __forceinline__ uint32_t bucket_of(uint16_t m, uint64_t rec) {
+    const uint32_t k = m >> 10, first = m & 1023u;
+    if (k < 2) return first;
+    return first + (uint32_t)(((rec * 0x9E3779B97F4A7C15ull) >> 32) % k);
+}
 
 constexpr uint32_t KB_FLAT_MAX = 16384;  // partitions of one heavy bin's flat lists (kbin_bins.hip FLAT_MAX)
 

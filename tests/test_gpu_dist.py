@@ -115,6 +115,46 @@ def test_route_scatter(K, M, G, engine):
     assert union == ora
 
 
+@pytest.mark.parametrize("spread", ["1", "0"])
+def test_receiver_learned_map(spread, engine, monkeypatch):
+    """a receiver reused over passes learns its bucket map from its own bins
+    (few mmers per shard: large ones spread over runs of buckets) and converts
+    received records by it -- every pass equals the oracle's share"""
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    monkeypatch.setenv("KB_BIN_BALANCE_MIN", "0")
+    monkeypatch.setenv("KB_BIN_SPREAD", spread)
+    K, M, G = 31, 7, 4
+    reads = _reads()
+    bases, lens = kbin.pack_reads(reads)
+    ids = np.arange(len(reads), dtype=np.int32)
+    rw = skmer_ref.rec_words(K, M)
+    with kbin.Engine(K, M, cutoff=1, max_read_len=300) as eng:
+        eng.submit(bases=bases, lens=lens, ids=ids)
+        small = torch.zeros(G * 8 * rw, dtype=torch.int64, device="cuda")
+        ok, need = eng.route_scatter(G, small.data_ptr(), 8)
+        cap = int(need.max())
+        regions = torch.zeros(G * cap * rw, dtype=torch.int64, device="cuda")
+        ok, counts = eng.route_scatter(G, regions.data_ptr(), cap)
+        assert ok
+        torch.cuda.synchronize()
+    ora = skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, True, ids=ids))
+    union = {}
+    for d in range(G):
+        with kbin.Engine(K, M, cutoff=1, max_read_len=300) as shard:
+            first = None
+            for _ in range(3):  # the first pass learns the map, the next ones use it
+                shard.reset()
+                shard.submit_superkmers_device(regions[d * cap * rw:].data_ptr(), int(counts[d]))
+                shard.finalize(prune=True)
+                part = _result_dict(shard.export())
+                if first is None:
+                    first = part
+                assert part == first
+        union.update(part)
+    assert union == ora
+
+
 @pytest.mark.parametrize("P", [2, 5])
 def test_partitioned_routing(P, engine):
     """kb_set_partition on the sender: each pass routes (ordered plan/pack on

@@ -229,14 +229,17 @@ def test_partitioned_passes(P, radix, long_reads, K, M, engine, monkeypatch):
     assert tuple(dig) == kbin.result_digest(ora)  # digests add over partitions
 
 
-@pytest.mark.parametrize("K,M", [(21, 5), (63, 7)])
-def test_balanced_buckets(K, M, engine, monkeypatch):
+@pytest.mark.parametrize("K,M,spread", [(21, 5, "1"), (63, 7, "1"), (21, 5, "0")])
+def test_balanced_buckets(K, M, spread, engine, monkeypatch):
     """after a pass the host packs the mmers into local buckets by their
-    record counts (largest first, least-loaded bucket); later passes route
-    records by that map, per partition key -- every pass equals the oracle"""
+    record counts (largest first, least-loaded bucket; an mmer above twice the
+    mean load gets a run of buckets of its own, laid out as one bin); later
+    passes route records by that map, per partition key -- every pass equals
+    the oracle"""
     if engine != "binned":
         pytest.skip("binned engine only")
     monkeypatch.setenv("KB_BIN_BALANCE_MIN", "0")
+    monkeypatch.setenv("KB_BIN_SPREAD", spread)
     rng = np.random.default_rng(K)
     genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20000)
     reads = []
