@@ -1388,6 +1388,9 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         la.long_q = c->long_q.p;
         la.long_n = c->misc.p + 4;
         HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : ecap, c->s));
+#ifdef KB_BIN_PROF
+        lists_prof_report(c->s);
+#endif
         REC(5);
         HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));

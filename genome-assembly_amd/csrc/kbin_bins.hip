@@ -1481,6 +1481,10 @@ void bins_prof_report(hipStream_t s) {
 }
 #endif
 
+// workgroup barrier ordering LDS accesses only (no wait for outstanding global
+// stores); the memory clobber keeps the compiler from moving memory ops across
+DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // ---------------------------------------------------------------------------
 // phase C: every list into reverse call order (binning.c:1061-1068 prepends,
 // so a list reads newest call first = descending ordinal), ordinals -> ids.
@@ -1710,7 +1714,7 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
     uint32_t* const ibuf = lds;
     uint32_t* const buf = lds;
     __shared__ uint32_t big[LIST_THREADS], mid[LIST_THREADS];
-    __shared__ uint32_t n_big, n_mid, w_lo, w_hi;
+    __shared__ uint32_t n_big, n_mid, s_long, w_lo[2], w_hi[2];
     const uint32_t tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     const uint64_t n_entries = A.totals[0];
@@ -1718,8 +1722,13 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
          e0 += (uint64_t)gridDim.x * LIST_THREADS) {
         const uint32_t ne = (uint32_t)min<uint64_t>(LIST_THREADS, n_entries - e0);
         const uint64_t ob = A.e_off[e0], span = A.e_off[e0 + ne] - ob;
-        if (tid == 0) n_big = 0;
-        __syncthreads();
+        // (barriers in the staged path order LDS only: a full __syncthreads
+        // also waits for the previous window's global stores to land)
+        if (tid == 0) {
+            n_big = 0;
+            s_long = 0;
+        }
+        lds_barrier();
         // this thread's entry; lists > 256 leave the staged windows: up to
         // WAVE_LIST_MAX to lists_bucket_kernel, longer ones to this block below
         const uint32_t n_me = tid < ne ? A.e_cnt[e0 + tid] : 0u;
@@ -1728,7 +1737,9 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
         if (tid < ne && !short_me) {
             if (n_me <= WAVE_LIST_MAX) A.long_q[atomicAdd(A.long_n, 1u)] = (uint32_t)(e0 + tid);
             else big[atomicAdd(&n_big, 1u)] = tid;
+            s_long = 1;
         }
+        lds_barrier();
         // Staged windows: the chunk's id range cut every LIST_WIN ids; a short
         // list belongs to the window its first id falls in, and a window stages
         // [first start, last end) of its lists (<= LIST_WIN + 256 ids) with
@@ -1737,25 +1748,26 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
         // stores.  (Ids of a long list inside the range are written back
         // unsorted; its own kernel rewrites them later on the stream.)
         // (the common case -- every list short, the chunk fits -- is one window)
-        const bool one = !__syncthreads_or(tid < ne && !short_me) && span + 8 <= LIST_SPAN;
+        const bool one = !s_long && span + 8 <= LIST_SPAN;
         const uint32_t nw = one ? 1u : (uint32_t)((span + LIST_WIN - 1) / LIST_WIN);
         const uint32_t wk = rel / LIST_WIN;
         for (uint32_t k = 0; k < nw; k++) {
+            const uint32_t wb = k & 1u;  // double-buffered: a lane may still read the last window's range
             if (tid == 0) {
-                w_lo = one ? 0u : 0xFFFFFFFFu;
-                w_hi = one ? (uint32_t)span : 0u;
+                w_lo[wb] = one ? 0u : 0xFFFFFFFFu;
+                w_hi[wb] = one ? (uint32_t)span : 0u;
                 n_mid = 0;
             }
-            __syncthreads();
+            lds_barrier();
             const bool in_w = short_me && (one || wk == k);
             if (!one) {
                 if (in_w) {
-                    atomicMin(&w_lo, rel);
-                    atomicMax(&w_hi, rel + n_me);
+                    atomicMin(&w_lo[wb], rel);
+                    atomicMax(&w_hi[wb], rel + n_me);
                 }
-                __syncthreads();
+                lds_barrier();
             }
-            const uint32_t lo_w = w_lo, hi_w = w_hi;
+            const uint32_t lo_w = w_lo[wb], hi_w = w_hi[wb];
             if (lo_w >= hi_w) continue;  // uniform: no short list starts here
             LPROF(0);
             const uint64_t base = (ob + lo_w) & ~3ull;   // staging is 16-B aligned
@@ -1776,13 +1788,13 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
                     if (g < nv) ib4[g] = make_uint4(v[q].x + 1u, v[q].y + 1u, v[q].z + 1u, v[q].w + 1u);
                 }
             }
-            __syncthreads();
+            lds_barrier();
             LPROF(1);
             if (in_w) {
                 if (n_me <= 32) sort32_inplace(ibuf + sh + (rel - lo_w), n_me);
                 else mid[atomicAdd(&n_mid, 1u)] = tid;
             }
-            __syncthreads();
+            lds_barrier();
             LPROF(2);
             const uint32_t nmid = n_mid;
             for (uint32_t q = wid; q < nmid; q += LIST_THREADS / 64) {
@@ -1793,7 +1805,7 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
                 else wave_sort_desc<4>(p, n, lane);
                 wave_sync();
             }
-            __syncthreads();
+            lds_barrier();
             LPROF(3);
             {
                 // full groups as 16-B stores, the partial first/last group per id
@@ -1814,15 +1826,20 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
                     }
                 }
             }
-            __syncthreads();
+            // the staging area is reused: every lane's LDS reads must be done (they
+            // fed its stores), but its global stores need not have landed -- a
+            // full __syncthreads() would wait for them (vmcnt), 36 % of the kernel
+            lds_barrier();
             LPROF(4);
 #ifdef KB_BIN_PROF
             if (tid == 0) lacc[5]++, lacc[6] += nmid;
 #endif
         }
-        __threadfence_block();
-        __syncthreads();
         const uint32_t nbig = n_big;  // lists > WAVE_LIST_MAX: the whole block
+        if (nbig) {  // it rewrites ids the windows wrote: let those land first
+            __threadfence_block();
+            __syncthreads();
+        }
         for (uint32_t q = 0; q < nbig; q++) {
             const uint64_t ge = e0 + big[q];
             const uint32_t n = A.e_cnt[ge];
@@ -1918,7 +1935,7 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
                 __syncthreads();
             }
         }
-        __syncthreads();
+        lds_barrier();  // (LDS only: big[], n_big and the staging area are reused)
     }
 #ifdef KB_BIN_PROF
     if (tid == 0)
