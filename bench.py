@@ -156,6 +156,8 @@ def main():
                     help="reads timed on the CPU oracle (0 = skip)")
     ap.add_argument("--ref-sample", type=int, default=120_000,
                     help="reads timed on the compiled reference (oracle/_ref; 0 = port only)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N>1: no overlap of the next unit's record exchange with this unit's binning")
     ap.add_argument("--routed", action="store_true",
                     help="N=1 through the multi-GPU path (route, all-to-all over a 1-rank group, "
                          "receive): measures the routing overhead on one GPU")
@@ -212,18 +214,40 @@ def main():
         from kbin import dist as kdist
         runner = kdist.ShardedBinner(K, M, args.cutoff, L, device=local, group=None)
         eng = runner.engine
+        pipeline = not args.no_pipeline
+        pending = []  # pipelined: the next unit, already scattered, its records in flight
+
+        def send(p):
+            return runner.send(words, lens, n, wpr, first_id=rank * n, part=p, n_parts=P)
 
         def step(digest=False):
             pass_log.clear()
             dig = [0, 0, 0, 0]
             for p in range(P):
-                runner.step(words, lens, n, wpr, first_id=rank * n, part=p, n_parts=P)
+                if pipeline:
+                    # unit (step, pass p): its records were sent with the last
+                    # unit (or now, at the start); the next unit's -- the next
+                    # pass, or the next step's first -- go out before it is binned
+                    unit = pending.pop() if pending else send(p)
+                    pending.append(send((p + 1) % P))
+                    runner.receive(unit)
+                else:
+                    runner.step(words, lens, n, wpr, first_id=rank * n, part=p, n_parts=P)
                 pass_log.append((eng.export_device(), eng.timing(), runner.last_times))
                 if digest:
                     dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
             return dig
+
+        def drain():
+            # no unit crosses into the timed region: the timed steps send their
+            # own first unit (and one last prefetch goes unused -- counted in)
+            while pending:
+                runner.wait(pending.pop())
     else:
         eng = kbin.Engine(K, M, cutoff=args.cutoff, max_read_len=L, device=local)
+
+        def drain():
+            pass
 
         def step(digest=False):
             pass_log.clear()
@@ -242,6 +266,7 @@ def main():
     eng.set_timing(True)
     for _ in range(args.warmup):
         step()
+    drain()
 
     def barrier():
         if dist is not None:
@@ -260,6 +285,7 @@ def main():
             route_t.append({k: sum(r[k] for r in rts) for k in rts[0]})
     barrier()
     elapsed = time.perf_counter() - t0
+    drain()
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64,
                           device="cuda" if backend == "nccl" else "cpu")
@@ -304,6 +330,7 @@ def main():
     digest = None
     if args.digest:  # this rank's share (ranks own disjoint mmers: shares add up)
         digest = [hex(x) for x in step(digest=True)]
+        drain()
 
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world,
@@ -316,8 +343,10 @@ def main():
                    "reads_per_gpu": n, "read_len": L, "K": K, "M": M, "cutoff": args.cutoff,
                    "genome_len": args.genome, "err_ppm": args.err_ppm,
                    **({"mmer_partitions": args.parts} if args.parts > 1 else {}),
-                   "parallelism": f"mmer-sharded x{world}" if world > 1 else
-                                  ("single GPU, routed path" if args.routed else "single GPU")},
+                   "parallelism": (f"mmer-sharded x{world}" if world > 1 else
+                                   ("single GPU, routed path" if args.routed else "single GPU"))
+                                  + (", pipelined exchange" if (world > 1 or args.routed)
+                                     and not args.no_pipeline else "")},
         "roofline": roof,
         "phases_ms": phases,
         **({"route_ms": {k: round(float(np.mean([r[k] for r in route_t])), 4) for k in route_t[0]}}

@@ -99,6 +99,45 @@ def exchange_regions(regions: torch.Tensor, counts, cap: int, rec_words: int, gr
     return recvs, rc
 
 
+def exchange_records_async(send: torch.Tensor, counts, rec_words: int, group=None):
+    """exchange_records with the record all-to-all left in flight: returns
+    ([received tensor], per-source counts, work handle or None)"""
+    dev = send.device
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        recv, rc = exchange_records(send, counts, rec_words, group)
+        return [recv], rc, None
+    cnt = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    rc = [int(x) for x in rcnt.cpu().tolist()]
+    recv = torch.empty(sum(rc) * rec_words, dtype=torch.int64, device=dev)
+    work = dist.all_to_all_single(recv, send[: int(sum(counts)) * rec_words],
+                                  output_split_sizes=[c * rec_words for c in rc],
+                                  input_split_sizes=[int(c) * rec_words for c in counts], group=group,
+                                  async_op=True)
+    return [recv], rc, work
+
+
+def exchange_regions_async(regions: torch.Tensor, counts, cap: int, rec_words: int, group=None):
+    """exchange_regions with the record all-to-all left in flight: returns
+    (received tensors, per-source counts, work handle or None).  The counts
+    exchange synchronises; the records land when work.wait() returns (the
+    gloo rehearsal completes at once)."""
+    dev = regions.device
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        recvs, rc = exchange_regions(regions, counts, cap, rec_words, group)
+        return recvs, rc, None
+    G = len(counts)
+    sends = [regions[d * cap * rec_words:(d * cap + int(counts[d])) * rec_words] for d in range(G)]
+    cnt = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    rc = [int(x) for x in rcnt.cpu().tolist()]
+    recvs = [torch.empty(c * rec_words, dtype=torch.int64, device=dev) for c in rc]
+    work = dist.all_to_all(recvs, sends, group=group, async_op=True)
+    return recvs, rc, work
+
+
 class ShardedBinner:
     """One rank's share of a mmer-sharded binning job."""
 
@@ -118,19 +157,33 @@ class ShardedBinner:
         self._regions = torch.empty(0, dtype=torch.int64, device=self.device)
         self._cap = 0
         self.scatter = True  # one-pass sender while the engine accepts it
+        # pipelined steps (send / receive): a sender context of its own and
+        # two region buffers, so one unit's records can be in flight while
+        # the previous unit is binned
+        self._engine_args = (K, M, cutoff, max_read_len, device, flags)
+        self._sender = None
+        self._pregions = [torch.empty(0, dtype=torch.int64, device=self.device) for _ in range(2)]
+        self._slot = 0
 
-    def _scatter(self, n_reads: int):
+    def _scatter(self, n_reads: int, engine=None, slot=None):
         """kb_route_scatter with a learned region capacity; None when the
-        engine cannot take this path (the caller plans and packs instead)"""
+        engine cannot take this path (the caller plans and packs instead).
+        slot: one of the pipelined region buffers instead of self._regions."""
         from . import KB_EINVAL, KbError
+        engine = engine or self.engine
         if self._cap == 0:  # ~10 records per 150-bp read, spread over the ranks
             self._cap = int(n_reads * 12 / self.world * 1.25) + 4096
         for _ in range(2):
             need = self.world * self._cap * self.rec_words
-            if self._regions.numel() < need:
-                self._regions = torch.empty(need, dtype=torch.int64, device=self.device)
+            buf = self._regions if slot is None else self._pregions[slot]
+            if buf.numel() < need:
+                buf = torch.empty(need, dtype=torch.int64, device=self.device)
+                if slot is None:
+                    self._regions = buf
+                else:
+                    self._pregions[slot] = buf
             try:
-                ok, counts = self.engine.route_scatter(self.world, self._regions.data_ptr(), self._cap)
+                ok, counts = engine.route_scatter(self.world, buf.data_ptr(), self._cap)
             except KbError as e:
                 if e.code != KB_EINVAL:
                     raise
@@ -188,3 +241,67 @@ class ShardedBinner:
         # host wall time per stage (each ends in a stream synchronisation)
         self.last_times = {k: (t[i + 1] - t[i]) * 1e3
                            for i, k in enumerate(("plan_ms", "pack_ms", "exchange_ms", "receive_ms"))}
+
+    # ---- pipelined steps: the record exchange of the next unit overlaps the
+    # binning of this one.  send() scatters a unit on the sender context and
+    # starts its all-to-all; receive() waits for it and bins on self.engine.
+    # Every rank must call them in the same order (the collectives pair up).
+    def send(self, words: torch.Tensor, lens: torch.Tensor, n_reads: int, words_per_read: int,
+             first_id: int, part: int = 0, n_parts: int = 1):
+        if self._sender is None:
+            K, M, cutoff, max_read_len, device, flags = self._engine_args
+            self._sender = Engine(K, M, cutoff=cutoff, max_read_len=max_read_len, device=device,
+                                  flags=flags)
+        eng = self._sender
+        t0 = time.perf_counter()
+        eng.reset()
+        eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n_reads, words_per_read,
+                                 first_id)
+        if n_parts > 1:
+            eng.set_partition(part, n_parts)
+        slot = self._slot
+        self._slot ^= 1  # (the other buffer may still be in flight)
+        counts = self._scatter(n_reads, engine=eng, slot=slot) if self.scatter else None
+        if counts is not None:  # one pass: records straight into destination regions
+            t1 = time.perf_counter()
+            recvs, rc, work = exchange_regions_async(self._pregions[slot], counts.tolist(), self._cap,
+                                                     self.rec_words, self.group)
+        else:  # plan / pack (table engine): destination-major, read order
+            counts = eng.route_plan(self.world)
+            words_needed = int(counts.sum()) * self.rec_words
+            if self._pregions[slot].numel() < words_needed:
+                self._pregions[slot] = torch.empty(int(words_needed * 1.25) + 1024, dtype=torch.int64,
+                                                   device=self.device)
+            eng.route_pack(self._pregions[slot].data_ptr())  # synchronises the engine stream
+            t1 = time.perf_counter()
+            recvs, rc, work = exchange_records_async(self._pregions[slot], counts.tolist(), self.rec_words,
+                                                     self.group)
+        t2 = time.perf_counter()
+        return {"recvs": recvs, "rc": rc, "work": work, "part": part, "n_parts": n_parts,
+                "counts": counts.tolist(), "times": (t1 - t0, t2 - t1)}
+
+    def wait(self, unit) -> None:
+        """the unit's records have landed (also drops a unit nobody receives)"""
+        if unit["work"] is not None:
+            unit["work"].wait()
+            unit["work"] = None
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def receive(self, unit, prune: bool = True) -> None:
+        eng = self.engine
+        t0 = time.perf_counter()
+        self.wait(unit)
+        t1 = time.perf_counter()
+        eng.reset()
+        if unit["n_parts"] > 1:
+            eng.set_partition(unit["part"], unit["n_parts"])
+        self._recv = unit["recvs"]  # referenced by the engine until the next reset
+        self.last_counts = (unit["counts"], unit["rc"])
+        for r in unit["recvs"]:
+            if r.numel():
+                eng.submit_superkmers_device(r.data_ptr(), r.numel() // self.rec_words)
+        eng.finalize(prune=prune)
+        t2 = time.perf_counter()
+        self.last_times = {"plan_ms": unit["times"][0] * 1e3, "pack_ms": 0.0,
+                           "exchange_ms": unit["times"][1] * 1e3 + (t1 - t0) * 1e3,
+                           "receive_ms": (t2 - t1) * 1e3}

@@ -37,6 +37,17 @@ def main():
     np.savez(out_dir / f"rank{rank}.npz", mmer=r.mmer, hi=r.kmer_hi, lo=r.kmer_lo, count=r.count,
              offset=r.offset, ids=r.ids, sent=np.array(sb.last_counts[0]),
              recv=np.array(sb.last_counts[1]))
+    # the pipelined path (send / receive, the next unit's exchange in flight
+    # while a unit is binned): three units, and a last prefetch nobody receives
+    unit = sb.send(words, lens, n, wpr, first_id=rank * n)
+    for _ in range(3):
+        nxt = sb.send(words, lens, n, wpr, first_id=rank * n)
+        sb.receive(unit)
+        unit = nxt
+    sb.wait(unit)
+    r = sb.engine.export()
+    np.savez(out_dir / f"rank{rank}_pipe.npz", mmer=r.mmer, hi=r.kmer_hi, lo=r.kmer_lo, count=r.count,
+             offset=r.offset, ids=r.ids)
     # also the rank's raw reads, for the single-GPU reference run
     np.save(out_dir / f"words{rank}.npy", words.cpu().numpy())
     dist.barrier()

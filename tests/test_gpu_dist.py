@@ -236,8 +236,8 @@ def test_track_first_through_routing():
 
 def test_ranks_rehearsal(tmp_path):
     """Two real ranks (torch.distributed.run, gloo rehearsal on one GPU) run
-    kbin.dist.ShardedBinner end to end; the union of what they own equals a
-    single-GPU engine over both shards' reads."""
+    kbin.dist.ShardedBinner end to end, stepwise and pipelined; the union of
+    what they own equals a single-GPU engine over both shards' reads."""
     import socket
     import subprocess
     import sys
@@ -263,6 +263,9 @@ def test_ranks_rehearsal(tmp_path):
         z = np.load(tmp_path / f"rank{r}.npz")
         res = kbin.Result(z["mmer"], z["hi"], z["lo"], z["count"], z["offset"], z["ids"], 0, 0)
         part = _result_dict(res)
+        zp = np.load(tmp_path / f"rank{r}_pipe.npz")  # pipelined send / receive: the same share
+        assert _result_dict(kbin.Result(zp["mmer"], zp["hi"], zp["lo"], zp["count"], zp["offset"],
+                                        zp["ids"], 0, 0)) == part
         assert all(kbin.dist.owner_of(mm, 2) == r for mm, _ in part)
         assert not (set(part) & set(union))
         union.update(part)
