@@ -1369,7 +1369,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.id_off = (uint32_t)(affine ? id_c : 0);
         a.max_entries = ecap - 1;
         a.max_ids = N;
-        HIPCHK(launch_bins(a, max_bins, KW, c->s));
+        HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr));
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
 #endif
@@ -1435,6 +1435,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(hipEventElapsedTime(&c->tm.runs_ms, c->ev[3], c->ev[4]));
         HIPCHK(hipEventElapsedTime(&c->tm.emit_ms, c->ev[4], c->ev[5]));
         HIPCHK(hipEventElapsedTime(&c->tm.total_ms, c->ev[0], c->ev[5]));
+        HIPCHK(hipEventElapsedTime(&c->tm.bin_kernel_ms, c->ev[6], c->ev[7]));
     }
     c->tm.table_slots = 1ull << ts_log2;
     c->tm.n_bins = (uint32_t)c->h_totals[2];

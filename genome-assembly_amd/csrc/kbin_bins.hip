@@ -2456,7 +2456,7 @@ size_t bins_lds_bytes(uint32_t ts_log2, int KW) {
 }
 
 template <int KW>
-static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_t s) {
+static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_t s, hipEvent_t* ev_bin) {
     const uint32_t TS = 1u << a.ts_log2;
     const size_t lds = bins_lds_bytes(a.ts_log2, KW);
     if (TS < (uint32_t)BIN_THREADS || lds > 160 * 1024) return hipErrorInvalidValue;  // (the prune loop)
@@ -2470,9 +2470,14 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     BinArgs a2 = a;
     a2.split_occ = a.flat_l && a.split_div ? a.n_occ / ((uint64_t)blocks * a.split_div) + 1 : 0;
     a2.big_occ = a.flat_l && a.big_div ? a.n_occ / ((uint64_t)blocks * a.big_div) + 1 : 0;
+    if (ev_bin) {
+        e = hipEventRecord(ev_bin[0], s);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS), lds, s,
                        a2);
     e = hipGetLastError();
+    if (e == hipSuccess && ev_bin) e = hipEventRecord(ev_bin[1], s);
     if (e != hipSuccess || !a.flat_l) return e;
     // the published bins: counts, offsets, flat lists -- every kernel exits at
     // once without any -- then their partitions, spread over every CU
@@ -2485,9 +2490,9 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     return hipGetLastError();
 }
 
-hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s) {
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin) {
     if (!max_bins) return hipSuccess;
-    return KW == 1 ? launch_bins_kw<1>(a, max_bins, s) : launch_bins_kw<2>(a, max_bins, s);
+    return KW == 1 ? launch_bins_kw<1>(a, max_bins, s, ev_bin) : launch_bins_kw<2>(a, max_bins, s, ev_bin);
 }
 
 __global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,

@@ -245,7 +245,8 @@ hipError_t launch_sk_kmers_total(const unsigned long long* part, uint64_t n, uns
                                  hipStream_t s);
 hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
                             hipStream_t s);
-hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s);
+// ev_bin[2]: recorded right before and right after bin_kernel (timing), or null
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin = nullptr);
 hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uint32_t* order, uint64_t max_bins,
                              hipStream_t s);
 hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s);

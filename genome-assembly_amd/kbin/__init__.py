@@ -48,8 +48,7 @@ class KbError(RuntimeError):
 class kb_params(C.Structure):
     _fields_ = [("K", C.c_int32), ("M", C.c_int32), ("cutoff", C.c_int32),
                 ("max_read_len", C.c_int32), ("device", C.c_int32), ("flags", C.c_int32),
-                ("table_slots", C.c_uint64), ("engine", C.c_uint32), ("n_bins", C.c_uint32),
-                ("n_superkmers", C.c_uint64)]
+                ("table_slots", C.c_uint64)]
 
 
 class kb_csr(C.Structure):
@@ -72,7 +71,7 @@ class kb_timing(C.Structure):
                 ("runs_ms", C.c_float), ("emit_ms", C.c_float), ("total_ms", C.c_float),
                 ("scan_insert_launches", C.c_uint32), ("sort_passes", C.c_uint32),
                 ("table_slots", C.c_uint64), ("engine", C.c_uint32), ("n_bins", C.c_uint32),
-                ("n_superkmers", C.c_uint64)]
+                ("n_superkmers", C.c_uint64), ("bin_kernel_ms", C.c_float)]
 
 
 _lib = None

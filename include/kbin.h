@@ -110,6 +110,8 @@ typedef struct {
     uint32_t engine;        /* KB_ENG_TABLE or KB_ENG_BINNED                     */
     uint32_t n_bins;        /* binned: non-empty mmer bins                       */
     uint64_t n_superkmers;  /* binned: super-k-mer records                       */
+    float bin_kernel_ms;    /* binned: bin_kernel alone (runs_ms also holds the
+                               heavy-bin kernels and bins_final)                */
 } kb_timing;
 
 /* Create a context (kb_create replaces zcreate_hash_table for the level-1
