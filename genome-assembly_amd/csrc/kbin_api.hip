@@ -144,7 +144,7 @@ struct kb_ctx {
     DevBuf<uint64_t> kstage;   // heavy bins: per-occurrence k-mer code + 1
     DevBuf<uint32_t> long_q;   // entries with 257..4096 ids (lists_long_kernel)
     DevBuf<uint32_t> border;   // bin processing order
-    DevBuf<uint32_t> bcount, bmmer;  // bin descriptors (with starts)
+    DevBuf<uint32_t> bcount, bmmer, bocc;  // bin descriptors (with starts); bocc: k-mers
     DevBuf<uint32_t> flat_list, flat_next, flat_l0, flat_off, flat_cur, flat_chunk, pool_bin, chunk_bin;  // heavy bins published for phase 1
     DevBuf<unsigned long long> flat_sbase, flat_obase, flat_n;  // flat_n[0] bins, [1] offset pool
     DevBuf<uint64_t> regions;  // local bucket regions (pay layout)
@@ -266,7 +266,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
     c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bcount.release(); c->bmmer.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
     c->regions.release(); c->bfill.release(); c->bbase.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
@@ -1210,6 +1210,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     HIPCHK(c->starts.ensure(max_bins + 1));
     HIPCHK(c->bcount.ensure(max_bins));
     HIPCHK(c->bmmer.ensure(max_bins));
+    if (bucketed) HIPCHK(c->bocc.ensure(max_bins));
     HIPCHK(c->srec.ensure(RWD * R));
     HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));  // ids by ordinal (+ radix ping-pong)
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
@@ -1248,6 +1249,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         ba.bstart = c->starts.p;
         ba.bcount = c->bcount.p;
         ba.bmmer = c->bmmer.p;
+        ba.bocc = c->bocc.p;
         ba.max_bins = max_bins;
         ba.status = c->misc.p;
         HIPCHK(launch_bucket_sort(ba, NB, c->s));
@@ -1305,6 +1307,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.bstart = c->starts.p;
         a.bcount = c->bcount.p;
         a.bmmer = c->bmmer.p;
+        a.bocc = bucketed ? c->bocc.p : nullptr;
         a.max_bins = max_bins;
         a.stage_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 10);
         a.order = c->border.p;

@@ -945,10 +945,15 @@ DEV void bin_body(const BinArgs& A) {
         // occurrences of the bin -> first partition depth
         uint64_t occ_tot = 0;
         if (PHASE == 0) {
-            uint64_t occ = 0;
-            for (uint32_t rec = lo + tid; rec < hi; rec += BIN_THREADS)
-                occ += (A.hdr[rec] >> 32) & 63u;
-            (void)block_excl_scan_u64(occ, S.red, occ_tot);
+            // the bucket ordering counted them (its length rows), else a pass
+            // over the record headers
+            occ_tot = A.bocc ? A.bocc[b] : 0u;
+            if (!occ_tot) {
+                uint64_t occ = 0;
+                for (uint32_t rec = lo + tid; rec < hi; rec += BIN_THREADS)
+                    occ += (A.hdr[rec] >> 32) & 63u;
+                (void)block_excl_scan_u64(occ, S.red, occ_tot);
+            }
             // the bin's stage range (one slot per occurrence, reused per partition)
             if (tid == 0) S.stage_base = atomicAdd(A.stage_ctr, (unsigned long long)occ_tot);
             __syncthreads();
@@ -2206,6 +2211,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     __shared__ uint64_t red[BK_THREADS / 64];
     __shared__ unsigned long long s_base, s_bin;
     __shared__ uint32_t s_nb, s_full;
+    __shared__ uint32_t socc[BK_SLOTS];  // occurrences (k-mers) per slot
     const uint32_t tid = threadIdx.x, bk = blockIdx.x;
     const uint64_t cnt = min<uint64_t>(A.bfill[bk], A.cap);
     constexpr int RWD = 1 + SPW;  // record words
@@ -2246,13 +2252,19 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     }
     // exclusive scan of the counters in (slot, row) order
     constexpr uint32_t PER = BK_SLOTS * ROWS / BK_THREADS;
+    static_assert(ROWS % PER == 0, "a thread's counters lie in one slot");
     uint32_t loc[PER];
     uint64_t mine = 0;
+    uint32_t kmers = 0;  // this thread's slot: k-mers = records x n, n = ROWS - row
 #pragma unroll
     for (uint32_t k = 0; k < PER; k++) {
         loc[k] = hist[tid * PER + k];
         mine += loc[k];
+        kmers += loc[k] * (ROWS - (tid * PER + k) % ROWS);
     }
+    if (tid < BK_SLOTS) socc[tid] = 0;
+    __syncthreads();
+    if (kmers) atomicAdd(&socc[(tid * PER) / ROWS], kmers);
     const int lane = tid & 63, wid = tid >> 6;
     const uint64_t inc = wave_incl_scan(mine, lane);
     if (lane == 63) red[wid] = inc;
@@ -2280,6 +2292,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
                 A.bstart[bi] = (uint32_t)A.bbase[bk];
                 A.bcount[bi] = (uint32_t)n;
                 A.bmmer[bi] = A.brun_mmer[bk];
+                if (A.bocc) A.bocc[bi] = 0;  // (its buckets' counts are not summed: bin_kernel counts)
             }
         }
     }
@@ -2299,6 +2312,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
             A.bstart[bi] = (uint32_t)s_base + first;
             A.bcount[bi] = last - first;
             A.bmmer[bi] = keys[tid] - 1u;
+            if (A.bocc) A.bocc[bi] = socc[tid];
         }
     }
     __syncthreads();

@@ -130,6 +130,7 @@ struct BucketArgs {
     uint64_t* bbase;           // [NB + 1] output base of each bucket (bucket_bases_kernel)
     const uint16_t* brun;      // [NB] or null: spread runs (BK_RUN_CONT, or the run length at its head)
     const uint32_t* brun_mmer; // [NB] the canonical mmer of a run's head bucket
+    uint32_t* bocc;            // [max_bins] k-mer occurrences of the bin (0: not counted), or null
     unsigned long long* bin_ctr;   // bins (zeroed; = totals[2])
     uint32_t* bstart;          // [max_bins] first record of bin
     uint32_t* bcount;          // [max_bins] records of bin
@@ -160,6 +161,7 @@ struct BinArgs {
     const uint32_t* bstart;    // [nbins] first record of bin
     const uint32_t* bcount;    // [nbins] records of bin
     const uint32_t* bmmer;     // [nbins] canonical mmer of bin
+    const uint32_t* bocc;      // [nbins] its k-mer occurrences (0 or null: count them)
     uint64_t max_bins;         // capacity of the descriptors (nbins never exceeds it)
     unsigned long long* stage_ctr;  // stage allocation (zeroed): each bin takes its occurrences
     const uint32_t* order;     // [nbins] processing order (largest bins first)
