@@ -1989,6 +1989,7 @@ __global__ __launch_bounds__(256) void lists_long_kernel(ListArgs A) {
 // (clustered ordinals) is queued for the network (lists_long_kernel).
 constexpr uint32_t LB_WAVES = 4;
 constexpr uint32_t LB_SPAN = WAVE_LIST_MAX;  // ids per wave in LDS
+constexpr uint32_t LB_ILP = 8;               // loads in flight per lane
 
 // n <= 64 values in registers, sorted descending (0 pads last)
 template <int W>
@@ -2012,21 +2013,22 @@ DEV void lane_sort_desc(uint32_t (&v)[W]) {
     }
 }
 
+
+// one lane's bucket buf[off, off + c) sorted ascending in place (values >= 1)
 template <int W>
-DEV void lane_bucket_out(const uint32_t* buf, uint32_t off, uint32_t c, int32_t* dst, uint32_t out,
-                         const int32_t* read_ids, uint32_t id_off) {
+DEV void lane_bucket_sort_asc(uint32_t* buf, uint32_t off, uint32_t c) {
     uint32_t v[W];
 #pragma unroll
     for (int j = 0; j < W; j++) v[j] = (uint32_t)j < c ? buf[off + j] : 0u;
-    lane_sort_desc<W>(v);
+    lane_sort_desc<W>(v);  // the c values first, descending
 #pragma unroll
     for (int j = 0; j < W; j++)
-        if ((uint32_t)j < c) dst[out + j] = id_of(v[j] - 1u, read_ids, id_off);
+        if ((uint32_t)j < c) buf[off + c - 1u - (uint32_t)j] = v[j];
 }
 
 __global__ __launch_bounds__(LB_WAVES * 64) void lists_bucket_kernel(ListArgs A) {
     __shared__ uint32_t sbuf[LB_WAVES][LB_SPAN];
-    __shared__ uint32_t scnt[LB_WAVES][128], scur[LB_WAVES][128];
+    __shared__ uint32_t scnt[LB_WAVES][256], scur[LB_WAVES][256];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t* buf = sbuf[wid];
     uint32_t* cnt = scnt[wid];
@@ -2038,55 +2040,95 @@ __global__ __launch_bounds__(LB_WAVES * 64) void lists_bucket_kernel(ListArgs A)
         const uint64_t o = A.e_off[e];
         const uint32_t* src = A.ids_ord + o;
         int32_t* dst = A.ids_out + o;
+        // three passes over the list, each with LB_ILP loads in flight per lane
+        // (one dependent load per iteration left every wave waiting on HBM)
         uint32_t mn = 0xFFFFFFFFu, mx = 0;
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t x = src[i];
-            mn = min(mn, x);
-            mx = max(mx, x);
+        for (uint32_t i0 = lane; i0 < n; i0 += 64u * LB_ILP) {
+            uint32_t x[LB_ILP];
+#pragma unroll
+            for (uint32_t k = 0; k < LB_ILP; k++) x[k] = i0 + 64u * k < n ? src[i0 + 64u * k] : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < LB_ILP; k++)
+                if (i0 + 64u * k < n) {
+                    mn = min(mn, x[k]);
+                    mx = max(mx, x[k]);
+                }
         }
         mx = wave_max_u32(mx);
         mn = ~wave_max_u32(~mn);
-        const uint32_t nb = n <= 2048 ? 64u : 128u;
+        // about 16 ids per bucket: each lane then sorts its buckets with
+        // 16- or 32-input networks (64 buckets for 4096 ids took 64-input ones)
+        const uint32_t nb = n <= 1024 ? 64u : n <= 2048 ? 128u : 256u;
         // order-preserving bucket of an ordinal: floor((x - mn) * nb / range)
         const float scale = (float)nb / ((float)(mx - mn) + 1.0f);
         for (uint32_t b = lane; b < nb; b += 64) cnt[b] = 0;
         wave_sync();
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t b = min(nb - 1u, (uint32_t)((float)(src[i] - mn) * scale));
-            atomicAdd(&cnt[b], 1u);
+        for (uint32_t i0 = lane; i0 < n; i0 += 64u * LB_ILP) {
+            uint32_t x[LB_ILP];
+#pragma unroll
+            for (uint32_t k = 0; k < LB_ILP; k++) x[k] = i0 + 64u * k < n ? src[i0 + 64u * k] : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < LB_ILP; k++)
+                if (i0 + 64u * k < n) atomicAdd(&cnt[min(nb - 1u, (uint32_t)((float)(x[k] - mn) * scale))], 1u);
         }
         wave_sync();
-        // lane l owns buckets ba, ba + 1 (nb = 128: ba = 2 l) or ba = l (nb = 64):
-        // adjacent buckets, so one wave scan of the per-lane totals places both
-        const uint32_t ba = nb > 64 ? 2u * (uint32_t)lane : (uint32_t)lane;
-        const uint32_t c0 = cnt[ba], c1 = nb > 64 ? cnt[ba + 1] : 0u;
-        const uint32_t big = wave_max_u32(max(c0, c1));
+        // lane l owns the npl = nb / 64 adjacent buckets from ba = npl l, so one
+        // wave scan of the per-lane totals places them all
+        const uint32_t npl = nb / 64u, ba = npl * (uint32_t)lane;
+        uint32_t c[4], tot = 0, big = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            c[k] = k < npl ? cnt[ba + k] : 0u;
+            tot += c[k];
+            big = max(big, c[k]);
+        }
+        big = wave_max_u32(big);
         if (big > 64) {  // clustered ordinals: the sorting network takes the list
             if (lane == 0) A.long_q[A.long_cap + atomicAdd(A.long_n + 1, 1u)] = e;
             continue;
         }
-        const uint32_t base = wave_incl_scan(c0 + c1, lane) - (c0 + c1);  // ascending offsets
+        const uint32_t base = wave_incl_scan(tot, lane) - tot;  // ascending offsets
         wave_sync();
-        cur[ba] = base;
-        if (nb > 64) cur[ba + 1] = base + c0;
-        wave_sync();
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t x = src[i];
-            const uint32_t b = min(nb - 1u, (uint32_t)((float)(x - mn) * scale));
-            buf[atomicAdd(&cur[b], 1u)] = x + 1u;
+        {
+            uint32_t run = base;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++)
+                if (k < npl) {
+                    cur[ba + k] = run;
+                    run += c[k];
+                }
         }
         wave_sync();
-        // descending list: bucket at ascending offset a with c ids starts at n - a - c
-        if (big <= 16) {
-            lane_bucket_out<16>(buf, base, c0, dst, n - base - c0, A.read_ids, A.id_off);
-            if (nb > 64) lane_bucket_out<16>(buf, base + c0, c1, dst, n - base - c0 - c1, A.read_ids, A.id_off);
-        } else if (big <= 32) {
-            lane_bucket_out<32>(buf, base, c0, dst, n - base - c0, A.read_ids, A.id_off);
-            if (nb > 64) lane_bucket_out<32>(buf, base + c0, c1, dst, n - base - c0 - c1, A.read_ids, A.id_off);
-        } else {
-            lane_bucket_out<64>(buf, base, c0, dst, n - base - c0, A.read_ids, A.id_off);
-            if (nb > 64) lane_bucket_out<64>(buf, base + c0, c1, dst, n - base - c0 - c1, A.read_ids, A.id_off);
+        for (uint32_t i0 = lane; i0 < n; i0 += 64u * LB_ILP) {
+            uint32_t x[LB_ILP];
+#pragma unroll
+            for (uint32_t k = 0; k < LB_ILP; k++) x[k] = i0 + 64u * k < n ? src[i0 + 64u * k] : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < LB_ILP; k++)
+                if (i0 + 64u * k < n) {
+                    const uint32_t b = min(nb - 1u, (uint32_t)((float)(x[k] - mn) * scale));
+                    buf[atomicAdd(&cur[b], 1u)] = x[k] + 1u;
+                }
         }
+        wave_sync();
+        // each lane sorts its buckets in place (ascending), so buf holds the
+        // whole list ascending; the wave then writes it reversed -- descending,
+        // binning.c:1065-1068 -- with coalesced stores (lanes writing their own
+        // buckets straight to HBM touched 64 lines per store instruction)
+        uint32_t a0 = base;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            if (k >= npl) break;  // (wave-uniform)
+            if (big <= 16)
+                lane_bucket_sort_asc<16>(buf, a0, c[k]);
+            else if (big <= 32)
+                lane_bucket_sort_asc<32>(buf, a0, c[k]);
+            else
+                lane_bucket_sort_asc<64>(buf, a0, c[k]);
+            a0 += c[k];
+        }
+        wave_sync();
+        for (uint32_t j = lane; j < n; j += 64) dst[j] = id_of(buf[n - 1u - j] - 1u, A.read_ids, A.id_off);
         wave_sync();
     }
 }
