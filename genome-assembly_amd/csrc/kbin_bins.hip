@@ -1989,7 +1989,7 @@ __global__ __launch_bounds__(256) void lists_long_kernel(ListArgs A) {
 // (clustered ordinals) is queued for the network (lists_long_kernel).
 constexpr uint32_t LB_WAVES = 4;
 constexpr uint32_t LB_SPAN = WAVE_LIST_MAX;  // ids per wave in LDS
-constexpr uint32_t LB_ILP = 8;               // loads in flight per lane
+constexpr uint32_t LB_ILP = 16;              // loads in flight per lane
 
 // n <= 64 values in registers, sorted descending (0 pads last)
 template <int W>
