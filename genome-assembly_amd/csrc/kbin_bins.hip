@@ -1098,13 +1098,35 @@ DEV void bin_body(const BinArgs& A) {
             } else {
                 // the partition's flat list, two entries per lane; a deeper split
                 // (Lv > l0) filters it, entries keep their index (sweep 2 filters too)
+                // (the next chunk's entries are loaded before this chunk's
+                // inserts: the lists stream from HBM)
                 const uint32_t nf = fb - fa, pmask = (1u << Lv) - 1u;
-                for (uint32_t c0 = (uint32_t)(tid >> 6) * 128u; c0 < nf; c0 += BIN_THREADS * 2) {
-                    const uint32_t lane = tid & 63u, i0 = c0 + lane, i1 = c0 + 64u + lane;
+                const uint32_t lane = tid & 63u;
+                uint32_t c0 = (uint32_t)(tid >> 6) * 128u;
+                TKey<KW> n0{}, n1{};
+                uint64_t ne0 = 0, ne1 = 0;
+                if (c0 + lane < nf) {
+                    n0 = kst_load<KW>(kst, fa + c0 + lane);
+                    ne0 = stage[c0 + lane];
+                }
+                if (c0 + 64u + lane < nf) {
+                    n1 = kst_load<KW>(kst, fa + c0 + 64u + lane);
+                    ne1 = stage[c0 + 64u + lane];
+                }
+                for (; c0 < nf; c0 += BIN_THREADS * 2) {
+                    const uint32_t i0 = c0 + lane, i1 = c0 + 64u + lane;
                     bool v0 = i0 < nf, v1 = i1 < nf;
-                    const TKey<KW> k0 = v0 ? kst_load<KW>(kst, fa + i0) : TKey<KW>{};
-                    const TKey<KW> k1 = v1 ? kst_load<KW>(kst, fa + i1) : TKey<KW>{};
-                    const uint64_t e0 = v0 ? stage[i0] & M48 : 0ull, e1 = v1 ? stage[i1] & M48 : 0ull;
+                    const TKey<KW> k0 = n0, k1 = n1;
+                    const uint64_t e0 = ne0 & M48, e1 = ne1 & M48;
+                    const uint32_t c1 = c0 + BIN_THREADS * 2;
+                    if (c1 + lane < nf) {
+                        n0 = kst_load<KW>(kst, fa + c1 + lane);
+                        ne0 = stage[c1 + lane];
+                    }
+                    if (c1 + 64u + lane < nf) {
+                        n1 = kst_load<KW>(kst, fa + c1 + 64u + lane);
+                        ne1 = stage[c1 + 64u + lane];
+                    }
                     if (Lv > l0) {
                         v0 = v0 && (k0.part() & pmask) == P;
                         v1 = v1 && (k1.part() & pmask) == P;
