@@ -830,11 +830,23 @@ template <int KW, int NT = BIN_THREADS, typename G>
 DEV void expand_bin(const BinArgs& A, uint32_t lo, uint32_t hi, G&& g) {
     const int K = A.K;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint32_t base = lo + wid * 64; base < hi; base += NT) {
-        const uint32_t r = base + lane;
-        const uint64_t hd = r < hi ? A.hdr[r] : 0ull;
-        Span<KW> sp{};
-        if (r < hi) sp.load(A, r);
+    // (the next record's loads are issued before this one is expanded)
+    uint32_t base = lo + wid * 64;
+    uint64_t nhd = 0;
+    Span<KW> nsp{};
+    if (base + lane < hi) {
+        nhd = A.hdr[base + lane];
+        nsp.load(A, base + lane);
+    }
+    for (; base < hi; base += NT) {
+        const uint64_t hd = nhd;
+        Span<KW> sp = nsp;
+        const uint32_t nxt = base + NT + lane;
+        nhd = 0;
+        if (nxt < hi) {
+            nhd = A.hdr[nxt];
+            nsp.load(A, nxt);
+        }
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
         const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);
@@ -1454,11 +1466,22 @@ __global__ __launch_bounds__(FB_THREADS) void flat_scatter_kernel(BinArgs A) {
             }
             const uint64_t lt = (1ull << lane) - 1ull;
             const int K = A.K;
-            for (uint32_t base = lo + (uint32_t)wid * 64u; base < hi; base += FB_THREADS) {
-                const uint32_t r = base + (uint32_t)lane;
-                const uint64_t hd = r < hi ? A.hdr[r] : 0ull;
-                Span<KW> sp{};
-                if (r < hi) sp.load(A, r);
+            uint32_t base = lo + (uint32_t)wid * 64u;
+            uint64_t nhd = 0;
+            Span<KW> nsp{};
+            if (base + (uint32_t)lane < hi) {
+                nhd = A.hdr[base + lane];
+                nsp.load(A, base + lane);
+            }
+            for (; base < hi; base += FB_THREADS) {  // (next record's loads first)
+                const uint64_t hd = nhd;
+                Span<KW> sp = nsp;
+                const uint32_t nxt = base + FB_THREADS + (uint32_t)lane;
+                nhd = 0;
+                if (nxt < hi) {
+                    nhd = A.hdr[nxt];
+                    nsp.load(A, nxt);
+                }
                 const int n = (int)((hd >> 32) & 63u);
                 const uint32_t ord = (uint32_t)hd;
                 const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);
