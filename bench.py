@@ -156,6 +156,9 @@ def main():
                     help="reads timed on the CPU oracle (0 = skip)")
     ap.add_argument("--ref-sample", type=int, default=120_000,
                     help="reads timed on the compiled reference (oracle/_ref; 0 = port only)")
+    ap.add_argument("--no-scan-once", action="store_true",
+                    help="P>1 on one GPU: every pass rescans the reads (kb_set_partition) instead of "
+                         "one kb_split_passes scan into the passes' regions")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: no overlap of the next unit's record exchange with this unit's binning")
     ap.add_argument("--routed", action="store_true",
@@ -245,18 +248,53 @@ def main():
                 runner.wait(pending.pop())
     else:
         eng = kbin.Engine(K, M, cutoff=args.cutoff, max_read_len=L, device=local)
+        # P > 1: one super-k-mer pass over the reads (kb_split_passes) fills the
+        # passes' regions; each pass then bins its region (no rescans)
+        # (two-word k-mers keep the rescans: C5's regions beside its per-pass
+        # buffers exceed the HBM)
+        # (~10 super-k-mers per 150-bp read; the partition hash splits them
+        # evenly, and a short region is retried bigger).  Gated on the HBM: the
+        # regions sit beside the pass's own buffers
+        split = {"cap": int(n * (L / 15.0) / P * 1.1) + 4096, "buf": None, "counts": None}
+        split_bytes = P * split["cap"] * (1 + 2 * ((K + 31) // 32)) * 8
+        scan_once = (P > 1 and K <= 31 and not args.no_scan_once
+                     and split_bytes < 0.1 * torch.cuda.get_device_properties(local).total_memory)
+        sender = kbin.Engine(K, M, cutoff=args.cutoff, max_read_len=L, device=local) if scan_once else None
+        rw = eng.record_words()
 
         def drain():
             pass
 
+        def scan():
+            sender.reset()
+            sender.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, first_id=0)
+            for _ in range(3):
+                need = P * split["cap"] * rw
+                if split["buf"] is None or split["buf"].numel() < need:
+                    split["buf"] = None  # (free the old one first)
+                    split["buf"] = torch.empty(need, dtype=torch.int64, device="cuda")
+                ok, counts = sender.split_passes(P, split["buf"].data_ptr(), split["cap"])
+                if ok:
+                    split["counts"] = [int(c) for c in counts]
+                    return
+                split["cap"] = int(int(counts.max()) * 1.1) + 1024
+            raise RuntimeError("kb_split_passes: region capacity not converging")
+
         def step(digest=False):
             pass_log.clear()
             dig = [0, 0, 0, 0]
+            if scan_once:
+                scan()
             for p in range(P):
                 eng.reset()
-                eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, first_id=0)
-                if P > 1:
+                if scan_once:
                     eng.set_partition(p, P)
+                    eng.submit_superkmers_device(split["buf"][p * split["cap"] * rw:].data_ptr(),
+                                                 split["counts"][p])
+                else:
+                    eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, first_id=0)
+                    if P > 1:
+                        eng.set_partition(p, P)
                 eng.finalize(prune=True)
                 pass_log.append((eng.export_device(), eng.timing(), None))
                 if digest:

@@ -649,10 +649,27 @@ extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
     return KB_OK;
 }
 
+// kb_route_scatter (destinations = owner ranks) and kb_split_passes
+// (destinations = kb_set_partition passes): one super-k-mer pass into
+// per-destination regions, the destination a hash of the canonical mmer
+static int scatter_regions(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions, uint64_t region_cap,
+                           uint64_t* h_counts, uint64_t salt, bool by_pass);
+
 extern "C" int kb_route_scatter(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions, uint64_t region_cap,
                                 uint64_t* h_counts) {
+    return scatter_regions(c, n_dest, d_regions, region_cap, h_counts, 0x5851F42D4C957F2Dull, false);
+}
+
+extern "C" int kb_split_passes(kb_ctx* c, uint32_t n_parts, uint64_t* d_regions, uint64_t region_cap,
+                               uint64_t* h_counts) {
+    return scatter_regions(c, n_parts, d_regions, region_cap, h_counts, 0x9E3779B97F4A7C15ull, true);
+}
+
+static int scatter_regions(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions, uint64_t region_cap,
+                           uint64_t* h_counts, uint64_t salt, bool by_pass) {
     if (!c || !h_counts) return fail(KB_EINVAL, "null argument");
     if (n_dest < 1 || n_dest > 64) return fail(KB_EINVAL, "n_dest=%u outside [1,64]", n_dest);
+    if (by_pass && c->part_n > 1) return fail(KB_ESTATE, "kb_split_passes on a partitioned context");
     if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
     if (!binned_applies(c)) return fail(KB_EINVAL, "kb_route_scatter needs the binned engine (use plan/pack)");
     for (auto& b : c->batches)
@@ -683,10 +700,11 @@ extern "C" int kb_route_scatter(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions,
         a.regions = d_regions;
         a.region_cap = region_cap;
         a.dest_ctr = c->rcount.p;
+        (void)by_pass;
         a.read_ids = affine ? nullptr : c->read_ids.p;
         a.id_off = (uint32_t)(affine ? id_c : 0);
         a.G = n_dest;
-        a.dest_salt = 0x5851F42D4C957F2Dull;  // owner_of (kbin_kernels.hip)
+        a.dest_salt = salt;  // owner_of (kbin_kernels.hip), or in_part's PART_SALT (kbin_bins.hip)
         a.rw = rec_words(c);
         HIPCHK(launch_sk(a, true, c->s));
     }

@@ -35,7 +35,7 @@ EXPORTED = [
     "kb_finalize", "kb_export", "kb_export_device", "kb_reset", "kb_set_timing",
     "kb_get_timing", "kb_generate_reads_device", "kb_unpack_reads_to_host", "kb_stream",
     "kb_last_error", "kb_abi_version", "kb_record_words", "kb_route_plan", "kb_route_pack",
-    "kb_submit_superkmers_device", "kb_route_scatter", "kb_set_partition", "kb_digest",
+    "kb_submit_superkmers_device", "kb_route_scatter", "kb_split_passes", "kb_set_partition", "kb_digest",
 ]
 
 
@@ -114,6 +114,7 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_route_pack.argtypes = [vp, vp]
     lib.kb_submit_superkmers_device.argtypes = [vp, vp, u64]
     lib.kb_route_scatter.argtypes = [vp, C.c_uint32, vp, u64, C.POINTER(C.c_uint64)]
+    lib.kb_split_passes.argtypes = [vp, C.c_uint32, vp, u64, C.POINTER(C.c_uint64)]
     lib.kb_set_partition.argtypes = [vp, u32, u32]
     lib.kb_digest.argtypes = [vp, C.POINTER(u64)]
     lib.kb_stream.argtypes = [vp]
@@ -320,6 +321,17 @@ class Engine:
         cnt = np.zeros(n_dest, dtype=np.uint64)
         rc = self.lib.kb_route_scatter(self._h, n_dest, C.c_void_p(regions_ptr), int(region_cap),
                                        cnt.ctypes.data_as(C.POINTER(C.c_uint64)))
+        if rc == KB_EOVERFLOW:
+            return False, cnt
+        _check(self.lib, rc)
+        return True, cnt
+
+    def split_passes(self, n_parts: int, regions_ptr: int, region_cap: int):
+        """kb_split_passes: one super-k-mer pass into the regions of the
+        n_parts kb_set_partition passes; (ok, counts) as route_scatter"""
+        cnt = np.zeros(n_parts, dtype=np.uint64)
+        rc = self.lib.kb_split_passes(self._h, n_parts, C.c_void_p(regions_ptr), int(region_cap),
+                                      cnt.ctypes.data_as(C.POINTER(C.c_uint64)))
         if rc == KB_EOVERFLOW:
             return False, cnt
         _check(self.lib, rc)

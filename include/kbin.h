@@ -210,6 +210,16 @@ int kb_submit_superkmers_device(kb_ctx *ctx, const uint64_t *d_records, uint64_t
 int kb_route_scatter(kb_ctx *ctx, uint32_t n_dest, uint64_t *d_regions,
                      uint64_t region_cap, uint64_t *h_counts);
 
+/* kb_route_scatter with the destinations being the n_parts passes of
+ * kb_set_partition instead of ranks: ONE super-k-mer pass over the reads
+ * serves every partitioned pass.  Region p goes to a context that calls
+ * kb_set_partition(p, n_parts), kb_submit_superkmers_device(region p) and
+ * kb_finalize; the passes' union is the single-pass result (read ids are the
+ * list order key, as for routed records).  Replaces the reference's single
+ * process_read loop (binning.c:1150-1166) at scales one finalize cannot hold. */
+int kb_split_passes(kb_ctx *ctx, uint32_t n_parts, uint64_t *d_regions,
+                    uint64_t region_cap, uint64_t *h_counts);
+
 /* ---- partitioned passes (capacity) -------------
  * One context holds at most 2^32 - 1 k-mer occurrences per finalize.  Larger
  * inputs are binned in passes over disjoint slices of the canonical-mmer

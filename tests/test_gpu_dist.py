@@ -155,6 +155,47 @@ def test_receiver_learned_map(spread, engine, monkeypatch):
     assert union == ora
 
 
+@pytest.mark.parametrize("K,M,P", [(31, 7, 3), (63, 7, 4), (21, 5, 2)])
+def test_split_passes(K, M, P, engine):
+    """kb_split_passes: ONE super-k-mer pass into the regions of P
+    kb_set_partition passes; a context set to pass p bins region p -- equal to
+    the direct partitioned pass, and the union equals the oracle"""
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    reads = _reads()
+    bases, lens = kbin.pack_reads(reads)
+    ids = np.arange(len(reads), dtype=np.int32)
+    rw = skmer_ref.rec_words(K, M)
+    with kbin.Engine(K, M, cutoff=1, max_read_len=300) as eng:
+        eng.submit(bases=bases, lens=lens, ids=ids)
+        small = torch.zeros(P * 8 * rw, dtype=torch.int64, device="cuda")
+        ok, need = eng.split_passes(P, small.data_ptr(), 8)
+        assert not ok
+        cap = int(need.max())
+        regions = torch.zeros(P * cap * rw, dtype=torch.int64, device="cuda")
+        ok, counts = eng.split_passes(P, regions.data_ptr(), cap)
+        assert ok and counts.tolist() == need.tolist()
+        torch.cuda.synchronize()
+    ora = skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, True, ids=ids))
+    union = {}
+    with kbin.Engine(K, M, cutoff=1, max_read_len=300) as rx, \
+            kbin.Engine(K, M, cutoff=1, max_read_len=300) as direct:
+        for p in range(P):
+            rx.reset()
+            rx.set_partition(p, P)
+            rx.submit_superkmers_device(regions[p * cap * rw:].data_ptr(), int(counts[p]))
+            rx.finalize(prune=True)
+            part = _result_dict(rx.export())
+            direct.reset()
+            direct.submit(bases=bases, lens=lens, ids=ids)
+            direct.set_partition(p, P)
+            direct.finalize(prune=True)
+            assert part == _result_dict(direct.export())
+            assert not (set(part) & set(union))
+            union.update(part)
+    assert union == ora
+
+
 @pytest.mark.parametrize("P", [2, 5])
 def test_partitioned_routing(P, engine):
     """kb_set_partition on the sender: each pass routes (ordered plan/pack on
