@@ -8,10 +8,10 @@ Inputs are generated on the device before the timed region (seeded, SURVEY
 §8(d) C2 at N=1: 1M x 150 bp, genome 5 Mbp, 0.1% substitutions, seed 2,
 K=31 M=7, cutoff 1); outputs stay device-resident (CSR).
 
-N>1 (torchrun, one rank per GPU): every rank generates its own 1M-read shard
-of its own 5-Mbp genome (weak scaling at constant coverage) and k-mers are
-routed to the GPU that owns their canonical mmer with an RCCL all-to-all
-(genome-assembly_amd/kbin/dist.py).
+N>1 (torchrun, one rank per GPU): rank r generates reads [r n, (r+1) n) of
+the workload's ONE genome (weak scaling: n reads per GPU; coverage grows with
+N) and k-mers are routed to the GPU that owns their canonical mmer with an
+RCCL all-to-all (genome-assembly_amd/kbin/dist.py).
 
 Prints ONE JSON line on rank 0 (contract in the task statement); extra
 objects: "roofline" for the dominant kernel (bin_kernel; scan_insert_kernel
@@ -55,6 +55,12 @@ WORKLOADS = {
     "c5": {"reads": 62_500_000, "read_len": 250, "K": 63, "M": 7, "err_ppm": 10000,
            "genome": 3_100_000_000, "seed": 5, "parts": 4, "name": "C5 (per-GPU share)"},
 }
+
+
+def gen_seed(seed: int) -> int:
+    """generator seed of workload seed `seed` (rank 0's stream of round 1, so
+    the C3 digest recorded in DESIGN.md stays comparable)"""
+    return seed * 1000003
 
 
 def algorithmic_bytes_per_read(L: int, K: int) -> float:
@@ -116,7 +122,9 @@ def cpu_baseline(words, lens, n_sample, wpr, L, K, M, cutoff, ref_sample):
 
 def load_traffic(tag: str, kernel: str):
     """Per-launch HBM bytes of the roofline kernel from the committed rocprofv3
-    --pmc passes (profiles/traffic.json, written by tools/pmc_traffic.py)."""
+    --pmc passes (profiles/traffic.json, written by tools/pmc_traffic.py):
+    the steady-state launches (every dispatch after the first) and the cold
+    first one, reported separately."""
     p = REPO / "profiles" / "traffic.json"
     if not p.exists():
         return None
@@ -126,7 +134,10 @@ def load_traffic(tag: str, kernel: str):
             return None
         k = kernel.split("<")[0]
         row = next((v for name, v in d.get("per_kernel", {}).items() if k in name), None)
-        return {"hbm_bytes_per_launch": row["bytes"]} if row else None
+        if not row or "steady" not in row:
+            return None
+        return {"hbm_bytes_per_launch": row["steady"]["bytes"], "cold_bytes": row["cold"]["bytes"],
+                "source": f"profiles/traffic.json[{tag}]"}
     except Exception:
         return None
 
@@ -156,6 +167,10 @@ def main():
                     help="reads timed on the CPU oracle (0 = skip)")
     ap.add_argument("--ref-sample", type=int, default=120_000,
                     help="reads timed on the compiled reference (oracle/_ref; 0 = port only)")
+    ap.add_argument("--input", choices=("auto", "fresh", "replay"), default="auto",
+                    help="fresh: every step bins new reads of the same genome (all sets generated before "
+                         "timing); replay: the same reads every step; auto: fresh when the sets fit in "
+                         "5%% of the HBM")
     ap.add_argument("--no-scan-once", action="store_true",
                     help="P>1 on one GPU: every pass rescans the reads (kb_set_partition) instead of "
                          "one kb_split_passes scan into the passes' regions")
@@ -166,11 +181,17 @@ def main():
                          "receive): measures the routing overhead on one GPU")
     args = ap.parse_args()
     wl = WORKLOADS[args.workload]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    genome_given = args.genome is not None
     for k in ("reads", "genome", "seed", "parts", "read_len", "K", "M", "err_ppm"):
         if getattr(args, k) is None:
             setattr(args, k, wl[k])
+    if args.workload == "c2" and not genome_given:
+        # weak scaling of the headline: N ranks bin N x 1M reads of ONE genome of
+        # N x 5 Mbp -- per GPU the same reads, coverage (30x) and owned key count
+        # as C2; C4/C5 keep their fixed 3.1-Gbp genome
+        args.genome *= world
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -201,15 +222,33 @@ def main():
     L, K, M = args.read_len, args.K, args.M
     wpr = (L + 31) // 32
     n = args.reads
-    words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
-    lens = torch.empty(n, dtype=torch.int32, device="cuda")
-    # rank r samples its n reads from its own genome (the generator seeds the
-    # genome from the shard seed): the N-rank job bins N x 1M reads of N
-    # genomes of `genome` bp at a constant 30x coverage, each rank owning 1/N of
-    # the canonical mmers (bins N x larger per GPU)
-    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, args.genome,
-                               args.err_ppm, args.seed * 1000003 + rank, device=local)
+    # ONE genome per workload (seeded by the workload seed), one read stream:
+    # rank r holds reads [r n, (r + 1) n) of it (kb_generate_reads_device_at),
+    # so the N-rank job bins the first N n reads of that genome -- C4's shape
+    # (1B reads of one 3.1-Gbp genome split by id range); every
+    # rank owns 1/N of the canonical mmers and receives its keys from all ranks.
+    # Fresh input: step i bins the i-th such batch of the same stream
+    # (reads [(i N + r) n, (i N + r + 1) n)), every set generated and resident
+    # before the timed region; replay: set 0 every step.
+    set_bytes = n * wpr * 8 + n * 4
+    n_sets = args.warmup + args.steps + 1
+    hbm = torch.cuda.get_device_properties(local).total_memory
+    fresh = args.input == "fresh" or (args.input == "auto" and n_sets * set_bytes <= 0.05 * hbm)
+    if not fresh:
+        n_sets = 1
+    sets = []
+    for i in range(n_sets):
+        w_i = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+        l_i = torch.empty(n, dtype=torch.int32, device="cuda")
+        kbin.generate_reads_device(w_i.data_ptr(), l_i.data_ptr(), n, L, args.genome, args.err_ppm,
+                                   gen_seed(args.seed), device=local, read_base=(i * world + rank) * n)
+        sets.append((w_i, l_i))
     torch.cuda.synchronize()
+    cur = [0]  # the set the next step bins
+    pinned = [False]  # replay leg and digest: set 0 every step
+
+    def reads(off=0):
+        return sets[0] if pinned[0] else sets[(cur[0] + off) % n_sets]
 
     P = args.parts
     pass_log = []  # (export_device, timing[, route times]) of every pass of the last step
@@ -220,8 +259,9 @@ def main():
         pipeline = not args.no_pipeline
         pending = []  # pipelined: the next unit, already scattered, its records in flight
 
-        def send(p):
-            return runner.send(words, lens, n, wpr, first_id=rank * n, part=p, n_parts=P)
+        def send(p, off=0):
+            w, ln = reads(off)
+            return runner.send(w, ln, n, wpr, first_id=rank * n, part=p, n_parts=P)
 
         def step(digest=False):
             pass_log.clear()
@@ -232,13 +272,15 @@ def main():
                     # unit (or now, at the start); the next unit's -- the next
                     # pass, or the next step's first -- go out before it is binned
                     unit = pending.pop() if pending else send(p)
-                    pending.append(send((p + 1) % P))
+                    pending.append(send((p + 1) % P, 1 if p + 1 == P else 0))
                     runner.receive(unit)
                 else:
-                    runner.step(words, lens, n, wpr, first_id=rank * n, part=p, n_parts=P)
+                    w, ln = reads()
+                    runner.step(w, ln, n, wpr, first_id=rank * n, part=p, n_parts=P)
                 pass_log.append((eng.export_device(), eng.timing(), runner.last_times))
                 if digest:
                     dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
+            cur[0] += 1
             return dig
 
         def drain():
@@ -267,7 +309,8 @@ def main():
 
         def scan():
             sender.reset()
-            sender.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, first_id=0)
+            w, ln = reads()
+            sender.submit_packed_device(w.data_ptr(), ln.data_ptr(), n, wpr, first_id=0)
             for _ in range(3):
                 need = P * split["cap"] * rw
                 if split["buf"] is None or split["buf"].numel() < need:
@@ -292,24 +335,34 @@ def main():
                     eng.submit_superkmers_device(split["buf"][p * split["cap"] * rw:].data_ptr(),
                                                  split["counts"][p])
                 else:
-                    eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, first_id=0)
+                    w, ln = reads()
+                    eng.submit_packed_device(w.data_ptr(), ln.data_ptr(), n, wpr, first_id=0)
                     if P > 1:
                         eng.set_partition(p, P)
                 eng.finalize(prune=True)
                 pass_log.append((eng.export_device(), eng.timing(), None))
                 if digest:
                     dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
+            cur[0] += 1
             return dig
-
-    eng.set_timing(True)
-    for _ in range(args.warmup):
-        step()
-    drain()
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
+
+    eng.set_timing(True)
+    cold_ms = None
+    for i in range(args.warmup):
+        if i == 0:  # the first step of fresh contexts: nothing learned yet
+            barrier()
+            tc = time.perf_counter()
+            step()
+            barrier()
+            cold_ms = (time.perf_counter() - tc) * 1e3
+        else:
+            step()
+    drain()
 
     steps_log = []  # per step: [(export_device, timing)] of each finalize (pass)
     barrier()
@@ -365,6 +418,8 @@ def main():
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+            **({"traffic_cold_launch": traffic["cold_bytes"], "traffic_source": traffic["source"]}
+               if traffic else {}),
             "kernel_ms": round(avg_kernel_ms, 4),
             "kmers_per_launch": int(kmers_per_launch),
             "bytes_per_kmer": round(bpk, 3),
@@ -373,8 +428,28 @@ def main():
     # device time per step (all passes of a step added up)
     phases = {k: round(float(np.mean([sum(t[k] for _, t in st) for st in steps_log])), 4)
               for k in ("scan_insert_ms", "sort_ms", "runs_ms", "emit_ms", "total_ms")}
+    replay = None
+    if fresh and args.steps:
+        # the same number of steps replaying one set (round 1's headline mode)
+        drain()
+        barrier()
+        tr = time.perf_counter()
+        pinned[0] = True
+        for _ in range(args.steps):
+            step()
+        barrier()
+        t_rep = time.perf_counter() - tr
+        drain()
+        if dist is not None:
+            tt = torch.tensor([t_rep], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t_rep = float(tt.item())
+        replay = {"value": round(total_scanned * args.steps / t_rep, 1),
+                  "ms_per_step": round(t_rep / args.steps * 1e3, 4)}
     digest = None
-    if args.digest:  # this rank's share (ranks own disjoint mmers: shares add up)
+    if args.digest:  # this rank's share of set 0 (ranks own disjoint mmers: shares add up)
+        drain()
+        pinned[0] = True
         digest = [hex(x) for x in step(digest=True)]
         drain()
 
@@ -393,6 +468,11 @@ def main():
                                    ("single GPU, routed path" if args.routed else "single GPU"))
                                   + (", pipelined exchange" if (world > 1 or args.routed)
                                      and not args.no_pipeline else "")},
+        "input": {"mode": "fresh" if fresh else "replay",
+                  "note": ("every step bins the next n reads of the same genome, all sets resident before "
+                           "the timed region" if fresh else "every step re-bins the same resident reads"),
+                  "cold_first_step_ms": None if cold_ms is None else round(cold_ms, 3),
+                  **({"replay": replay} if replay else {})},
         "roofline": roof,
         "phases_ms": phases,
         **({"route_ms": {k: round(float(np.mean([r[k] for r in route_t])), 4) for k in route_t[0]}}
@@ -405,7 +485,7 @@ def main():
                    "bins": int(tim[-1]["n_bins"]), "superkmers": int(tim[-1]["n_superkmers"])},
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(words, lens, min(args.cpu_sample, n), wpr, L, K, M,
+        out["cpu_baseline"] = cpu_baseline(sets[0][0], sets[0][1], min(args.cpu_sample, n), wpr, L, K, M,
                                            args.cutoff, args.ref_sample)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -143,6 +143,7 @@ struct kb_ctx {
     DevBuf<uint64_t> stage;    // per-occurrence (slot, ordinal) staging
     DevBuf<uint64_t> kstage;   // heavy bins: per-occurrence k-mer code + 1
     DevBuf<uint32_t> long_q;   // entries with 257..4096 ids (lists_long_kernel)
+    DevBuf<uint64_t> lq;       // list items for lists_kernel (BinArgs::lq_items); [0] the counter
     DevBuf<uint32_t> border;   // bin processing order
     DevBuf<uint32_t> bcount, bmmer, bocc;  // bin descriptors (with starts); bocc: k-mers
     DevBuf<uint32_t> flat_list, flat_next, flat_l0, flat_off, flat_cur, flat_chunk, pool_bin, chunk_bin;  // heavy bins published for phase 1
@@ -154,6 +155,7 @@ struct kb_ctx {
     uint64_t bucket_cap_used = 0;  // the capacity (region stride) the regions were written with
     DevBuf<uint64_t> kpart;    // per-block k-mer sums of the count pass
     float rho = 0.f;           // learned distinct / occurrences
+    float kept_ratio = 1.f;    // learned kept ids / occurrences (the LDS list window's depth)
     bool bucket_failed = false;  // a bucket overflowed its mmer map: radix path from now on
     uint64_t n_occ_entries_hint = 0;  // entries of the last finalize (lists grid)
     uint64_t ecap_hint = 0;    // entry capacity for the next binned finalize
@@ -293,6 +295,7 @@ extern "C" int kb_reset(kb_ctx* c) {
     free_batches(c);
     c->finalized = false;
     c->exported = false;
+    c->bucket_failed = false;  // a new input gets the bucketed path again
     c->n_entries = c->n_ids = c->n_distinct = 0;
     c->part = 0;  // back to one full pass
     c->part_n = 1;
@@ -621,6 +624,8 @@ extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
         a.n_reads = b.n_reads;
         a.offs = b.route_offs;
         a.G = n_dest;
+        a.part = c->part;
+        a.part_n = c->part_n;
         a.rec_words = rec_words(c);
         a.RW = b.RW;
         a.K = c->p.K;
@@ -766,6 +771,8 @@ extern "C" int kb_route_pack(kb_ctx* c, uint64_t* d_send) {
         a.adj = adj.p;
         a.out = d_send;
         a.G = G;
+        a.part = c->part;  // the same records the plan counted
+        a.part_n = c->part_n;
         a.rec_words = rec_words(c);
         a.RW = b.RW;
         a.K = c->p.K;
@@ -1390,6 +1397,16 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.id_off = (uint32_t)(affine ? id_c : 0);
         a.max_entries = ecap - 1;
         a.max_ids = N;
+        if (env_int("KB_BIN_LDS_LISTS", 0)) {
+            // items <= entries (every item holds >= 1 entry): one slot per entry
+            HIPCHK(c->lq.ensure(ecap + 1));
+            HIPCHK(hipMemsetAsync(c->lq.p, 0, sizeof(uint64_t), c->s));
+            a.lq_n = reinterpret_cast<unsigned long long*>(c->lq.p);
+            a.lq_items = c->lq.p + 1;
+            a.lq_cap = ecap;
+        }
+        a.kept_ratio = c->kept_ratio;
+        a.win_fill = (float)std::min(1.2, std::max(0.3, env_int("KB_BIN_WIN_PCT", 100) / 100.0));
         HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr));
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
@@ -1405,6 +1422,9 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         la.read_ids = a.read_ids;
         la.id_off = a.id_off;
         la.long_cap = N / 256 + 2;  // lists of > 256 ids
+        la.lq_items = a.lq_items;
+        la.lq_n = a.lq_n;
+        la.lq_cap = a.lq_cap;
         HIPCHK(c->long_q.ensure(2 * la.long_cap));
         la.long_q = c->long_q.p;
         la.long_n = c->misc.p + 4;
@@ -1419,9 +1439,22 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         else c->h_misc[8] = 0;
         HIPCHK(hipStreamSynchronize(c->s));
-        if (c->h_misc[0] & ST_BUCKET_FULL) {  // a bucket held too many mmers: redo with the radix
-            c->bucket_failed = true;              // path (K <= 31) or the table engine (K > 31)
+        if (c->h_misc[0] & ST_BUCKET_FULL) {  // a bucket held too many mmers
             c->finalized = false;
+            // a learned map packed them: forget it and rerun on the hash routing
+            for (size_t i = 0; i < c->bmaps.size(); i++)
+                if (c->bmaps[i].key == bmap_key(c) && c->bmaps[i].nb == NB) {
+                    auto& m = c->bmaps[i];
+                    m.map.release(); m.run.release(); m.run_mmer.release();
+                    c->bmaps.erase(c->bmaps.begin() + (long)i);
+                    return finalize_binned(c, prune, affine, id_c, received);
+                }
+            // the hash itself overflowed: the radix path (K <= 31) or the
+            // table engine (K > 31, which has no partitioned passes)
+            if (KW == 2 && c->part_n > 1)
+                return fail(KB_EINVAL, "a local bucket overflowed with two-word k-mers in a partitioned "
+                                       "pass (M too large for %u buckets)", NB);
+            c->bucket_failed = true;  // until kb_reset
             if (KW == 1) return finalize_binned(c, prune, affine, id_c, received);
             return kb_finalize(c, prune);
         }
@@ -1450,6 +1483,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     c->n_occ_entries_hint = c->n_entries;
     c->ecap_hint = c->n_entries + c->n_entries / 4 + 1024;
     if (N) c->rho = (float)((double)c->n_distinct / (double)N);
+    if (N) c->kept_ratio = std::max(0.01f, (float)((double)c->n_ids / (double)N));
     if (c->timing) {
         HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));
         HIPCHK(hipEventElapsedTime(&c->tm.sort_ms, c->ev[2], c->ev[3]));
@@ -1739,16 +1773,23 @@ extern "C" int kb_export(kb_ctx* c, kb_csr* out) {
     return KB_OK;
 }
 
-extern "C" int kb_generate_reads_device(int device, uint64_t* d_words, uint32_t* d_lens,
-                                        uint64_t n_reads, uint32_t read_len, uint64_t genome_len,
-                                        uint32_t err_ppm, uint64_t seed) {
+extern "C" int kb_generate_reads_device_at(int device, uint64_t* d_words, uint32_t* d_lens,
+                                           uint64_t n_reads, uint32_t read_len, uint64_t genome_len,
+                                           uint32_t err_ppm, uint64_t seed, uint64_t read_base) {
     if (!d_words || !d_lens) return fail(KB_EINVAL, "null device pointers");
     if (read_len < 1 || genome_len < read_len) return fail(KB_EINVAL, "bad read_len/genome_len");
     if (err_ppm > 1000000) return fail(KB_EINVAL, "err_per_million > 1e6");
     HIPCHK(hipSetDevice(device));
-    HIPCHK(launch_generate(d_words, d_lens, n_reads, read_len, genome_len, err_ppm, seed, 0));
+    HIPCHK(launch_generate(d_words, d_lens, n_reads, read_len, genome_len, err_ppm, seed, read_base, 0));
     HIPCHK(hipStreamSynchronize(0));
     return KB_OK;
+}
+
+extern "C" int kb_generate_reads_device(int device, uint64_t* d_words, uint32_t* d_lens,
+                                        uint64_t n_reads, uint32_t read_len, uint64_t genome_len,
+                                        uint32_t err_ppm, uint64_t seed) {
+    return kb_generate_reads_device_at(device, d_words, d_lens, n_reads, read_len, genome_len, err_ppm,
+                                       seed, 0);
 }
 
 extern "C" int kb_unpack_reads_to_host(int device, const uint64_t* d_words, const uint32_t* d_lens,

@@ -888,6 +888,77 @@ constexpr uint32_t SPLIT_BIT = 0x100u;     // flat_l0: a split bin's partitions 
 constexpr uint32_t PRUNED = 0x80000000u;  // cursor of a pruned (or empty) slot in sweep 2
 constexpr uint64_t M48 = (1ull << 48) - 1ull;
 
+// LDS path of one partition, after its prune: the kept occurrences' ordinals
+// go to an LDS window at their list positions (cursor atomics on cnt), each
+// list is put in reverse call order there (binning.c:1065-1068 prepends:
+// descending call ordinal) -- lists <= 32 in one lane's registers, 33..256 by
+// one wavefront -- and the window is written to ids_out as read ids with
+// coalesced stores: no scattered HBM stores, no lists_kernel pass.  Lists
+// > 256 leave their ordinals in ids_ord and a one-entry item for the list
+// kernels.  The partition's entries [e0, e0 + n_ent) are read back densely
+// from e_cnt / e_off (this block wrote them: L2).  Not inlined: its sorting
+// registers stay out of the sweeps' allocation.
+DEV void sort32_inplace(uint32_t* p, uint32_t n);
+template <int R>
+DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane);
+
+template <int KW>
+DEV void lds_lists(const BinArgs& A, uint32_t* cnt, uint32_t* win, uint32_t ns,
+                                                    unsigned long long e0, unsigned long long i0, uint32_t n_ent,
+                                                    uint32_t n_ids, const uint64_t* stage, bool filt,
+                                                    const uint64_t* kst, uint32_t P, uint32_t pmask) {
+    const uint32_t tid = threadIdx.x;
+    const int lane = (int)(tid & 63u);
+    // ---- sweep 2 into the window (the claim words and rings are dead)
+    for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
+        if (filt && (kst_load<KW>(kst, i).part() & pmask) != P) continue;
+        const uint64_t v = stage[i];
+        const uint32_t pos = atomicAdd(&cnt[(uint32_t)(v >> 48)], 1u);
+        if (pos < PRUNED) win[pos] = (uint32_t)v + 1u;  // ordinal + 1 (0 pads the sorts)
+    }
+    __syncthreads();
+    // ---- every list in place: a wave takes 64 entries at a time
+    for (uint32_t eb = (tid & ~63u); eb < n_ent; eb += BIN_THREADS) {
+        const uint32_t e = eb + (uint32_t)lane;
+        const uint32_t c = e < n_ent ? A.e_cnt[e0 + e] : 0u;
+        const uint32_t st_me = e < n_ent ? (uint32_t)(A.e_off[e0 + e] - i0) : 0u;
+        if (c >= 2 && c <= 32) sort32_inplace(win + st_me, c);
+        uint64_t m = __ballot(c > 32u);
+        while (m) {
+            const int src = __builtin_ctzll(m);
+            m &= m - 1ull;
+            const uint32_t n = (uint32_t)__shfl((int)c, src, 64);
+            const uint32_t st = (uint32_t)__shfl((int)st_me, src, 64);
+            wave_sync();
+            if (n <= 64) wave_sort_desc<1>(win + st, n, lane);
+            else if (n <= 128) wave_sort_desc<2>(win + st, n, lane);
+            else if (n <= 256) wave_sort_desc<4>(win + st, n, lane);
+            else {  // the list kernels order it from ids_ord (one-entry item)
+                for (uint32_t j = (uint32_t)lane; j < n; j += 64) A.ids_ord[i0 + st + j] = win[st + j] - 1u;
+                if (lane == 0) {
+                    const unsigned long long q = atomicAdd(A.lq_n, 1ull);
+                    if (q < A.lq_cap) A.lq_items[q] = ((e0 + eb + (uint32_t)src) << 16) | 1ull;
+                }
+            }
+            wave_sync();
+        }
+    }
+    __syncthreads();
+    // ---- the window as read ids, 16-B stores where aligned
+    const uint32_t head = min((uint32_t)((4u - (uint32_t)(i0 & 3u)) & 3u), n_ids);
+    if (tid < head) A.ids_out[i0 + tid] = id_of(win[tid] - 1u, A.read_ids, A.id_off);
+    const uint32_t body = (n_ids - head) / 4u;
+    int4* dst4 = reinterpret_cast<int4*>(A.ids_out + i0 + head);
+    for (uint32_t g = tid; g < body; g += BIN_THREADS) {
+        const uint4 v = *reinterpret_cast<const uint4*>(win + head + 4u * g);
+        dst4[g] = make_int4(id_of(v.x - 1u, A.read_ids, A.id_off), id_of(v.y - 1u, A.read_ids, A.id_off),
+                            id_of(v.z - 1u, A.read_ids, A.id_off), id_of(v.w - 1u, A.read_ids, A.id_off));
+    }
+    for (uint32_t j = head + 4u * body + tid; j < n_ids; j += BIN_THREADS)
+        A.ids_out[i0 + j] = id_of(win[j] - 1u, A.read_ids, A.id_off);
+    __syncthreads();  // (the window is the next partition's table)
+}
+
 template <int KW, int PHASE>
 DEV void bin_body(const BinArgs& A) {
     constexpr uint32_t Q = bin_q<KW>();
@@ -895,10 +966,15 @@ DEV void bin_body(const BinArgs& A) {
     BinShared& S = *reinterpret_cast<BinShared*>(smem);      // all LDS in one dynamic array
     const uint32_t TS = 1u << A.ts_log2, bmask = TS / 4 - 1;  // buckets of four slots
     BinTable<KW> T;
-    T.ca = smem + sizeof(BinShared) / 8;                     // [TS] claim words
+    // cnt | claim words | low words | rings: after the prune everything past
+    // cnt is dead, and the LDS path's id window takes it (win_cap ids)
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + sizeof(BinShared) / 8);  // [TS] count, then cursor
+    T.ca = reinterpret_cast<uint64_t*>(cnt + TS);            // [TS] claim words (TS even: 8-B aligned)
     T.cb = KW == 2 ? T.ca + TS : nullptr;                    // [TS] published low words
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(T.ca + KW * TS);  // [TS] count, then cursor
-    uint64_t* ring0 = reinterpret_cast<uint64_t*>(cnt + TS);
+    uint64_t* ring0 = T.ca + KW * TS;
+    uint32_t* const win = reinterpret_cast<uint32_t*>(T.ca);
+    const uint32_t win_cap = (KW * TS * 8u + (uint32_t)BIN_WAVES * Q * (8u * KW + 6u)) / 4u;
+    const bool lds_ok = A.lq_items && !A.e_first;  // (first occurrences need the claim words)
     const uint32_t wq = (threadIdx.x >> 6) * Q;
     uint64_t* qa = ring0 + wq;
     uint64_t* qb = KW == 2 ? ring0 + BIN_WAVES * Q + wq : nullptr;
@@ -999,6 +1075,13 @@ DEV void bin_body(const BinArgs& A) {
             const uint32_t lmax = A.flat_l ? A.flat_l - 1u : 3u;
             while (l0 < lmax && (occ_tot >> l0) > A.split_occ) l0++;
             split = l0 >= 1;
+        }
+        if (PHASE == 0 && !flat && !split && lds_ok) {
+            // the LDS path needs a partition's kept ids in the window: deepen
+            // the first split until the expected ones fit (a partition that
+            // still overflows it takes the global path)
+            const double kept = (double)occ_tot * (double)A.kept_ratio;
+            while (l0 < 12 && kept > (double)A.win_fill * (double)win_cap * (double)(1u << l0)) l0++;
         }
         uint64_t* kst = A.kstage + KW * S.stage_base;
         if ((split || flat) && PHASE == 0) {
@@ -1223,6 +1306,13 @@ DEV void bin_body(const BinArgs& A) {
             __syncthreads();
             PROF_MARK(3);
             if (!room) continue;
+            const uint32_t n_ent = (uint32_t)tot, n_ids = (uint32_t)(tot >> 32);
+            if (lds_ok && n_ids <= win_cap) {
+                lds_lists<KW>(A, cnt, win, S.n_stage, e0, i0, n_ent, n_ids, stage, flat && Lv > l0,
+                              kst + KW * (uint64_t)fa, P, (1u << Lv) - 1u);
+                PROF_MARK(4);
+                continue;
+            }
             // ---- sweep 2: drop every surviving occurrence's call ordinal in place
             {
 #ifdef KB_BIN_PROF
@@ -1257,10 +1347,17 @@ DEV void bin_body(const BinArgs& A) {
                     if (cnt[i] < PRUNED) A.e_first[e0 + e++] = T.ca[i];
                 }
             }
+            // lists are put in reverse call order by lists_kernel: queue them
+            if (A.lq_items && tid == 0 && n_ent) {
+                const uint32_t nit = (n_ent + 255u) / 256u;
+                const unsigned long long q = atomicAdd(A.lq_n, (unsigned long long)nit);
+                for (uint32_t k = 0; k < nit; k++)
+                    if (q + k < A.lq_cap)
+                        A.lq_items[q + k] = ((e0 + 256ull * k) << 16) | (uint64_t)min(256u, n_ent - 256u * k);
+            }
             __threadfence_block();
             __syncthreads();
             PROF_MARK(4);
-            // lists are put in reverse call order by lists_kernel
             __syncthreads();
             PROF_MARK(6);
         }
@@ -1768,9 +1865,25 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
     const uint32_t tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     const uint64_t n_entries = A.totals[0];
-    for (uint64_t e0 = (uint64_t)blockIdx.x * LIST_THREADS; e0 < n_entries;
-         e0 += (uint64_t)gridDim.x * LIST_THREADS) {
-        const uint32_t ne = (uint32_t)min<uint64_t>(LIST_THREADS, n_entries - e0);
+    // items: the bin kernels' queue (partitions whose ids took the global
+    // path, and long lists of the LDS path), else every entry in chunks of 256
+    // (an entry-capacity overflow publishes no entries, bins_final_kernel: the
+    // queued items' neighbours then have unwritten offsets -- no work at all,
+    // the host reruns the bin phase)
+    const uint64_t n_items = !n_entries ? 0ull
+                             : A.lq_items ? min<uint64_t>(*A.lq_n, A.lq_cap)
+                                          : (n_entries + LIST_THREADS - 1) / LIST_THREADS;
+    for (uint64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
+        uint64_t e0;
+        uint32_t ne;
+        if (A.lq_items) {
+            const uint64_t x = A.lq_items[it];
+            e0 = x >> 16;
+            ne = (uint32_t)(x & 0xFFFFu);
+        } else {
+            e0 = it * LIST_THREADS;
+            ne = (uint32_t)min<uint64_t>(LIST_THREADS, n_entries - e0);
+        }
         const uint64_t ob = A.e_off[e0], span = A.e_off[e0 + ne] - ob;
         // (barriers in the staged path order LDS only: a full __syncthreads
         // also waits for the previous window's global stores to land)

@@ -52,6 +52,7 @@ struct RouteArgs {
     const uint64_t* adj;       // [G] per-destination base adjustment (pack pass)
     uint64_t* out;             // send buffer (pack pass)
     uint32_t G;
+    uint32_t part, part_n;     // kb_set_partition: route only this mmer partition's records
     int rec_words;
     int RW, K, M;
 };
@@ -212,6 +213,15 @@ struct BinArgs {
     const int32_t* read_ids;
     uint32_t id_off;
     uint64_t max_entries, max_ids;
+    // list items for lists_kernel: (first entry << 16 | entries <= 256) of every
+    // partition whose ids took the global path (and one-entry items for lists
+    // > 256 of the LDS path); the LDS path leaves its lists final in ids_out.
+    // null: the global path for every partition, lists_kernel over all entries
+    uint64_t* lq_items;
+    unsigned long long* lq_n;  // (zeroed) items
+    uint64_t lq_cap;
+    float kept_ratio;          // expected kept ids per occurrence (last finalize)
+    float win_fill;            // target share of the LDS id window when choosing the depth
 };
 
 struct ListArgs {
@@ -226,6 +236,9 @@ struct ListArgs {
                                // lists_bucket_kernel, [long_cap, 2 long_cap) passed on to lists_long_kernel
     uint64_t long_cap;
     unsigned int* long_n;      // [2] (zeroed) queue lengths
+    const uint64_t* lq_items;  // BinArgs::lq_items (null: every entry, chunks of 256)
+    const unsigned long long* lq_n;
+    uint64_t lq_cap;
 };
 
 hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s);
@@ -308,7 +321,7 @@ uint64_t scan_u32_scratch_elems(uint64_t n);
 hipError_t launch_fill_ids(int32_t* d_ids, uint64_t n, int32_t first, hipStream_t s);
 hipError_t launch_generate(uint64_t* d_words, uint32_t* d_lens, uint64_t n_reads,
                            uint32_t read_len, uint64_t genome_len, uint32_t err_ppm,
-                           uint64_t seed, hipStream_t s);
+                           uint64_t seed, uint64_t read_base, hipStream_t s);
 hipError_t launch_unpack(const uint64_t* d_words, const uint32_t* d_lens, uint64_t n_reads,
                          int RW, const uint64_t* d_off, uint8_t* d_bases, hipStream_t s);
 

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void generate_kernel(uint64_t* __restrict__ wo
                                                        uint32_t* __restrict__ lens,
                                                        uint64_t n_reads, uint32_t L, int RW,
                                                        uint64_t G, uint32_t err_ppm,
-                                                       uint64_t seed) {
+                                                       uint64_t seed, uint64_t read_base) {
     const uint64_t total = n_reads * (uint64_t)RW;
     const uint64_t s_genome = mix64(seed ^ 0x1111111111111111ull);
     const uint64_t s_start = mix64(seed ^ 0x2222222222222222ull);
@@ -126,7 +126,8 @@ __global__ __launch_bounds__(256) void generate_kernel(uint64_t* __restrict__ wo
          g += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t r = g / RW;
         const int w = (int)(g - r * RW);
-        const uint64_t start = rng(s_start, r) % (G - L + 1);
+        const uint64_t rg = read_base + r;  // global read index: the stream is one genome's
+        const uint64_t start = rng(s_start, rg) % (G - L + 1);
         uint64_t word = 0;
         for (int j = 0; j < 32; j++) {
             const uint32_t b = (uint32_t)w * 32u + (uint32_t)j;
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(256) void generate_kernel(uint64_t* __restrict__ wo
             // 32 genome bases per RNG draw
             uint32_t v = (uint32_t)(rng(s_genome, pos >> 5) >> (2 * (pos & 31))) & 3u;
             if (err_ppm) {
-                const uint64_t u = rng(s_err, r * (uint64_t)L + b);
+                const uint64_t u = rng(s_err, rg * (uint64_t)L + b);
                 if ((uint32_t)(u % 1000000ull) < err_ppm)
                     v = (v + 1u + (uint32_t)((u >> 32) % 3ull)) & 3u;
             }
@@ -147,14 +148,15 @@ __global__ __launch_bounds__(256) void generate_kernel(uint64_t* __restrict__ wo
 }
 
 hipError_t launch_generate(uint64_t* d_words, uint32_t* d_lens, uint64_t n_reads, uint32_t read_len,
-                           uint64_t genome_len, uint32_t err_ppm, uint64_t seed, hipStream_t s) {
+                           uint64_t genome_len, uint32_t err_ppm, uint64_t seed, uint64_t read_base,
+                           hipStream_t s) {
     const int RW = (int)((read_len + 31) / 32);
     const uint64_t total = n_reads * (uint64_t)RW;
     if (!total) return hipSuccess;
     uint64_t blocks = (total + 255) / 256;
     if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL(generate_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_words, d_lens,
-                       n_reads, read_len, RW, genome_len, err_ppm, seed);
+                       n_reads, read_len, RW, genome_len, err_ppm, seed, read_base);
     return hipGetLastError();
 }
 
@@ -470,6 +472,10 @@ hipError_t launch_scan_insert(const ScanArgs& a, int KW, hipStream_t s) {
 DEV uint32_t owner_of(uint32_t mmer, uint32_t G) {
     return (uint32_t)((mix64((uint64_t)mmer + 0x5851F42D4C957F2Dull) >> 32) % G);
 }
+// kb_set_partition membership (= in_part, kbin_bins.hip: PART_SALT)
+DEV bool route_in_part(uint32_t mmer, uint32_t part, uint32_t part_n) {
+    return part_n <= 1 || (uint32_t)((mix64((uint64_t)mmer + 0x9E3779B97F4A7C15ull) >> 32) % part_n) == part;
+}
 
 template <bool PACK>
 __global__ __launch_bounds__(256) void route_kernel(RouteArgs A) {
@@ -508,7 +514,9 @@ __global__ __launch_bounds__(256) void route_kernel(RouteArgs A) {
                 const uint32_t c = key >> 16;
                 const int n = min(sig, nK - 1) - seg_lo + 1;
                 const uint32_t dest = owner_of(c, A.G);
-                if (PACK) {
+                // another pass's super-k-mer: neither counted nor written
+                const bool mine = route_in_part(c, A.part, A.part_n);
+                if (PACK && mine) {
                     const uint64_t pos = (uint64_t)(uint32_t)__shfl((int)run, (int)dest, 64);
                     uint64_t* rec = A.out + pos * (uint64_t)A.rec_words;
                     if (lane == 0)
@@ -519,7 +527,7 @@ __global__ __launch_bounds__(256) void route_kernel(RouteArgs A) {
                         rec[lane] = p < L ? window64(sw, p) : 0ull;
                     }
                 }
-                if (lane == (int)dest) run++;
+                if (mine && lane == (int)dest) run++;
                 seg_lo = sig + 1;
             }
         }

@@ -33,7 +33,7 @@ _ERRNAMES = {0: "KB_OK", 1: "KB_EINVAL", 2: "KB_ENOMEM", 3: "KB_EDEVICE", 4: "KB
 EXPORTED = [
     "kb_create", "kb_destroy", "kb_submit", "kb_submit_ids", "kb_submit_packed_device",
     "kb_finalize", "kb_export", "kb_export_device", "kb_reset", "kb_set_timing",
-    "kb_get_timing", "kb_generate_reads_device", "kb_unpack_reads_to_host", "kb_stream",
+    "kb_get_timing", "kb_generate_reads_device", "kb_generate_reads_device_at", "kb_unpack_reads_to_host", "kb_stream",
     "kb_last_error", "kb_abi_version", "kb_record_words", "kb_route_plan", "kb_route_pack",
     "kb_submit_superkmers_device", "kb_route_scatter", "kb_split_passes", "kb_set_partition", "kb_digest",
 ]
@@ -108,6 +108,7 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_set_timing.argtypes = [vp, C.c_int]
     lib.kb_get_timing.argtypes = [vp, C.POINTER(kb_timing)]
     lib.kb_generate_reads_device.argtypes = [C.c_int, vp, vp, u64, u32, u64, u32, u64]
+    lib.kb_generate_reads_device_at.argtypes = [C.c_int, vp, vp, u64, u32, u64, u32, u64, u64]
     lib.kb_unpack_reads_to_host.argtypes = [C.c_int, vp, vp, u64, u32, C.c_char_p, C.POINTER(u32)]
     lib.kb_record_words.argtypes = [vp, C.POINTER(u32)]
     lib.kb_route_plan.argtypes = [vp, u32, C.POINTER(u64)]
@@ -393,10 +394,14 @@ class Engine:
 
 
 def generate_reads_device(words_ptr: int, lens_ptr: int, n_reads: int, read_len: int,
-                          genome_len: int, err_per_million: int, seed: int, device: int = 0) -> None:
+                          genome_len: int, err_per_million: int, seed: int, device: int = 0,
+                          read_base: int = 0) -> None:
+    """reads read_base .. read_base + n_reads - 1 of the stream `seed` defines
+    (one genome per seed; kb_generate_reads_device_at)"""
     lib = load_library()
-    _check(lib, lib.kb_generate_reads_device(device, C.c_void_p(words_ptr), C.c_void_p(lens_ptr),
-                                             n_reads, read_len, genome_len, err_per_million, seed))
+    _check(lib, lib.kb_generate_reads_device_at(device, C.c_void_p(words_ptr), C.c_void_p(lens_ptr),
+                                                n_reads, read_len, genome_len, err_per_million, seed,
+                                                int(read_base)))
 
 
 def unpack_reads_to_host(words_ptr: int, lens_ptr: int, n_reads: int, words_per_read: int,

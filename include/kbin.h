@@ -177,6 +177,17 @@ int kb_generate_reads_device(int device, uint64_t *d_words, uint32_t *d_lens,
                              uint64_t genome_len, uint32_t err_per_million,
                              uint64_t seed);
 
+/* The same generator from read index read_base on: reads read_base ..
+ * read_base + n_reads - 1 of the one read stream that seed defines (the genome
+ * depends on seed only).  Ranks r = 0..G-1 of a sharded job call it with
+ * read_base = r * n_reads and together hold the first G * n_reads reads of
+ * ONE genome (BASELINE C4/C5: one genome, reads split by id range, SURVEY
+ * §8(e)); kb_generate_reads_device is read_base 0. */
+int kb_generate_reads_device_at(int device, uint64_t *d_words, uint32_t *d_lens,
+                                uint64_t n_reads, uint32_t read_len,
+                                uint64_t genome_len, uint32_t err_per_million,
+                                uint64_t seed, uint64_t read_base);
+
 /* Unpack device packed reads to host ASCII (bases concatenated, lens). */
 int kb_unpack_reads_to_host(int device, const uint64_t *d_words,
                             const uint32_t *d_lens, uint64_t n_reads,

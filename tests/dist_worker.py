@@ -27,8 +27,9 @@ def main():
     wpr = (L + 31) // 32
     words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
     lens = torch.empty(n, dtype=torch.int32, device="cuda")
-    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, 300000, 2000, 77 + rank,
-                               device=dev)
+    # one genome, reads split by id range (C4's shape): rank r holds reads [r n, (r + 1) n)
+    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, 300000, 2000, 77,
+                               device=dev, read_base=rank * n)
     torch.cuda.synchronize()
     sb = ShardedBinner(K, M, 1, L, device=dev)
     for _ in range(2):  # twice: buffers and contexts are reused across steps

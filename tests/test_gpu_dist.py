@@ -196,15 +196,16 @@ def test_split_passes(K, M, P, engine):
     assert union == ora
 
 
-@pytest.mark.parametrize("P", [2, 5])
-def test_partitioned_routing(P, engine):
+@pytest.mark.parametrize("P,K,M", [(2, 31, 7), (5, 31, 7), (3, 63, 7), (4, 40, 6)])
+def test_partitioned_routing(P, K, M, engine):
     """kb_set_partition on the sender: each pass routes (ordered plan/pack on
     even passes, one-pass scatter on odd ones) only its mmer slice; the
     per-destination counts add up to the single pass and the union over
-    passes and shards equals the oracle"""
+    passes and shards equals the oracle.  Two-word k-mers (K > 31) plan/pack
+    through route_kernel, which filters by partition as the binned sender does"""
     if engine != "binned":
         pytest.skip("partitioned passes are the binned engine's")
-    K, M, G = 31, 7, 3
+    G = 3
     reads = _reads()
     bases, lens = kbin.pack_reads(reads)
     ids = np.arange(len(reads), dtype=np.int32) * 2 + 5

@@ -1,16 +1,21 @@
 #!/usr/bin/env python3
 """Per-kernel HBM traffic from two separate rocprofv3 PMC passes
 (--pmc FETCH_SIZE, --pmc WRITE_SIZE; MI355X_MICROARCH.md "rocprofv3 PMC
-slots": they do not fit one pass).  Values are in KiB per dispatch.
+slots": they do not fit one pass).  Counter values are KiB per dispatch.
 
-usage: pmc_traffic.py <fetch_dir> <write_dir> <out.json> <tag>
-Writes/updates profiles/traffic.json[tag] with the dominant kernel's
-per-launch bytes (what bench.py reports as roofline.traffic) and a per-kernel
-table.  Correction (MI355X_MICROARCH.md §HBM, calibrated for our access widths
-by tools/pmc_calib.hip, profiles/r01/pmc_calib.txt): FETCH_SIZE reports half the
-bytes of coalesced 8-B and 16-B per lane reads, so reads count x2; WRITE_SIZE
-is exact for coalesced 8-B stores and counts a scattered 4-B store as a ~32-B
-partial-line write (7.56 x the bytes on the calibration pattern) -- real
+usage: pmc_traffic.py <fetch_dir> <write_dir> <out.json> <tag> [--skip-gen]
+
+Every kernel's dispatches are split into the COLD first dispatch (a fresh
+context: nothing learned yet -- the first bench warmup step) and the STEADY
+ones (every later dispatch; the mean is reported, with min/max).  Writes
+out.json[tag]: the roofline kernel's steady per-launch bytes (what bench.py
+reports as roofline.traffic), its cold bytes, and a per-kernel table.
+
+Correction (MI355X_MICROARCH.md §HBM, calibrated for our access widths by
+tools/pmc_calib.hip, profiles/pmc_calib.txt): FETCH_SIZE reports half the
+bytes of coalesced 8-B and 16-B per-lane reads, so reads count x2; WRITE_SIZE
+is exact for coalesced 8-B/16-B stores and counts a scattered 4-B store as a
+~32-B partial-line write (7.56 x its bytes on the calibration pattern) -- real
 memory-side write requests, so it is kept as is."""
 import collections
 import csv
@@ -19,32 +24,54 @@ import pathlib
 import sys
 
 
-def per_kernel(d):
-    agg = collections.defaultdict(list)
-    files = sorted(pathlib.Path(d).rglob("*counter_collection.csv"))
-    for f in files:
+def dispatches(d):
+    """kernel -> [KiB per dispatch] in dispatch order"""
+    rows = []
+    for f in sorted(pathlib.Path(d).rglob("*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"].split("(")[0], float(r["Counter_Value"])))
+    agg = collections.defaultdict(list)
+    for _, k, v in sorted(rows):
+        agg[k].append(v)
+    return agg
+
+
+def split(v):
+    steady = v[1:] or v
+    return v[0], sum(steady) / len(steady), min(steady), max(steady), len(steady)
 
 
 def main():
     fetch, write, out, tag = sys.argv[1:5]
-    f, w = per_kernel(fetch), per_kernel(write)
-    table = {k: {"fetch_kib": round(f.get(k, 0.0), 1), "write_kib": round(w.get(k, 0.0), 1),
-                 "bytes": round((2.0 * f.get(k, 0.0) + w.get(k, 0.0)) * 1024)} for k in sorted(set(f) | set(w))}
-    scan = [k for k in table if "bin_kernel" in k] or [k for k in table if "scan_insert_kernel" in k]
+    f, w = dispatches(fetch), dispatches(write)
+    table = {}
+    for k in sorted(set(f) | set(w)):
+        fc, fs, fmin, fmax, n = split(f.get(k, [0.0]))
+        wc, ws, wmin, wmax, _ = split(w.get(k, [0.0]))
+        table[k] = {"dispatches": n + 1,
+                    "steady": {"fetch_kib": round(fs, 1), "write_kib": round(ws, 1),
+                               "bytes": round((2.0 * fs + ws) * 1024),
+                               "bytes_min": round((2.0 * fmin + wmin) * 1024),
+                               "bytes_max": round((2.0 * fmax + wmax) * 1024)},
+                    "cold": {"fetch_kib": round(fc, 1), "write_kib": round(wc, 1),
+                             "bytes": round((2.0 * fc + wc) * 1024)}}
+    roof = [k for k in table if "bin_kernel" in k] or [k for k in table if "scan_insert_kernel" in k]
     p = pathlib.Path(out)
     doc = json.loads(p.read_text()) if p.exists() else {}
-    doc[tag] = {"hbm_bytes_per_launch": table[scan[0]]["bytes"] if scan else None,
-                "kernel": scan[0] if scan else None,
+    doc[tag] = {"hbm_bytes_per_launch": table[roof[0]]["steady"]["bytes"] if roof else None,
+                "cold_hbm_bytes": table[roof[0]]["cold"]["bytes"] if roof else None,
+                "kernel": roof[0] if roof else None,
                 "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes, KiB*1024; "
                           "bytes = 2 x FETCH (calibrated: coalesced 8/16-B reads count half) + WRITE "
-                          "(exact for coalesced stores; scattered 4-B stores as 32-B partial writes)",
+                          "(exact for coalesced stores; scattered 4-B stores as 32-B partial writes); "
+                          "steady = mean over every dispatch after the first, cold = the first",
                 "per_kernel": table}
     p.write_text(json.dumps(doc, indent=1) + "\n")
-    for k, v in sorted(table.items(), key=lambda x: -x[1]["bytes"]):
-        print(f"{k:45s} {v['bytes'] / 1e9:8.3f} GB  (fetch {v['fetch_kib'] / 1e6:.3f} GiB-ish, write {v['write_kib'] / 1e6:.3f})")
+    step = sum(v["steady"]["bytes"] for v in table.values())
+    print(f"{tag}: steady-state bytes per step (all kernels) {step / 1e9:.3f} GB")
+    for k, v in sorted(table.items(), key=lambda x: -x[1]["steady"]["bytes"]):
+        print(f"{k:45s} steady {v['steady']['bytes'] / 1e9:8.3f} GB  cold {v['cold']['bytes'] / 1e9:8.3f} GB"
+              f"  (x{v['dispatches']})")
 
 
 if __name__ == "__main__":
