@@ -9,6 +9,10 @@
 #
 #   build_ref.sh K M [C]          ref_k<K>_m<M>_c<C>: reference hot path + our
 #                                 ref_harness.c main -> canonical post-prune dump
+#   build_ref.sh g K M [C]        refg_k<K>_m<M>_c<C>: the same harness, the
+#                                 reference compiled with its makefile's flags
+#                                 (makefile:2: -g, no -O) -- BASELINE.md's
+#                                 "as shipped" CPU row
 #   build_ref.sh full K M [C]     full_k<K>_m<M>_c<C>: the reference program as
 #                                 shipped (its own main: bin, prune, expand,
 #                                 unitig extension, print_kmers)
@@ -21,7 +25,7 @@
 # No-op when /root/reference is absent (e.g. on the GPU box).
 set -euo pipefail
 MODE=harness
-if [ "${1:-}" = "full" ] || [ "${1:-}" = "dropin" ]; then MODE=$1; shift; fi
+case "${1:-}" in full|dropin|g) MODE=$1; shift ;; esac
 K=${1:?K}; M=${2:?M}; C=${3:-1}
 REF=${KB_REFERENCE_DIR:-/root/reference}
 HERE="$(cd "$(dirname "$0")" && pwd)"
@@ -29,6 +33,7 @@ REPO="$(cd "$HERE/.." && pwd)"
 OUT="$HERE/_ref"
 case $MODE in
   harness) BIN="$OUT/ref_k${K}_m${M}_c${C}" ;;
+  g)       BIN="$OUT/refg_k${K}_m${M}_c${C}" ;;
   full)    BIN="$OUT/full_k${K}_m${M}_c${C}" ;;
   dropin)  BIN="$OUT/dropin_k${K}_m${M}_c${C}" ;;
 esac
@@ -52,6 +57,13 @@ case $MODE in
     gcc -O2 -w -I"$REF" -c "$REF/llist.c" -o "$TMP/llist.o"
     gcc -O2 -w -I"$REF" $DEFS -c "$HERE/ref_harness.c" -o "$TMP/harness.o"
     gcc -O2 "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/harness.o" -o "$BIN"
+    ;;
+  g)
+    gcc -g -w -I"$REF" $DEFS -Dmain=binning_main -c "$TMP/binning_guarded.c" -o "$TMP/binning.o"
+    gcc -g -w -I"$REF" -c "$REF/zhash.c" -o "$TMP/zhash.o"
+    gcc -g -w -I"$REF" -c "$REF/llist.c" -o "$TMP/llist.o"
+    gcc -O2 -w -I"$REF" $DEFS -c "$HERE/ref_harness.c" -o "$TMP/harness.o"
+    gcc "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/harness.o" -o "$BIN"
     ;;
   full|dropin)
     # makefile:2-5 flags (-g, no -O): calls stay relocations against the
