@@ -569,6 +569,7 @@ struct alignas(16) BinShared {
     uint32_t flat_idx, fa, fb, l0;
     uint32_t stack_p[BIN_STACK], stack_l[BIN_STACK];
     uint64_t red[BIN_THREADS / 64];
+    unsigned long long dummy[64];  // zero: the claim target of lanes with nothing to claim
 };
 static_assert(sizeof(BinShared) % 16 == 0, "LDS carve must stay 16-B aligned (guide G17)");
 
@@ -689,10 +690,25 @@ struct BinTable {
     // the key's slot in bucket bk, -1 (absent: the bucket has an empty slot),
     // -2 (not here, bucket full), -3 (a-match whose low word is unpublished)
     DEV int in_bucket(uint32_t bk, const TKey<KW>& k, int& empty) const {
-        const uint32_t s0 = bk * 4u;
         uint64_t w[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) w[j] = lds_load_u64(&ca[s0 + j]);
+        for (int j = 0; j < 4; j++) w[j] = lds_load_u64(&ca[bk * 4u + j]);
+        return match(bk, w, k, empty);
+    }
+    // the bucket's four claim words with plain 16-B loads: straight-line code
+    // only (the probe pair of a flush), where nothing can hoist them out of a
+    // retry loop; they may race a concurrent claim, which match() then treats
+    // as absent (the claim that follows fails and takes the full path)
+    DEV void load_bucket(uint32_t bk, uint64_t (&w)[4]) const {
+        const uint4* q = reinterpret_cast<const uint4*>(ca + bk * 4u);
+        const uint4 x = q[0], y = q[1];
+        w[0] = (uint64_t)x.x | ((uint64_t)x.y << 32);
+        w[1] = (uint64_t)x.z | ((uint64_t)x.w << 32);
+        w[2] = (uint64_t)y.x | ((uint64_t)y.y << 32);
+        w[3] = (uint64_t)y.z | ((uint64_t)y.w << 32);
+    }
+    DEV int match(uint32_t bk, const uint64_t (&w)[4], const TKey<KW>& k, int& empty) const {
+        const uint32_t s0 = bk * 4u;
         empty = -1;
 #pragma unroll
         for (int j = 3; j >= 0; j--)
@@ -765,6 +781,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
     const int K = A.K;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t pmask = (1u << l) - 1u;
+    const bool track = A.e_first != nullptr;  // k-mer positions only for KB_TRACK_FIRST
     uint32_t head = 0, fill = 0;  // wave-uniform ring state
     auto ring = [&](uint32_t i) {
         if constexpr (KW == 1) return TKey<1>{qa[i]};
@@ -772,12 +789,17 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
     };
     auto flush = [&](uint32_t cnt) {  // cnt <= FL entries from head
         wave_sync();
-        uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(ctr, cnt);
-        b = (uint32_t)__shfl((int)b, 0, 64);
+        // the stage reservation and every ring read go out together: one LDS
+        // round trip (LDS returns in order) before the probes
         const uint32_t i0 = (head + lane) & (Q - 1), i1 = (head + 64 + lane) & (Q - 1);
         const bool v0 = (uint32_t)lane < cnt, v1 = FL > 64 && (uint32_t)lane + 64 < cnt;
-        f(ring(i0), qo[i0], qp[i0], b + lane, v0, ring(i1), qo[i1], qp[i1], b + 64 + lane, v1);
+        const TKey<KW> k0 = ring(i0), k1 = ring(i1);
+        const uint32_t o0 = qo[i0], o1 = qo[i1];
+        const uint16_t p0 = track ? qp[i0] : (uint16_t)0, p1 = track ? qp[i1] : (uint16_t)0;
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(ctr, cnt);
+        b = (uint32_t)rfl((int)b);
+        f(k0, o0, p0, b + lane, v0, k1, o1, p1, b + 64 + lane, v1);
         head = (head + cnt) & (Q - 1);
         fill -= cnt;
         wave_sync();
@@ -815,7 +837,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
                 qa[pos] = key.a;
                 if constexpr (KW == 2) qb[pos] = key.b;
                 qo[pos] = ord;
-                qp[pos] = (uint16_t)(rlo + (uint32_t)j);
+                if (track) qp[pos] = (uint16_t)(rlo + (uint32_t)j);
             }
             fill += (uint32_t)__popcll(m);
             if (fill >= FL) flush(FL);
@@ -988,6 +1010,7 @@ DEV void bin_body(const BinArgs& A) {
     unsigned long long pacc[16] = {};
     unsigned long long pt = clock64();
 #endif
+    if (tid < 64) S.dummy[tid] = 0;  // (the first loop barrier publishes it)
 
     while (true) {
         // phase 0: persistent blocks take bins from a shared counter, largest
@@ -1158,11 +1181,37 @@ DEV void bin_body(const BinArgs& A) {
                 if (A.ablate == 1) return;  // expansion only
 #endif
                 const uint32_t h0 = k0.hash(), h1 = k1.hash();
-                // home buckets of both k-mers in flight together; the rest
-                // (new key, full bucket) takes the full insert path
+                // home buckets of both k-mers in flight together
                 int e0_, e1_;
-                int l0 = T.in_bucket(h0 & bmask, k0, e0_);
-                int l1 = T.in_bucket(h1 & bmask, k1, e1_);
+                uint64_t w0[4], w1[4];
+                T.load_bucket(h0 & bmask, w0);
+                T.load_bucket(h1 & bmask, w1);
+                int l0 = T.match(h0 & bmask, w0, k0, e0_);
+                int l1 = T.match(h1 & bmask, w1, k1, e1_);
+                // a new key claims its home bucket's first empty slot right
+                // away (both claims in flight together); the key count is
+                // added per wave and checked against the limit after the
+                // sweep.  A lost claim or a full bucket takes the full insert
+                // path (rare)
+                const uint32_t c0 = (h0 & bmask) * 4u + (uint32_t)e0_, c1 = (h1 & bmask) * 4u + (uint32_t)e1_;
+                // (every lane issues both claims, so they go out back to back:
+                // a lane with nothing to claim compares 1 against its own
+                // always-zero dummy word, which never matches)
+                const bool t0 = v0 && l0 == -1, t1 = v1 && l1 == -1;
+                const uint32_t ln = threadIdx.x & 63u;
+                unsigned long long* a0 = t0 ? (unsigned long long*)&T.ca[c0] : &S.dummy[ln];
+                unsigned long long* a1 = t1 ? (unsigned long long*)&T.ca[c1] : &S.dummy[ln];
+                const uint64_t old0 = atomicCAS(a0, t0 ? 0ull : 1ull, (unsigned long long)k0.a);
+                const uint64_t old1 = atomicCAS(a1, t1 ? 0ull : 1ull, (unsigned long long)k1.a);
+                const bool n0 = t0 && old0 == 0, n1 = t1 && old1 == 0;
+                if constexpr (KW == 2) {
+                    if (n0) __hip_atomic_store(&T.cb[c0], k0.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (n1) __hip_atomic_store(&T.cb[c1], k1.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                if (n0 || (KW == 1 && t0 && old0 == k0.a)) l0 = (int)c0;
+                if (n1 || (KW == 1 && t1 && old1 == k1.a)) l1 = (int)c1;
+                const uint32_t nn = (uint32_t)__popcll(__ballot(n0)) + (uint32_t)__popcll(__ballot(n1));
+                if (nn && (threadIdx.x & 63u) == 0) atomicAdd(&S.n_keys, nn);
                 if (v0 && l0 < 0) l0 = T.insert(bmask, k0, h0, &S.n_keys, limit);
                 if (v1 && l1 < 0) l1 = T.insert(bmask, k1, h1, &S.n_keys, limit);
                 if (v0) {
@@ -1233,7 +1282,7 @@ DEV void bin_body(const BinArgs& A) {
             }
             __syncthreads();
             PROF_MARK(2);
-            if (S.overflow) {  // uniform: split this partition in two and redo both
+            if (S.overflow || S.n_keys > limit) {  // uniform: split this partition in two and redo both
                 PROF_CNT(9, 1);
                 if (tid == 0) {
                     if (Lv >= 20 || S.sp + 2 > BIN_STACK) {

@@ -1,7 +1,4 @@
 # scratch recipe for the current gpurun call (see tools/gpu.sh)
-bash tools/gpu.sh bench base --cpu-sample 0 --steps 20 && \
-KB_BIN_LDS_LISTS=1 bash tools/gpu.sh bench lds100 --cpu-sample 0 --steps 20 && \
-KB_BIN_LDS_LISTS=1 KB_BIN_WIN_PCT=80 bash tools/gpu.sh bench lds80 --cpu-sample 0 --steps 20 && \
-KB_BIN_LDS_LISTS=1 KB_BIN_WIN_PCT=60 bash tools/gpu.sh bench lds60 --cpu-sample 0 --steps 20 && \
-KB_BIN_LDS_LISTS=1 bash tools/gpu.sh test tests/test_gpu_parity.py -k "not dropin" && \
-bash tools/gpu.sh bench cpu --steps 5
+for ab in 0 1 2; do
+KB_BIN_ABLATE=$ab KB_LIB_PATH=genome-assembly_amd/lib/prof/libkbin.so timeout -k 10 300 python bench.py --steps 5 --warmup 2 --cpu-sample 0 --input replay > gpurun_out/prof_ab$ab.json 2> gpurun_out/prof_ab$ab.err || exit 1
+done
