@@ -21,6 +21,7 @@ port beside it, on a bounded sample of the same workload, rank 0 only).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import pathlib
@@ -179,6 +180,85 @@ def cpu_baseline(words, lens, n_avail, n_sample, wpr, L, K, M, cutoff, ref_sampl
             "rows": rows, "port": port}
 
 
+def host_input_leg(words, lens, n, wpr, L, K, M, cutoff, device, batch=1 << 16, reps=3):
+    """The host-ingest path (H2D of input and D2H of output
+    reported separately): the workload's reads as host ASCII go through
+    kb_submit in batches (pinned double-buffered staging, H2D + pack on the
+    context's stream), then kb_finalize, then kb_export (D2H of the CSR into
+    pinned buffers).  Best of `reps` runs; not the bench value."""
+    bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n, wpr, n * L, device=device)
+    raw = np.frombuffer(bases, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(hl.astype(np.int64))])
+    chunks = [(bytes(raw[offs[a]:offs[min(a + batch, n)]]), hl[a:a + batch], a) for a in range(0, n, batch)]
+    best = None
+    with kbin.Engine(K, M, cutoff=cutoff, max_read_len=L, device=device) as eng:
+        for _ in range(reps + 1):  # (the first run sizes the pool and buffers)
+            eng.reset()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for b, ln, a in chunks:
+                eng.submit(bases=b, lens=ln, first_id=int(a))
+            t_ret = time.perf_counter()
+            torch.cuda.synchronize()  # every H2D copy and pack done
+            t1 = time.perf_counter()
+            eng.finalize(prune=True)
+            t2 = time.perf_counter()
+            csr = kbin.kb_csr()  # kb_export alone: the D2H into its pinned buffers, no Python copies
+            rc = eng.lib.kb_export(eng._h, ctypes.byref(csr))
+            t3 = time.perf_counter()
+            if rc:
+                raise RuntimeError(f"kb_export failed: {rc}")
+            row = {"ingest_ms": (t1 - t0) * 1e3, "submit_return_ms": (t_ret - t0) * 1e3,
+                   "finalize_ms": (t2 - t1) * 1e3, "export_ms": (t3 - t2) * 1e3,
+                   "end_to_end_ms": (t3 - t0) * 1e3}
+            if best is None or row["end_to_end_ms"] < best["end_to_end_ms"]:
+                best = row
+        out_bytes = int(csr.n_entries) * (4 + 8 + 8 + 4 + 8) + 8 + int(csr.n_ids) * 4
+    in_bytes = len(raw) + n * 4
+    kmers = n * max(0, L - K + 1)
+    return {"batch_reads": batch, "reads": n,
+            **{k: round(v, 3) for k, v in best.items()},
+            "h2d_GBps": round(in_bytes / best["ingest_ms"] / 1e6, 2),
+            "d2h_GBps": round(out_bytes / best["export_ms"] / 1e6, 2),
+            "end_to_end_kmers_per_s": round(kmers / best["end_to_end_ms"] * 1e3, 1),
+            "note": "host ASCII reads -> kb_submit batches (H2D + 2-bit pack) -> kb_finalize -> kb_export "
+                    "(D2H of the CSR); ingest_ms includes the pack kernel, export_ms the whole CSR copy"}
+
+
+def dropin_leg(words, lens, n, wpr, L, K, M, cutoff, device):
+    """The reference surface end to end: kbin_main is
+    binning.c's main up to the prune -- fgets loop, process_read per read,
+    prune_data -- over libkbin_host (the process_read / prune_data shim) and
+    libkbin.so, on the workload's reads written one per line.  prune_data
+    finalises on the GPU, exports the CSR and materialises the reference's
+    ZHashTable / ll_node tables (first-occurrence insertion order), then
+    prunes them; its phases come from kbh_last_times.  Not the bench value."""
+    import subprocess
+    import tempfile
+    exe = REPO / "genome-assembly_amd" / "lib" / "kbin_main"
+    if not exe.is_file():
+        return {"note": "kbin_main not built"}
+    bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n, wpr, n * L, device=device)
+    raw = np.frombuffer(bases, dtype=np.uint8).reshape(n, L)
+    with tempfile.NamedTemporaryFile(suffix=".txt") as f:
+        f.write(np.concatenate([raw, np.full((n, 1), 10, np.uint8)], axis=1).tobytes())
+        f.flush()
+        env = dict(os.environ, KBH_TIMING="1", KBH_NODUMP="1")
+        t0 = time.perf_counter()
+        r = subprocess.run([str(exe), f.name, str(K), str(M), str(L + 2), str(cutoff), "1", str(device)],
+                           capture_output=True, text=True, timeout=600, env=env)
+        wall = time.perf_counter() - t0
+    if r.returncode:
+        return {"note": f"kbin_main failed rc={r.returncode}: {r.stderr[-300:]}"}
+    row = json.loads(r.stderr.strip().splitlines()[-1])
+    row["process_wall_ms"] = round(wall * 1e3, 1)
+    row["kmers_per_s"] = round(row["kmers"] / row["total_ms"] * 1e3, 1)
+    row["note"] = ("kbin_main: fgets + process_read loop (async batched kb_submit) -> prune_data "
+                   "(kb_finalize, kb_export, materialise zhash/ll_node tables, prune); process_wall_ms adds "
+                   "process start, HIP init and the file read")
+    return row
+
+
 def load_traffic(tag: str, kernel: str):
     """Per-launch HBM bytes of the roofline kernel from the committed rocprofv3
     --pmc passes (profiles/traffic.json, written by tools/pmc_traffic.py):
@@ -230,6 +310,12 @@ def main():
                     help="fresh: every step bins new reads of the same genome (all sets generated before "
                          "timing); replay: the same reads every step; auto: fresh when the sets fit in "
                          "5%% of the HBM")
+    ap.add_argument("--host-input", action="store_true",
+                    help="N=1: also time the host-ingest path (kb_submit of host ASCII, finalize, "
+                         "kb_export) with H2D and D2H reported separately")
+    ap.add_argument("--dropin", action="store_true",
+                    help="N=1: also time the reference surface (kbin_main: fgets + process_read loop, "
+                         "prune_data with materialised zhash tables) on the workload's reads")
     ap.add_argument("--no-scan-once", action="store_true",
                     help="P>1 on one GPU: every pass rescans the reads (kb_set_partition) instead of "
                          "one kb_split_passes scan into the passes' regions")
@@ -543,6 +629,10 @@ def main():
                    "engine": {1: "table", 2: "binned"}.get(int(tim[-1]["engine"]), "?"),
                    "bins": int(tim[-1]["n_bins"]), "superkmers": int(tim[-1]["n_superkmers"])},
     }
+    if rank == 0 and world == 1 and args.host_input and P == 1:
+        out["host_input"] = host_input_leg(sets[0][0], sets[0][1], n, wpr, L, K, M, args.cutoff, local)
+    if rank == 0 and world == 1 and args.dropin and P == 1:
+        out["dropin"] = dropin_leg(sets[0][0], sets[0][1], n, wpr, L, K, M, args.cutoff, local)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(sets[0][0], sets[0][1], n, min(args.cpu_sample, n), wpr, L, K, M,
                                            args.cutoff, args.ref_sample)

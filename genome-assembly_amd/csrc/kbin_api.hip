@@ -75,6 +75,79 @@ struct DevBuf {
     }
 };
 
+// pinned host buffer (page-locked: full-rate DMA both ways), grown on demand
+template <typename T>
+struct PinBuf {
+    T* p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t n) {
+        if (n <= cap && p) return hipSuccess;
+        release();
+        const uint64_t want = std::max<uint64_t>(n, 1) + std::max<uint64_t>(n, 1) / 8;
+        hipError_t e = hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        else p = nullptr;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// Bump allocator over device chunks for the read batches of one context
+// (packed words, lengths, ids, k-mer offsets): kb_reset rewinds it and keeps
+// the chunks, so a streaming job submits batch after batch without a
+// hipMalloc / hipFree per batch.
+struct DevPool {
+    struct Chunk {
+        uint8_t* p;
+        uint64_t cap;
+    };
+    std::vector<Chunk> chunks;
+    size_t cur = 0;
+    uint64_t off = 0;
+    template <typename T>
+    hipError_t alloc(uint64_t n, T** out) {
+        const uint64_t bytes = (std::max<uint64_t>(n, 1) * sizeof(T) + 255) & ~255ull;
+        for (; cur < chunks.size(); cur++, off = 0)
+            if (off + bytes <= chunks[cur].cap) {
+                *out = reinterpret_cast<T*>(chunks[cur].p + off);
+                off += bytes;
+                return hipSuccess;
+            }
+        Chunk ch{nullptr, std::max<uint64_t>(bytes, 64ull << 20)};
+        hipError_t e = hipMalloc((void**)&ch.p, ch.cap);
+        if (e != hipSuccess) return e;
+        chunks.push_back(ch);
+        cur = chunks.size() - 1;
+        off = bytes;
+        *out = reinterpret_cast<T*>(ch.p);
+        return hipSuccess;
+    }
+    void reset() {
+        cur = 0;
+        off = 0;
+    }
+    void release() {
+        for (auto& ch : chunks) (void)hipFree(ch.p);
+        chunks.clear();
+        reset();
+    }
+};
+
+// Host ingest: two staging slots, each a pinned buffer and its device twin
+// (bases | offsets | ids).  kb_submit fills one slot while the other's H2D
+// copy and pack kernel run; `done` (recorded after the slot's pack) gates its
+// reuse, two submits later.
+struct IngestSlot {
+    PinBuf<uint8_t> h;
+    DevBuf<uint8_t> d;
+    hipEvent_t done = nullptr;
+    bool used = false;
+};
+
 struct Batch {
     const uint64_t* words = nullptr;  // adopted or owned
     const uint32_t* lens = nullptr;
@@ -113,11 +186,13 @@ struct kb_ctx {
     int64_t route_id_c = 0;
     DevBuf<unsigned long long> rcount;  // records per destination
 
-    // staging for host submissions
-    char* h_stage = nullptr;
-    uint64_t h_stage_cap = 0;
-    DevBuf<uint8_t> d_bases;
-    DevBuf<uint64_t> d_off;
+    // host ingest (kb_submit): double-buffered pinned staging, pooled batches
+    IngestSlot ring[2];
+    int ring_next = 0;
+    DevPool pool;
+    uint32_t* h_alpha = nullptr;  // pinned: the pack status word after each slot's pack
+    bool alpha_bad = false;       // a submitted read had a byte outside ACGT (sticky until kb_reset)
+    bool ingest_unchecked = false;  // host batches whose alphabet status is not read yet
 
     // finalize working set
     DevBuf<uint64_t> table;
@@ -181,9 +256,9 @@ struct kb_ctx {
     // results
     bool finalized = false;
     uint64_t n_entries = 0, n_ids = 0, n_distinct = 0;
-    std::vector<uint32_t> h_mmer, h_cnt;
-    std::vector<uint64_t> h_hi, h_lo, h_off, h_first;
-    std::vector<int32_t> h_ids;
+    PinBuf<uint32_t> h_mmer, h_cnt;  // pinned: kb_export's D2H at full rate
+    PinBuf<uint64_t> h_hi, h_lo, h_off, h_first;
+    PinBuf<int32_t> h_ids;
     bool exported = false;
 
     // timing
@@ -237,6 +312,13 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
     e = hipHostMalloc((void**)&c->h_totals, 16 * sizeof(uint64_t), hipHostMallocDefault);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
+    e = hipHostMalloc((void**)&c->h_alpha, 2 * sizeof(uint32_t), hipHostMallocDefault);
+    if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
+    c->h_alpha[0] = c->h_alpha[1] = 0;
+    for (auto& sl : c->ring) {
+        e = hipEventCreateWithFlags(&sl.done, hipEventDisableTiming);
+        if (e != hipSuccess) { kb_destroy(c); return fail(KB_EDEVICE, "hipEventCreate"); }
+    }
     if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(16) != hipSuccess ||
         hipMemsetAsync(c->misc.p, 0, 16 * sizeof(uint32_t), c->s) != hipSuccess ||
         hipMemsetAsync(c->totals.p, 0, 16 * sizeof(uint64_t), c->s) != hipSuccess) {
@@ -247,15 +329,13 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     return KB_OK;
 }
 
+// (a batch's words, lengths, ids and k-mer offsets live in c->pool: rewound here)
 static void free_batches(kb_ctx* c) {
     for (auto& b : c->batches) {
-        if (b.own_words) (void)hipFree(b.own_words);
-        if (b.own_lens) (void)hipFree(b.own_lens);
-        if (b.kmer_base) (void)hipFree(b.kmer_base);
-        if (b.ids) (void)hipFree(b.ids);
         if (b.rec_base) (void)hipFree(b.rec_base);
         if (b.route_offs) (void)hipFree(b.route_offs);
     }
+    c->pool.reset();
     c->route_G = 0;
     c->batches.clear();
     c->n_reads = 0;
@@ -267,7 +347,16 @@ extern "C" void kb_destroy(kb_ctx* c) {
     (void)hipSetDevice(c->dev);
     if (c->s) (void)hipStreamSynchronize(c->s);
     free_batches(c);
-    c->d_bases.release(); c->d_off.release(); c->table.release(); c->occ_a.release();
+    for (auto& sl : c->ring) {
+        sl.h.release();
+        sl.d.release();
+        if (sl.done) (void)hipEventDestroy(sl.done);
+    }
+    c->pool.release();
+    c->h_mmer.release(); c->h_cnt.release(); c->h_hi.release(); c->h_lo.release(); c->h_off.release();
+    c->h_first.release(); c->h_ids.release();
+    if (c->h_alpha) (void)hipHostFree(c->h_alpha);
+    c->table.release(); c->occ_a.release();
     c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
     c->regions.release(); c->bfill.release(); c->bbase.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
@@ -279,7 +368,6 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->flat_cur.release(); c->flat_chunk.release(); c->pool_bin.release(); c->chunk_bin.release();
     c->flat_sbase.release(); c->flat_obase.release(); c->flat_n.release();
     if (c->h_totals) (void)hipHostFree(c->h_totals);
-    if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -296,6 +384,11 @@ extern "C" int kb_reset(kb_ctx* c) {
     c->finalized = false;
     c->exported = false;
     c->bucket_failed = false;  // a new input gets the bucketed path again
+    c->alpha_bad = false;
+    c->ingest_unchecked = false;
+    c->h_alpha[0] = c->h_alpha[1] = 0;
+    for (auto& sl : c->ring) sl.used = false;
+    HIPCHK(hipMemsetAsync(c->misc.p + 12, 0, sizeof(uint32_t), c->s));
     c->n_entries = c->n_ids = c->n_distinct = 0;
     c->part = 0;  // back to one full pass
     c->part_n = 1;
@@ -336,7 +429,7 @@ extern "C" int kb_set_partition(kb_ctx* c, uint32_t part, uint32_t n_parts) {
 
 // k-mer offsets of a batch (device scan) and its occurrence total (host sync)
 static int batch_offsets(kb_ctx* c, Batch& b) {
-    HIPCHK(hipMalloc((void**)&b.kmer_base, (b.n_reads + 1) * sizeof(uint64_t)));
+    HIPCHK(c->pool.alloc(b.n_reads + 1, &b.kmer_base));
     const uint64_t need = kmer_base_scratch_elems(b.n_reads);
     HIPCHK(c->scratch.ensure(std::max<uint64_t>(need, c->scratch.cap)));
     HIPCHK(launch_kmer_base(b.lens, b.n_reads, c->p.K, b.kmer_base, c->scratch.p, c->scratch.cap, c->s));
@@ -351,11 +444,32 @@ static int batch_offsets(kb_ctx* c, Batch& b) {
 // the ids array of an affine batch, materialised only where a path needs it
 static int batch_ids(kb_ctx* c, Batch& b) {
     if (b.ids || b.superkmers) return KB_OK;
-    HIPCHK(hipMalloc((void**)&b.ids, std::max<uint64_t>(b.n_reads, 1) * sizeof(int32_t)));
+    HIPCHK(c->pool.alloc(b.n_reads, &b.ids));
     HIPCHK(launch_fill_ids(b.ids, b.n_reads, (int32_t)b.first_id, c->s));
     return KB_OK;
 }
 
+// The alphabet status of the host batches packed so far: the slot snapshot
+// taken after each pack (no wait) or, with sync, the device word itself.
+static int ingest_check(kb_ctx* c, bool sync) {
+    if (!c->alpha_bad && c->ingest_unchecked && sync) {
+        HIPCHK(hipMemcpyAsync(c->h_alpha, c->misc.p + 12, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));
+        c->ingest_unchecked = false;
+        if (c->h_alpha[0] & ST_ALPHABET) c->alpha_bad = true;
+    }
+    if (c->alpha_bad)
+        return fail(KB_EALPHABET, "read byte outside {A,C,G,T} in a submitted batch (see DESIGN.md: alphabet)");
+    return KB_OK;
+}
+
+// binning.c:1150-1166 feeds process_read one fgets line at a time; here the
+// host hands over batches.  A batch is copied into a pinned staging slot (the
+// caller may reuse its buffer on return, as binning.c:1154 does), sent H2D and
+// packed to 2-bit words on the context's stream, and kb_submit returns
+// without waiting: the next submit fills the other slot meanwhile.  The
+// alphabet check rides along (the pack kernel's sticky status word, read back
+// two submits later or by kb_finalize).
 static int submit_common(kb_ctx* c, const char* bases, const uint32_t* lens, uint64_t n_reads,
                          const int32_t* ids, int32_t first_id) {
     if (!c) return fail(KB_EINVAL, "null ctx");
@@ -366,58 +480,58 @@ static int submit_common(kb_ctx* c, const char* bases, const uint32_t* lens, uin
         return fail(KB_EOVERFLOW, "more than 2^32 reads per context");
     int rc = set_device(c);
     if (rc) return rc;
-    // host-side validation (lengths) and offsets
-    std::vector<uint64_t> off(n_reads + 1);
-    off[0] = 0;
     uint32_t maxlen = 0;
+    uint64_t nb = 0;
     for (uint64_t r = 0; r < n_reads; r++) {
         if (lens[r] > (uint32_t)c->p.max_read_len)
             return fail(KB_ETOOLONG, "read %llu has %u bases > max_read_len %d",
                         (unsigned long long)r, lens[r], c->p.max_read_len);
         maxlen = std::max(maxlen, lens[r]);
-        off[r + 1] = off[r] + lens[r];
+        nb += lens[r];
     }
-    const uint64_t nb = off[n_reads];
     const int RW = (int)((std::max<uint32_t>(maxlen, 1) + 31) / 32);
-    // stage through pinned memory (the caller may reuse its buffer on return)
-    if (c->h_stage_cap < nb) {
-        if (c->h_stage) (void)hipHostFree(c->h_stage);
-        c->h_stage = nullptr;
-        c->h_stage_cap = 0;
-        HIPCHK(hipHostMalloc((void**)&c->h_stage, std::max<uint64_t>(nb, 1), hipHostMallocDefault));
-        c->h_stage_cap = std::max<uint64_t>(nb, 1);
+    // slot layout: bases | offsets (u64, 8-B aligned) | ids
+    const uint64_t o_off = (nb + 7) & ~7ull;
+    const uint64_t o_ids = o_off + (n_reads + 1) * sizeof(uint64_t);
+    const uint64_t bytes = o_ids + (ids ? n_reads * sizeof(int32_t) : 0);
+    const int si = c->ring_next;
+    IngestSlot& sl = c->ring[si];
+    if (sl.used) {  // its last H2D + pack (two submits ago) must be done
+        HIPCHK(hipEventSynchronize(sl.done));
+        if (c->h_alpha[si] & ST_ALPHABET) c->alpha_bad = true;
     }
-    HIPCHK(hipStreamSynchronize(c->s));  // staging buffer reuse
-    memcpy(c->h_stage, bases, nb);
-    HIPCHK(c->d_bases.ensure(nb));
-    HIPCHK(c->d_off.ensure(n_reads + 1));
-    HIPCHK(hipMemcpyAsync(c->d_bases.p, c->h_stage, nb, hipMemcpyHostToDevice, c->s));
-    HIPCHK(hipMemcpyAsync(c->d_off.p, off.data(), (n_reads + 1) * sizeof(uint64_t),
-                          hipMemcpyHostToDevice, c->s));
+    rc = ingest_check(c, false);
+    if (rc) return rc;
+    HIPCHK(sl.h.ensure(bytes));
+    HIPCHK(sl.d.ensure(bytes));
+    memcpy(sl.h.p, bases, nb);
+    uint64_t* hoff = reinterpret_cast<uint64_t*>(sl.h.p + o_off);
+    hoff[0] = 0;
+    for (uint64_t r = 0; r < n_reads; r++) hoff[r + 1] = hoff[r] + lens[r];
+    if (ids) memcpy(sl.h.p + o_ids, ids, n_reads * sizeof(int32_t));
+    HIPCHK(hipMemcpyAsync(sl.d.p, sl.h.p, bytes, hipMemcpyHostToDevice, c->s));
     Batch b;
     b.n_reads = n_reads;
     b.RW = RW;
     b.ord_base = c->n_reads;
-    HIPCHK(hipMalloc((void**)&b.own_words, n_reads * (uint64_t)RW * sizeof(uint64_t)));
-    HIPCHK(hipMalloc((void**)&b.own_lens, n_reads * sizeof(uint32_t)));
-    if (ids) HIPCHK(hipMalloc((void**)&b.ids, n_reads * sizeof(int32_t)));
+    HIPCHK(c->pool.alloc(n_reads * (uint64_t)RW, &b.own_words));
+    HIPCHK(c->pool.alloc(n_reads, &b.own_lens));
     b.words = b.own_words;
     b.lens = b.own_lens;
-    HIPCHK(hipMemsetAsync(c->misc.p, 0, sizeof(uint32_t), c->s));
-    HIPCHK(launch_pack(c->d_bases.p, c->d_off.p, n_reads, RW, b.own_words, b.own_lens, c->misc.p, c->s));
+    HIPCHK(launch_pack(sl.d.p, reinterpret_cast<const uint64_t*>(sl.d.p + o_off),
+                       n_reads, RW, b.own_words, b.own_lens, c->misc.p + 12, c->s));
     if (ids) {
-        HIPCHK(hipMemcpyAsync(b.ids, ids, n_reads * sizeof(int32_t), hipMemcpyHostToDevice, c->s));
+        HIPCHK(c->pool.alloc(n_reads, &b.ids));
+        HIPCHK(hipMemcpyAsync(b.ids, sl.d.p + o_ids, n_reads * sizeof(int32_t), hipMemcpyDeviceToDevice, c->s));
     } else {
         b.affine = true;
         b.first_id = first_id;
     }
-    uint32_t st = 0;
-    HIPCHK(hipMemcpyAsync(&st, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
-    if (st & ST_ALPHABET) {
-        (void)hipFree(b.own_words); (void)hipFree(b.own_lens); (void)hipFree(b.ids);
-        return fail(KB_EALPHABET, "read byte outside {A,C,G,T} (see DESIGN.md: alphabet)");
-    }
+    HIPCHK(hipMemcpyAsync(c->h_alpha + si, c->misc.p + 12, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipEventRecord(sl.done, c->s));
+    sl.used = true;
+    c->ring_next ^= 1;
+    c->ingest_unchecked = true;
     c->n_reads += n_reads;
     c->batches.push_back(b);
     return KB_OK;
@@ -1506,6 +1620,8 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     if (c->finalized) return fail(KB_ESTATE, "already finalized (call kb_reset)");
     int rc = set_device(c);
     if (rc) return rc;
+    rc = ingest_check(c, true);  // every host batch packed so far was ACGT
+    if (rc) return rc;
     // active batches: unrouted reads, or received super-k-mers (not both)
     bool any_reads = false, any_sk = false;
     for (auto& b : c->batches) {
@@ -1735,27 +1851,27 @@ extern "C" int kb_export(kb_ctx* c, kb_csr* out) {
     if (rc) return rc;
     if (!c->exported) {
         const uint64_t n = c->n_entries;
-        c->h_mmer.resize(n);
-        c->h_cnt.resize(n);
-        c->h_hi.resize(n);
-        c->h_lo.resize(n);
-        c->h_off.resize(n + 1);
         const bool tf = (c->p.flags & KB_TRACK_FIRST) != 0;
-        c->h_first.resize(tf ? n : 0);
-        c->h_ids.resize(c->n_ids);
+        HIPCHK(c->h_mmer.ensure(n));
+        HIPCHK(c->h_cnt.ensure(n));
+        HIPCHK(c->h_hi.ensure(n));
+        HIPCHK(c->h_lo.ensure(n));
+        HIPCHK(c->h_off.ensure(n + 1));
+        if (tf) HIPCHK(c->h_first.ensure(n));
+        HIPCHK(c->h_ids.ensure(c->n_ids));
         if (n) {
-            HIPCHK(hipMemcpyAsync(c->h_mmer.data(), c->e_mmer.p, n * 4, hipMemcpyDeviceToHost, c->s));
-            HIPCHK(hipMemcpyAsync(c->h_cnt.data(), c->e_cnt.p, n * 4, hipMemcpyDeviceToHost, c->s));
-            HIPCHK(hipMemcpyAsync(c->h_hi.data(), c->e_hi.p, n * 8, hipMemcpyDeviceToHost, c->s));
-            HIPCHK(hipMemcpyAsync(c->h_lo.data(), c->e_lo.p, n * 8, hipMemcpyDeviceToHost, c->s));
-            HIPCHK(hipMemcpyAsync(c->h_off.data(), c->e_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_mmer.p, c->e_mmer.p, n * 4, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_cnt.p, c->e_cnt.p, n * 4, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_hi.p, c->e_hi.p, n * 8, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_lo.p, c->e_lo.p, n * 8, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_off.p, c->e_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->s));
             if (tf)
-                HIPCHK(hipMemcpyAsync(c->h_first.data(), c->e_first.p, n * 8, hipMemcpyDeviceToHost, c->s));
+                HIPCHK(hipMemcpyAsync(c->h_first.p, c->e_first.p, n * 8, hipMemcpyDeviceToHost, c->s));
         } else {
-            c->h_off[0] = 0;
+            c->h_off.p[0] = 0;
         }
         if (c->n_ids)
-            HIPCHK(hipMemcpyAsync(c->h_ids.data(), c->ids_out.p, c->n_ids * 4, hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_ids.p, c->ids_out.p, c->n_ids * 4, hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipStreamSynchronize(c->s));
         c->exported = true;
     }
@@ -1763,13 +1879,13 @@ extern "C" int kb_export(kb_ctx* c, kb_csr* out) {
     out->n_ids = c->n_ids;
     out->n_kmers = c->n_occ;
     out->n_distinct = c->n_distinct;
-    out->mmer = c->h_mmer.data();
-    out->kmer_hi = c->h_hi.data();
-    out->kmer_lo = c->h_lo.data();
-    out->count = c->h_cnt.data();
-    out->offset = c->h_off.data();
-    out->ids = c->h_ids.data();
-    out->first = (c->p.flags & KB_TRACK_FIRST) ? c->h_first.data() : nullptr;
+    out->mmer = c->h_mmer.p;
+    out->kmer_hi = c->h_hi.p;
+    out->kmer_lo = c->h_lo.p;
+    out->count = c->h_cnt.p;
+    out->offset = c->h_off.p;
+    out->ids = c->h_ids.p;
+    out->first = (c->p.flags & KB_TRACK_FIRST) ? c->h_first.p : nullptr;
     return KB_OK;
 }
 

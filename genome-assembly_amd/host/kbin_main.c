@@ -5,10 +5,15 @@
  * materialised two-level table (instead of the reference's unitig steps).
  *
  *   kbin_main <reads-file> <K> <M> <READ_LENGTH> <cutoff> <prune 0|1> [device]
+ *
+ * KBH_TIMING=1 in the environment: one JSON line of wall-clock phases on
+ * stderr (read loop = fgets + process_read; then prune_data's phases);
+ * KBH_NODUMP=1 skips the dump (timing runs).
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/binning_gpu.h"
 
@@ -28,20 +33,37 @@ int main(int argc, char **argv)
         perror(argv[1]);
         return 2;
     }
+    const char *tenv = getenv("KBH_TIMING"), *denv = getenv("KBH_NODUMP");
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     struct ZHashTable *hash_table = zcreate_hash_table();
     char *read = malloc((size_t)rl + 1);
     int read_id = 0;
+    long long kmers = 0;
     while (fgets(read, rl, file) != NULL) { /* binning.c:1158-1166 */
         int len = (int)strlen(read);
         read[--len] = '\0';
+        if (len >= K) kmers += len - K + 1;
         process_read(hash_table, read, read_id++);
     }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
     fclose(file);
     free(read);
     if (prune)
         prune_data(hash_table);
     else
         kbh_finish_unpruned(hash_table);
-    kbh_dump_table(hash_table, stdout);
+    if (tenv && *tenv == '1') {
+        kbh_times t;
+        kbh_last_times(&t);
+        const double loop = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6;
+        fprintf(stderr,
+                "{\"reads\": %d, \"kmers\": %lld, \"read_loop_ms\": %.3f, \"finalize_ms\": %.3f, "
+                "\"export_ms\": %.3f, \"materialise_ms\": %.3f, \"prune_ms\": %.3f, \"total_ms\": %.3f, "
+                "\"entries\": %llu, \"ids\": %llu, \"nodes\": %llu}\n",
+                read_id, kmers, loop, t.finalize_ms, t.export_ms, t.materialise_ms, t.prune_ms, loop + t.total_ms,
+                (unsigned long long)t.entries, (unsigned long long)t.ids, (unsigned long long)t.nodes);
+    }
+    if (!(denv && *denv == '1')) kbh_dump_table(hash_table, stdout);
     return 0;
 }

@@ -44,6 +44,19 @@ int kbh_configure(int K, int M, int cutoff, int device);
 /* like prune_data but without the prune (every key kept) */
 struct ZHashTable *kbh_finish_unpruned(struct ZHashTable *hash_table);
 
+/* wall-clock phases of the last prune_data / kbh_finish_unpruned */
+typedef struct {
+    double finalize_ms;     /* flush + kb_finalize (device binning, every key) */
+    double export_ms;       /* kb_export: D2H of the CSR */
+    double materialise_ms;  /* zhash / ll_node tables in first-occurrence order */
+    double prune_ms;        /* prune_kmers semantics on the tables */
+    double total_ms;
+    uint64_t entries;       /* keys materialised (all, before the prune) */
+    uint64_t ids;           /* ids exported */
+    uint64_t nodes;         /* ll_nodes allocated (kept keys only when pruning) */
+} kbh_times;
+int kbh_last_times(kbh_times *out);
+
 /* drop the engine context bound to hash_table (the tables stay) */
 void kbh_release(struct ZHashTable *hash_table);
 

@@ -122,7 +122,13 @@ void kb_destroy(kb_ctx *ctx);
 /* Append a batch of reads from host memory.  Reads are concatenated in
  * `bases`, `lens[r]` bytes each; read r gets id first_id + r and call ordinal
  * (its position in the stream of all submitted reads).  The bytes are copied
- * before return (the caller may reuse its buffer, as binning.c:1154/1158 does).
+ * into one of two pinned staging slots before return (the caller may reuse its
+ * buffer, as binning.c:1154/1158 does); the H2D copy and the 2-bit pack run
+ * asynchronously on the context's stream while the caller prepares the next
+ * batch (a submit waits only for the slot it reuses, two submits back).  Batch
+ * memory comes from a per-context device pool that kb_reset rewinds.
+ * A byte outside ACGT is reported as KB_EALPHABET by a later kb_submit or, at
+ * the latest, by kb_finalize; the context then stays failed until kb_reset.
  * Replaces the per-call process_read(hash, read, id) (binning.c:902). */
 int kb_submit(kb_ctx *ctx, const char *bases, const uint32_t *lens,
               uint64_t n_reads, int32_t first_id);

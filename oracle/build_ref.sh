@@ -79,8 +79,8 @@ case $MODE in
       objcopy --weaken-symbol=process_read --weaken-symbol=prune_data "$TMP/binning.o"
       # the shim includes our kb_zhash.h (same layout as zhash.h/llist.h); its
       # container calls resolve to the reference's zhash.o / llist.o
-      gcc -O2 -w $DEFS -c "$REPO/genome-assembly_amd/host/binning_gpu.c" -o "$TMP/shim.o"
-      gcc "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/shim.o" -L"$LIB" -lkbin \
+      gcc -O2 -w -pthread $DEFS -c "$REPO/genome-assembly_amd/host/binning_gpu.c" -o "$TMP/shim.o"
+      gcc -pthread "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/shim.o" -L"$LIB" -lkbin \
           -Wl,-rpath,"\$ORIGIN/../../genome-assembly_amd/lib" -o "$BIN"
     fi
     ;;

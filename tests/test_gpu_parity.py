@@ -397,11 +397,50 @@ def test_split_bins(genome, flat_l, ts_log2, K, engine, monkeypatch):
 
 
 def test_alphabet_rejected():
-    """bytes outside ACGT are rejected loudly (alphabet)"""
+    """bytes outside ACGT are rejected loudly (alphabet): kb_submit
+    returns before the pack kernel has run, so the error surfaces at the next
+    submits or at the latest at kb_finalize, and sticks until kb_reset"""
     with kbin.Engine(11, 4) as eng:
         with pytest.raises(kbin.KbError) as ei:
             eng.submit([b"ACGTNACGTACGTACG"])
+            for _ in range(3):
+                eng.submit([b"ACGTACGTACGTACG"])
+            eng.finalize(True)
         assert ei.value.code == kbin.KB_EALPHABET
+        with pytest.raises(kbin.KbError) as ei:
+            eng.finalize(True)
+        assert ei.value.code == kbin.KB_EALPHABET
+        eng.reset()  # a new input is clean again
+        reads = [b"ACGTACGTTCGTACGTA", b"ACGTACGTTCGTACGTA", b"GGCATTACGAGGTTACA"]
+        eng.submit(reads)
+        eng.finalize(True)
+        assert_same(eng.export(), oracle.bin_reads(b"".join(reads), [len(r) for r in reads], 11, 4, 1, True))
+
+
+def test_streaming_submits_reuse_buffer():
+    """kb_submit copies in and returns without waiting (double-buffered pinned
+    staging, pooled device batches): 40 batches of varying size, each written
+    into ONE host buffer that is overwritten right after its submit, equal the
+    oracle on the whole input; then again after kb_reset (pool and slots reused)"""
+    import ctypes as C
+    rng = np.random.default_rng(17)
+    L, n = 150, 24_000
+    genome = rng.integers(0, 4, 400_000)
+    st = rng.integers(0, len(genome) - L + 1, n)
+    raw = np.frombuffer(b"TGCA", dtype=np.uint8)[genome[st[:, None] + np.arange(L)]].reshape(-1)
+    lens = np.full(n, L, dtype=np.uint32)
+    ora = oracle.bin_reads(raw.tobytes(), lens, 31, 7, 1, True)
+    cuts = np.unique(np.concatenate([[0, n], rng.integers(0, n, 39)]))
+    buf = C.create_string_buffer(len(raw))
+    with kbin.Engine(31, 7, cutoff=1, max_read_len=L) as eng:
+        for _ in range(2):
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                C.memmove(buf, raw[a * L:b * L].tobytes(), int(b - a) * L)
+                eng.submit(bases=buf, lens=lens[a:b], first_id=int(a))
+                C.memset(buf, ord("N"), len(raw))  # the caller's buffer is free on return
+            eng.finalize(True)
+            assert_same(eng.export(), ora)
+            eng.reset()
 
 
 def test_host_cli_process_read_prune_data(digests, golden_dir):
