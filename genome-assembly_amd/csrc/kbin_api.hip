@@ -51,10 +51,11 @@ struct DevBuf {
     uint64_t cap = 0;
     hipError_t ensure(uint64_t n) {
         if (n <= cap && p) return hipSuccess;
-        // growing an existing buffer: 1/8 headroom, so passes whose sizes
-        // wander by a few percent do not free and map tens of GB each time
+        // 1/8 headroom, so passes whose sizes wander by a few percent (the
+        // partitioned passes of one job) do not free and map tens of GB each
+        // time (fresh device memory is cleared at roughly 20-25 GB/s)
         uint64_t want = std::max<uint64_t>(n, 1);
-        if (p) want += want / 8;
+        want += want / 8;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -226,11 +227,15 @@ struct kb_ctx {
     DevBuf<uint64_t> regions;  // local bucket regions (pay layout)
     DevBuf<unsigned long long> bfill;  // records per bucket
     DevBuf<uint64_t> bbase;  // [NB + 1] bucket output bases (bucket_bases_kernel)
+    DevBuf<uint64_t> rbase;  // [NB + 1] exact region bases (a pass without a learned map)
+    bool rexact = false;     // the regions of the last record pass use rbase
     uint64_t bucket_cap = 0;   // learned region capacity (records per bucket)
     uint64_t bucket_cap_used = 0;  // the capacity (region stride) the regions were written with
     DevBuf<uint64_t> kpart;    // per-block k-mer sums of the count pass
     float rho = 0.f;           // learned distinct / occurrences
     float kept_ratio = 1.f;    // learned kept ids / occurrences (the LDS list window's depth)
+    float rho_tab = 0.f;       // learned table keys / occurrences under the singleton pre-filter
+    DevBuf<uint32_t> hll;      // cold pass: HyperLogLog registers (launch_hll)
     bool bucket_failed = false;  // a bucket overflowed its mmer map: radix path from now on
     uint64_t n_occ_entries_hint = 0;  // entries of the last finalize (lists grid)
     uint64_t ecap_hint = 0;    // entry capacity for the next binned finalize
@@ -358,7 +363,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->h_alpha) (void)hipHostFree(c->h_alpha);
     c->table.release(); c->occ_a.release();
     c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
-    c->regions.release(); c->bfill.release(); c->bbase.release(); c->kpart.release(); c->rcount.release();
+    c->regions.release(); c->bfill.release(); c->bbase.release(); c->rbase.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
@@ -366,7 +371,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     for (auto& m : c->bmaps) { m.map.release(); m.run.release(); m.run_mmer.release(); }
     c->flat_list.release(); c->flat_next.release(); c->flat_l0.release(); c->flat_off.release();
     c->flat_cur.release(); c->flat_chunk.release(); c->pool_bin.release(); c->chunk_bin.release();
-    c->flat_sbase.release(); c->flat_obase.release(); c->flat_n.release();
+    c->flat_sbase.release(); c->flat_obase.release(); c->flat_n.release(); c->hll.release();
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
     for (auto& ev : c->ev)
@@ -1166,6 +1171,9 @@ static int bmap_build(kb_ctx* c, uint32_t NB) {
     m->stale = false;
     m->want_max = want_max;
     m->want_tot = want_tot;
+    // the region stride the next map-routed pass starts with (one pass when
+    // the packing holds; a larger bucket reruns it bigger)
+    c->bucket_cap = std::max<uint64_t>(c->bucket_cap, want_max + want_max / 4 + 1024);
     return KB_OK;
 }
 
@@ -1193,27 +1201,36 @@ static int bmap_learn(kb_ctx* c, uint32_t NB, uint64_t R, uint64_t nbins) {
 // received: the block-aggregated converter.  Returns R and N (one sync per try).
 static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, uint64_t& N) {
     const int M = c->p.M;
-    uint64_t nrec = 0;
-    for (auto& b : c->batches)
-        if (!b.routed) nrec += b.superkmers ? b.n_reads : b.n_reads * 16;
     kb_ctx::BucketMap* bm = bmap_find(c, NB);
     const uint16_t* bmap = bm ? bm->map.p : nullptr;
+    // Without a learned map for this (part, part_n) key (a context's first
+    // pass, or a partition's first) the records are routed by hash and the
+    // buckets are uneven (the largest ~8x the mean): a counting pass first
+    // (capacity 0: every record counted, none written), then regions laid out
+    // exactly (rbase).  With a map, one pass into regions of the learned
+    // capacity (stride), rerun bigger on overflow.
+    const bool exact = bmap == nullptr;
+    HIPCHK(c->bfill.ensure(NB));
+    uint64_t kp = 1;
+    for (auto& b : c->batches) kp = std::max(kp, sk_blocks(b.n_reads, b.RW));
+    HIPCHK(c->kpart.ensure(kp));
+    if (exact) HIPCHK(c->rbase.ensure(NB + 1));
+    HIPCHK(c->regions.ensure(1));  // (non-null: the record kernel's region mode keys on it)
+    const uint64_t RWD = 1 + 2 * (uint64_t)c->KW;
     for (int attempt = 0; attempt < 3; attempt++) {
-        const uint64_t cap = c->bucket_cap ? c->bucket_cap : nrec / NB + 1024;
-        HIPCHK(c->regions.ensure(NB * cap * (1 + 2 * c->KW)));
-        HIPCHK(c->bfill.ensure(NB));
+        const bool counting = exact && attempt == 0;
+        const bool use_base = exact && attempt > 0;
+        const uint64_t cap = exact ? 0 : c->bucket_cap;
         HIPCHK(hipMemsetAsync(c->bfill.p, 0, NB * sizeof(unsigned long long), c->s));
         HIPCHK(hipMemsetAsync(c->totals.p + 8, 0, sizeof(uint64_t), c->s));
         HIPCHK(hipMemsetAsync(c->misc.p, 0, sizeof(uint32_t), c->s));
-        uint64_t kp = 1;
-        for (auto& b : c->batches) kp = std::max(kp, sk_blocks(b.n_reads, b.RW));
-        HIPCHK(c->kpart.ensure(kp));
+        if (!counting && !use_base) HIPCHK(c->regions.ensure(NB * cap * RWD));
         for (auto& b : c->batches) {
             if (b.routed || !b.n_reads) continue;
             if (received) {
                 if (!b.superkmers) continue;
                 HIPCHK(launch_sk_convert_buckets(b.recs, b.n_reads, rec_words(c), 2 * c->KW, M, NB, bmap, c->regions.p, cap,
-                                                 c->bfill.p, c->misc.p,
+                                                 use_base ? c->rbase.p : nullptr, c->bfill.p, c->misc.p,
                                                  reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
             } else {
                 if (b.superkmers) continue;
@@ -1229,10 +1246,11 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
                 a.M = M;
                 a.regions = c->regions.p;
                 a.region_cap = cap;
+                a.region_base = use_base ? c->rbase.p : nullptr;
                 a.dest_ctr = c->bfill.p;
                 a.G = NB;
                 a.dest_salt = sk_bucket_salt();
-                a.rw = 1 + 2 * c->KW;  // header + span words
+                a.rw = (int)RWD;  // header + span words
                 a.bucket_map = bmap;
                 a.binned_fmt = 1;
                 a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p);
@@ -1243,11 +1261,11 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
             }
             c->tm.scan_insert_launches++;
         }
-        std::vector<unsigned long long> fill(NB);  // (bmap: see below)
+        std::vector<unsigned long long> fill(NB);
         HIPCHK(hipMemcpyAsync(fill.data(), c->bfill.p, NB * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
-        HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync: R and N size the rest
+        HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync (two without a map): R and N size the rest
         if (c->h_misc[0] & ST_NEG_ID)
             return fail(KB_EINVAL, "routed read ids must be non-negative (they order the id lists)");
         R = 0;
@@ -1257,14 +1275,23 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
             mx = std::max<uint64_t>(mx, fill[d]);
         }
         N = c->h_totals[8];
+        if (counting) {  // exact bases for the writing pass
+            std::vector<uint64_t> base(NB + 1, 0);
+            for (uint32_t d = 0; d < NB; d++) base[d + 1] = base[d] + fill[d];
+            HIPCHK(c->regions.ensure(std::max<uint64_t>(R, 1) * RWD));
+            HIPCHK(hipMemcpyAsync(c->rbase.p, base.data(), (NB + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->s));
+            HIPCHK(hipStreamSynchronize(c->s));  // (base is a local)
+            continue;
+        }
         // a map that no longer fits (largest bucket > 1.5x what the packing
         // expected, scaled to this pass's records): relearn it after this pass
         if (bm && R && bm->want_tot &&
             (double)mx > 1.5 * (double)bm->want_max * (double)R / (double)bm->want_tot + 64.0)
             bm->stale = true;
-        if (mx <= cap) {
-            c->bucket_cap_used = cap;  // the region stride of this pass
-            c->bucket_cap = std::max<uint64_t>(c->bucket_cap, mx + mx / 8 + 1024);  // next passes
+        if (use_base || mx <= cap) {
+            c->rexact = use_base;
+            c->bucket_cap_used = cap;  // the region stride of this pass (0: exact bases)
+            if (!use_base) c->bucket_cap = std::max<uint64_t>(c->bucket_cap, mx + mx / 8 + 1024);  // next passes
             if (N >= 0xFFFFFFFFull)
                 return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
                             (unsigned long long)N);
@@ -1273,7 +1300,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
                             (unsigned long long)N);
             return KB_OK;
         }
-        c->bucket_cap = mx + mx / 4 + 1024;  // grow and rerun the pass
+        c->bucket_cap = mx + mx / 8 + 1024;  // grow and rerun the pass
     }
     return fail(KB_EDEVICE, "internal: bucket capacity did not converge");
 }
@@ -1369,6 +1396,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         BucketArgs ba{};
         ba.regions = c->regions.p;
         ba.cap = c->bucket_cap_used;
+        ba.rbase = c->rexact ? c->rbase.p : nullptr;
         ba.bfill = c->bfill.p;
         ba.M = M;
         ba.hdr = c->srec.p;
@@ -1416,6 +1444,23 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     }
     HIPCHK(c->border.ensure(max_bins));
     HIPCHK(launch_bins_order(c->bcount.p, c->totals.p, c->border.p, max_bins, c->s));
+    if (c->rho <= 0.f && N && env_int("KB_BIN_HLL", 1)) {
+        // the context's first finalize: distinct keys per occurrence from one
+        // HyperLogLog over the records (no learned density yet)
+        BinArgs h{};
+        h.hdr = c->srec.p;
+        h.w0 = c->srec.p + R;
+        h.w1 = c->srec.p + 2 * R;
+        h.w2 = KW == 2 ? c->srec.p + 3 * R : nullptr;
+        h.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
+        h.K = c->p.K;
+        HIPCHK(c->hll.ensure(4096));
+        HIPCHK(launch_hll(h, R, KW, c->hll.p, c->s));
+        std::vector<uint32_t> regs(4096);
+        HIPCHK(hipMemcpyAsync(regs.data(), c->hll.p, 4096 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));
+        c->rho = (float)std::min(1.0, std::max(1e-4, hll_estimate(regs.data()) / (double)N));
+    }
     REC(3);
     // ---- one workgroup per bin.  Entry capacity: learned (or N/8), rerun once
     // with the exact need when the packed counter says it was exceeded.
@@ -1433,7 +1478,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(c->e_off.ensure(ecap));
         if (attempt) {  // the bin kernel's counters and status start again
             HIPCHK(hipMemsetAsync(c->totals.p + 4, 0, 4 * sizeof(uint64_t), c->s));
-            HIPCHK(hipMemsetAsync(c->totals.p + 10, 0, sizeof(uint64_t), c->s));
+            HIPCHK(hipMemsetAsync(c->totals.p + 10, 0, 2 * sizeof(uint64_t), c->s));
             HIPCHK(hipMemsetAsync(c->misc.p + 2, 0, sizeof(uint32_t), c->s));
             REC(3);
         }
@@ -1520,6 +1565,16 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             a.lq_cap = ecap;
         }
         a.kept_ratio = c->kept_ratio;
+        // singleton pre-filter for the heavy bins: where most distinct keys are
+        // pruned singletons (high error rates, low coverage: C5), learned from
+        // the last finalize; exact because a key seen once has count 1 <= cutoff
+        {
+            const int pf_env = env_int("KB_BIN_PF", -1);
+            const bool pf_ok = prune && c->p.cutoff >= 1 && !(c->p.flags & KB_TRACK_FIRST) && flat_l;
+            a.pf = pf_ok && (pf_env == 1 || (pf_env < 0 && c->rho >= 0.3f && c->rho_tab > 0.f)) ? 1u : 0u;
+            a.rho_tab = c->rho_tab > 0.f ? c->rho_tab : a.rho;
+            a.tab_keys = reinterpret_cast<unsigned long long*>(c->totals.p + 11);
+        }
         a.win_fill = (float)std::min(1.2, std::max(0.3, env_int("KB_BIN_WIN_PCT", 100) / 100.0));
         HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr));
 #ifdef KB_BIN_PROF
@@ -1547,7 +1602,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         lists_prof_report(c->s);
 #endif
         REC(5);
-        HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 12 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         if (R && !bucketed)
             HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
@@ -1598,6 +1653,10 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     c->ecap_hint = c->n_entries + c->n_entries / 4 + 1024;
     if (N) c->rho = (float)((double)c->n_distinct / (double)N);
     if (N) c->kept_ratio = std::max(0.01f, (float)((double)c->n_ids / (double)N));
+    // keys the tables will hold under the pre-filter: measured when it ran,
+    // else the kept keys plus a margin for sketch collisions and counts 2..cutoff
+    if (N) c->rho_tab = a.pf ? (float)((double)c->h_totals[11] / (double)N * 1.05)
+                             : std::min(c->rho, (float)((double)c->n_entries / (double)N * 1.3 + 0.01));
     if (c->timing) {
         HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));
         HIPCHK(hipEventElapsedTime(&c->tm.sort_ms, c->ev[2], c->ev[3]));

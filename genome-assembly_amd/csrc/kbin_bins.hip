@@ -21,6 +21,7 @@
 // Nothing in the hot loops touches HBM at random except the read-word gathers
 // (L2/MALL-resident packed reads) and the output writes.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 
 #include "kbin_internal.h"
@@ -284,8 +285,8 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     } else if (route) {  // many destinations: one record, its own slot
                         const uint32_t d = region_of(A, (uint32_t)best, (r << 16) | (uint64_t)lo);
                         const uint64_t i = atomicAdd(&A.dest_ctr[d], 1ull);
-                        if (i < A.region_cap)
-                            put_record(A, A.regions + (d * A.region_cap + i) * (uint64_t)A.rw,
+                        if (i < region_room(A.region_base, A.region_cap, d))
+                            put_record(A, A.regions + (region_off(A.region_base, A.region_cap, d) + i) * (uint64_t)A.rw,
                                        A.ord_base + (uint32_t)r, (uint64_t)lo, n, (uint64_t)(sig - lo), rev, sw);
                     } else {  // ordered records beyond the staging area: direct (scattered) stores
                         const uint64_t t = rbase + nseg;
@@ -336,9 +337,9 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                         (uint64_t)dbase[d] +
                         (agg ? wave_dest_add(dcnt2, d)
                              : ((atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1))) >> (16 * (d & 1))) & 0xFFFFu));
-                    if (slot >= A.region_cap) continue;  // counted: the caller retries bigger
+                    if (slot >= region_room(A.region_base, A.region_cap, d)) continue;  // counted: the caller retries bigger
                     const uint32_t row = (uint32_t)((e >> 29) & 0xFFu);
-                    put_record(A, A.regions + (d * A.region_cap + slot) * (uint64_t)A.rw,
+                    put_record(A, A.regions + (region_off(A.region_base, A.region_cap, d) + slot) * (uint64_t)A.rw,
                                A.ord_base + (uint32_t)(r0 + row), e & 0xFFFFu, (e >> 16) & 63u, (e >> 22) & 63u,
                                (e >> 28) & 1u, smem + row * RS);
                 }
@@ -565,6 +566,7 @@ DEV uint64_t lds_load_u64(const uint64_t* p) {
 
 struct alignas(16) BinShared {
     uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, part0;
+    uint32_t n_single, pad_[3];  // pre-filter: keys seen once in this partition
     unsigned long long e0, i0, stage_base;
     uint32_t flat_idx, fa, fb, l0;
     uint32_t stack_p[BIN_STACK], stack_l[BIN_STACK];
@@ -908,6 +910,17 @@ constexpr int FB_THREADS = 256;        // the build kernels' blocks
 constexpr uint32_t FB_CHUNK = 1024;    // records per build item
 constexpr uint32_t SPLIT_BIT = 0x100u;     // flat_l0: a split bin's partitions (no flat lists)
 constexpr uint32_t PRUNED = 0x80000000u;  // cursor of a pruned (or empty) slot in sweep 2
+constexpr uint32_t PF_BIT = 0x200u;        // flat_l0: a heavy bin sized for the singleton pre-filter
+constexpr double PF_LOAD = 0.06;           // sketch load (distinct keys / cells) the partition depth aims at
+
+// the pre-filter's sketch cell of a key (independent of the table hash, whose
+// bucket comes from the low bits, and of the partition bits)
+DEV uint32_t sk_cell(const TKey<1>& k, uint32_t cells) {
+    return (uint32_t)(((mix64(k.a - 1ull) >> 32) * (uint64_t)cells) >> 32);
+}
+DEV uint32_t sk_cell(const TKey<2>& k, uint32_t cells) {
+    return (uint32_t)((((k.h64() >> 8) & 0xFFFFFFFFull) * (uint64_t)cells) >> 32);
+}
 constexpr uint64_t M48 = (1ull << 48) - 1ull;
 
 // LDS path of one partition, after its prune: the kept occurrences' ordinals
@@ -935,7 +948,8 @@ DEV void lds_lists(const BinArgs& A, uint32_t* cnt, uint32_t* win, uint32_t ns,
     for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
         if (filt && (kst_load<KW>(kst, i).part() & pmask) != P) continue;
         const uint64_t v = stage[i];
-        const uint32_t pos = atomicAdd(&cnt[(uint32_t)(v >> 48)], 1u);
+        if (!(v >> 48)) continue;  // a pre-filtered single
+        const uint32_t pos = atomicAdd(&cnt[(uint32_t)(v >> 48) - 1u], 1u);
         if (pos < PRUNED) win[pos] = (uint32_t)v + 1u;  // ordinal + 1 (0 pads the sorts)
     }
     __syncthreads();
@@ -1106,6 +1120,18 @@ DEV void bin_body(const BinArgs& A) {
             const double kept = (double)occ_tot * (double)A.kept_ratio;
             while (l0 < 12 && kept > (double)A.win_fill * (double)win_cap * (double)(1u << l0)) l0++;
         }
+        // pre-filtered heavy bin: partitions sized by the keys that enter the
+        // table and by the sketch (both fewer than the distinct keys)
+        const uint32_t sk_words = (uint32_t)BIN_WAVES * Q * (8u * KW + 6u) / 4u, sk_cells = sk_words * 16u;
+        bool pfb = PHASE == 1 ? flat && (S.l0 & PF_BIT) : false;
+        if (PHASE == 0 && flat && A.pf) {
+            const double want_t = (double)occ_tot * A.rho_tab / ((double)A.fill * TS);
+            const double want_s = (double)occ_tot * A.rho / (PF_LOAD * (double)sk_cells);
+            const double want = want_t > want_s ? want_t : want_s;
+            l0 = 0;
+            while ((double)(1u << l0) < want && l0 < 16) l0++;
+            pfb = true;
+        }
         uint64_t* kst = A.kstage + KW * S.stage_base;
         if ((split || flat) && PHASE == 0) {
             // publish: flat_count_kernel counts the k-mers per partition (any
@@ -1130,7 +1156,7 @@ DEV void bin_body(const BinArgs& A) {
             if (tid == 0) {
                 A.flat_obase[b] = S.e0;
                 A.flat_sbase[b] = S.stage_base;
-                A.flat_l0[b] = l0 | (split ? SPLIT_BIT : 0u);
+                A.flat_l0[b] = l0 | (split ? SPLIT_BIT : 0u) | (pfb ? PF_BIT : 0u);
                 A.flat_chunk[b] = (uint32_t)S.i0;
                 A.flat_list[atomicAdd(A.flat_n, 1ull)] = b;
             }
@@ -1161,12 +1187,16 @@ DEV void bin_body(const BinArgs& A) {
                 S.n_keys = 0;
                 S.overflow = 0;
                 S.n_stage = 0;
+                S.n_single = 0;
             }
             for (uint32_t i = tid; i < TS; i += BIN_THREADS) {
                 T.ca[i] = 0;
                 if constexpr (KW == 2) T.cb[i] = 0;
                 cnt[i] = 0;
             }
+            uint32_t* const sk = reinterpret_cast<uint32_t*>(ring0);  // (flat partitions use no rings)
+            if (pfb)
+                for (uint32_t i = tid; i < sk_words; i += BIN_THREADS) sk[i] = 0;
             __syncthreads();
             PROF_MARK(1);
             const uint32_t P = S.cur_p, Lv = S.cur_l;
@@ -1174,7 +1204,8 @@ DEV void bin_body(const BinArgs& A) {
             PROF_CNT(8, 1);
             // ---- sweep 1: insert + count (binning.c:1042-1069 semantics per key)
             // each occurrence is staged as (slot, ordinal) for sweep 2
-            // stage entry: LDS slot << 48 | position in the read << 32 | call ordinal
+            // stage entry: (LDS slot + 1) << 48 | position in the read << 32 | call
+            // ordinal (slot field 0: not in the table -- a pre-filtered single)
             auto insert2 = [&](const TKey<KW>& k0, uint32_t o0, uint16_t p0, uint32_t s0, bool v0,
                                const TKey<KW>& k1, uint32_t o1, uint16_t p1, uint32_t s1, bool v1) {
 #ifdef KB_BIN_PROF
@@ -1222,7 +1253,7 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_PROF
                         if (A.ablate != 2)
 #endif
-                        stage[s0] = ((uint64_t)l0 << 48) | ((uint64_t)p0 << 32) | o0;
+                        stage[s0] = ((uint64_t)(l0 + 1) << 48) | ((uint64_t)p0 << 32) | o0;
                     }
                 }
                 if (v1) {
@@ -1233,7 +1264,7 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_PROF
                         if (A.ablate != 2)
 #endif
-                        stage[s1] = ((uint64_t)l1 << 48) | ((uint64_t)p1 << 32) | o1;
+                        stage[s1] = ((uint64_t)(l1 + 1) << 48) | ((uint64_t)p1 << 32) | o1;
                     }
                 }
             };
@@ -1246,6 +1277,26 @@ DEV void bin_body(const BinArgs& A) {
                 // inserts: the lists stream from HBM)
                 const uint32_t nf = fb - fa, pmask = (1u << Lv) - 1u;
                 const uint32_t lane = tid & 63u;
+                if (pfb) {
+                    // ---- sweep 0: every k-mer of the partition into the sketch
+                    // (bit 2c: seen, bit 2c+1: seen again); four loads in flight
+                    for (uint32_t i0 = tid; i0 < nf; i0 += 4u * BIN_THREADS) {
+                        TKey<KW> kk[4];
+#pragma unroll
+                        for (int u = 0; u < 4; u++)
+                            if (i0 + u * BIN_THREADS < nf) kk[u] = kst_load<KW>(kst, fa + i0 + u * BIN_THREADS);
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            if (i0 + u * BIN_THREADS >= nf) continue;
+                            if (Lv > l0 && (kk[u].part() & pmask) != P) continue;
+                            const uint32_t cl = sk_cell(kk[u], sk_cells);
+                            const uint32_t bit = 1u << (2u * (cl & 15u));
+                            if (atomicOr(&sk[cl >> 4], bit) & bit) atomicOr(&sk[cl >> 4], bit << 1);
+                        }
+                    }
+                    __syncthreads();
+                }
+                uint32_t singles = 0;
                 uint32_t c0 = (uint32_t)(tid >> 6) * 128u;
                 TKey<KW> n0{}, n1{};
                 uint64_t ne0 = 0, ne1 = 0;
@@ -1275,9 +1326,24 @@ DEV void bin_body(const BinArgs& A) {
                         v0 = v0 && (k0.part() & pmask) == P;
                         v1 = v1 && (k1.part() & pmask) == P;
                     }
+                    if (pfb) {  // keys seen once: counted, not inserted (their stage slot field stays 0)
+                        const uint32_t q0 = sk_cell(k0, sk_cells), q1 = sk_cell(k1, sk_cells);
+                        const bool s0 = v0 && !((sk[q0 >> 4] >> (2u * (q0 & 15u) + 1u)) & 1u);
+                        const bool s1 = v1 && !((sk[q1 >> 4] >> (2u * (q1 & 15u) + 1u)) & 1u);
+                        singles += (uint32_t)__popcll(__ballot(s0)) + (uint32_t)__popcll(__ballot(s1));
+                        // after an overflow a redo may find a slot field from the
+                        // parent's attempt: clear it
+                        if (Lv > l0) {
+                            if (s0) stage[i0] = e0;
+                            if (s1) stage[i1] = e1;
+                        }
+                        v0 = v0 && !s0;
+                        v1 = v1 && !s1;
+                    }
                     insert2(k0, (uint32_t)e0, (uint16_t)(e0 >> 32), i0, v0, k1, (uint32_t)e1, (uint16_t)(e1 >> 32),
                             i1, v1);
                 }
+                if (singles && lane == 0) atomicAdd(&S.n_single, singles);
                 if (tid == 0) S.n_stage = nf;
             }
             __syncthreads();
@@ -1310,7 +1376,8 @@ DEV void bin_body(const BinArgs& A) {
             uint64_t ex = block_excl_scan_u64(mine, S.red, tot);
             if (tid == 0) {
                 const uint32_t ne = (uint32_t)tot, ni = (uint32_t)(tot >> 32);
-                atomicAdd(&A.gcount[2], (unsigned long long)S.n_keys);  // distinct before prune
+                atomicAdd(&A.gcount[2], (unsigned long long)(S.n_keys + S.n_single));  // distinct before prune
+                if (A.tab_keys) atomicAdd(A.tab_keys, (unsigned long long)S.n_keys);
                 // entries and ids from ONE packed counter (entries << 32 | ids; both
                 // totals < 2^32): consecutive entries own consecutive id ranges,
                 // so offset[e + 1] ends entry e's list (the CSR contract)
@@ -1374,7 +1441,8 @@ DEV void bin_body(const BinArgs& A) {
                 for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
                     if (filt && (kst_load<KW>(kst, fa + i).part() & pmask) != P) continue;
                     const uint64_t v = stage[i];
-                    const uint32_t ls = (uint32_t)(v >> 48);
+                    if (!(v >> 48)) continue;  // a pre-filtered single
+                    const uint32_t ls = (uint32_t)(v >> 48) - 1u;
                     // one returning atomic: a pruned key's cursor starts at PRUNED and
                     // takes at most cutoff adds, so it never reaches a real position
                     const uint32_t pos = atomicAdd(&cnt[ls], 1u);
@@ -2364,6 +2432,72 @@ DEV uint32_t order_class(uint32_t c) {
     return msb * 8u + ((c >> (msb - 3u)) & 7u);  // <= 255
 }
 
+// ---------------------------------------------------------------------------
+// Cold-pass density estimate.  The partition depth of a bin comes from the
+// expected distinct keys per occurrence (rho), learned from the last
+// finalize; a context's first finalize has none, and a wrong guess costs
+// either overflow re-splits (distinct-heavy data, C5: 2.4 s instead of 0.13 s
+// per pass) or far too many partitions (high coverage).  One HyperLogLog over
+// every k-mer of the bin-ordered records (2^12 registers: about 1.6 % error)
+// gives rho before the bins run.  Only the k-mer is hashed (its mmer follows
+// from it in all but a few sticky-signature cases): an estimate, not a count.
+// ---------------------------------------------------------------------------
+constexpr int HLL_LOG2 = 12;
+constexpr int HLL_THREADS = 256;
+
+template <int KW>
+__global__ __launch_bounds__(HLL_THREADS) void hll_kernel(BinArgs A, uint64_t R, uint32_t* __restrict__ regs) {
+    __shared__ uint32_t reg[1 << HLL_LOG2];
+    for (int i = threadIdx.x; i < (1 << HLL_LOG2); i += HLL_THREADS) reg[i] = 0;
+    __syncthreads();
+    for (uint64_t r = (uint64_t)blockIdx.x * HLL_THREADS + threadIdx.x; r < R; r += (uint64_t)gridDim.x * HLL_THREADS) {
+        const uint64_t hd = A.hdr[r];
+        const int n = (int)((hd >> 32) & 63u);
+        const uint64_t fl = 0ull - ((hd >> 44) & 1ull);
+        Span<KW> sp;
+        sp.load(A, (uint32_t)r);
+        for (int j = 0; j < n; j++) {
+            uint64_t hi, lo;
+            sp.key(A.K, fl).code(hi, lo);
+            sp.step();
+            const uint64_t h = mix64(lo ^ mix64(hi + 0x2545F4914F6CDD1Dull));
+            const uint32_t ix = (uint32_t)(h >> (64 - HLL_LOG2));
+            const uint32_t rank = (uint32_t)__builtin_clzll((h << HLL_LOG2) | (1ull << (HLL_LOG2 - 1))) + 1u;
+            atomicMax(&reg[ix], rank);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (1 << HLL_LOG2); i += HLL_THREADS)
+        if (reg[i]) atomicMax(&regs[i], reg[i]);
+}
+
+hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(regs, 0, sizeof(uint32_t) << HLL_LOG2, s);
+    if (e != hipSuccess || !R) return e;
+    int dev = 0, cus = 0;
+    e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    const uint64_t want = (R + HLL_THREADS - 1) / HLL_THREADS;
+    const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)std::max(1, cus) * 8));
+    if (KW == 1) hipLaunchKernelGGL(hll_kernel<1>, dim3(blocks), dim3(HLL_THREADS), 0, s, a, R, regs);
+    else hipLaunchKernelGGL(hll_kernel<2>, dim3(blocks), dim3(HLL_THREADS), 0, s, a, R, regs);
+    return hipGetLastError();
+}
+
+double hll_estimate(const uint32_t* regs) {
+    const double m = (double)(1 << HLL_LOG2);
+    double sum = 0.0;
+    int zeros = 0;
+    for (int i = 0; i < (1 << HLL_LOG2); i++) {
+        sum += std::ldexp(1.0, -(int)regs[i]);
+        zeros += regs[i] == 0;
+    }
+    const double est = 0.7213 / (1.0 + 1.079 / m) * m * m / sum;
+    if (est <= 2.5 * m && zeros) return m * std::log(m / zeros);  // small range: linear counting
+    return est;
+}
+
 __global__ __launch_bounds__(1024) void bins_order_kernel(const uint32_t* __restrict__ bcount,
                                                           const uint64_t* __restrict__ totals,
                                                           uint32_t* __restrict__ order, uint64_t max_bins) {
@@ -2462,9 +2596,9 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     __shared__ uint32_t s_nb, s_full;
     __shared__ uint32_t socc[BK_SLOTS];  // occurrences (k-mers) per slot
     const uint32_t tid = threadIdx.x, bk = blockIdx.x;
-    const uint64_t cnt = min<uint64_t>(A.bfill[bk], A.cap);
+    const uint64_t cnt = min<uint64_t>(A.bfill[bk], region_room(A.rbase, A.cap, bk));
     constexpr int RWD = 1 + SPW;  // record words
-    const uint64_t* src = A.regions + (uint64_t)bk * A.cap * RWD;
+    const uint64_t* src = A.regions + region_off(A.rbase, A.cap, bk) * RWD;
     for (uint32_t i = tid; i < BK_SLOTS; i += BK_THREADS) keys[i] = 0;
     for (uint32_t i = tid; i < BK_SLOTS * ROWS; i += BK_THREADS) hist[i] = 0;
     if (tid == 0) {
@@ -2601,10 +2735,11 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
 
 // exclusive prefix of the bucket fills (clamped to the capacity) -> bbase[NB + 1]
 __global__ __launch_bounds__(1024) void bucket_bases_kernel(const unsigned long long* __restrict__ bfill, uint64_t cap,
-                                                          uint32_t NB, uint64_t* __restrict__ bbase) {
+                                                          const uint64_t* __restrict__ rbase, uint32_t NB,
+                                                          uint64_t* __restrict__ bbase) {
     __shared__ uint64_t red[16];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t v = threadIdx.x < NB ? min<uint64_t>(bfill[threadIdx.x], cap) : 0ull;
+    const uint64_t v = threadIdx.x < NB ? min<uint64_t>(bfill[threadIdx.x], region_room(rbase, cap, threadIdx.x)) : 0ull;
     const uint64_t inc = wave_incl_scan(v, lane);
     if (lane == 63) red[wid] = inc;
     __syncthreads();
@@ -2620,7 +2755,7 @@ __global__ __launch_bounds__(1024) void bucket_bases_kernel(const unsigned long 
 hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s) {
     if (!NB) return hipSuccess;
     if (NB > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(bucket_bases_kernel, dim3(1), dim3(1024), 0, s, a.bfill, a.cap, NB, a.bbase);
+    hipLaunchKernelGGL(bucket_bases_kernel, dim3(1), dim3(1024), 0, s, a.bfill, a.cap, a.rbase, NB, a.bbase);
     if (a.spw == 2)
         hipLaunchKernelGGL(bucket_kernel<2>, dim3(NB), dim3(BK_THREADS), 0, s, a);
     else if (a.spw == 4)
@@ -2637,6 +2772,7 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
                                                                  int rw, int M, uint32_t NB,
                                                                  const uint16_t* __restrict__ bucket_map,
                                                                  uint64_t* __restrict__ regions, uint64_t cap,
+                                                                 const uint64_t* __restrict__ rbase,
                                                                  unsigned long long* bfill, uint32_t* status,
                                                                  unsigned long long* n_kmers) {
     constexpr int PERT = 8;
@@ -2682,8 +2818,8 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
         for (int j = 0; j < PERT; j++) {
             if (dst[j] == 0xFFFFFFFFu) continue;
             const uint64_t slot = base[dst[j]] + atomicAdd(&cnt[dst[j]], 1u);
-            if (slot >= cap) continue;  // counted: the caller retries bigger
-            uint64_t* o = regions + ((uint64_t)dst[j] * cap + slot) * (1 + SPW);
+            if (slot >= region_room(rbase, cap, dst[j])) continue;  // counted: the caller retries bigger
+            uint64_t* o = regions + (region_off(rbase, cap, dst[j]) + slot) * (1 + SPW);
             o[0] = pay0[j];
 #pragma unroll
             for (int w = 0; w < SPW; w++) o[1 + w] = ps[j][w];
@@ -2697,17 +2833,18 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
 }
 
 hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
-                                     const uint16_t* bucket_map, uint64_t* regions, uint64_t cap, unsigned long long* bfill,
+                                     const uint16_t* bucket_map, uint64_t* regions, uint64_t cap, const uint64_t* rbase,
+                                     unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s) {
     if (!n_rec) return hipSuccess;
     if (NB < 1 || NB > SK_MAX_DEST || (spw != 2 && spw != 4)) return hipErrorInvalidValue;
     const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
     if (spw == 2)
         hipLaunchKernelGGL(sk_convert_buckets_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, bucket_map, regions, cap, bfill, status, n_kmers);
+                           NB, bucket_map, regions, cap, rbase, bfill, status, n_kmers);
     else
         hipLaunchKernelGGL(sk_convert_buckets_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, bucket_map, regions, cap, bfill, status, n_kmers);
+                           NB, bucket_map, regions, cap, rbase, bfill, status, n_kmers);
     return hipGetLastError();
 }
 

@@ -100,6 +100,8 @@ struct SkScanArgs {
     // 3 for K <= 31, 5 for K <= 63)
     uint64_t* regions;
     uint64_t region_cap;
+    const uint64_t* region_base;   // [G + 1] or null: destination d's records at region_base[d]
+                                   // (exact layout after a counting pass), else at d * region_cap
     unsigned long long* dest_ctr;  // [G] records per destination (zeroed)
     const int32_t* read_ids;       // ordinal -> id (null: affine, id = ordinal + id_off)
     uint32_t id_off;
@@ -120,6 +122,7 @@ struct SkScanArgs {
 struct BucketArgs {
     const uint64_t* regions;   // NB regions of cap records, pay layout (1 + spw words)
     uint64_t cap;
+    const uint64_t* rbase;     // [NB + 1] or null: region d at rbase[d], rbase[d+1]-rbase[d] records
     const unsigned long long* bfill;  // [NB] records per bucket
     int M;
     uint64_t* hdr;             // [R] SoA output, bins contiguous, longest records first
@@ -141,6 +144,14 @@ struct BucketArgs {
 };
 
 constexpr uint16_t BK_RUN_CONT = 0xFFFF;  // brun: a spread mmer's bucket after the first
+
+// region d of a record region set: fixed stride cap, or exact bases
+__device__ __forceinline__ uint64_t region_off(const uint64_t* base, uint64_t cap, uint32_t d) {
+    return base ? base[d] : (uint64_t)d * cap;
+}
+__device__ __forceinline__ uint64_t region_room(const uint64_t* base, uint64_t cap, uint32_t d) {
+    return base ? base[d + 1] - base[d] : cap;
+}
 
 // Bucket map entry (u16 per canonical mmer): the bucket, or for a large mmer
 // spread over a run of k >= 2 consecutive buckets (each holding only it),
@@ -222,6 +233,14 @@ struct BinArgs {
     uint64_t lq_cap;
     float kept_ratio;          // expected kept ids per occurrence (last finalize)
     float win_fill;            // target share of the LDS id window when choosing the depth
+    // singleton pre-filter of heavy (flat) bins: a partition's k-mers first
+    // go through a 2-bit "seen twice" sketch in LDS; keys seen once are
+    // counted (distinct) but never enter the table, the stage or sweep 2
+    // (with cutoff >= 1 they are pruned anyway: exact).  Partitions are then
+    // sized by the keys that do enter the table (rho_tab) and by the sketch
+    uint32_t pf;               // 1: pre-filter the flat bins (prune, cutoff >= 1, no first-occurrence tracking)
+    float rho_tab;             // expected table keys per occurrence under the pre-filter
+    unsigned long long* tab_keys;  // (zeroed) keys that entered a table
 };
 
 struct ListArgs {
@@ -262,6 +281,10 @@ hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t 
                             hipStream_t s);
 // ev_bin[2]: recorded right before and right after bin_kernel (timing), or null
 hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin = nullptr);
+// HyperLogLog of the k-mers of the bin-ordered records (2^12 u32 registers,
+// zeroed here) and its estimate (host): the cold pass's distinct keys
+hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, hipStream_t s);
+double hll_estimate(const uint32_t* regs);
 hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uint32_t* order, uint64_t max_bins,
                              hipStream_t s);
 hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s);
@@ -273,7 +296,7 @@ hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, co
 // received records into local bucket regions (block-aggregated reservations)
 hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
                                      const uint16_t* bucket_map,
-                                     uint64_t* regions, uint64_t cap, unsigned long long* bfill,
+                                     uint64_t* regions, uint64_t cap, const uint64_t* rbase, unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s);
 size_t bins_lds_bytes(uint32_t ts_log2, int KW);
 #ifdef KB_BIN_PROF

@@ -10,15 +10,19 @@ records (a run of consecutive k-mers of a read that share one signature,
 ~10 per 150-bp read at k31/m7 -- about 2 B per k-mer on the wire instead of
 a 12-16 B per-k-mer record) over RCCL (torch.distributed "nccl") / xGMI.
 
-Per step on every rank (binned engine, K <= 31):
+Per step on every rank, wherever the binned engine applies (K <= 31 on any
+read length; K <= 63 on reads of <= 512 bp -- the default; kbin.h
+KB_ENGINE_BINNED):
   kb_route_scatter (one pass: records straight into per-destination regions)
   ->  all_to_all_single of the counts, all_to_all of the region slices  ->
   kb_submit_superkmers_device (one batch per source rank)  ->  kb_finalize.
-Otherwise (table engine: K > 31 or first-occurrence tracking):
+Otherwise (the table engine: forced, or two-word k-mers on reads > 512 bp):
   kb_route_plan (counts per destination)  ->  kb_route_pack (dest-major send
   buffer, read order)  ->  all_to_all_single (counts, then records)  ->
   kb_submit_superkmers_device (received, concatenated by source rank)  ->
-  kb_finalize.
+  kb_finalize.  Both senders honour kb_set_partition (only the pass's mmer
+  partition is counted and shipped), so step(part, n_parts) is valid on
+  either; the receivers' union equals the single-GPU result in every case.
 Read ids must increase with the global call order (rank r's ids below rank
 r+1's): they are the reverse-call-order key of every id list.
 """

@@ -364,6 +364,49 @@ def test_heavy_bins_flat_lists(ts_log2, flat_l, fill, K, engine, monkeypatch):
             assert int((res.first & np.uint64(0xFFFF)).max()) <= L - K
 
 
+@pytest.mark.parametrize("K,ts_log2,cutoff,parts,err", [(31, 10, 1, 1, 30000), (31, 12, 2, 3, 30000),
+                                                        (63, 10, 1, 1, 20000), (63, 11, 1, 2, 50000),
+                                                        (31, 13, 1, 1, 1000)])
+def test_singleton_prefilter(K, ts_log2, cutoff, parts, err, engine, monkeypatch):
+    """the heavy bins' singleton pre-filter (KB_BIN_PF=1; small tables force
+    every bin onto the flat lists): reads with 2-5 % errors, so most distinct
+    keys are seen once -- they go through the LDS sketch only, never the
+    table; the result and the distinct count (before the prune) equal the
+    oracle's, with cutoffs 1 and 2, partitioned passes, both key widths, and
+    a low-error case where the sketch passes nearly everything"""
+    import torch
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    monkeypatch.setenv("KB_BIN_TS_LOG2", str(ts_log2))
+    monkeypatch.setenv("KB_BIN_FLAT_L", "1")
+    monkeypatch.setenv("KB_BIN_PF", "1")
+    n, L = 30000, 150
+    wpr = (L + 31) // 32
+    words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, 60000, err, 21)
+    torch.cuda.synchronize()
+    bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n, wpr, n * L)
+    ora = oracle.bin_reads(bases, hl, K, 7, cutoff, True)
+    distinct = oracle.bin_reads(bases, hl, K, 7, cutoff, False).n_entries
+    if err >= 20000:
+        assert distinct > 2 * ora.n_entries  # singleton-heavy
+    with kbin.Engine(K, 7, cutoff=cutoff, max_read_len=L) as eng:
+        for _ in range(2):  # the second run sizes the partitions from the learned densities
+            eng.reset()
+            eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
+            got, nd = [], 0
+            for p in range(parts):
+                if parts > 1:
+                    eng.set_partition(p, parts)
+                eng.finalize(True)
+                r = eng.export()
+                nd += r.n_distinct
+                got.append(r)
+            assert_same(kbin.Result.concat(got) if parts > 1 else got[0], ora)
+            assert nd == distinct
+
+
 @pytest.mark.parametrize("genome,flat_l,ts_log2,K", [(3000, 3, 13, 31), (3000, 2, 10, 31), (200000, 3, 13, 31),
                                                       (200000, 3, 11, 31), (3000, 3, 12, 63), (200000, 3, 11, 63)])
 def test_split_bins(genome, flat_l, ts_log2, K, engine, monkeypatch):
