@@ -271,7 +271,7 @@ def load_traffic(tag: str, kernel: str):
         d = json.loads(p.read_text()).get(tag)
         if not d:
             return None
-        k = kernel.split("<")[0]
+        k = "bin phase" if kernel.startswith("bin phase") else kernel.split("<")[0]
         row = next((v for name, v in d.get("per_kernel", {}).items() if k in name), None)
         if not row or "steady" not in row:
             return None
@@ -436,16 +436,17 @@ def main():
     else:
         eng = kbin.Engine(K, M, cutoff=args.cutoff, max_read_len=L, device=local)
         # P > 1: one super-k-mer pass over the reads (kb_split_passes) fills the
-        # passes' regions; each pass then bins its region (no rescans)
-        # (two-word k-mers keep the rescans: C5's regions beside its per-pass
-        # buffers exceed the HBM)
-        # (~10 super-k-mers per 150-bp read; the partition hash splits them
-        # evenly, and a short region is retried bigger).  Gated on the HBM: the
+        # passes' regions; each pass then bins its region (no rescans).
+        # Super-k-mers per read: about 2 (L - K + 1) / (K - M + 2) (a sticky
+        # signature holds for half a window on average; ~10 at 150 bp K31 M7,
+        # ~7 at 250 bp K63 M7), with a margin; the partition hash splits them
+        # evenly, and a short region is retried bigger.  Gated on the HBM: the
         # regions sit beside the pass's own buffers
-        split = {"cap": int(n * (L / 15.0) / P * 1.1) + 4096, "buf": None, "counts": None}
-        split_bytes = P * split["cap"] * (1 + 2 * ((K + 31) // 32)) * 8
-        scan_once = (P > 1 and K <= 31 and not args.no_scan_once
-                     and split_bytes < 0.1 * torch.cuda.get_device_properties(local).total_memory)
+        per_read = 2.0 * max(1, L - K + 1) / (K - M + 2) * 1.25 + 1.0
+        split = {"cap": int(n * per_read / P * 1.1) + 4096, "buf": None, "counts": None}
+        split_bytes = P * split["cap"] * (1 + (2 * K - M + 31) // 32) * 8
+        scan_once = (P > 1 and not args.no_scan_once
+                     and split_bytes < 0.15 * torch.cuda.get_device_properties(local).total_memory)
         sender = kbin.Engine(K, M, cutoff=args.cutoff, max_read_len=L, device=local) if scan_once else None
         rw = eng.record_words()
 

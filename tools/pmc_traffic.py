@@ -56,6 +56,16 @@ def main():
                     "cold": {"fetch_kib": round(fc, 1), "write_kib": round(wc, 1),
                              "bytes": round((2.0 * fc + wc) * 1024)}}
     roof = [k for k in table if "bin_kernel" in k] or [k for k in table if "scan_insert_kernel" in k]
+    # the bin phase as one "kernel" (bench.py's roofline kernel when heavy bins
+    # dominate: C3, C5): every kernel between the bucket ordering and the lists
+    phase = [k for k in table if any(x in k for x in ("bin_kernel", "flat_count_kernel", "flat_scan_kernel",
+                                                        "flat_scatter_kernel", "bin_parts_kernel",
+                                                        "bins_final_kernel"))]
+    if phase:
+        table["bin phase"] = {"dispatches": min(table[k]["dispatches"] for k in phase),
+                              "members": sorted(phase),
+                              "steady": {"bytes": sum(table[k]["steady"]["bytes"] for k in phase)},
+                              "cold": {"bytes": sum(table[k]["cold"]["bytes"] for k in phase)}}
     p = pathlib.Path(out)
     doc = json.loads(p.read_text()) if p.exists() else {}
     doc[tag] = {"hbm_bytes_per_launch": table[roof[0]]["steady"]["bytes"] if roof else None,
@@ -67,7 +77,7 @@ def main():
                           "steady = mean over every dispatch after the first, cold = the first",
                 "per_kernel": table}
     p.write_text(json.dumps(doc, indent=1) + "\n")
-    step = sum(v["steady"]["bytes"] for v in table.values())
+    step = sum(v["steady"]["bytes"] for k, v in table.items() if k != "bin phase")
     print(f"{tag}: steady-state bytes per step (all kernels) {step / 1e9:.3f} GB")
     for k, v in sorted(table.items(), key=lambda x: -x[1]["steady"]["bytes"]):
         print(f"{k:45s} steady {v['steady']['bytes'] / 1e9:8.3f} GB  cold {v['cold']['bytes'] / 1e9:8.3f} GB"
