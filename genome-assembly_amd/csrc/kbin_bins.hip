@@ -1195,7 +1195,7 @@ DEV void bin_body(const BinArgs& A) {
                 cnt[i] = 0;
             }
             uint32_t* const sk = reinterpret_cast<uint32_t*>(ring0);  // (flat partitions use no rings)
-            if (pfb)
+            if (PHASE == 1 && pfb)
                 for (uint32_t i = tid; i < sk_words; i += BIN_THREADS) sk[i] = 0;
             __syncthreads();
             PROF_MARK(1);
@@ -1268,9 +1268,11 @@ DEV void bin_body(const BinArgs& A) {
                     }
                 }
             };
-            if (!flat) {
+            // (phase 0 never sweeps a flat partition: a flat bin is published
+            // above -- each kernel compiles only its own paths)
+            if (PHASE == 0 || !flat) {
                 for_each_kmer<KW>(A, lo, hi, P, Lv, qa, qb, qo, qp, &S.n_stage, insert2);
-            } else {
+            } else if constexpr (PHASE == 1) {
                 // the partition's flat list, two entries per lane; a deeper split
                 // (Lv > l0) filters it, entries keep their index (sweep 2 filters too)
                 // (the next chunk's entries are loaded before this chunk's
@@ -1436,12 +1438,12 @@ DEV void bin_body(const BinArgs& A) {
 #else
                 const uint32_t ns = S.n_stage;
 #endif
-                const bool filt = flat && Lv > l0;
+                const bool filt = PHASE == 1 && flat && Lv > l0;
                 const uint32_t pmask = (1u << Lv) - 1u;
                 for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
                     if (filt && (kst_load<KW>(kst, fa + i).part() & pmask) != P) continue;
                     const uint64_t v = stage[i];
-                    if (!(v >> 48)) continue;  // a pre-filtered single
+                    if (PHASE == 1 && !(v >> 48)) continue;  // a pre-filtered single (flat partitions only)
                     const uint32_t ls = (uint32_t)(v >> 48) - 1u;
                     // one returning atomic: a pruned key's cursor starts at PRUNED and
                     // takes at most cutoff adds, so it never reaches a real position

@@ -1,5 +1,6 @@
 # scratch recipe for the current gpurun call (see tools/gpu.sh)
-bash tools/gpu.sh bench c2 --host-input --dropin && \
-bash tools/gpu.sh ktrace c2 --steps 10 --warmup 3 && \
-bash tools/gpu.sh pmc c2 --steps 4 --warmup 1 && \
-KB_BIN_PF=0 bash tools/gpu.sh bench c5nopf --workload c5 --steps 1 --warmup 1 --digest --cpu-sample 0
+for i in 1 2; do
+KB_LIB_PATH=genome-assembly_amd/lib/ab/libkbin.so bash tools/gpu.sh bench old$i --cpu-sample 0 --steps 20 --input replay && \
+bash tools/gpu.sh bench new$i --cpu-sample 0 --steps 20 --input replay || exit 1
+done
+bash tools/gpu.sh test tests/test_gpu_parity.py -k "prefilter or heavy or split or c2 or golden"
