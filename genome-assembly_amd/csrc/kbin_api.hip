@@ -221,6 +221,7 @@ struct kb_ctx {
     DevBuf<uint32_t> long_q;   // entries with 257..4096 ids (lists_long_kernel)
     DevBuf<uint64_t> lq;       // list items for lists_kernel (BinArgs::lq_items); [0] the counter
     DevBuf<uint32_t> border;   // bin processing order
+    DevBuf<uint4> bdesc;       // [2 max_bins] per processing slot: bin descriptor + stage base
     DevBuf<uint32_t> bcount, bmmer, bocc;  // bin descriptors (with starts); bocc: k-mers
     DevBuf<uint32_t> flat_list, flat_next, flat_l0, flat_off, flat_cur, flat_chunk, pool_bin, chunk_bin;  // heavy bins published for phase 1
     DevBuf<unsigned long long> flat_sbase, flat_obase, flat_n;  // flat_n[0] bins, [1] offset pool
@@ -362,7 +363,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->h_first.release(); c->h_ids.release();
     if (c->h_alpha) (void)hipHostFree(c->h_alpha);
     c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
     c->regions.release(); c->bfill.release(); c->bbase.release(); c->rbase.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
@@ -1444,6 +1445,12 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     }
     HIPCHK(c->border.ensure(max_bins));
     HIPCHK(launch_bins_order(c->bcount.p, c->totals.p, c->border.p, max_bins, c->s));
+    const bool use_desc = bucketed && env_int("KB_BIN_DESC", 1);
+    if (use_desc) {  // (bocc: the bucket ordering counted every bin's occurrences)
+        HIPCHK(c->bdesc.ensure(2 * max_bins));
+        HIPCHK(launch_bins_desc(c->border.p, c->starts.p, c->bcount.p, c->bmmer.p, c->bocc.p, c->totals.p, max_bins,
+                                c->bdesc.p, reinterpret_cast<unsigned long long*>(c->totals.p + 10), c->s));
+    }
     if (c->rho <= 0.f && N && env_int("KB_BIN_HLL", 1)) {
         // the context's first finalize: distinct keys per occurrence from one
         // HyperLogLog over the records (no learned density yet)
@@ -1480,6 +1487,10 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             HIPCHK(hipMemsetAsync(c->totals.p + 4, 0, 4 * sizeof(uint64_t), c->s));
             HIPCHK(hipMemsetAsync(c->totals.p + 10, 0, 2 * sizeof(uint64_t), c->s));
             HIPCHK(hipMemsetAsync(c->misc.p + 2, 0, sizeof(uint32_t), c->s));
+            if (use_desc)  // (the stage counter starts after the described ranges)
+                HIPCHK(launch_bins_desc(c->border.p, c->starts.p, c->bcount.p, c->bmmer.p, c->bocc.p, c->totals.p,
+                                        max_bins, c->bdesc.p, reinterpret_cast<unsigned long long*>(c->totals.p + 10),
+                                        c->s));
             REC(3);
         }
         a = BinArgs{};
@@ -1495,6 +1506,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.max_bins = max_bins;
         a.stage_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 10);
         a.order = c->border.p;
+        a.bdesc = use_desc ? c->bdesc.p : nullptr;
         a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
         a.stage = c->stage.p;
         a.kstage = flat_l ? c->kstage.p : nullptr;

@@ -1063,13 +1063,28 @@ DEV void bin_body(const BinArgs& A) {
             }
             __syncthreads();
         }
-        const uint32_t b = PHASE == 0 ? A.order[S.item] : S.item;
-        const uint32_t lo = A.bstart[b], hi = lo + A.bcount[b];
-        const uint32_t mmer = A.bmmer[b];
+        // phase 0 with descriptors (bucketed path): one 32-B load per bin --
+        // bin, records, mmer, occurrences and stage base, in processing order
+        // (bins_desc_kernel) -- instead of the order -> descriptor -> stage
+        // counter chain of dependent global round trips
+        uint4 d0 = make_uint4(0u, 0u, 0u, 0u), d1 = make_uint4(0u, 0u, 0u, 0u);
+        if (PHASE == 0 && A.bdesc) {
+            d0 = A.bdesc[2 * (uint64_t)S.item];
+            d1 = A.bdesc[2 * (uint64_t)S.item + 1];
+        }
+        const bool have_desc = PHASE == 0 && A.bdesc;
+        const uint32_t b = have_desc ? d0.x : PHASE == 0 ? A.order[S.item] : S.item;
+        const uint32_t lo = have_desc ? d0.y : A.bstart[b];
+        const uint32_t hi = lo + (have_desc ? d0.z : A.bcount[b]);
+        const uint32_t mmer = have_desc ? d0.w : A.bmmer[b];
 
         // occurrences of the bin -> first partition depth
         uint64_t occ_tot = 0;
-        if (PHASE == 0) {
+        if (PHASE == 0 && have_desc && d1.x) {  // (0: a spread run's bin, counted below)
+            occ_tot = d1.x;
+            if (tid == 0) S.stage_base = (uint64_t)d1.y | ((uint64_t)d1.z << 32);
+            __syncthreads();
+        } else if (PHASE == 0) {
             // the bucket ordering counted them (its length rows), else a pass
             // over the record headers
             occ_tot = A.bocc ? A.bocc[b] : 0u;
@@ -2525,6 +2540,52 @@ __global__ __launch_bounds__(1024) void bins_order_kernel(const uint32_t* __rest
 hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uint32_t* order, uint64_t max_bins,
                              hipStream_t s) {
     hipLaunchKernelGGL(bins_order_kernel, dim3(1), dim3(1024), 0, s, bcount, totals, order, max_bins);
+    return hipGetLastError();
+}
+
+// one descriptor per processing slot: {bin, first record, records, mmer},
+// {occurrences, stage base lo, hi, 0}; stage bases are the exclusive prefix of
+// the occurrences in processing order (each bin's range, as the stage counter
+// handed them out before)
+__global__ __launch_bounds__(1024) void bins_desc_kernel(const uint32_t* __restrict__ order,
+                                                         const uint32_t* __restrict__ bstart,
+                                                         const uint32_t* __restrict__ bcount,
+                                                         const uint32_t* __restrict__ bmmer,
+                                                         const uint32_t* __restrict__ bocc,
+                                                         const uint64_t* __restrict__ totals, uint64_t max_bins,
+                                                         uint4* __restrict__ desc, unsigned long long* stage_ctr) {
+    __shared__ uint64_t red[16];
+    const uint32_t nbins = (uint32_t)min(totals[2], max_bins);
+    const uint32_t per = (nbins + 1023u) / 1024u, i0 = threadIdx.x * per;
+    uint64_t mine = 0;
+    for (uint32_t k = 0; k < per; k++)
+        if (i0 + k < nbins) mine += bocc[order[i0 + k]];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t inc = wave_incl_scan(mine, lane);
+    if (lane == 63) red[wid] = inc;
+    __syncthreads();
+    uint64_t run = inc - mine;
+    for (int w = 0; w < 16; w++)
+        if (w < wid) run += red[w];
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t i = i0 + k;
+        if (i >= nbins) break;
+        const uint32_t b = order[i];
+        const uint32_t occ = bocc[b];
+        desc[2 * (uint64_t)i] = make_uint4(b, bstart[b], bcount[b], bmmer[b]);
+        desc[2 * (uint64_t)i + 1] = make_uint4(occ, (uint32_t)run, (uint32_t)(run >> 32), 0u);
+        run += occ;
+    }
+    // bins without a count (spread runs: bocc 0) take their stage ranges from
+    // the stage counter, after every described range
+    if (threadIdx.x == 1023) *stage_ctr = run;
+}
+
+hipError_t launch_bins_desc(const uint32_t* order, const uint32_t* bstart, const uint32_t* bcount,
+                            const uint32_t* bmmer, const uint32_t* bocc, const uint64_t* totals, uint64_t max_bins,
+                            uint4* desc, unsigned long long* stage_ctr, hipStream_t s) {
+    hipLaunchKernelGGL(bins_desc_kernel, dim3(1), dim3(1024), 0, s, order, bstart, bcount, bmmer, bocc, totals,
+                       max_bins, desc, stage_ctr);
     return hipGetLastError();
 }
 

@@ -177,6 +177,8 @@ struct BinArgs {
     uint64_t max_bins;         // capacity of the descriptors (nbins never exceeds it)
     unsigned long long* stage_ctr;  // stage allocation (zeroed): each bin takes its occurrences
     const uint32_t* order;     // [nbins] processing order (largest bins first)
+    const uint4* bdesc;        // [2 nbins] or null: per processing slot {bin, start, count, mmer},
+                               // {occurrences, stage base lo, hi, 0} (bins_desc_kernel)
     unsigned long long* work;  // work counter (zeroed)
     uint64_t* stage;           // [N] (LDS slot << 48 | position << 32 | ordinal) per occurrence
     uint64_t* kstage;          // [KW N] heavy bins: the k-mer's table key per occurrence, parallel to stage
@@ -281,6 +283,9 @@ hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t 
                             hipStream_t s);
 // ev_bin[2]: recorded right before and right after bin_kernel (timing), or null
 hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin = nullptr);
+hipError_t launch_bins_desc(const uint32_t* order, const uint32_t* bstart, const uint32_t* bcount,
+                            const uint32_t* bmmer, const uint32_t* bocc, const uint64_t* totals, uint64_t max_bins,
+                            uint4* desc, unsigned long long* stage_ctr, hipStream_t s);
 // HyperLogLog of the k-mers of the bin-ordered records (2^12 u32 registers,
 // zeroed here) and its estimate (host): the cold pass's distinct keys
 hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, hipStream_t s);
