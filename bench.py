@@ -31,6 +31,7 @@ import time
 REPO = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "genome-assembly_amd"))
 
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402  (loaded before libkbin: one HIP runtime per process)
 
@@ -282,6 +283,12 @@ def load_traffic(tag: str, kernel: str):
 
 
 def main():
+    # stdout carries exactly ONE JSON line (rank 0): native libraries print to
+    # fd 1 (RCCL's version banner, gloo's connection notes), so fd 1 points at
+    # stderr for the run and the result goes to a private copy of the real stdout
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -638,7 +645,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(sets[0][0], sets[0][1], n, min(args.cpu_sample, n), wpr, L, K, M,
                                            args.cutoff, args.ref_sample)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

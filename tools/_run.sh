@@ -1,7 +1,3 @@
 # scratch recipe for the current gpurun call (see tools/gpu.sh)
-for i in 1 2; do
-KB_LIB_PATH=genome-assembly_amd/lib/ab/libkbin.so bash tools/gpu.sh bench old$i --cpu-sample 0 --steps 20 --input replay && \
-KB_BIN_DESC=0 bash tools/gpu.sh bench nodesc$i --cpu-sample 0 --steps 20 --input replay && \
-bash tools/gpu.sh bench new$i --cpu-sample 0 --steps 20 --input replay || exit 1
-done
-bash tools/gpu.sh test tests/test_gpu_parity.py tests/test_gpu_dist.py
+KB_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 > gpurun_out/bench_n2gloo.json 2> gpurun_out/bench_n2gloo.err && \
+timeout -k 10 600 python bench.py --routed --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/bench_routed.json 2> gpurun_out/bench_routed.err
