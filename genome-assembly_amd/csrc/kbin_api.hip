@@ -1301,7 +1301,9 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
                             (unsigned long long)N);
             return KB_OK;
         }
-        c->bucket_cap = mx + mx / 8 + 1024;  // grow and rerun the pass
+        // grow and rerun the pass; with headroom, so a later pass's slightly
+        // larger bucket does not regrow (each growth maps the regions afresh)
+        c->bucket_cap = mx + mx / 2 + 1024;
     }
     return fail(KB_EDEVICE, "internal: bucket capacity did not converge");
 }
@@ -1577,6 +1579,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             a.lq_cap = ecap;
         }
         a.kept_ratio = c->kept_ratio;
+        a.fs_lds = (uint32_t)(env_int("KB_BIN_FSL", 1) != 0);
         // singleton pre-filter for the heavy bins: where most distinct keys are
         // pruned singletons (high error rates, low coverage: C5), learned from
         // the last finalize; exact because a key seen once has count 1 <= cutoff

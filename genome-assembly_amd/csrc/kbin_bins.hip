@@ -908,9 +908,11 @@ constexpr uint32_t FLAT_MAX = 1u << FLAT_LOG2;  // (a 64-KiB LDS histogram in th
 static_assert(FLAT_MAX == KB_FLAT_MAX, "host and device agree on the flat list count");
 constexpr int FB_THREADS = 256;        // the build kernels' blocks
 constexpr uint32_t FB_CHUNK = 1024;    // records per build item
+constexpr uint32_t FSL_NP = 2048;      // flat_scatter_lds_kernel: most partitions of the bins it writes
 constexpr uint32_t SPLIT_BIT = 0x100u;     // flat_l0: a split bin's partitions (no flat lists)
 constexpr uint32_t PRUNED = 0x80000000u;  // cursor of a pruned (or empty) slot in sweep 2
 constexpr uint32_t PF_BIT = 0x200u;        // flat_l0: a heavy bin sized for the singleton pre-filter
+constexpr uint32_t FSL_BIT = 0x400u;       // flat_l0: its lists written by flat_scatter_lds_kernel
 constexpr double PF_LOAD = 0.06;           // sketch load (distinct keys / cells) the partition depth aims at
 
 // the pre-filter's sketch cell of a key (independent of the table hash, whose
@@ -1157,6 +1159,10 @@ DEV void bin_body(const BinArgs& A) {
                 if (l0 > FLAT_LOG2) l0 = FLAT_LOG2;
             }
             const uint32_t np = 1u << l0;
+            // LDS-staged list writes where a build chunk gives each partition
+            // short runs (under 64 entries); longer runs coalesce by themselves
+            const bool fsl = flat && A.fs_lds && np <= FSL_NP &&
+                             (uint64_t)FB_CHUNK * occ_tot < 64ull * np * (uint64_t)(hi - lo);
             if (tid == 0) S.e0 = atomicAdd(A.flat_octr, (unsigned long long)(np + 1));  // this bin's pool range
             __syncthreads();
             for (uint32_t i = tid; i <= np; i += BIN_THREADS) {
@@ -1169,9 +1175,10 @@ DEV void bin_body(const BinArgs& A) {
             __syncthreads();
             for (uint32_t k = tid; k < nch; k += BIN_THREADS) A.chunk_bin[S.i0 + k] = b;
             if (tid == 0) {
+                if (fsl) atomicAdd(&A.flat_n[6], 1ull);  // (LDS-staged lists)
                 A.flat_obase[b] = S.e0;
                 A.flat_sbase[b] = S.stage_base;
-                A.flat_l0[b] = l0 | (split ? SPLIT_BIT : 0u) | (pfb ? PF_BIT : 0u);
+                A.flat_l0[b] = l0 | (split ? SPLIT_BIT : 0u) | (pfb ? PF_BIT : 0u) | (fsl ? FSL_BIT : 0u);
                 A.flat_chunk[b] = (uint32_t)S.i0;
                 A.flat_list[atomicAdd(A.flat_n, 1ull)] = b;
             }
@@ -1648,6 +1655,7 @@ __global__ __launch_bounds__(FB_THREADS) void flat_scatter_kernel(BinArgs A) {
         __syncthreads();
         if (!s_ok) break;
         const uint32_t b = s_b, l0 = A.flat_l0[b] & 0xFFu, np = 1u << l0, pm = np - 1u;
+        if (A.flat_l0[b] & FSL_BIT) continue;  // flat_scatter_lds_kernel's
         const uint32_t lo = A.bstart[b] + s_c * FB_CHUNK, hi = min(lo + FB_CHUNK, A.bstart[b] + A.bcount[b]);
         for (uint32_t i = threadIdx.x; i < np; i += FB_THREADS) hist[i] = 0;
         __syncthreads();
@@ -1741,6 +1749,144 @@ __global__ __launch_bounds__(FB_THREADS) void flat_scatter_kernel(BinArgs A) {
                 kst_store<KW>(kst, i, key);
                 stage[i] = ((uint64_t)pos << 32) | ord;
             });
+        }
+    }
+}
+
+// Heavy bins whose build chunks give each partition short runs (fewer than 64
+// entries; up to 2048 partitions): the chunk's entries are staged in
+// LDS sorted by partition and written out with consecutive lanes on
+// consecutive entries of one partition's range, so a store instruction covers
+// whole runs of lines.  (Scattered straight to HBM, the ~40 entries a chunk
+// gives each of a few hundred partitions left lines partly written: the PMC
+// passes counted 3.7x the list bytes written at C4, 2.8x at C5.)  A chunk is
+// cut into segments of at most FSL_E entries (record k-mer counts come from
+// the headers); per segment: count per partition (expansion 1), reserve each
+// partition's range with one global atomic and place the partitions in LDS
+// (scan), stage key, value and partition (expansion 2), copy out.
+constexpr int FSL_THREADS = 1024;
+template <int KW>
+constexpr uint32_t fsl_entries() { return KW == 1 ? 7168u : 4864u; }
+template <int KW>
+constexpr size_t fsl_lds_bytes() {
+    return (size_t)fsl_entries<KW>() * (8u * KW + 8u + 2u) + 3u * FSL_NP * sizeof(uint32_t) + 64;
+}
+
+template <int KW>
+__global__ __launch_bounds__(FSL_THREADS) void flat_scatter_lds_kernel(BinArgs A) {
+    constexpr uint32_t E = fsl_entries<KW>();
+    extern __shared__ __attribute__((aligned(16))) uint64_t fsm[];
+    uint64_t* const skey = fsm;                                        // [KW E]
+    uint64_t* const sval = skey + KW * E;                              // [E]
+    uint32_t* const cnt = reinterpret_cast<uint32_t*>(sval + E);       // [FSL_NP] counts, then cursors
+    uint32_t* const loff = cnt + FSL_NP;                               // [FSL_NP] first staged entry
+    uint32_t* const gbase = loff + FSL_NP;                             // [FSL_NP] first list entry
+    uint16_t* const spart = reinterpret_cast<uint16_t*>(gbase + FSL_NP);  // [E]
+    __shared__ uint32_t s_b, s_c, s_ok, s_seg, s_tot;
+    __shared__ uint32_t red[FSL_THREADS / 64];
+    if (!A.flat_n[6]) return;  // no bin with that many partitions this time
+    const uint32_t tid = threadIdx.x;
+    const int lane = (int)(tid & 63u), wid = (int)(tid >> 6);
+    unsigned long long it = blockIdx.x;
+    for (;; it += gridDim.x) {
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t b = 0, c = 0;
+            s_ok = fb_claim(A, true, it, b, c);
+            s_b = b;
+            s_c = c;
+        }
+        __syncthreads();
+        if (!s_ok) break;
+        const uint32_t b = s_b, l0 = A.flat_l0[b] & 0xFFu, np = 1u << l0, pm = np - 1u;
+        if (!(A.flat_l0[b] & FSL_BIT)) continue;  // (flat_scatter_kernel's)
+        const uint32_t c_lo = A.bstart[b] + s_c * FB_CHUNK, c_hi = min(c_lo + FB_CHUNK, A.bstart[b] + A.bcount[b]);
+        uint32_t* cur = A.flat_cur + A.flat_obase[b];
+        const uint64_t sb = A.flat_sbase[b];
+        uint64_t* kst = A.kstage + KW * sb;
+        uint64_t* stage = A.stage + sb;
+        for (uint32_t lo = c_lo; lo < c_hi;) {
+            // ---- this segment: the longest record run from lo within E entries
+            {
+                const uint32_t r = lo + tid;
+                const uint32_t n = r < c_hi ? (uint32_t)((A.hdr[r] >> 32) & 63u) : 0u;
+                const uint32_t inc = wave_incl_scan(n, lane);
+                if (lane == 63) red[wid] = inc;
+                __syncthreads();
+                uint32_t before = 0;
+                for (int w = 0; w < wid; w++) before += red[w];
+                const uint32_t incl = before + inc;
+                // records [lo, lo + k) fit when their inclusive sum <= E: count them
+                const uint64_t fit = __ballot(r < c_hi && incl <= E);
+                if (tid == 0) s_seg = 0;
+                __syncthreads();
+                if (lane == 0 && fit) atomicAdd(&s_seg, (uint32_t)__popcll(fit));
+                __syncthreads();
+            }
+            const uint32_t hi = lo + max(1u, s_seg);  // (one record always fits: n <= 63 < E)
+            for (uint32_t i = tid; i < np; i += FSL_THREADS) cnt[i] = 0;
+            __syncthreads();
+            expand_bin<KW, FSL_THREADS>(A, lo, hi, [&](const TKey<KW>& key, uint32_t, uint32_t) {
+                atomicAdd(&cnt[key.part() & pm], 1u);
+            });
+            __syncthreads();
+            // ---- partitions: global range (one atomic each), staged offsets (scan)
+            {
+                constexpr uint32_t PER = FSL_NP / FSL_THREADS;
+                uint32_t c[PER], sum = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < PER; k++) {
+                    const uint32_t p = tid * PER + k;
+                    c[k] = p < np ? cnt[p] : 0u;
+                    sum += c[k];
+                }
+                const uint32_t inc = wave_incl_scan(sum, lane);
+                __syncthreads();
+                if (lane == 63) red[wid] = inc;
+                __syncthreads();
+                uint32_t run = inc - sum;
+                for (int w = 0; w < wid; w++) run += red[w];
+#pragma unroll
+                for (uint32_t k = 0; k < PER; k++) {
+                    const uint32_t p = tid * PER + k;
+                    if (p < np) {
+                        loff[p] = run;
+                        cnt[p] = run;  // cursor
+                        if (c[k]) gbase[p] = atomicAdd(&cur[p], c[k]);
+                        run += c[k];
+                    }
+                }
+                if (tid == FSL_THREADS - 1) s_tot = run;
+            }
+            __syncthreads();
+            expand_bin<KW, FSL_THREADS>(A, lo, hi, [&](const TKey<KW>& key, uint32_t ord, uint32_t pos) {
+                const uint32_t p = key.part() & pm;
+                const uint32_t i = atomicAdd(&cnt[p], 1u);
+                if constexpr (KW == 1) {
+                    skey[i] = key.a;
+                } else {
+                    skey[2 * i] = key.a;
+                    skey[2 * i + 1] = key.b;
+                }
+                sval[i] = ((uint64_t)pos << 32) | ord;
+                spart[i] = (uint16_t)p;
+            });
+            __syncthreads();
+            // ---- copy out: consecutive staged entries of one partition go to
+            // consecutive list entries
+            const uint32_t tot = s_tot;
+            for (uint32_t i = tid; i < tot; i += FSL_THREADS) {
+                const uint32_t p = spart[i];
+                const uint32_t g = gbase[p] + (i - loff[p]);
+                if constexpr (KW == 1) {
+                    kst[g] = skey[i];
+                } else {
+                    kst[2 * (uint64_t)g] = skey[2 * i];
+                    kst[2 * (uint64_t)g + 1] = skey[2 * i + 1];
+                }
+                stage[g] = sval[i];
+            }
+            lo = hi;
         }
     }
 }
@@ -2949,6 +3095,9 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     hipLaunchKernelGGL(flat_count_kernel<KW>, dim3(fb_blocks), dim3(FB_THREADS), fb_lds, s, a2);
     hipLaunchKernelGGL(flat_scan_kernel, dim3(1024), dim3(1024), 0, s, a2);
     hipLaunchKernelGGL(flat_scatter_kernel<KW>, dim3(fb_blocks), dim3(FB_THREADS), fb_lds, s, a2);
+    if (a2.fs_lds)
+        hipLaunchKernelGGL(flat_scatter_lds_kernel<KW>, dim3((unsigned)std::max(1, cus)), dim3(FSL_THREADS),
+                           fsl_lds_bytes<KW>(), s, a2);
     hipLaunchKernelGGL(bin_parts_kernel<KW>, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a2);
     return hipGetLastError();
 }

@@ -241,6 +241,7 @@ struct BinArgs {
     // (with cutoff >= 1 they are pruned anyway: exact).  Partitions are then
     // sized by the keys that do enter the table (rho_tab) and by the sketch
     uint32_t pf;               // 1: pre-filter the flat bins (prune, cutoff >= 1, no first-occurrence tracking)
+    uint32_t fs_lds;           // 1: heavy bins with 9..2048 partitions write their lists LDS-staged
     float rho_tab;             // expected table keys per occurrence under the pre-filter
     unsigned long long* tab_keys;  // (zeroed) keys that entered a table
 };
