@@ -234,7 +234,6 @@ struct kb_ctx {
     uint64_t bucket_cap_used = 0;  // the capacity (region stride) the regions were written with
     DevBuf<uint64_t> kpart;    // per-block k-mer sums of the count pass
     float rho = 0.f;           // learned distinct / occurrences
-    float kept_ratio = 1.f;    // learned kept ids / occurrences (the LDS list window's depth)
     float rho_tab = 0.f;       // learned table keys / occurrences under the singleton pre-filter
     DevBuf<uint32_t> hll;      // cold pass: HyperLogLog registers (launch_hll)
     bool bucket_failed = false;  // a bucket overflowed its mmer map: radix path from now on
@@ -1570,7 +1569,10 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.id_off = (uint32_t)(affine ? id_c : 0);
         a.max_entries = ecap - 1;
         a.max_ids = N;
-        if (env_int("KB_BIN_LDS_LISTS", 0)) {
+        // lists placed and ordered in LDS id windows by the bins (lists_kernel
+        // then takes only the queued items: lists > 256 ids, partitions whose
+        // ids took the global path)
+        if (env_int("KB_BIN_LDS_LISTS", 1)) {
             // items <= entries (every item holds >= 1 entry): one slot per entry
             HIPCHK(c->lq.ensure(ecap + 1));
             HIPCHK(hipMemsetAsync(c->lq.p, 0, sizeof(uint64_t), c->s));
@@ -1578,7 +1580,6 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             a.lq_items = c->lq.p + 1;
             a.lq_cap = ecap;
         }
-        a.kept_ratio = c->kept_ratio;
         a.fs_lds = (uint32_t)(env_int("KB_BIN_FSL", 1) != 0);
         // singleton pre-filter for the heavy bins: where most distinct keys are
         // pruned singletons (high error rates, low coverage: C5), learned from
@@ -1590,7 +1591,6 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             a.rho_tab = c->rho_tab > 0.f ? c->rho_tab : a.rho;
             a.tab_keys = reinterpret_cast<unsigned long long*>(c->totals.p + 11);
         }
-        a.win_fill = (float)std::min(1.2, std::max(0.3, env_int("KB_BIN_WIN_PCT", 100) / 100.0));
         HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr));
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
@@ -1667,7 +1667,6 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     c->n_occ_entries_hint = c->n_entries;
     c->ecap_hint = c->n_entries + c->n_entries / 4 + 1024;
     if (N) c->rho = (float)((double)c->n_distinct / (double)N);
-    if (N) c->kept_ratio = std::max(0.01f, (float)((double)c->n_ids / (double)N));
     // keys the tables will hold under the pre-filter: measured when it ran,
     // else the kept keys plus a margin for sketch collisions and counts 2..cutoff
     if (N) c->rho_tab = a.pf ? (float)((double)c->h_totals[11] / (double)N * 1.05)

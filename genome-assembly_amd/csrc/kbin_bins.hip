@@ -566,7 +566,9 @@ DEV uint64_t lds_load_u64(const uint64_t* p) {
 
 struct alignas(16) BinShared {
     uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, part0;
-    uint32_t n_single, pad_[3];  // pre-filter: keys seen once in this partition
+    uint32_t n_single;  // pre-filter: keys seen once in this partition
+    uint32_t maxc;      // the partition's longest kept list (the LDS id windows)
+    unsigned long long wkey;  // LDS id windows: cursor << 32 | entry << 16 | slot of the next window's start
     unsigned long long e0, i0, stage_base;
     uint32_t flat_idx, fa, fb, l0;
     uint32_t stack_p[BIN_STACK], stack_l[BIN_STACK];
@@ -940,61 +942,113 @@ template <int R>
 DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane);
 
 template <int KW>
-DEV void lds_lists(const BinArgs& A, uint32_t* cnt, uint32_t* win, uint32_t ns,
-                                                    unsigned long long e0, unsigned long long i0, uint32_t n_ent,
-                                                    uint32_t n_ids, const uint64_t* stage, bool filt,
-                                                    const uint64_t* kst, uint32_t P, uint32_t pmask) {
+DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, uint32_t* win, uint32_t win_cap,
+                   uint32_t ns, unsigned long long e0, unsigned long long i0, uint32_t n_ent, uint32_t n_ids,
+                   const uint64_t* stage, bool filt, const uint64_t* kst, uint32_t P, uint32_t pmask,
+                   uint32_t e_mine) {
     const uint32_t tid = threadIdx.x;
     const int lane = (int)(tid & 63u);
-    // ---- sweep 2 into the window (the claim words and rings are dead)
-    for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
-        if (filt && (kst_load<KW>(kst, i).part() & pmask) != P) continue;
-        const uint64_t v = stage[i];
-        if (!(v >> 48)) continue;  // a pre-filtered single
-        const uint32_t pos = atomicAdd(&cnt[(uint32_t)(v >> 48) - 1u], 1u);
-        if (pos < PRUNED) win[pos] = (uint32_t)v + 1u;  // ordinal + 1 (0 pads the sorts)
-    }
-    __syncthreads();
-    // ---- every list in place: a wave takes 64 entries at a time
-    for (uint32_t eb = (tid & ~63u); eb < n_ent; eb += BIN_THREADS) {
-        const uint32_t e = eb + (uint32_t)lane;
-        const uint32_t c = e < n_ent ? A.e_cnt[e0 + e] : 0u;
-        const uint32_t st_me = e < n_ent ? (uint32_t)(A.e_off[e0 + e] - i0) : 0u;
-        if (c >= 2 && c <= 32) sort32_inplace(win + st_me, c);
-        uint64_t m = __ballot(c > 32u);
-        while (m) {
-            const int src = __builtin_ctzll(m);
-            m &= m - 1ull;
-            const uint32_t n = (uint32_t)__shfl((int)c, src, 64);
-            const uint32_t st = (uint32_t)__shfl((int)st_me, src, 64);
-            wave_sync();
-            if (n <= 64) wave_sort_desc<1>(win + st, n, lane);
-            else if (n <= 128) wave_sort_desc<2>(win + st, n, lane);
-            else if (n <= 256) wave_sort_desc<4>(win + st, n, lane);
-            else {  // the list kernels order it from ids_ord (one-entry item)
-                for (uint32_t j = (uint32_t)lane; j < n; j += 64) A.ids_ord[i0 + st + j] = win[st + j] - 1u;
-                if (lane == 0) {
-                    const unsigned long long q = atomicAdd(A.lq_n, 1ull);
-                    if (q < A.lq_cap) A.lq_items[q] = ((e0 + eb + (uint32_t)src) << 16) | 1ull;
-                }
+    const uint32_t per = TS / BIN_THREADS;
+    const uint32_t cap = win_cap - 3u;  // (a window starts at its ids' 16-B phase)
+    // Windows: runs of whole lists.  The prune scan hands out entries and ids
+    // in slot order, so a window is a slot range [slo, shi), an entry range
+    // [elo, ehi) and an id range [wlo, whi) at once; each window re-reads the
+    // partition's stage (MALL-resident: written moments ago) instead of
+    // re-expanding the records (every list <= win_cap - 3 ids: the caller checked)
+    uint32_t wlo = 0, elo = 0, slo = 0;
+    while (wlo < n_ids) {  // uniform
+        uint32_t whi = n_ids, ehi = n_ent, shi = TS;
+        const unsigned long long g0 = i0 + wlo;
+        // id wlo sits at win[sh]: window and ids_out share their 16-B phase
+        const uint32_t sh = (uint32_t)(g0 & 3u);
+        uint32_t* const wv = win + sh;
+        if (n_ids - wlo > cap) {
+            // the window ends where the list holding id wlo + win_cap starts:
+            // the kept slot with the largest cursor <= that position (earlier
+            // windows' cursors have reached their list ends, <= wlo)
+            const uint32_t X = wlo + cap;
+            if (tid == 0) S.wkey = 0;
+            __syncthreads();
+            unsigned long long best = 0;
+            uint32_t e = e_mine;
+            for (uint32_t k = 0; k < per; k++) {
+                const uint32_t i = tid * per + k, c = cnt[i];
+                if (c >= PRUNED) continue;
+                if (c <= X) best = ((unsigned long long)c << 32) | ((unsigned long long)e << 16) | i;
+                e++;
             }
-            wave_sync();
+            if (best) atomicMax(&S.wkey, best);
+            __syncthreads();
+            const unsigned long long w = S.wkey;
+            whi = (uint32_t)(w >> 32);
+            ehi = (uint32_t)(w >> 16) & 0xFFFFu;
+            shi = (uint32_t)w & 0xFFFFu;
         }
+        // ---- this window's occurrences into LDS at their list positions
+        // (the claim words and rings are dead); four stage loads in flight
+        for (uint32_t i0s = tid; i0s < ns; i0s += 4u * BIN_THREADS) {
+            uint64_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0s + (uint32_t)u * BIN_THREADS;
+                v[u] = i < ns ? stage[i] : 0ull;
+                if (filt && i < ns && (kst_load<KW>(kst, i).part() & pmask) != P) v[u] = 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (!(v[u] >> 48)) continue;  // (a pre-filtered single, or nothing)
+                const uint32_t ls = (uint32_t)(v[u] >> 48) - 1u;
+                if (ls - slo >= shi - slo) continue;  // another window's list
+                const uint32_t pos = atomicAdd(&cnt[ls], 1u);
+                if (pos < PRUNED) wv[pos - wlo] = (uint32_t)v[u] + 1u;  // ordinal + 1 (0 pads the sorts)
+            }
+        }
+        __syncthreads();
+        // ---- every list in place: a wave takes 64 entries at a time
+        for (uint32_t eb = elo + (tid & ~63u); eb < ehi; eb += BIN_THREADS) {
+            const uint32_t e = eb + (uint32_t)lane;
+            const uint32_t c = e < ehi ? A.e_cnt[e0 + e] : 0u;
+            const uint32_t st_me = e < ehi ? (uint32_t)(A.e_off[e0 + e] - i0) - wlo : 0u;
+            if (c >= 2 && c <= 32) sort32_inplace(wv + st_me, c);
+            uint64_t m = __ballot(c > 32u);
+            while (m) {
+                const int src = __builtin_ctzll(m);
+                m &= m - 1ull;
+                const uint32_t n = (uint32_t)__shfl((int)c, src, 64);
+                const uint32_t st = (uint32_t)__shfl((int)st_me, src, 64);
+                wave_sync();
+                if (n <= 64) wave_sort_desc<1>(wv + st, n, lane);
+                else if (n <= 128) wave_sort_desc<2>(wv + st, n, lane);
+                else if (n <= 256) wave_sort_desc<4>(wv + st, n, lane);
+                else {  // the list kernels order it from ids_ord (one-entry item)
+                    for (uint32_t j = (uint32_t)lane; j < n; j += 64) A.ids_ord[g0 + st + j] = wv[st + j] - 1u;
+                    if (lane == 0) {
+                        const unsigned long long q = atomicAdd(A.lq_n, 1ull);
+                        if (q < A.lq_cap) A.lq_items[q] = ((e0 + eb + (uint32_t)src) << 16) | 1ull;
+                    }
+                }
+                wave_sync();
+            }
+        }
+        __syncthreads();
+        // ---- the window as read ids, 16-B stores where aligned
+        const uint32_t nw = whi - wlo;
+        const uint32_t head = min((4u - sh) & 3u, nw);
+        if (tid < head) A.ids_out[g0 + tid] = id_of(wv[tid] - 1u, A.read_ids, A.id_off);
+        const uint32_t body = (nw - head) / 4u;
+        int4* dst4 = reinterpret_cast<int4*>(A.ids_out + g0 + head);
+        for (uint32_t g = tid; g < body; g += BIN_THREADS) {
+            const uint4 x = *reinterpret_cast<const uint4*>(wv + head + 4u * g);
+            dst4[g] = make_int4(id_of(x.x - 1u, A.read_ids, A.id_off), id_of(x.y - 1u, A.read_ids, A.id_off),
+                                id_of(x.z - 1u, A.read_ids, A.id_off), id_of(x.w - 1u, A.read_ids, A.id_off));
+        }
+        for (uint32_t j = head + 4u * body + tid; j < nw; j += BIN_THREADS)
+            A.ids_out[g0 + j] = id_of(wv[j] - 1u, A.read_ids, A.id_off);
+        __syncthreads();  // (the window is the next window's, then the next partition's table)
+        wlo = whi;
+        elo = ehi;
+        slo = shi;
     }
-    __syncthreads();
-    // ---- the window as read ids, 16-B stores where aligned
-    const uint32_t head = min((uint32_t)((4u - (uint32_t)(i0 & 3u)) & 3u), n_ids);
-    if (tid < head) A.ids_out[i0 + tid] = id_of(win[tid] - 1u, A.read_ids, A.id_off);
-    const uint32_t body = (n_ids - head) / 4u;
-    int4* dst4 = reinterpret_cast<int4*>(A.ids_out + i0 + head);
-    for (uint32_t g = tid; g < body; g += BIN_THREADS) {
-        const uint4 v = *reinterpret_cast<const uint4*>(win + head + 4u * g);
-        dst4[g] = make_int4(id_of(v.x - 1u, A.read_ids, A.id_off), id_of(v.y - 1u, A.read_ids, A.id_off),
-                            id_of(v.z - 1u, A.read_ids, A.id_off), id_of(v.w - 1u, A.read_ids, A.id_off));
-    }
-    for (uint32_t j = head + 4u * body + tid; j < n_ids; j += BIN_THREADS)
-        A.ids_out[i0 + j] = id_of(win[j] - 1u, A.read_ids, A.id_off);
-    __syncthreads();  // (the window is the next partition's table)
 }
 
 template <int KW, int PHASE>
@@ -1130,13 +1184,6 @@ DEV void bin_body(const BinArgs& A) {
             while (l0 < lmax && (occ_tot >> l0) > A.split_occ) l0++;
             split = l0 >= 1;
         }
-        if (PHASE == 0 && !flat && !split && lds_ok) {
-            // the LDS path needs a partition's kept ids in the window: deepen
-            // the first split until the expected ones fit (a partition that
-            // still overflows it takes the global path)
-            const double kept = (double)occ_tot * (double)A.kept_ratio;
-            while (l0 < 12 && kept > (double)A.win_fill * (double)win_cap * (double)(1u << l0)) l0++;
-        }
         // pre-filtered heavy bin: partitions sized by the keys that enter the
         // table and by the sketch (both fewer than the distinct keys)
         const uint32_t sk_words = (uint32_t)BIN_WAVES * Q * (8u * KW + 6u) / 4u, sk_cells = sk_words * 16u;
@@ -1210,6 +1257,7 @@ DEV void bin_body(const BinArgs& A) {
                 S.overflow = 0;
                 S.n_stage = 0;
                 S.n_single = 0;
+                S.maxc = 0;
             }
             for (uint32_t i = tid; i < TS; i += BIN_THREADS) {
                 T.ca[i] = 0;
@@ -1414,12 +1462,14 @@ DEV void bin_body(const BinArgs& A) {
             __syncthreads();
             const unsigned long long e0 = S.e0, i0 = S.i0;
             const bool room = !(e0 + (uint32_t)tot > A.max_entries || i0 + (uint32_t)(tot >> 32) > A.max_ids);
+            uint32_t mc = 0;  // (the longest kept list: the LDS windows hold whole lists)
             {
                 uint32_t e = (uint32_t)ex, off = (uint32_t)(ex >> 32);
                 for (uint32_t k = 0; k < per; k++) {
                     const uint32_t i = tid * per + k;
                     const uint32_t c = cnt[i];
                     if (T.ca[i] && c > A.keep_gt) {
+                        mc = max(mc, c);
                         if (room) {
                             const uint64_t ge = e0 + e;
                             TKey<KW> key;
@@ -1442,14 +1492,15 @@ DEV void bin_body(const BinArgs& A) {
                     }
                 }
             }
+            if (lds_ok && mc) atomicMax(&S.maxc, mc);
             __threadfence_block();
             __syncthreads();
             PROF_MARK(3);
             if (!room) continue;
             const uint32_t n_ent = (uint32_t)tot, n_ids = (uint32_t)(tot >> 32);
-            if (lds_ok && n_ids <= win_cap) {
-                lds_lists<KW>(A, cnt, win, S.n_stage, e0, i0, n_ent, n_ids, stage, flat && Lv > l0,
-                              kst + KW * (uint64_t)fa, P, (1u << Lv) - 1u);
+            if (lds_ok && S.maxc <= win_cap - 3u) {
+                lds_lists<KW>(A, S, cnt, TS, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage, flat && Lv > l0,
+                              kst + KW * (uint64_t)fa, P, (1u << Lv) - 1u, (uint32_t)ex);
                 PROF_MARK(4);
                 continue;
             }

@@ -233,8 +233,6 @@ struct BinArgs {
     uint64_t* lq_items;
     unsigned long long* lq_n;  // (zeroed) items
     uint64_t lq_cap;
-    float kept_ratio;          // expected kept ids per occurrence (last finalize)
-    float win_fill;            // target share of the LDS id window when choosing the depth
     // singleton pre-filter of heavy (flat) bins: a partition's k-mers first
     // go through a 2-bit "seen twice" sketch in LDS; keys seen once are
     // counted (distinct) but never enter the table, the stage or sweep 2

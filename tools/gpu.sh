@@ -7,7 +7,7 @@
 #   ktrace TAG [bench.py args]  rocprofv3 kernel trace + stats -> gpurun_out/kt_TAG/
 #   pmc TAG [bench.py args]     FETCH_SIZE and WRITE_SIZE in two separate --pmc
 #                               passes -> gpurun_out/pmc_TAG_{fetch,write}/
-#   sq TAG [bench.py args]      one --pmc pass of 8 SQ counters -> gpurun_out/sq_TAG/
+#   sq TAG [bench.py args]      one --pmc pass of 8 SQ counters (or $SQ_SET) -> gpurun_out/sq_TAG/
 #
 # Every GPU step runs under its own `timeout -k 10`; a failing step ends the
 # script with its exit status (callers chain modes with &&).
@@ -37,8 +37,9 @@ case $mode in
       -- python3 bench.py --cpu-sample 0 "$@" > gpurun_out/pmc_${tag}_write.log 2>&1 ;;
   sq)
     tag=${1:?tag}; shift
-    timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
-      SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv \
+    # SQ_SET: another 8 counters for the same pass (one block, at most 8 SQ_)
+    timeout -k 10 600 rocprofv3 --pmc ${SQ_SET:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+      SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE} --output-format csv \
       -d gpurun_out/sq_$tag -o sq -- python3 bench.py --cpu-sample 0 "$@" > gpurun_out/sq_$tag.log 2>&1 ;;
   *) echo "unknown mode $mode" >&2; exit 2 ;;
 esac

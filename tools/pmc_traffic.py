@@ -59,7 +59,8 @@ def main():
     # the bin phase as one "kernel" (bench.py's roofline kernel when heavy bins
     # dominate: C3, C5): every kernel between the bucket ordering and the lists
     phase = [k for k in table if any(x in k for x in ("bin_kernel", "flat_count_kernel", "flat_scan_kernel",
-                                                        "flat_scatter_kernel", "bin_parts_kernel",
+                                                        "flat_scatter_kernel", "flat_scatter_lds_kernel",
+                                                        "bin_parts_kernel",
                                                         "bins_final_kernel"))]
     if phase:
         table["bin phase"] = {"dispatches": min(table[k]["dispatches"] for k in phase),
