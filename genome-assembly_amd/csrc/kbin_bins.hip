@@ -1498,7 +1498,10 @@ DEV void bin_body(const BinArgs& A) {
             PROF_MARK(3);
             if (!room) continue;
             const uint32_t n_ent = (uint32_t)tot, n_ids = (uint32_t)(tot >> 32);
-            if (lds_ok && S.maxc <= win_cap - 3u) {
+            // LDS id windows for the light bins' short lists (high coverage --
+            // long lists -- and the heavy bins' partitions measured slower:
+            // C3 357 -> 479 ms, C5 624 -> 641 ms per step)
+            if (PHASE == 0 && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
                 lds_lists<KW>(A, S, cnt, TS, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage, flat && Lv > l0,
                               kst + KW * (uint64_t)fa, P, (1u << Lv) - 1u, (uint32_t)ex);
                 PROF_MARK(4);
