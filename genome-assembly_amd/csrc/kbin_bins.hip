@@ -552,12 +552,19 @@ __device__ unsigned long long g_bin_prof[16];
         }                                                          \
     } while (0)
 #define PROF_CNT(i, v) do { if (tid == 0) pacc[i] += (v); } while (0)
+#define PROF_PARAMS , unsigned long long *pacc, unsigned long long &pt
+#define PROF_ARGS , pacc, pt
 #else
+#define PROF_PARAMS
+#define PROF_ARGS
 #define PROF_MARK(ph) do {} while (0)
 #define PROF_CNT(i, v) do {} while (0)
 #endif
 
-constexpr int BIN_THREADS = 1024;
+#ifndef KB_BIN_THREADS
+#define KB_BIN_THREADS 1024
+#endif
+constexpr int BIN_THREADS = KB_BIN_THREADS;  // (A/B builds: -DKB_BIN_THREADS=512 with KB_BIN_TS_LOG2=12)
 constexpr int BIN_STACK = 32;
 
 DEV uint64_t lds_load_u64(const uint64_t* p) {
@@ -568,7 +575,7 @@ struct alignas(16) BinShared {
     uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, part0;
     uint32_t n_single;  // pre-filter: keys seen once in this partition
     uint32_t maxc;      // the partition's longest kept list (the LDS id windows)
-    unsigned long long wkey;  // LDS id windows: cursor << 32 | entry << 16 | slot of the next window's start
+    unsigned long long wkey;  // LDS id windows: cursor << 32 | entry << 16 | scan index of the next window's start
     unsigned long long e0, i0, stage_base;
     uint32_t flat_idx, fa, fb, l0;
     uint32_t stack_p[BIN_STACK], stack_l[BIN_STACK];
@@ -619,7 +626,11 @@ struct TKey;
 template <>
 struct TKey<1> {
     uint64_t a;
-    DEV uint32_t hash() const { return (uint32_t)mix64(a - 1ull); }
+    // the table bucket (low bits): the top bits of one 32-bit multiplicative
+    // hash of the folded code, bit-reversed -- 4 instructions where a full
+    // 64-bit mix took ~15 (bucket overflow measured the same on genome k-mers:
+    // 6.3 % vs 6.1 % of the keys past their home bucket at 60 % fill)
+    DEV uint32_t hash() const { return __builtin_bitreverse32(((uint32_t)a ^ (uint32_t)(a >> 32)) * 0x85EBCA6Bu); }
     DEV uint32_t part() const { return part_of(a - 1ull); }
     DEV void code(uint64_t& hi, uint64_t& lo) const {
         hi = 0;
@@ -937,7 +948,7 @@ constexpr uint64_t M48 = (1ull << 48) - 1ull;
 // kernels.  The partition's entries [e0, e0 + n_ent) are read back densely
 // from e_cnt / e_off (this block wrote them: L2).  Not inlined: its sorting
 // registers stay out of the sweeps' allocation.
-DEV void sort32_inplace(uint32_t* p, uint32_t n);
+DEV void sort_lists_lane(uint32_t* p, uint32_t n);
 template <int R>
 DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane);
 
@@ -945,14 +956,15 @@ template <int KW>
 DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, uint32_t* win, uint32_t win_cap,
                    uint32_t ns, unsigned long long e0, unsigned long long i0, uint32_t n_ent, uint32_t n_ids,
                    const uint64_t* stage, bool filt, const uint64_t* kst, uint32_t P, uint32_t pmask,
-                   uint32_t e_mine) {
+                   uint32_t e_mine PROF_PARAMS) {
     const uint32_t tid = threadIdx.x;
     const int lane = (int)(tid & 63u);
     const uint32_t per = TS / BIN_THREADS;
     const uint32_t cap = win_cap - 3u;  // (a window starts at its ids' 16-B phase)
     // Windows: runs of whole lists.  The prune scan hands out entries and ids
-    // in slot order, so a window is a slot range [slo, shi), an entry range
-    // [elo, ehi) and an id range [wlo, whi) at once; each window re-reads the
+    // in scan order (thread t, then its k-th slot t + 1024 k), so a window is
+    // a range [slo, shi) of that order, an entry range [elo, ehi) and an id
+    // range [wlo, whi) at once; each window re-reads the
     // partition's stage (MALL-resident: written moments ago) instead of
     // re-expanding the records (every list <= win_cap - 3 ids: the caller checked)
     uint32_t wlo = 0, elo = 0, slo = 0;
@@ -972,9 +984,9 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
             unsigned long long best = 0;
             uint32_t e = e_mine;
             for (uint32_t k = 0; k < per; k++) {
-                const uint32_t i = tid * per + k, c = cnt[i];
+                const uint32_t i = tid + k * BIN_THREADS, c = cnt[i];
                 if (c >= PRUNED) continue;
-                if (c <= X) best = ((unsigned long long)c << 32) | ((unsigned long long)e << 16) | i;
+                if (c <= X) best = ((unsigned long long)c << 32) | ((unsigned long long)e << 16) | (tid * per + k);
                 e++;
             }
             if (best) atomicMax(&S.wkey, best);
@@ -998,18 +1010,20 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
             for (int u = 0; u < 4; u++) {
                 if (!(v[u] >> 48)) continue;  // (a pre-filtered single, or nothing)
                 const uint32_t ls = (uint32_t)(v[u] >> 48) - 1u;
-                if (ls - slo >= shi - slo) continue;  // another window's list
+                const uint32_t o = (ls & (BIN_THREADS - 1u)) * per + ls / BIN_THREADS;  // (scan order)
+                if (o - slo >= shi - slo) continue;  // another window's list
                 const uint32_t pos = atomicAdd(&cnt[ls], 1u);
                 if (pos < PRUNED) wv[pos - wlo] = (uint32_t)v[u] + 1u;  // ordinal + 1 (0 pads the sorts)
             }
         }
         __syncthreads();
+        PROF_MARK(4);
         // ---- every list in place: a wave takes 64 entries at a time
         for (uint32_t eb = elo + (tid & ~63u); eb < ehi; eb += BIN_THREADS) {
             const uint32_t e = eb + (uint32_t)lane;
             const uint32_t c = e < ehi ? A.e_cnt[e0 + e] : 0u;
             const uint32_t st_me = e < ehi ? (uint32_t)(A.e_off[e0 + e] - i0) - wlo : 0u;
-            if (c >= 2 && c <= 32) sort32_inplace(wv + st_me, c);
+            sort_lists_lane(wv + st_me, c);
             uint64_t m = __ballot(c > 32u);
             while (m) {
                 const int src = __builtin_ctzll(m);
@@ -1031,6 +1045,7 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
             }
         }
         __syncthreads();
+        PROF_MARK(5);
         // ---- the window as read ids, 16-B stores where aligned
         const uint32_t nw = whi - wlo;
         const uint32_t head = min((4u - sh) & 3u, nw);
@@ -1045,6 +1060,7 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
         for (uint32_t j = head + 4u * body + tid; j < nw; j += BIN_THREADS)
             A.ids_out[g0 + j] = id_of(wv[j] - 1u, A.read_ids, A.id_off);
         __syncthreads();  // (the window is the next window's, then the next partition's table)
+        PROF_MARK(6);
         wlo = whi;
         elo = ehi;
         slo = shi;
@@ -1081,6 +1097,10 @@ DEV void bin_body(const BinArgs& A) {
     unsigned long long pt = clock64();
 #endif
     if (tid < 64) S.dummy[tid] = 0;  // (the first loop barrier publishes it)
+    // phase 0: block thread 0 claims the next bin one bin ahead, so the
+    // claim's round trip overlaps this bin's work instead of opening the next
+    unsigned long long next_item = 0;
+    if (PHASE == 0 && tid == 0) next_item = atomicAdd(A.work, 1ull);
 
     while (true) {
         // phase 0: persistent blocks take bins from a shared counter, largest
@@ -1090,7 +1110,8 @@ DEV void bin_body(const BinArgs& A) {
         __syncthreads();
         if (tid == 0) {
             if (PHASE == 0) {
-                S.item = (uint32_t)atomicAdd(A.work, 1ull);
+                S.item = (uint32_t)min(next_item, 0xFFFFFFFFull);
+                if (next_item < nbins) next_item = atomicAdd(A.work, 1ull);
             } else {
                 // items are offset-pool indices: entry e0 + p of a published
                 // bin is its partition p (the bin's last entry is no item)
@@ -1287,14 +1308,35 @@ DEV void bin_body(const BinArgs& A) {
                 uint64_t w0[4], w1[4];
                 T.load_bucket(h0 & bmask, w0);
                 T.load_bucket(h1 & bmask, w1);
-                int l0 = T.match(h0 & bmask, w0, k0, e0_);
-                int l1 = T.match(h1 & bmask, w1, k1, e1_);
-                // a new key claims its home bucket's first empty slot right
+                uint32_t bk0 = h0 & bmask, bk1 = h1 & bmask;
+                int l0 = T.match(bk0, w0, k0, e0_);
+                int l1 = T.match(bk1, w1, k1, e1_);
+                // a full home bucket without the key: its next bucket (the
+                // probe order), one more straight-line round for the wave's
+                // few such lanes (at 60 % fill 7 % of the keys live past their
+                // home bucket, so nearly every flush has some; the loop in
+                // insert() re-read the home bucket and serialised on the rest)
+                {
+                    const bool x0 = v0 && l0 == -2, x1 = v1 && l1 == -2;
+                    if (__ballot(x0 || x1)) {  // (wave-uniform)
+                        if (x0) {
+                            bk0 = (bk0 + 1u) & bmask;
+                            T.load_bucket(bk0, w0);
+                        }
+                        if (x1) {
+                            bk1 = (bk1 + 1u) & bmask;
+                            T.load_bucket(bk1, w1);
+                        }
+                        if (x0) l0 = T.match(bk0, w0, k0, e0_);
+                        if (x1) l1 = T.match(bk1, w1, k1, e1_);
+                    }
+                }
+                // a new key claims the first empty slot of its bucket right
                 // away (both claims in flight together); the key count is
                 // added per wave and checked against the limit after the
-                // sweep.  A lost claim or a full bucket takes the full insert
+                // sweep.  A lost claim or two full buckets take the full insert
                 // path (rare)
-                const uint32_t c0 = (h0 & bmask) * 4u + (uint32_t)e0_, c1 = (h1 & bmask) * 4u + (uint32_t)e1_;
+                const uint32_t c0 = bk0 * 4u + (uint32_t)e0_, c1 = bk1 * 4u + (uint32_t)e1_;
                 // (every lane issues both claims, so they go out back to back:
                 // a lane with nothing to claim compares 1 against its own
                 // always-zero dummy word, which never matches)
@@ -1436,11 +1478,13 @@ DEV void bin_body(const BinArgs& A) {
                 __syncthreads();
                 continue;
             }
-            // ---- prune (binning.c:1094-1102) + CSR allocation
+            // ---- prune (binning.c:1094-1102) + CSR allocation.  Thread t owns
+            // slots t, t + 1024, ...: a wave's reads of the table are consecutive
+            // words (owning 8 adjacent slots put 16 lanes on one LDS bank)
             uint64_t mine = 0;  // (ids << 32) | entries over this thread's slots
             const uint32_t per = TS / BIN_THREADS;  // TS >= BIN_THREADS
             for (uint32_t k = 0; k < per; k++) {
-                const uint32_t i = tid * per + k;
+                const uint32_t i = tid + k * BIN_THREADS;
                 const uint32_t c = cnt[i];
                 if (T.ca[i] && c > A.keep_gt) mine += ((uint64_t)c << 32) + 1ull;
             }
@@ -1466,7 +1510,7 @@ DEV void bin_body(const BinArgs& A) {
             {
                 uint32_t e = (uint32_t)ex, off = (uint32_t)(ex >> 32);
                 for (uint32_t k = 0; k < per; k++) {
-                    const uint32_t i = tid * per + k;
+                    const uint32_t i = tid + k * BIN_THREADS;
                     const uint32_t c = cnt[i];
                     if (T.ca[i] && c > A.keep_gt) {
                         mc = max(mc, c);
@@ -1503,7 +1547,7 @@ DEV void bin_body(const BinArgs& A) {
             // C3 357 -> 479 ms, C5 624 -> 641 ms per step)
             if (PHASE == 0 && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
                 lds_lists<KW>(A, S, cnt, TS, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage, flat && Lv > l0,
-                              kst + KW * (uint64_t)fa, P, (1u << Lv) - 1u, (uint32_t)ex);
+                              kst + KW * (uint64_t)fa, P, (1u << Lv) - 1u, (uint32_t)ex PROF_ARGS);
                 PROF_MARK(4);
                 continue;
             }
@@ -1538,7 +1582,7 @@ DEV void bin_body(const BinArgs& A) {
                 __syncthreads();
                 uint32_t e = (uint32_t)ex;
                 for (uint32_t k = 0; k < per; k++) {
-                    const uint32_t i = tid * per + k;
+                    const uint32_t i = tid + k * BIN_THREADS;
                     if (cnt[i] < PRUNED) A.e_first[e0 + e++] = T.ca[i];
                 }
             }
@@ -1950,7 +1994,7 @@ void bins_prof_report(hipStream_t s) {
     unsigned long long h[16];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bin_prof), sizeof(h));
-    static const char* nm[16] = {"occ", "zero", "sweep1", "prune/entries", "sweep2", "small sort", "big sort", "flat",
+    static const char* nm[16] = {"occ", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
                                  "partitions", "overflows", "big lists", "bins", "slowest-bin-occ", "slowest-bin-cycles",
                                  "occ", "-"};
     fprintf(stderr, "[bin_prof]");
@@ -2143,30 +2187,51 @@ DEV void wave_sort_list(const uint32_t* __restrict__ src, int32_t* __restrict__ 
 }
 
 // up to 32 values (ordinal + 1) sorted descending in one lane's registers, in place
-DEV void sort32_inplace(uint32_t* p, uint32_t n) {
-    uint32_t v[32];
+// Batcher's odd-even merge network on NP = 2^k inputs, descending (the larger
+// of every pair to the lower index), keeping only the comparators whose upper
+// index is < N: a list of n <= N ids padded with zeros (below every id + 1)
+// keeps its pads in place, so the pruned network sorts it.  NP = 32: 191
+// comparators (the bitonic network: 240); N = 24: 132; 16: 63; 8: 19
+template <int N, int NP>
+DEV void sort_net_desc(uint32_t* p, uint32_t n) {
+    uint32_t v[N];
 #pragma unroll
-    for (int j = 0; j < 32; j++) v[j] = (uint32_t)j < n ? p[j] : 0u;
+    for (int j = 0; j < N; j++) v[j] = (uint32_t)j < n ? p[j] : 0u;
 #pragma unroll
-    for (int kk = 2; kk <= 32; kk <<= 1) {
+    for (int q = 1; q < NP; q <<= 1)
 #pragma unroll
-        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+        for (int k = q; k >= 1; k >>= 1)
 #pragma unroll
-            for (int i = 0; i < 32; i++) {
-                const int l2 = i ^ jj;
-                if (l2 > i) {
-                    const uint32_t x = v[i], y = v[l2];
-                    const bool desc = (i & kk) == 0;
-                    const bool sw = desc ? (x < y) : (x > y);
-                    v[i] = sw ? y : x;
-                    v[l2] = sw ? x : y;
+            for (int j = k % q; j + k < NP; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; i++) {
+                    const int a = i + j, b = i + j + k;
+                    if (b < N && a / (2 * q) == b / (2 * q)) {
+                        const uint32_t x = v[a], y = v[b < N ? b : 0];
+                        v[a] = x > y ? x : y;
+                        v[b < N ? b : 0] = x > y ? y : x;
+                    }
                 }
-            }
-        }
-    }
 #pragma unroll
-    for (int j = 0; j < 32; j++)
+    for (int j = 0; j < N; j++)
         if ((uint32_t)j < n) p[j] = v[j];
+}
+
+// every lane's list of 2..32 ids (n outside that: nothing) in descending
+// order in its registers, with the smallest network that holds the wave's
+// longest such list (wave-uniform call)
+DEV void sort_lists_lane(uint32_t* p, uint32_t n) {
+    const bool me = n >= 2 && n <= 32;
+    const uint32_t m = wave_max_u32(me ? n : 0u);
+    if (m > 24) {
+        if (me) sort_net_desc<32, 32>(p, n);
+    } else if (m > 16) {
+        if (me) sort_net_desc<24, 32>(p, n);
+    } else if (m > 8) {
+        if (me) sort_net_desc<16, 16>(p, n);
+    } else if (m >= 2) {
+        if (me) sort_net_desc<8, 8>(p, n);
+    }
 }
 
 #ifdef KB_BIN_PROF
@@ -2287,10 +2352,8 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
             }
             lds_barrier();
             LPROF(1);
-            if (in_w) {
-                if (n_me <= 32) sort32_inplace(ibuf + sh + (rel - lo_w), n_me);
-                else mid[atomicAdd(&n_mid, 1u)] = tid;
-            }
+            sort_lists_lane(ibuf + sh + (rel - lo_w), in_w ? n_me : 0u);
+            if (in_w && n_me > 32) mid[atomicAdd(&n_mid, 1u)] = tid;
             lds_barrier();
             LPROF(2);
             const uint32_t nmid = n_mid;
