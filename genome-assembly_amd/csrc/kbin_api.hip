@@ -1551,6 +1551,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.rho = c->rho > 0.f ? c->rho : 0.25f;
         a.fill = (float)std::min(0.85, std::max(0.3, env_int("KB_BIN_FILL_PCT", 60) / 100.0));
         a.ablate = env_int("KB_BIN_ABLATE", 0);
+        a.ringfree = (uint32_t)(env_int("KB_BIN_RINGFREE", 1) != 0);
         a.gcount = reinterpret_cast<unsigned long long*>(c->totals.p + 4);
         a.status = c->misc.p + 2;  // the bin kernel's own status word
         a.e_mmer = c->e_mmer.p;

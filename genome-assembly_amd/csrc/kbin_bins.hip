@@ -561,6 +561,9 @@ __device__ unsigned long long g_bin_prof[16];
 #define PROF_CNT(i, v) do {} while (0)
 #endif
 
+#ifdef KB_BIN_PROF
+#define KB_BIN_ABL  // (diagnostic builds: KB_BIN_ABLATE switches parts of bin_kernel off)
+#endif
 #ifndef KB_BIN_THREADS
 #define KB_BIN_THREADS 1024
 #endif
@@ -797,6 +800,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t pmask = (1u << l) - 1u;
     const bool track = A.e_first != nullptr;  // k-mer positions only for KB_TRACK_FIRST
+    const bool ringfree = A.ringfree != 0;
     uint32_t head = 0, fill = 0;  // wave-uniform ring state
     auto ring = [&](uint32_t i) {
         if constexpr (KW == 1) return TKey<1>{qa[i]};
@@ -812,6 +816,20 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
         const uint32_t o0 = qo[i0], o1 = qo[i1];
         const uint16_t p0 = track ? qp[i0] : (uint16_t)0, p1 = track ? qp[i1] : (uint16_t)0;
         uint32_t b = 0;
+#ifdef KB_BIN_ABL
+        if (A.ablate == 8) {  // flushes without their stage reservation
+            f(k0, o0, p0, lane, v0, k1, o1, p1, 64 + lane, v1);
+            head = (head + cnt) & (Q - 1);
+            fill -= cnt;
+            wave_sync();
+            return;
+        }
+        if (A.ablate == 9) {  // no flush work at all: the ring writes alone
+            head = (head + cnt) & (Q - 1);
+            fill -= cnt;
+            return;
+        }
+#endif
         if (lane == 0) b = atomicAdd(ctr, cnt);
         b = (uint32_t)rfl((int)b);
         f(k0, o0, p0, b + lane, v0, k1, o1, p1, b + 64 + lane, v1);
@@ -821,6 +839,9 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
     };
     uint32_t base = lo + wid * 64;
     uint64_t nhd = 0;
+#ifdef KB_BIN_ABL
+    uint64_t abl_acc = 0;
+#endif
     Span<KW> nsp{};
     if (base + lane < hi) {
         nhd = A.hdr[base + lane];
@@ -842,23 +863,80 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
         // records of a bin are sorted longest first: lane 0 holds the chunk's max
         int nmax = rfl(n);
         if (__ballot(n > nmax)) nmax = rfl((int)wave_max_u32((uint32_t)n));
-        for (int j = 0; j < nmax; j++) {
-            const TKey<KW> key = sp.key(K, fl);
-            sp.step();
-            const bool take = j < n && (l == 0 || (key.part() & pmask) == p);
-            const uint64_t m = __ballot(take);
-            if (take) {
-                const uint32_t pos = (head + fill + lanes_below(m)) & (Q - 1);
-                qa[pos] = key.a;
-                if constexpr (KW == 2) qb[pos] = key.b;
-                qo[pos] = ord;
-                if (track) qp[pos] = (uint16_t)(rlo + (uint32_t)j);
+#ifdef KB_BIN_ABL
+        if (A.ablate == 7) {  // the record loads alone
+            abl_acc ^= hd ^ sp.key(K, fl).a;
+            continue;
+        }
+        if (A.ablate == 6) {  // the k-mer windows without the ring
+            for (int j = 0; j < nmax; j++) {
+                const TKey<KW> key = sp.key(K, fl);
+                sp.step();
+                if (j < n) abl_acc ^= key.a;
             }
-            fill += (uint32_t)__popcll(m);
+            continue;
+        }
+#endif
+        if (KW == 1 && l == 0 && ringfree) {
+            // an unpartitioned bin: every k-mer is taken, so the lanes hand
+            // their own records' k-mers j, j + 1 straight to f (records are
+            // sorted longest first: the valid lanes of a step are a prefix,
+            // so the stage stores stay contiguous) -- no ring writes and
+            // reads; the chunk's stage range is reserved once
+            const uint32_t tot = (uint32_t)rfl((int)wave_sum_u32((uint32_t)n));
+            uint32_t cb = 0;
+            if (lane == 0 && tot) cb = atomicAdd(ctr, tot);
+            cb = (uint32_t)rfl((int)cb);
+            for (int j = 0; j < nmax; j += 2) {
+                const TKey<KW> k0 = sp.key(K, fl);
+                sp.step();
+                const TKey<KW> k1 = sp.key(K, fl);
+                sp.step();
+                const bool v0 = j < n, v1 = j + 1 < n;
+                const uint64_t m0 = __ballot(v0), m1 = __ballot(v1);
+                const uint32_t s0 = cb + lanes_below(m0);
+                cb += (uint32_t)__popcll(m0);
+                const uint32_t s1 = cb + lanes_below(m1);
+                cb += (uint32_t)__popcll(m1);
+                f(k0, ord, (uint16_t)(rlo + (uint32_t)j), s0, v0, k1, ord, (uint16_t)(rlo + (uint32_t)j + 1u), s1,
+                  v1);
+            }
+            continue;
+        }
+        // U k-mer positions per trip (one fill update and flush check): the
+        // ring holds FL - 1 + 64 U entries, so U = (Q - FL) / 64
+        constexpr int U = (int)((Q - FL) / 64u);
+        for (int j = 0; j < nmax; j += U) {
+            TKey<KW> key[U];
+            bool take[U];
+            uint64_t m[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                key[u] = sp.key(K, fl);
+                sp.step();
+                take[u] = j + u < n && (l == 0 || (key[u].part() & pmask) == p);
+                m[u] = __ballot(take[u]);
+            }
+            uint32_t f0 = fill;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (take[u]) {
+                    const uint32_t pos = (head + f0 + lanes_below(m[u])) & (Q - 1);
+                    qa[pos] = key[u].a;
+                    if constexpr (KW == 2) qb[pos] = key[u].b;
+                    qo[pos] = ord;
+                    if (track) qp[pos] = (uint16_t)(rlo + (uint32_t)(j + u));
+                }
+                f0 += (uint32_t)__popcll(m[u]);
+            }
+            fill = f0;
             if (fill >= FL) flush(FL);
         }
     }
     if (fill) flush(fill);
+#ifdef KB_BIN_ABL
+    if (abl_acc == 0x123456789ull) qo[0] = 1u;  // (keeps the ablated work alive)
+#endif
 }
 
 // Every k-mer of the bin's records, once, to g(key, ordinal, position) on
@@ -961,6 +1039,9 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
     const int lane = (int)(tid & 63u);
     const uint32_t per = TS / BIN_THREADS;
     const uint32_t cap = win_cap - 3u;  // (a window starts at its ids' 16-B phase)
+#ifdef KB_BIN_ABL
+    if (A.ablate == 2 || A.ablate == 3 || A.ablate >= 5) return;  // no id windows (2, 5+: nothing staged)
+#endif
     // Windows: runs of whole lists.  The prune scan hands out entries and ids
     // in scan order (thread t, then its k-th slot t + 1024 k), so a window is
     // a range [slo, shi) of that order, an entry range [elo, ehi) and an id
@@ -1023,6 +1104,9 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
             const uint32_t e = eb + (uint32_t)lane;
             const uint32_t c = e < ehi ? A.e_cnt[e0 + e] : 0u;
             const uint32_t st_me = e < ehi ? (uint32_t)(A.e_off[e0 + e] - i0) - wlo : 0u;
+#ifdef KB_BIN_ABL
+            if (A.ablate == 4) continue;  // windows without their sorts
+#endif
             sort_lists_lane(wv + st_me, c);
             uint64_t m = __ballot(c > 32u);
             while (m) {
@@ -1299,8 +1383,8 @@ DEV void bin_body(const BinArgs& A) {
             // ordinal (slot field 0: not in the table -- a pre-filtered single)
             auto insert2 = [&](const TKey<KW>& k0, uint32_t o0, uint16_t p0, uint32_t s0, bool v0,
                                const TKey<KW>& k1, uint32_t o1, uint16_t p1, uint32_t s1, bool v1) {
-#ifdef KB_BIN_PROF
-                if (A.ablate == 1) return;  // expansion only
+#ifdef KB_BIN_ABL
+                if (A.ablate == 1 || A.ablate >= 8) return;  // expansion only
 #endif
                 const uint32_t h0 = k0.hash(), h1 = k1.hash();
                 // home buckets of both k-mers in flight together
@@ -1362,7 +1446,7 @@ DEV void bin_body(const BinArgs& A) {
                         S.overflow = 1;
                     } else {
                         atomicAdd(&cnt[l0], 1u);
-#ifdef KB_BIN_PROF
+#ifdef KB_BIN_ABL
                         if (A.ablate != 2)
 #endif
                         stage[s0] = ((uint64_t)(l0 + 1) << 48) | ((uint64_t)p0 << 32) | o0;
@@ -1373,7 +1457,7 @@ DEV void bin_body(const BinArgs& A) {
                         S.overflow = 1;
                     } else {
                         atomicAdd(&cnt[l1], 1u);
-#ifdef KB_BIN_PROF
+#ifdef KB_BIN_ABL
                         if (A.ablate != 2)
 #endif
                         stage[s1] = ((uint64_t)(l1 + 1) << 48) | ((uint64_t)p1 << 32) | o1;
@@ -1383,6 +1467,9 @@ DEV void bin_body(const BinArgs& A) {
             // (phase 0 never sweeps a flat partition: a flat bin is published
             // above -- each kernel compiles only its own paths)
             if (PHASE == 0 || !flat) {
+#ifdef KB_BIN_ABL
+                if (A.ablate != 5)  // 5: no sweep 1 at all (the per-bin overheads alone)
+#endif
                 for_each_kmer<KW>(A, lo, hi, P, Lv, qa, qb, qo, qp, &S.n_stage, insert2);
             } else if constexpr (PHASE == 1) {
                 // the partition's flat list, two entries per lane; a deeper split
@@ -1553,7 +1640,7 @@ DEV void bin_body(const BinArgs& A) {
             }
             // ---- sweep 2: drop every surviving occurrence's call ordinal in place
             {
-#ifdef KB_BIN_PROF
+#ifdef KB_BIN_ABL
                 const uint32_t ns = A.ablate ? 0u : S.n_stage;
 #else
                 const uint32_t ns = S.n_stage;

@@ -33,6 +33,12 @@ DEV uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
+DEV uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
+    return v;
+}
+
 template <typename T>
 DEV T wave_incl_scan(T v, int lane) {
 #pragma unroll

@@ -212,7 +212,9 @@ struct BinArgs {
     uint32_t ts_log2;
     float rho;                 // expected distinct keys per occurrence
     float fill;                // target table load when choosing the partition depth
-    int ablate;                // diagnostic build (KB_BIN_PROF) only: 1 expansion only, 2 no staging
+    uint32_t ringfree;         // unpartitioned bins expand without the per-wave ring (KB_BIN_RINGFREE)
+    int ablate;                // diagnostic builds (KB_BIN_PROF / KB_BIN_ABL) only: 1 expansion only,
+                               // 2 no staging, 3 no id windows, 4 windows without sorts
     unsigned long long* gcount;  // [0] entries << 32 | ids  [2] distinct keys before prune
     uint32_t* status;
     uint32_t* e_mmer;
