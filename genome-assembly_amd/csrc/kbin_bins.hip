@@ -216,6 +216,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     const int sh = 64 - 2 * M;
     const uint32_t maskM = (1u << (2 * M)) - 1u;
     const uint32_t halfM = 1u << (2 * M - 1);
+    const bool one_word = K <= 31 && M <= 12;  // (scores < 2^24 keep 8 bits for the offset)
     const uint32_t tid = threadIdx.x;
     uint64_t* stg = smem + 256 * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
     __shared__ uint32_t span_end;
@@ -254,19 +255,38 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
         for (;;) {
             while (lo < nK) {
                 // leftmost strict argmax of the canonical score over the window
-                uint64_t x = window64(sw, lo), y = window64(sw, lo + 32);
                 int best = -1, sig = lo;
                 uint32_t bsm = 0;
-                for (int p = lo; p < lo + W; p++) {
-                    const uint32_t sm = (uint32_t)(x >> sh);
-                    const int c = (int)(sm >= halfM ? sm : maskM - sm);
-                    if (c > best) {
-                        best = c;
-                        sig = p;
-                        bsm = sm;
+                if (one_word) {
+                    // K <= 31: the window's W mmers all lie in the 64-bit word at
+                    // lo, so each score is one shift of it (no shifting chain),
+                    // and the argmax is a max over (score << 8 | 255 - offset):
+                    // larger score first, then the leftmost position
+                    const uint64_t x = window64(sw, lo);
+                    uint32_t bk = 0;
+#pragma unroll 5
+                    for (int i = 0; i < W; i++) {
+                        const uint32_t sm = (uint32_t)(x >> (sh - 2 * i)) & maskM;
+                        const uint32_t c = max(sm, sm ^ maskM);  // (maskM - sm = sm ^ maskM)
+                        bk = max(bk, (c << 8) | (uint32_t)(255 - i));
                     }
-                    x = (x << 2) | (y >> 62);
-                    y <<= 2;
+                    const int i = 255 - (int)(bk & 255u);
+                    sig = lo + i;
+                    best = (int)(bk >> 8);
+                    bsm = (uint32_t)(x >> (sh - 2 * i)) & maskM;
+                } else {
+                    uint64_t x = window64(sw, lo), y = window64(sw, lo + 32);
+                    for (int p = lo; p < lo + W; p++) {
+                        const uint32_t sm = (uint32_t)(x >> sh);
+                        const int c = (int)(sm >= halfM ? sm : maskM - sm);
+                        if (c > best) {
+                            best = c;
+                            sig = p;
+                            bsm = sm;
+                        }
+                        x = (x << 2) | (y >> 62);
+                        y <<= 2;
+                    }
                 }
                 const uint64_t n = (uint64_t)(min(sig, nK - 1) - lo + 1);
                 if (!in_part((uint32_t)best, A.part, A.part_n)) {  // another pass's super-k-mer
@@ -1033,8 +1053,7 @@ DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane);
 template <int KW>
 DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, uint32_t* win, uint32_t win_cap,
                    uint32_t ns, unsigned long long e0, unsigned long long i0, uint32_t n_ent, uint32_t n_ids,
-                   const uint64_t* stage, bool filt, const uint64_t* kst, uint32_t P, uint32_t pmask,
-                   uint32_t e_mine PROF_PARAMS) {
+                   const uint64_t* stage, uint32_t e_mine PROF_PARAMS) {
     const uint32_t tid = threadIdx.x;
     const int lane = (int)(tid & 63u);
     const uint32_t per = TS / BIN_THREADS;
@@ -1085,7 +1104,6 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
             for (int u = 0; u < 4; u++) {
                 const uint32_t i = i0s + (uint32_t)u * BIN_THREADS;
                 v[u] = i < ns ? stage[i] : 0ull;
-                if (filt && i < ns && (kst_load<KW>(kst, i).part() & pmask) != P) v[u] = 0ull;
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -1633,8 +1651,8 @@ DEV void bin_body(const BinArgs& A) {
             // long lists -- and the heavy bins' partitions measured slower:
             // C3 357 -> 479 ms, C5 624 -> 641 ms per step)
             if (PHASE == 0 && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
-                lds_lists<KW>(A, S, cnt, TS, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage, flat && Lv > l0,
-                              kst + KW * (uint64_t)fa, P, (1u << Lv) - 1u, (uint32_t)ex PROF_ARGS);
+                lds_lists<KW>(A, S, cnt, TS, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage,
+                              (uint32_t)ex PROF_ARGS);
                 PROF_MARK(4);
                 continue;
             }
