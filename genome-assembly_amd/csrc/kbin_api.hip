@@ -1199,7 +1199,7 @@ static int bmap_learn(kb_ctx* c, uint32_t NB, uint64_t R, uint64_t nbins) {
 // (hash of the mmer); the learned capacity grows (and the pass reruns) when a
 // bucket overflows.  Reads: the one-pass super-k-mer kernel in region mode;
 // received: the block-aggregated converter.  Returns R and N (one sync per try).
-static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, uint64_t& N) {
+static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, uint64_t& R, uint64_t& N) {
     const int M = c->p.M;
     kb_ctx::BucketMap* bm = bmap_find(c, NB);
     const uint16_t* bmap = bm ? bm->map.p : nullptr;
@@ -1221,9 +1221,13 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
         const bool counting = exact && attempt == 0;
         const bool use_base = exact && attempt > 0;
         const uint64_t cap = exact ? 0 : c->bucket_cap;
-        HIPCHK(hipMemsetAsync(c->bfill.p, 0, NB * sizeof(unsigned long long), c->s));
-        HIPCHK(hipMemsetAsync(c->totals.p + 8, 0, sizeof(uint64_t), c->s));
-        HIPCHK(hipMemsetAsync(c->misc.p, 0, sizeof(uint32_t), c->s));
+        if (attempt > 0 || !zeroed) {  // (the finalize's first clear zeroed them for attempt 0)
+            ClearList cl{};
+            cl.add(c->bfill.p, NB * sizeof(unsigned long long));
+            cl.add(c->totals.p + 8, sizeof(uint64_t));
+            cl.add(c->misc.p, sizeof(uint32_t));
+            HIPCHK(launch_clear(cl, c->s));
+        }
         if (!counting && !use_base) HIPCHK(c->regions.ensure(NB * cap * RWD));
         for (auto& b : c->batches) {
             if (b.routed || !b.n_reads) continue;
@@ -1261,18 +1265,30 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, uint64_t& R, ui
             }
             c->tm.scan_insert_launches++;
         }
-        std::vector<unsigned long long> fill(NB);
-        HIPCHK(hipMemcpyAsync(fill.data(), c->bfill.p, NB * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->s));
-        HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
-        HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        std::vector<unsigned long long> fill(counting ? NB : 0);
+        uint64_t mx = 0;
+        if (counting) {  // the exact layout needs every bucket's count
+            HIPCHK(hipMemcpyAsync(fill.data(), c->bfill.p, NB * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                  c->s));
+            HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        } else {  // R, the largest bucket and the status word folded next to N: one copy
+            HIPCHK(launch_bucket_stats(c->bfill.p, NB, c->misc.p, c->totals.p, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        }
         HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync (two without a map): R and N size the rest
+        if (!counting) c->h_misc[0] = (uint32_t)c->h_totals[14];
         if (c->h_misc[0] & ST_NEG_ID)
             return fail(KB_EINVAL, "routed read ids must be non-negative (they order the id lists)");
         R = 0;
-        uint64_t mx = 0;
-        for (uint32_t d = 0; d < NB; d++) {
-            R += fill[d];
-            mx = std::max<uint64_t>(mx, fill[d]);
+        if (counting) {
+            for (uint32_t d = 0; d < NB; d++) {
+                R += fill[d];
+                mx = std::max<uint64_t>(mx, fill[d]);
+            }
+        } else {
+            R = c->h_totals[12];
+            mx = c->h_totals[13];
         }
         N = c->h_totals[8];
         if (counting) {  // exact bases for the writing pass
@@ -1353,9 +1369,6 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     c->tm.engine = KB_ENG_BINNED;
     REC(0);
     HIPCHK(c->totals.ensure(16));
-    HIPCHK(hipMemsetAsync(c->totals.p, 0, 16 * sizeof(uint64_t), c->s));
-    HIPCHK(hipMemsetAsync(c->misc.p, 0, 3 * sizeof(uint32_t), c->s));
-    REC(1);
     c->tm.scan_insert_launches = 0;
     uint64_t R = 0, N = 0;
     // bucketed (default): records into local bucket regions, one workgroup
@@ -1369,7 +1382,22 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     // local buckets (power of two, <= 1024): more buckets, more workgroups in flight
     uint32_t NB = 1;
     while (NB < (uint32_t)std::min(1024, std::max(64, env_int("KB_BIN_NB", 1024)))) NB <<= 1;
-    int rc = bucketed ? binned_buckets(c, NB, received, R, N)
+    // every counter of this finalize's first attempt zeroed in one launch
+    HIPCHK(c->flat_n.ensure(8));
+    {
+        ClearList cl{};
+        cl.add(c->totals.p, 16 * sizeof(uint64_t));
+        cl.add(c->misc.p, 3 * sizeof(uint32_t));
+        cl.add(c->flat_n.p, 8 * sizeof(unsigned long long));
+        if (bucketed) {
+            HIPCHK(c->bfill.ensure(NB));
+            cl.add(c->bfill.p, NB * sizeof(unsigned long long));
+        }
+        if (c->lq.p) cl.add(c->lq.p, sizeof(uint64_t));
+        HIPCHK(launch_clear(cl, c->s));
+    }
+    REC(1);
+    int rc = bucketed ? binned_buckets(c, NB, received, true, R, N)
                       : (received ? binned_sk_records(c, R, N) : binned_read_records(c, R, N, false));
     if (rc) return rc;
     c->n_occ = N;
@@ -1528,8 +1556,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             HIPCHK(c->flat_chunk.ensure(max_bins));
             HIPCHK(c->pool_bin.ensure(c->flat_off.cap));
             HIPCHK(c->chunk_bin.ensure(R / 1024 + max_bins + 1));
-            HIPCHK(c->flat_n.ensure(8));
-            HIPCHK(hipMemsetAsync(c->flat_n.p, 0, 8 * sizeof(unsigned long long), c->s));
+            if (attempt) HIPCHK(hipMemsetAsync(c->flat_n.p, 0, 8 * sizeof(unsigned long long), c->s));
             a.flat_list = c->flat_list.p;
             a.flat_next = c->flat_next.p;
             a.flat_l0 = c->flat_l0.p;
@@ -1575,8 +1602,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         // ids took the global path)
         if (env_int("KB_BIN_LDS_LISTS", 1)) {
             // items <= entries (every item holds >= 1 entry): one slot per entry
+            const uint64_t* lq_was = c->lq.p;
             HIPCHK(c->lq.ensure(ecap + 1));
-            HIPCHK(hipMemsetAsync(c->lq.p, 0, sizeof(uint64_t), c->s));
+            // (the first clear zeroed the head of the queue it saw; a queue
+            // allocated since needs its own)
+            if (attempt || c->lq.p != lq_was) HIPCHK(hipMemsetAsync(c->lq.p, 0, sizeof(uint64_t), c->s));
             a.lq_n = reinterpret_cast<unsigned long long*>(c->lq.p);
             a.lq_items = c->lq.p + 1;
             a.lq_cap = ecap;

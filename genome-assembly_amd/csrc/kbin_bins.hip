@@ -3341,6 +3341,46 @@ __global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_
     e_off[ne] = ni;
 }
 
+__global__ __launch_bounds__(1024) void clear_kernel(ClearList l) {
+    for (int k = 0; k < l.n; k++)
+        for (uint32_t i = threadIdx.x; i < l.words[k]; i += 1024) l.p[k][i] = 0u;
+}
+
+__global__ __launch_bounds__(1024) void bucket_stats_kernel(const unsigned long long* bfill, uint32_t NB,
+                                                            const uint32_t* misc, uint64_t* totals) {
+    __shared__ unsigned long long s_sum, s_max;
+    if (threadIdx.x == 0) {
+        s_sum = 0;
+        s_max = 0;
+    }
+    __syncthreads();
+    unsigned long long sum = 0, mx = 0;
+    for (uint32_t d = threadIdx.x; d < NB; d += 1024) {
+        sum += bfill[d];
+        mx = max(mx, bfill[d]);
+    }
+    atomicAdd(&s_sum, sum);
+    atomicMax(&s_max, mx);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        totals[12] = s_sum;
+        totals[13] = s_max;
+        totals[14] = misc[0];
+    }
+}
+
+hipError_t launch_bucket_stats(const unsigned long long* bfill, uint32_t NB, const uint32_t* misc, uint64_t* totals,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(bucket_stats_kernel, dim3(1), dim3(1024), 0, s, bfill, NB, misc, totals);
+    return hipGetLastError();
+}
+
+hipError_t launch_clear(const ClearList& l, hipStream_t s) {
+    if (l.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(clear_kernel, dim3(1), dim3(1024), 0, s, l);
+    return hipGetLastError();
+}
+
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                              uint64_t max_entries, hipStream_t s) {
     hipLaunchKernelGGL(bins_final_kernel, dim3(1), dim3(1), 0, s, gcount, e_off, totals, max_entries);

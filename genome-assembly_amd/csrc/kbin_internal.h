@@ -312,6 +312,22 @@ void lists_prof_report(hipStream_t s);
 hipError_t launch_digest(const uint32_t* mmer, const uint64_t* hi, const uint64_t* lo, const uint32_t* cnt,
                          const uint64_t* off, const int32_t* ids, uint64_t n_entries, unsigned long long* out,
                          hipStream_t s);
+// zero up to 8 device ranges (u32 words) in one launch: a finalize's counters
+// (a hipMemsetAsync each cost a launch and a host round trip)
+struct ClearList {
+    uint32_t* p[8];
+    uint32_t words[8];
+    int n;
+    void add(void* q, uint64_t bytes) {
+        p[n] = static_cast<uint32_t*>(q);
+        words[n++] = (uint32_t)(bytes / 4);
+    }
+};
+hipError_t launch_clear(const ClearList& l, hipStream_t s);
+// totals[12] = sum of the NB bucket fills (records), totals[13] = the largest,
+// totals[14] = status word misc[0]: the record pass's results in one copy
+hipError_t launch_bucket_stats(const unsigned long long* bfill, uint32_t NB, const uint32_t* misc, uint64_t* totals,
+                               hipStream_t s);
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                              uint64_t max_entries, hipStream_t s);
 
