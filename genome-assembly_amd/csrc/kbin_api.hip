@@ -270,6 +270,8 @@ struct kb_ctx {
     bool timing = false;
     kb_timing tm{};
     uint32_t nbins_hint = 0;  // bins of the last binned finalize (flat-list threshold)
+    // grid hints for kernels that usually have nothing to do (~0: not seen yet)
+    uint64_t hint_heavy = ~0ull, hint_lq = ~0ull, hint_long[2] = {~0ull, ~0ull};
     hipEvent_t ev[8] = {};
 };
 
@@ -1387,7 +1389,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     {
         ClearList cl{};
         cl.add(c->totals.p, 16 * sizeof(uint64_t));
-        cl.add(c->misc.p, 3 * sizeof(uint32_t));
+        cl.add(c->misc.p, 6 * sizeof(uint32_t));  // (status words, the list kernels' queue lengths)
         cl.add(c->flat_n.p, 8 * sizeof(unsigned long long));
         if (bucketed) {
             HIPCHK(c->bfill.ensure(NB));
@@ -1579,6 +1581,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.fill = (float)std::min(0.85, std::max(0.3, env_int("KB_BIN_FILL_PCT", 60) / 100.0));
         a.ablate = env_int("KB_BIN_ABLATE", 0);
         a.ringfree = (uint32_t)(env_int("KB_BIN_RINGFREE", 1) != 0);
+        a.heavy_hint = attempt ? ~0ull : c->hint_heavy;
         a.gcount = reinterpret_cast<unsigned long long*>(c->totals.p + 4);
         a.status = c->misc.p + 2;  // the bin kernel's own status word
         a.e_mmer = c->e_mmer.p;
@@ -1626,7 +1629,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
 #endif
-        HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries, c->s));
+        HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries, flat_l ? c->flat_n.p : nullptr,
+                                 a.lq_n, c->s));
         REC(4);
         ListArgs la{};
         la.totals = c->totals.p;
@@ -1643,13 +1647,17 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(c->long_q.ensure(2 * la.long_cap));
         la.long_q = c->long_q.p;
         la.long_n = c->misc.p + 4;
+        la.long_n_zeroed = attempt == 0;  // (the finalize's first clear)
+        la.lq_hint = attempt ? ~0ull : c->hint_lq;
+        la.long_hint[0] = attempt ? ~0ull : c->hint_long[0];
+        la.long_hint[1] = attempt ? ~0ull : c->hint_long[1];
         HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : ecap, c->s));
 #ifdef KB_BIN_PROF
         lists_prof_report(c->s);
 #endif
         REC(5);
-        HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 12 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
-        HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 14 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         if (R && !bucketed)
             HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         else c->h_misc[8] = 0;
@@ -1680,6 +1688,10 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         }
         break;
     }
+    c->hint_heavy = c->h_totals[12];
+    c->hint_lq = c->h_totals[13];
+    c->hint_long[0] = c->h_misc[4];
+    c->hint_long[1] = c->h_misc[5];
     const uint32_t bst = c->h_misc[2];
     if (c->h_misc[8]) return fail(KB_EDEVICE, "radix look-back timed out (device error word %u)", c->h_misc[8]);
     if (c->h_totals[3]) return fail(KB_EDEVICE, "internal: %llu bins > %llu", (unsigned long long)c->h_totals[3],

@@ -2794,16 +2794,26 @@ __global__ __launch_bounds__(LB_WAVES * 64) void lists_bucket_kernel(ListArgs A)
 }
 
 hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s) {
-    const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>(1, (max_entries + LIST_THREADS - 1) / LIST_THREADS), 16384);
-    hipError_t e = hipMemsetAsync(a.long_n, 0, 2 * sizeof(unsigned int), s);
-    if (e != hipSuccess) return e;
+    uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>(1, (max_entries + LIST_THREADS - 1) / LIST_THREADS), 16384);
+    // queued items / long lists of the last finalize (~0: none seen yet) size
+    // the grids: every list kernel strides over its queue
+    auto grid = [](uint64_t hint, uint64_t per_block, uint64_t full) {
+        if (hint == ~0ull) return full;
+        return std::min<uint64_t>(full, std::max<uint64_t>(16, (hint + hint / 2 + 64) / per_block));
+    };
+    if (a.lq_items) blocks = grid(a.lq_hint, 1, blocks);
+    if (!a.long_n_zeroed) {
+        hipError_t e = hipMemsetAsync(a.long_n, 0, 2 * sizeof(unsigned int), s);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(lists_kernel, dim3((unsigned)blocks), dim3(LIST_THREADS), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lists_bucket_kernel, dim3((unsigned)grid(a.long_hint[0], LB_WAVES, 4096)), dim3(LB_WAVES * 64), 0,
+                       s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(lists_bucket_kernel, dim3(4096), dim3(LB_WAVES * 64), 0, s, a);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(lists_long_kernel, dim3(1024), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(lists_long_kernel, dim3((unsigned)grid(a.long_hint[1], 4, 1024)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
@@ -3312,15 +3322,19 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     if (e != hipSuccess || !a.flat_l) return e;
     // the published bins: counts, offsets, flat lists -- every kernel exits at
     // once without any -- then their partitions, spread over every CU
+    // (grids: small when the last finalize published no such bin -- an empty
+    // launch then costs its dispatch only; every kernel strides over its work,
+    // so a surprise heavy bin is still binned, more slowly, once)
+    const bool few = a.heavy_hint == 0;
     const size_t fb_lds = (size_t)FLAT_MAX * sizeof(uint32_t);
-    const unsigned fb_blocks = (unsigned)std::max(1, cus) * 8u;
+    const unsigned fb_blocks = few ? 32u : (unsigned)std::max(1, cus) * 8u;
     hipLaunchKernelGGL(flat_count_kernel<KW>, dim3(fb_blocks), dim3(FB_THREADS), fb_lds, s, a2);
-    hipLaunchKernelGGL(flat_scan_kernel, dim3(1024), dim3(1024), 0, s, a2);
+    hipLaunchKernelGGL(flat_scan_kernel, dim3(few ? 32u : 1024u), dim3(1024), 0, s, a2);
     hipLaunchKernelGGL(flat_scatter_kernel<KW>, dim3(fb_blocks), dim3(FB_THREADS), fb_lds, s, a2);
     if (a2.fs_lds)
-        hipLaunchKernelGGL(flat_scatter_lds_kernel<KW>, dim3((unsigned)std::max(1, cus)), dim3(FSL_THREADS),
-                           fsl_lds_bytes<KW>(), s, a2);
-    hipLaunchKernelGGL(bin_parts_kernel<KW>, dim3((unsigned)blocks), dim3(BIN_THREADS), lds, s, a2);
+        hipLaunchKernelGGL(flat_scatter_lds_kernel<KW>, dim3(few ? 32u : (unsigned)std::max(1, cus)),
+                           dim3(FSL_THREADS), fsl_lds_bytes<KW>(), s, a2);
+    hipLaunchKernelGGL(bin_parts_kernel<KW>, dim3(few ? 32u : (unsigned)blocks), dim3(BIN_THREADS), lds, s, a2);
     return hipGetLastError();
 }
 
@@ -3330,7 +3344,11 @@ hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t 
 }
 
 __global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
-                                  uint64_t max_entries) {
+                                  uint64_t max_entries, const unsigned long long* flat_n,
+                                  const unsigned long long* lq_n) {
+    // (the next finalize's grid hints: published heavy / split bins, queued list items)
+    totals[12] = flat_n ? flat_n[0] : 0ull;
+    totals[13] = lq_n ? *lq_n : 0ull;
     // on overflow the counters ran past the capacity (status says so) and the
     // bins past it wrote nothing, so no entry range is whole: publish none (the
     // lists kernel then has no work and the host reruns at the exact need)
@@ -3382,8 +3400,9 @@ hipError_t launch_clear(const ClearList& l, hipStream_t s) {
 }
 
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
-                             uint64_t max_entries, hipStream_t s) {
-    hipLaunchKernelGGL(bins_final_kernel, dim3(1), dim3(1), 0, s, gcount, e_off, totals, max_entries);
+                             uint64_t max_entries, const unsigned long long* flat_n, const unsigned long long* lq_n,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(bins_final_kernel, dim3(1), dim3(1), 0, s, gcount, e_off, totals, max_entries, flat_n, lq_n);
     return hipGetLastError();
 }
 

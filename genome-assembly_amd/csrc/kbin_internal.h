@@ -213,6 +213,7 @@ struct BinArgs {
     float rho;                 // expected distinct keys per occurrence
     float fill;                // target table load when choosing the partition depth
     uint32_t ringfree;         // unpartitioned bins expand without the per-wave ring (KB_BIN_RINGFREE)
+    uint64_t heavy_hint;       // heavy / split bins the last finalize published (0: small grids for their kernels)
     int ablate;                // diagnostic builds (KB_BIN_PROF / KB_BIN_ABL) only: 1 expansion only,
                                // 2 no staging, 3 no id windows, 4 windows without sorts
     unsigned long long* gcount;  // [0] entries << 32 | ids  [2] distinct keys before prune
@@ -258,6 +259,9 @@ struct ListArgs {
                                // lists_bucket_kernel, [long_cap, 2 long_cap) passed on to lists_long_kernel
     uint64_t long_cap;
     unsigned int* long_n;      // [2] (zeroed) queue lengths
+    uint32_t long_n_zeroed;    // long_n cleared by the caller already
+    uint64_t lq_hint;          // grid hints from the last finalize (~0: none): queued items,
+    uint64_t long_hint[2];     // long lists for lists_bucket_kernel / lists_long_kernel
     const uint64_t* lq_items;  // BinArgs::lq_items (null: every entry, chunks of 256)
     const unsigned long long* lq_n;
     uint64_t lq_cap;
@@ -329,7 +333,8 @@ hipError_t launch_clear(const ClearList& l, hipStream_t s);
 hipError_t launch_bucket_stats(const unsigned long long* bfill, uint32_t NB, const uint32_t* misc, uint64_t* totals,
                                hipStream_t s);
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
-                             uint64_t max_entries, hipStream_t s);
+                             uint64_t max_entries, const unsigned long long* flat_n, const unsigned long long* lq_n,
+                             hipStream_t s);
 
 // launch helpers implemented in kbin_kernels.hip (all asynchronous on `s`)
 hipError_t launch_pack(const uint8_t* d_bases, const uint64_t* d_off, uint64_t n_reads,
