@@ -272,6 +272,7 @@ struct kb_ctx {
     uint32_t nbins_hint = 0;  // bins of the last binned finalize (flat-list threshold)
     // grid hints for kernels that usually have nothing to do (~0: not seen yet)
     uint64_t hint_heavy = ~0ull, hint_lq = ~0ull, hint_long[2] = {~0ull, ~0ull};
+    uint64_t hint_entries = 0, hint_ids = 0;  // the last finalize's entries and ids (kb_reset keeps them)
     hipEvent_t ev[8] = {};
 };
 
@@ -1582,6 +1583,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.ablate = env_int("KB_BIN_ABLATE", 0);
         a.ringfree = (uint32_t)(env_int("KB_BIN_RINGFREE", 1) != 0);
         a.heavy_hint = attempt ? ~0ull : c->hint_heavy;
+        // LDS id windows in heavy-bin partitions where the last finalize's lists
+        // were short on average (C4 share: 588 -> 502 ms per step; C3's lists of
+        // ~2300 ids measured 342 -> 351 ms with them)
+        a.win_heavy = (uint32_t)(env_int("KB_BIN_WIN_HEAVY", 1) != 0 &&
+                                 (c->hint_entries == 0 || c->hint_ids <= 128 * c->hint_entries));
         a.gcount = reinterpret_cast<unsigned long long*>(c->totals.p + 4);
         a.status = c->misc.p + 2;  // the bin kernel's own status word
         a.e_mmer = c->e_mmer.p;
@@ -1692,6 +1698,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     c->hint_lq = c->h_totals[13];
     c->hint_long[0] = c->h_misc[4];
     c->hint_long[1] = c->h_misc[5];
+    c->hint_entries = c->h_totals[0];
+    c->hint_ids = c->h_totals[1];
     const uint32_t bst = c->h_misc[2];
     if (c->h_misc[8]) return fail(KB_EDEVICE, "radix look-back timed out (device error word %u)", c->h_misc[8]);
     if (c->h_totals[3]) return fail(KB_EDEVICE, "internal: %llu bins > %llu", (unsigned long long)c->h_totals[3],

@@ -1647,10 +1647,12 @@ DEV void bin_body(const BinArgs& A) {
             PROF_MARK(3);
             if (!room) continue;
             const uint32_t n_ent = (uint32_t)tot, n_ids = (uint32_t)(tot >> 32);
-            // LDS id windows for the light bins' short lists (high coverage --
-            // long lists -- and the heavy bins' partitions measured slower:
-            // C3 357 -> 479 ms, C5 624 -> 641 ms per step)
-            if (PHASE == 0 && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
+            // LDS id windows for short lists (mean <= 64 ids): light bins, and
+            // the heavy bins' unfiltered partitions with one-word keys (C4
+            // share 588 -> 502 ms per step); long lists (C3: 357 -> 479 ms)
+            // and two-word keys (C5: 624 -> 641 ms) keep the global path
+            const bool win_phase = PHASE == 0 || (KW == 1 && A.win_heavy && !(flat && Lv > l0));
+            if (win_phase && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
                 lds_lists<KW>(A, S, cnt, TS, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage,
                               (uint32_t)ex PROF_ARGS);
                 PROF_MARK(4);
