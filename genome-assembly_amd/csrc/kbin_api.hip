@@ -273,6 +273,7 @@ struct kb_ctx {
     // grid hints for kernels that usually have nothing to do (~0: not seen yet)
     uint64_t hint_heavy = ~0ull, hint_lq = ~0ull, hint_long[2] = {~0ull, ~0ull};
     uint64_t hint_entries = 0, hint_ids = 0;  // the last finalize's entries and ids (kb_reset keeps them)
+    bool alpha_dirty = false;  // a pack kernel may have set the sticky alphabet status since it was cleared
     hipEvent_t ev[8] = {};
 };
 
@@ -396,7 +397,10 @@ extern "C" int kb_reset(kb_ctx* c) {
     c->ingest_unchecked = false;
     c->h_alpha[0] = c->h_alpha[1] = 0;
     for (auto& sl : c->ring) sl.used = false;
-    HIPCHK(hipMemsetAsync(c->misc.p + 12, 0, sizeof(uint32_t), c->s));
+    if (c->alpha_dirty) {  // (only a pack kernel sets the sticky status word)
+        HIPCHK(hipMemsetAsync(c->misc.p + 12, 0, sizeof(uint32_t), c->s));
+        c->alpha_dirty = false;
+    }
     c->n_entries = c->n_ids = c->n_distinct = 0;
     c->part = 0;  // back to one full pass
     c->part_n = 1;
@@ -526,6 +530,7 @@ static int submit_common(kb_ctx* c, const char* bases, const uint32_t* lens, uin
     HIPCHK(c->pool.alloc(n_reads, &b.own_lens));
     b.words = b.own_words;
     b.lens = b.own_lens;
+    c->alpha_dirty = true;
     HIPCHK(launch_pack(sl.d.p, reinterpret_cast<const uint64_t*>(sl.d.p + o_off),
                        n_reads, RW, b.own_words, b.own_lens, c->misc.p + 12, c->s));
     if (ids) {
