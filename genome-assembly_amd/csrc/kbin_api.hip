@@ -1626,6 +1626,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             a.lq_cap = ecap;
         }
         a.fs_lds = (uint32_t)(env_int("KB_BIN_FSL", 1) != 0);
+        a.fsl_run = (uint32_t)std::max(1, env_int("KB_BIN_FSL_RUN", 64));
         // singleton pre-filter for the heavy bins: where most distinct keys are
         // pruned singletons (high error rates, low coverage: C5), learned from
         // the last finalize; exact because a key seen once has count 1 <= cutoff

@@ -1332,7 +1332,7 @@ DEV void bin_body(const BinArgs& A) {
             // LDS-staged list writes where a build chunk gives each partition
             // short runs (under 64 entries); longer runs coalesce by themselves
             const bool fsl = flat && A.fs_lds && np <= FSL_NP &&
-                             (uint64_t)FB_CHUNK * occ_tot < 64ull * np * (uint64_t)(hi - lo);
+                             (uint64_t)FB_CHUNK * occ_tot < (uint64_t)A.fsl_run * np * (uint64_t)(hi - lo);
             if (tid == 0) S.e0 = atomicAdd(A.flat_octr, (unsigned long long)(np + 1));  // this bin's pool range
             __syncthreads();
             for (uint32_t i = tid; i <= np; i += BIN_THREADS) {

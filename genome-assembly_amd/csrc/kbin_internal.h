@@ -213,6 +213,7 @@ struct BinArgs {
     float rho;                 // expected distinct keys per occurrence
     float fill;                // target table load when choosing the partition depth
     uint32_t ringfree;         // unpartitioned bins expand without the per-wave ring (KB_BIN_RINGFREE)
+    uint32_t fsl_run;          // LDS-staged flat lists below this many entries per partition per chunk
     uint32_t win_heavy;        // LDS id windows in the heavy bins' partitions too (KB_BIN_WIN_HEAVY)
     uint64_t heavy_hint;       // heavy / split bins the last finalize published (0: small grids for their kernels)
     int ablate;                // diagnostic builds (KB_BIN_PROF / KB_BIN_ABL) only: 1 expansion only,
