@@ -1279,6 +1279,7 @@ DEV void bin_body(const BinArgs& A) {
         }
         uint64_t* stage = A.stage + S.stage_base;  // (flat: moved to each partition's list)
         PROF_CNT(11, PHASE == 0);
+        PROF_CNT(0, PHASE == 0 ? (hi - lo) : 0u);  // records once per bin
         PROF_CNT(14, occ_tot);
 #ifdef KB_BIN_PROF
         const unsigned long long bin_t0 = clock64();
@@ -1395,6 +1396,7 @@ DEV void bin_body(const BinArgs& A) {
             const uint32_t P = S.cur_p, Lv = S.cur_l;
             if (Lv == 0xFFFFFFFFu) break;  // uniform
             PROF_CNT(8, 1);
+            PROF_CNT(15, (PHASE == 0 || !flat) ? (hi - lo) : 0u);  // records expanded (all partitions)
             // ---- sweep 1: insert + count (binning.c:1042-1069 semantics per key)
             // each occurrence is staged as (slot, ordinal) for sweep 2
             // stage entry: (LDS slot + 1) << 48 | position in the read << 32 | call
@@ -2101,9 +2103,9 @@ void bins_prof_report(hipStream_t s) {
     unsigned long long h[16];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bin_prof), sizeof(h));
-    static const char* nm[16] = {"occ", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
+    static const char* nm[16] = {"bin records", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
                                  "partitions", "overflows", "big lists", "bins", "slowest-bin-occ", "slowest-bin-cycles",
-                                 "occ", "-"};
+                                 "occ", "records expanded"};
     fprintf(stderr, "[bin_prof]");
     for (int i = 0; i < 16; i++)
         if (h[i]) fprintf(stderr, " %s=%llu", nm[i], h[i]);
