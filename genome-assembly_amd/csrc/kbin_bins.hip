@@ -193,7 +193,7 @@ DEV uint32_t wave_dest_add(uint32_t* cnt2, uint32_t d) {
 __device__ __host__ inline int sk_row_words(int RW, int rw) { return RW + (rw > 3 ? rw - 1 : 2); }
 
 // Thread-per-read variant for short reads (RW <= SK_THREAD_RW): a block
-// stages 256 reads in LDS rows and each lane walks its own read's sticky
+// stages SKT reads in LDS rows and each lane walks its own read's sticky
 // chain serially.  The wave-per-read kernel above keeps 64 lanes busy on a
 // window of only K-M+1 positions; one lane per read does the same argmax
 // with no cross-lane reduction and no idle lanes.  The window of mmer scores
@@ -204,11 +204,12 @@ constexpr int SK_THREAD_RW = 16;
 // staged records per block (8 B each): 256 reads of 150 bp make ~2.5 K; a
 // block past it stores the rest directly.  With the per-destination arrays
 // (16-bit counts, two per word) and the read rows the block fits four to a CU.
-constexpr uint32_t SK_STAGE = 2496;
+constexpr int SKT = 512;              // reads (lanes) per block
+constexpr uint32_t SK_STAGE = 4992;   // (two blocks per CU)
 constexpr uint32_t SK_MAX_DEST = 1024;  // destination regions (ranks or buckets)
 
 template <bool WRITE>
-__global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
+__global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const int RW = A.RW, K = A.K, M = A.M;
     const int W = K - M + 1;  // <= 57 (K <= 63): mmer starts lo..lo+W-1 end inside one 64-base window pair
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     const uint32_t halfM = 1u << (2 * M - 1);
     const bool one_word = K <= 31 && M <= 12;  // (scores < 2^24 keep 8 bits for the offset)
     const uint32_t tid = threadIdx.x;
-    uint64_t* stg = smem + 256 * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
+    uint64_t* stg = smem + SKT * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
     __shared__ uint32_t span_end;
     __shared__ unsigned long long s_base;
     __shared__ uint32_t dcnt2[SK_MAX_DEST / 2];  // per-destination counts, 16 bits each (< SK_STAGE)
@@ -227,10 +228,10 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
     const bool alloc = WRITE && (A.rec_ctr || route);  // records placed by block allocation
     const bool rounds = alloc && !(route && A.G > 64);  // see the walk below
     uint64_t kmers = 0;
-    for (uint64_t r0 = (uint64_t)blockIdx.x * 256; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * 256) {
-        const uint32_t nrows = (uint32_t)min<uint64_t>(256, A.n_reads - r0);
+    for (uint64_t r0 = (uint64_t)blockIdx.x * SKT; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * SKT) {
+        const uint32_t nrows = (uint32_t)min<uint64_t>(SKT, A.n_reads - r0);
         __syncthreads();
-        for (uint32_t i = tid; i < nrows * (uint32_t)RW; i += 256) {
+        for (uint32_t i = tid; i < nrows * (uint32_t)RW; i += SKT) {
             const uint32_t row = i / (uint32_t)RW, col = i - row * (uint32_t)RW;
             smem[row * RS + col] = A.words[r0 * RW + i];
         }
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                 if (WRITE) {
                     const uint64_t rev = bsm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
                     const uint64_t e = (uint64_t)lo | (n << 16) | ((uint64_t)(sig - lo) << 22) | (rev << 28) |
-                                       ((uint64_t)tid << 29) | ((uint64_t)(uint32_t)best << 37);
+                                       ((uint64_t)tid << 29) | ((uint64_t)(uint32_t)best << 38);
                     const uint64_t loc = alloc ? (uint64_t)atomicAdd(&span_end, 1u) : rbase + nseg - bfirst;
                     if (loc < SK_STAGE) {
                         stg[loc] = e;
@@ -329,36 +330,36 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
             const uint32_t span = min(span_end, SK_STAGE);
             if (route) {
                 // per destination: count, reserve a range, place (LDS cursors)
-                for (uint32_t d = tid; d < (A.G + 1) / 2; d += 256) dcnt2[d] = 0;
+                for (uint32_t d = tid; d < (A.G + 1) / 2; d += SKT) dcnt2[d] = 0;
                 __syncthreads();
                 const bool agg = A.G <= 64;  // ranks, not local buckets: aggregate per wave
-                for (uint32_t i = tid; i < span; i += 256) {
+                for (uint32_t i = tid; i < span; i += SKT) {
                     const uint64_t e = stg[i];
-                    const uint32_t d = region_of(A, (uint32_t)(e >> 37), ((r0 + ((e >> 29) & 0xFFu)) << 16) | (e & 0xFFFFu));
+                    const uint32_t d = region_of(A, (uint32_t)(e >> 38), ((r0 + ((e >> 29) & 0x1FFu)) << 16) | (e & 0xFFFFu));
                     if (agg)
                         wave_dest_add(dcnt2, d);
                     else
                         atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1)));
                 }
                 __syncthreads();
-                for (uint32_t d = tid; d < A.G; d += 256) {
+                for (uint32_t d = tid; d < A.G; d += SKT) {
                     const uint32_t nd = (dcnt2[d >> 1] >> (16 * (d & 1))) & 0xFFFFu;
                     dbase[d] = nd ? (uint32_t)min<unsigned long long>(
                                         atomicAdd(&A.dest_ctr[d], (unsigned long long)nd), 0xFFFFFFFFull)
                                   : 0u;
                 }
                 __syncthreads();
-                for (uint32_t d = tid; d < (A.G + 1) / 2; d += 256) dcnt2[d] = 0;
+                for (uint32_t d = tid; d < (A.G + 1) / 2; d += SKT) dcnt2[d] = 0;
                 __syncthreads();
-                for (uint32_t i = tid; i < span; i += 256) {
+                for (uint32_t i = tid; i < span; i += SKT) {
                     const uint64_t e = stg[i];
-                    const uint32_t d = region_of(A, (uint32_t)(e >> 37), ((r0 + ((e >> 29) & 0xFFu)) << 16) | (e & 0xFFFFu));
+                    const uint32_t d = region_of(A, (uint32_t)(e >> 38), ((r0 + ((e >> 29) & 0x1FFu)) << 16) | (e & 0xFFFFu));
                     const uint64_t slot =
                         (uint64_t)dbase[d] +
                         (agg ? wave_dest_add(dcnt2, d)
                              : ((atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1))) >> (16 * (d & 1))) & 0xFFFFu));
                     if (slot >= region_room(A.region_base, A.region_cap, d)) continue;  // counted: the caller retries bigger
-                    const uint32_t row = (uint32_t)((e >> 29) & 0xFFu);
+                    const uint32_t row = (uint32_t)((e >> 29) & 0x1FFu);
                     put_record(A, A.regions + (region_off(A.region_base, A.region_cap, d) + slot) * (uint64_t)A.rw,
                                A.ord_base + (uint32_t)(r0 + row), e & 0xFFFFu, (e >> 16) & 63u, (e >> 22) & 63u,
                                (e >> 28) & 1u, smem + row * RS);
@@ -369,9 +370,9 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                     __syncthreads();
                 }
                 const uint64_t tbase = alloc ? (uint64_t)s_base : bfirst;
-                for (uint32_t i = tid; i < span; i += 256) {
+                for (uint32_t i = tid; i < span; i += SKT) {
                     const uint64_t e = stg[i];
-                    const uint32_t elo = (uint32_t)(e & 0xFFFFu), row = (uint32_t)((e >> 29) & 0xFFu);
+                    const uint32_t elo = (uint32_t)(e & 0xFFFFu), row = (uint32_t)((e >> 29) & 0x1FFu);
                     const uint64_t en = (e >> 16) & 63u, so = (e >> 22) & 63u, rev = (e >> 28) & 1u;
                     const uint64_t* rw_ = smem + row * RS;
                     const uint64_t t = tbase + i;
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
                                        (rev << 44) | ((uint64_t)elo << 45);
                     A.pay[3 * t + 1] = window64(rw_, (int)elo);
                     A.pay[3 * t + 2] = window64(rw_, (int)elo + 32);
-                    A.keys[t] = ((e >> 37) << 38) | ((63ull - en) << 32) | (uint32_t)t;
+                    A.keys[t] = ((e >> 38) << 38) | ((63ull - en) << 32) | (uint32_t)t;
                 }
             }
             // another round while a walk stopped at the full stage
@@ -389,15 +390,21 @@ __global__ __launch_bounds__(256) void sk_thread_kernel(SkScanArgs A) {
         }
     }
     if (!WRITE || (alloc && (!route || A.binned_fmt))) {  // per-block k-mer sums (sk_kmers_total_kernel)
-        __shared__ uint64_t shs[4];
-        const uint64_t tot = block_sum256(kmers, shs);
-        if (tid == 0) A.n_kmers[blockIdx.x] = tot;
+        __shared__ unsigned long long shs;
+        if (tid == 0) shs = 0;
+        __syncthreads();
+        uint64_t w = kmers;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) w += (uint64_t)__shfl_xor((long long)w, off, 64);
+        if ((tid & 63u) == 0 && w) atomicAdd(&shs, (unsigned long long)w);
+        __syncthreads();
+        if (tid == 0) A.n_kmers[blockIdx.x] = shs;
     }
 }
 
 uint64_t sk_blocks(uint64_t n_reads, int RW) {
     if (!n_reads) return 0;
-    if (RW <= SK_THREAD_RW) return std::min<uint64_t>((n_reads + 255) / 256, 8192);
+    if (RW <= SK_THREAD_RW) return std::min<uint64_t>((n_reads + SKT - 1) / SKT, 8192);
     return std::min<uint64_t>((n_reads + 3) / 4, 4096);
 }
 
@@ -420,12 +427,12 @@ hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s) {
     if (!a.n_reads) return hipSuccess;
     const uint64_t blocks = sk_blocks(a.n_reads, a.RW);
     if (a.RW <= SK_THREAD_RW) {
-        const size_t lds = (size_t)256 * sk_row_words(a.RW, a.rw) * sizeof(uint64_t) +
+        const size_t lds = (size_t)SKT * sk_row_words(a.RW, a.rw) * sizeof(uint64_t) +
                            (write ? SK_STAGE * sizeof(uint64_t) : 0);
         if (write)
-            hipLaunchKernelGGL(sk_thread_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+            hipLaunchKernelGGL(sk_thread_kernel<true>, dim3((unsigned)blocks), dim3(SKT), lds, s, a);
         else
-            hipLaunchKernelGGL(sk_thread_kernel<false>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+            hipLaunchKernelGGL(sk_thread_kernel<false>, dim3((unsigned)blocks), dim3(SKT), lds, s, a);
         return hipGetLastError();
     }
     const size_t lds = (size_t)4 * (a.RW + 2) * sizeof(uint64_t);
