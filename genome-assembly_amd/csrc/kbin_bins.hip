@@ -206,6 +206,7 @@ constexpr int SK_THREAD_RW = 16;
 // (16-bit counts, two per word) and the read rows the block fits four to a CU.
 constexpr int SKT = 512;              // reads (lanes) per block
 constexpr uint32_t SK_STAGE = 4992;   // (two blocks per CU)
+static_assert(SKT <= 512, "a staged record keeps its row in 9 bits");
 constexpr uint32_t SK_MAX_DEST = 1024;  // destination regions (ranks or buckets)
 
 template <bool WRITE>
