@@ -267,7 +267,10 @@ static void materialise(struct ZHashTable *level1, const kb_csr *r, int prune)
     char ms[17];
     const uint64_t n = r->n_entries;
     const size_t nm = (size_t)1 << (2 * g_M);
+    double t = now_ms();
     uint64_t *order = first_order(r);
+    g_times.order_ms = now_ms() - t;
+    t = now_ms();
     /* stable grouping by mmer, groups in first-sight order */
     uint32_t *gid = malloc(nm * sizeof(uint32_t));
     struct ZHashTable **l2 = calloc(nm, sizeof(struct ZHashTable *));
@@ -298,7 +301,10 @@ static void materialise(struct ZHashTable *level1, const kb_csr *r, int prune)
     for (uint64_t g = 0; g < ng; g++) gcnt[g] = gstart[g];
     for (uint64_t o = 0; o < n; o++) grouped[gcnt[gid[r->mmer[order[o]]]]++] = order[o];
     fill_job j = {r, grouped, gstart, gmmer, l2, ng, 0, 0, prune};
+    g_times.group_ms = now_ms() - t;
+    t = now_ms();
     run_workers(fill_tables, &j, n_threads());
+    g_times.fill_ms = now_ms() - t;
     g_times.nodes += j.nodes;
     free(grouped);
     free(gstart);

@@ -54,6 +54,9 @@ typedef struct {
     uint64_t entries;       /* keys materialised (all, before the prune) */
     uint64_t ids;           /* ids exported */
     uint64_t nodes;         /* ll_nodes allocated (kept keys only when pruning) */
+    double order_ms;        /* materialise: first-occurrence order (radix sort) */
+    double group_ms;        /* materialise: level 1 + grouping by mmer (one thread) */
+    double fill_ms;         /* materialise: level-2 tables and lists (worker threads) */
 } kbh_times;
 int kbh_last_times(kbh_times *out);
 
