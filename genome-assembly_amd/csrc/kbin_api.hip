@@ -233,6 +233,8 @@ struct kb_ctx {
     uint64_t bucket_cap = 0;   // learned region capacity (records per bucket)
     uint64_t bucket_cap_used = 0;  // the capacity (region stride) the regions were written with
     DevBuf<uint64_t> kpart;    // per-block k-mer sums of the count pass
+    int ocut_km = -1;          // (K << 8 | M) the offset cut table was made for
+    uint8_t ocut[5][17] = {};  // offset partitions' ranges (offset_cuts)
     float rho = 0.f;           // learned distinct / occurrences
     float rho_tab = 0.f;       // learned table keys / occurrences under the singleton pre-filter
     DevBuf<uint32_t> hll;      // cold pass: HyperLogLog registers (launch_hll)
@@ -1372,6 +1374,64 @@ static int binned_sk_records(kb_ctx* c, uint64_t& R, uint64_t& N) {
     return KB_OK;
 }
 
+// Offset partitions.  A light bin that needs 2^l tables is split by the
+// minimizer's offset o inside the k-mer: o is the first occurrence of the
+// (canonical) mmer string in the (complemented) k-mer, a function of the key
+// (bin_body), so every key lands in exactly one range.  The ranges are chosen
+// to hold equal shares of the occurrences, whose distribution over o is
+// measured here once per (K, M) on seeded uniform random reads of the sticky
+// signature walk (binning.c:922-989): roughly triangular, offset 0 most
+// frequent (distinct keys per offset follow occurrences per offset).
+static void offset_cuts(int K, int M, uint8_t (&cut)[5][17]) {
+    const int W = K - M + 1, L = std::max(150, 4 * K);
+    std::vector<double> h(W, 0.0);
+    std::vector<uint8_t> r(L);
+    std::vector<uint32_t> cs(L);
+    const uint32_t full = (1u << (2 * M)) - 1u;
+    uint64_t x = 0x243F6A8885A308D3ull;
+    for (int read = 0; read < 2000; read++) {
+        for (int i = 0; i < L; i++) {
+            x += 0x9E3779B97F4A7C15ull;
+            uint64_t z = x;
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            r[i] = (uint8_t)((z ^ (z >> 31)) & 3u);
+        }
+        for (int p = 0; p + M <= L; p++) {
+            uint32_t s = 0;
+            for (int j = 0; j < M; j++) s = s * 4u + r[p + j];
+            cs[p] = std::max(s, full - s);
+        }
+        int sig = -1;
+        for (int i = 0; i + K <= L; i++) {
+            if (i > sig) {  // leftmost strict argmax (binning.c:972)
+                uint32_t best = 0;
+                for (int p = i; p <= i + K - M; p++)
+                    if (sig < i || cs[p] > best) {
+                        best = cs[p];
+                        sig = p;
+                    }
+            }
+            h[sig - i] += 1.0;
+        }
+    }
+    double tot = 0;
+    for (double v : h) tot += v;
+    for (int l = 0; l <= 4; l++) {
+        const int R = 1 << l;
+        cut[l][0] = 0;
+        double acc = 0;
+        int o = 0;
+        for (int rr = 1; rr < R; rr++) {
+            while (o < W && acc + h[o] * 0.5 < tot * rr / R) acc += h[o++];
+            // non-empty ranges where W allows
+            int c = std::max(o, (int)cut[l][rr - 1] + 1);
+            cut[l][rr] = (uint8_t)std::min(c, 63);
+        }
+        for (int rr = R; rr <= 16; rr++) cut[l][rr] = 64;
+    }
+}
+
 static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool received) {
     const int M = c->p.M;
     c->tm.engine = KB_ENG_BINNED;
@@ -1587,6 +1647,14 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.fill = (float)std::min(0.85, std::max(0.3, env_int("KB_BIN_FILL_PCT", 60) / 100.0));
         a.ablate = env_int("KB_BIN_ABLATE", 0);
         a.ringfree = (uint32_t)(env_int("KB_BIN_RINGFREE", 1) != 0);
+        a.opart = (uint32_t)std::min(4, std::max(0, env_int("KB_BIN_OPART", 4)));
+        if (a.opart) {
+            if (c->ocut_km != (c->p.K << 8 | M)) {
+                offset_cuts(c->p.K, M, c->ocut);
+                c->ocut_km = c->p.K << 8 | M;
+            }
+            memcpy(a.ocut, c->ocut, sizeof(a.ocut));
+        }
         a.heavy_hint = attempt ? ~0ull : c->hint_heavy;
         // LDS id windows in heavy-bin partitions where the last finalize's lists
         // were short on average (C4 share: 588 -> 502 ms per step; C3's lists of

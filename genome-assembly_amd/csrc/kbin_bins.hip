@@ -696,6 +696,12 @@ struct Span<1> {
         w = (w << 2) | (x >> 62);
         x <<= 2;
     }
+    DEV void advance(uint32_t s) {  // s steps at once (s < 32: W = K - M + 1 <= 31)
+        if (s) {
+            w = (w << (2u * s)) | (x >> (64u - 2u * s));
+            x <<= 2u * s;
+        }
+    }
 };
 template <>
 struct Span<2> {
@@ -719,6 +725,9 @@ struct Span<2> {
         s1 = (s1 << 2) | (s2 >> 62);
         s2 = (s2 << 2) | (s3 >> 62);
         s3 <<= 2;
+    }
+    DEV void advance(uint32_t s) {
+        for (uint32_t i = 0; i < s; i++) step();
     }
 };
 
@@ -820,13 +829,17 @@ struct BinTable {
 // block-unique index from *ctr (0 .. k-mers of the partition - 1).  The
 // partition filter is one multiply (KW = 1); the table hash is computed by f
 // on compacted k-mers.
+//   Offset range [olo, ohi) (offset partitions; [0, 64) = every offset): only
+// the k-mers j whose minimizer sits at offset so - j inside the k-mer, a
+// contiguous run [ja, jb) of each record.
 template <int KW, typename F>
-DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, uint32_t l, uint64_t* qa,
-                       uint64_t* qb, uint32_t* qo, uint16_t* qp, uint32_t* ctr, F&& f) {
+DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, uint32_t l, uint32_t olo,
+                       uint32_t ohi, uint64_t* qa, uint64_t* qb, uint32_t* qo, uint16_t* qp, uint32_t* ctr, F&& f) {
     constexpr uint32_t Q = bin_q<KW>(), FL = Q / 2;
     const int K = A.K;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t pmask = (1u << l) - 1u;
+    const bool ranged = ohi - olo < 64u;
     const bool track = A.e_first != nullptr;  // k-mer positions only for KB_TRACK_FIRST
     const bool ringfree = A.ringfree != 0;
     uint32_t head = 0, fill = 0;  // wave-uniform ring state
@@ -905,29 +918,41 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
             continue;
         }
 #endif
+        // offset range: this lane's k-mers [ja, ja + nl)
+        const int so = (int)((hd >> 38) & 63u);
+        int ja = 0, nl = n;
+        if (ranged) {
+            ja = max(0, so - (int)ohi + 1);
+            nl = max(0, min(n, so - (int)olo + 1) - ja);
+        }
         if (KW == 1 && l == 0 && ringfree) {
-            // an unpartitioned bin: every k-mer is taken, so the lanes hand
-            // their own records' k-mers j, j + 1 straight to f (records are
-            // sorted longest first: the valid lanes of a step are a prefix,
-            // so the stage stores stay contiguous) -- no ring writes and
-            // reads; the chunk's stage range is reserved once
-            const uint32_t tot = (uint32_t)rfl((int)wave_sum_u32((uint32_t)n));
+            // an unpartitioned bin (or an offset range of one): every k-mer
+            // of the lane's run is taken, so the lanes hand their own
+            // records' k-mers j, j + 1 straight to f (the ballots keep the
+            // stage stores contiguous) -- no ring writes and reads; the
+            // chunk's stage range is reserved once
+            const uint32_t tot = (uint32_t)rfl((int)wave_sum_u32((uint32_t)nl));
             uint32_t cb = 0;
             if (lane == 0 && tot) cb = atomicAdd(ctr, tot);
             cb = (uint32_t)rfl((int)cb);
-            for (int j = 0; j < nmax; j += 2) {
+            int jmax = nmax;
+            if (ranged) {
+                sp.advance((uint32_t)ja);
+                jmax = (int)rfl((int)wave_max_u32((uint32_t)nl));
+            }
+            for (int j = 0; j < jmax; j += 2) {
                 const TKey<KW> k0 = sp.key(K, fl);
                 sp.step();
                 const TKey<KW> k1 = sp.key(K, fl);
                 sp.step();
-                const bool v0 = j < n, v1 = j + 1 < n;
+                const bool v0 = j < nl, v1 = j + 1 < nl;
                 const uint64_t m0 = __ballot(v0), m1 = __ballot(v1);
                 const uint32_t s0 = cb + lanes_below(m0);
                 cb += (uint32_t)__popcll(m0);
                 const uint32_t s1 = cb + lanes_below(m1);
                 cb += (uint32_t)__popcll(m1);
-                f(k0, ord, (uint16_t)(rlo + (uint32_t)j), s0, v0, k1, ord, (uint16_t)(rlo + (uint32_t)j + 1u), s1,
-                  v1);
+                const uint32_t pj = rlo + (uint32_t)(ja + j);
+                f(k0, ord, (uint16_t)pj, s0, v0, k1, ord, (uint16_t)(pj + 1u), s1, v1);
             }
             continue;
         }
@@ -942,7 +967,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
             for (int u = 0; u < U; u++) {
                 key[u] = sp.key(K, fl);
                 sp.step();
-                take[u] = j + u < n && (l == 0 || (key[u].part() & pmask) == p);
+                take[u] = (uint32_t)(j + u - ja) < (uint32_t)nl && (l == 0 || (key[u].part() & pmask) == p);
                 m[u] = __ballot(take[u]);
             }
             uint32_t f0 = fill;
@@ -1366,11 +1391,27 @@ DEV void bin_body(const BinArgs& A) {
         }
         PROF_MARK(7);
         const uint32_t p_lo = PHASE == 0 ? 0u : S.part0, p_hi = PHASE == 0 ? (1u << l0) : S.part0 + 1u;
+        // Offset partitions (phase 0 light bins of depth 1..opart): partition
+        // p0 takes the k-mers whose minimizer sits at an offset in
+        // [ocut[l0][p0], ocut[l0][p0 + 1]) of the k-mer, a contiguous run of
+        // each record, so the bin's records are expanded about once in all
+        // rather than once per partition.  Exact: the offset is a function of
+        // the key.  The signature at s is the leftmost strict argmax over the
+        // window [i0, i0 + K - M] of the recompute that chose it
+        // (binning.c:922-989), and every k-mer i it serves has i0 <= i <= s;
+        // an earlier copy of the same canonical mmer string inside the
+        // complemented-or-not k-mer, at q in [i, s), would be the same read
+        // substring with the same canonical score inside that window, and the
+        // leftmost argmax would have taken q.  So s - i is the first
+        // occurrence of the key's mmer in the key's k-mer.  (A partition that
+        // still overflows splits by the key hash on top of its range.)
+        const bool omode = PHASE == 0 && !flat && !split && l0 >= 1 && l0 <= A.opart;
         for (uint32_t p0 = p_lo; p0 < p_hi; p0++) {
+        const uint32_t olo = omode ? A.ocut[l0][p0] : 0u, ohi = omode ? A.ocut[l0][p0 + 1] : 64u;
         if (tid == 0) {
             S.sp = 1;
-            S.stack_p[0] = p0;
-            S.stack_l[0] = l0;
+            S.stack_p[0] = omode ? 0u : p0;
+            S.stack_l[0] = omode ? 0u : l0;
         }
         __syncthreads();
         // flat: this partition's list is [fa, fb) of the bin's stage range
@@ -1498,7 +1539,7 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_ABL
                 if (A.ablate != 5)  // 5: no sweep 1 at all (the per-bin overheads alone)
 #endif
-                for_each_kmer<KW>(A, lo, hi, P, Lv, qa, qb, qo, qp, &S.n_stage, insert2);
+                for_each_kmer<KW>(A, lo, hi, P, Lv, olo, ohi, qa, qb, qo, qp, &S.n_stage, insert2);
             } else if constexpr (PHASE == 1) {
                 // the partition's flat list, two entries per lane; a deeper split
                 // (Lv > l0) filters it, entries keep their index (sweep 2 filters too)

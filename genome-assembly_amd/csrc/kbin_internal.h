@@ -213,6 +213,12 @@ struct BinArgs {
     float rho;                 // expected distinct keys per occurrence
     float fill;                // target table load when choosing the partition depth
     uint32_t ringfree;         // unpartitioned bins expand without the per-wave ring (KB_BIN_RINGFREE)
+    // offset partitions: a light bin of initial depth 1 <= l <= opart is split by
+    // the minimizer's offset inside the k-mer (a function of the key, see
+    // bin_body) instead of by a key hash, so each partition expands only its own
+    // k-mers of every record; range r of depth l is [ocut[l][r], ocut[l][r + 1])
+    uint32_t opart;            // deepest offset-partitioned depth (0: hash partitions only; KB_BIN_OPART)
+    uint8_t ocut[5][17];
     uint32_t fsl_run;          // LDS-staged flat lists below this many entries per partition per chunk
     uint32_t win_heavy;        // LDS id windows in the heavy bins' partitions too (KB_BIN_WIN_HEAVY)
     uint64_t heavy_hint;       // heavy / split bins the last finalize published (0: small grids for their kernels)
