@@ -1488,7 +1488,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev));
     const bool few_bins = c->nbins_hint && c->nbins_hint < 3u * (uint32_t)std::max(1, cus);
-    const uint32_t flat_l = (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", few_bins ? 4 : 3));
+    // offset partitions (bin_body) make a light bin of depth 3-4 cheaper than
+    // flat lists for one-word keys
+    const int opart = std::min(4, std::max(0, env_int("KB_BIN_OPART", 4)));
+    const uint32_t flat_l =
+        (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", few_bins ? 4 : (KW == 1 && opart >= 4) ? 5 : 3));
     if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(KW * N, 1)));
     if (bucketed) {
         BucketArgs ba{};
@@ -1647,7 +1651,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.fill = (float)std::min(0.85, std::max(0.3, env_int("KB_BIN_FILL_PCT", 60) / 100.0));
         a.ablate = env_int("KB_BIN_ABLATE", 0);
         a.ringfree = (uint32_t)(env_int("KB_BIN_RINGFREE", 1) != 0);
-        a.opart = (uint32_t)std::min(4, std::max(0, env_int("KB_BIN_OPART", 4)));
+        a.opart = (uint32_t)opart;
+        a.fill_light = (float)std::min(0.85, std::max(0.3, env_int("KB_BIN_FILL_LIGHT_PCT", 50) / 100.0));
         if (a.opart) {
             if (c->ocut_km != (c->p.K << 8 | M)) {
                 offset_cuts(c->p.K, M, c->ocut);

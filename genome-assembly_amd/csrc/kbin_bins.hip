@@ -1390,7 +1390,6 @@ DEV void bin_body(const BinArgs& A) {
             continue;  // (the next kernel launch sees every store)
         }
         PROF_MARK(7);
-        const uint32_t p_lo = PHASE == 0 ? 0u : S.part0, p_hi = PHASE == 0 ? (1u << l0) : S.part0 + 1u;
         // Offset partitions (phase 0 light bins of depth 1..opart): partition
         // p0 takes the k-mers whose minimizer sits at an offset in
         // [ocut[l0][p0], ocut[l0][p0 + 1]) of the k-mer, a contiguous run of
@@ -1405,7 +1404,17 @@ DEV void bin_body(const BinArgs& A) {
         // leftmost argmax would have taken q.  So s - i is the first
         // occurrence of the key's mmer in the key's k-mer.  (A partition that
         // still overflows splits by the key hash on top of its range.)
+        // Offset partitions cost no re-expansion, so light bins aim at a lower
+        // table load (fill_light: fewer second probe rounds) where that depth
+        // stays offset-partitioned
+        if (PHASE == 0 && !flat && !split && A.opart) {
+            const double want = (double)occ_tot * A.rho / ((double)A.fill_light * TS);
+            uint32_t l1 = 0;
+            while ((double)(1u << l1) < want && l1 < 16) l1++;
+            if (l1 <= A.opart && l1 > l0) l0 = l1;
+        }
         const bool omode = PHASE == 0 && !flat && !split && l0 >= 1 && l0 <= A.opart;
+        const uint32_t p_lo = PHASE == 0 ? 0u : S.part0, p_hi = PHASE == 0 ? (1u << l0) : S.part0 + 1u;
         for (uint32_t p0 = p_lo; p0 < p_hi; p0++) {
         const uint32_t olo = omode ? A.ocut[l0][p0] : 0u, ohi = omode ? A.ocut[l0][p0 + 1] : 64u;
         if (tid == 0) {
