@@ -1652,6 +1652,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.ablate = env_int("KB_BIN_ABLATE", 0);
         a.ringfree = (uint32_t)(env_int("KB_BIN_RINGFREE", 1) != 0);
         a.opart = (uint32_t)opart;
+        a.osplit = (uint32_t)(env_int("KB_BIN_OSPLIT", 0) != 0);
         a.fill_light = (float)std::min(0.85, std::max(0.3, env_int("KB_BIN_FILL_LIGHT_PCT", 50) / 100.0));
         if (a.opart) {
             if (c->ocut_km != (c->p.K << 8 | M)) {

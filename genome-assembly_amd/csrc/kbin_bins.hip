@@ -1057,6 +1057,7 @@ constexpr uint32_t SPLIT_BIT = 0x100u;     // flat_l0: a split bin's partitions 
 constexpr uint32_t PRUNED = 0x80000000u;  // cursor of a pruned (or empty) slot in sweep 2
 constexpr uint32_t PF_BIT = 0x200u;        // flat_l0: a heavy bin sized for the singleton pre-filter
 constexpr uint32_t FSL_BIT = 0x400u;       // flat_l0: its lists written by flat_scatter_lds_kernel
+constexpr uint32_t OSPLIT_BIT = 0x800u;    // flat_l0: a split bin partitioned by minimizer offset (bin_body)
 constexpr double PF_LOAD = 0.06;           // sketch load (distinct keys / cells) the partition depth aims at
 
 // the pre-filter's sketch cell of a key (independent of the table hash, whose
@@ -1328,15 +1329,33 @@ DEV void bin_body(const BinArgs& A) {
         // flat: a heavy bin (l0 >= flat_l), or a multi-table bin above a fair
         // share of one block's occurrences (few, large bins: N ranks, high
         // coverage) -- its build and its partitions then spread over the chip
-        const bool flat = PHASE == 1 ? !(S.l0 & SPLIT_BIT)
-                                     : (A.flat_l && (l0 >= A.flat_l || (A.big_occ && l0 >= 1 && occ_tot > A.big_occ)));
+        bool flat = PHASE == 1 ? !(S.l0 & SPLIT_BIT)
+                               : (A.flat_l && (l0 >= A.flat_l || (A.big_occ && l0 >= 1 && occ_tot > A.big_occ)));
+        // a big light bin (over a fair share of one block, or over the split
+        // threshold) whose depth at the light load stays offset-partitioned is
+        // split by offset range instead: phase 1 bins each range on any block,
+        // every range expanding only its own k-mers (no flat lists, no
+        // re-expansion)
+        bool osplit = PHASE == 1 && !flat && (S.l0 & OSPLIT_BIT);
+        if (PHASE == 0 && A.osplit && A.opart && A.flat_l && l0 < A.flat_l &&
+            ((A.big_occ && l0 >= 1 && occ_tot > A.big_occ) || (A.split_occ && occ_tot > A.split_occ))) {
+            const double want = (double)occ_tot * A.rho / ((double)A.fill_light * TS);
+            uint32_t l1 = 0;
+            while ((double)(1u << l1) < want && l1 < 16) l1++;
+            while (l1 < A.opart && A.big_occ && (occ_tot >> l1) > A.big_occ) l1++;
+            if (l1 <= A.opart) {
+                l0 = l1 < 1 ? 1u : l1;
+                flat = false;
+                osplit = true;
+            }
+        }
         // a large light bin (more occurrences than a fair share of one CU) is
         // split: its k-mers are counted per hash partition (flat_count_kernel,
         // no probes), each partition gets its own stage range, and phase 1
         // bins the partitions on any block, each re-expanding the records with
         // the partition filter -- the light path, in parallel
-        bool split = PHASE == 1 && !flat;
-        if (PHASE == 0 && !flat && A.split_occ && occ_tot > A.split_occ) {
+        bool split = (PHASE == 1 && !flat) || osplit;
+        if (PHASE == 0 && !flat && !osplit && A.split_occ && occ_tot > A.split_occ) {
             const uint32_t lmax = A.flat_l ? A.flat_l - 1u : 3u;
             while (l0 < lmax && (occ_tot >> l0) > A.split_occ) l0++;
             split = l0 >= 1;
@@ -1382,7 +1401,8 @@ DEV void bin_body(const BinArgs& A) {
                 if (fsl) atomicAdd(&A.flat_n[6], 1ull);  // (LDS-staged lists)
                 A.flat_obase[b] = S.e0;
                 A.flat_sbase[b] = S.stage_base;
-                A.flat_l0[b] = l0 | (split ? SPLIT_BIT : 0u) | (pfb ? PF_BIT : 0u) | (fsl ? FSL_BIT : 0u);
+                A.flat_l0[b] = l0 | (split ? SPLIT_BIT : 0u) | (pfb ? PF_BIT : 0u) | (fsl ? FSL_BIT : 0u) |
+                               (osplit ? OSPLIT_BIT : 0u);
                 A.flat_chunk[b] = (uint32_t)S.i0;
                 A.flat_list[atomicAdd(A.flat_n, 1ull)] = b;
             }
@@ -1413,7 +1433,7 @@ DEV void bin_body(const BinArgs& A) {
             while ((double)(1u << l1) < want && l1 < 16) l1++;
             if (l1 <= A.opart && l1 > l0) l0 = l1;
         }
-        const bool omode = PHASE == 0 && !flat && !split && l0 >= 1 && l0 <= A.opart;
+        const bool omode = (PHASE == 0 && !flat && !split && l0 >= 1 && l0 <= A.opart) || (PHASE == 1 && osplit);
         const uint32_t p_lo = PHASE == 0 ? 0u : S.part0, p_hi = PHASE == 0 ? (1u << l0) : S.part0 + 1u;
         for (uint32_t p0 = p_lo; p0 < p_hi; p0++) {
         const uint32_t olo = omode ? A.ocut[l0][p0] : 0u, ohi = omode ? A.ocut[l0][p0 + 1] : 64u;
@@ -1840,6 +1860,32 @@ __global__ __launch_bounds__(FB_THREADS) void flat_count_kernel(BinArgs A) {
         const uint32_t lo = A.bstart[b] + s_c * FB_CHUNK, hi = min(lo + FB_CHUNK, A.bstart[b] + A.bcount[b]);
         for (uint32_t i = threadIdx.x; i < np; i += FB_THREADS) hist[i] = 0;
         __syncthreads();
+        if (A.flat_l0[b] & OSPLIT_BIT) {
+            // offset ranges (np <= 16): each record adds the length of its
+            // run inside every range, from its header alone
+            uint32_t acc[16] = {};
+            for (uint32_t r = lo + threadIdx.x; r < hi; r += FB_THREADS) {
+                const uint64_t hd = A.hdr[r];
+                const int n = (int)((hd >> 32) & 63u), so = (int)((hd >> 38) & 63u);
+#pragma unroll
+                for (uint32_t q = 0; q < 16; q++) {
+                    if (q >= np) break;
+                    const int ja = max(0, so - (int)A.ocut[l0][q + 1] + 1), jb = min(n, so - (int)A.ocut[l0][q] + 1);
+                    acc[q] += (uint32_t)max(0, jb - ja);
+                }
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < 16; q++) {
+                if (q >= np) break;
+                const uint32_t c = wave_incl_scan(acc[q], (int)(threadIdx.x & 63));
+                if ((threadIdx.x & 63) == 63 && c) atomicAdd(&hist[q], c);
+            }
+            __syncthreads();
+            uint32_t* cnt = A.flat_off + A.flat_obase[b];
+            for (uint32_t i = threadIdx.x; i < np; i += FB_THREADS)
+                if (hist[i]) atomicAdd(&cnt[i], hist[i]);
+            continue;
+        }
         // up to 8 partitions: 8-bit counts packed in a lane's register (a lane
         // expands <= 4 records of <= 63 k-mers), added per wave -- 256 lanes
         // on 8 LDS words would serialise

@@ -219,6 +219,7 @@ struct BinArgs {
     // k-mers of every record; range r of depth l is [ocut[l][r], ocut[l][r + 1])
     uint32_t opart;            // deepest offset-partitioned depth (0: hash partitions only; KB_BIN_OPART)
     float fill_light;          // table load the depth of an offset-partitioned bin aims at
+    uint32_t osplit;           // big light bins split by offset range across blocks (KB_BIN_OSPLIT; experimental)
     uint8_t ocut[5][17];
     uint32_t fsl_run;          // LDS-staged flat lists below this many entries per partition per chunk
     uint32_t win_heavy;        // LDS id windows in the heavy bins' partitions too (KB_BIN_WIN_HEAVY)
