@@ -793,7 +793,9 @@ struct BinTable {
     // find-or-insert; -2 past the key limit, -1 table full
     DEV int insert(uint32_t bmask, const TKey<KW>& k, uint32_t h, uint32_t* n_keys, uint32_t limit) const {
         uint32_t bk = h & bmask;
-        for (uint32_t probe = 0; probe <= bmask;) {
+        // (at most 64 buckets: a table filled past its limit -- the sweep is
+        // redone split anyway -- would otherwise walk every bucket per new key)
+        for (uint32_t probe = 0; probe <= bmask && probe < 64u;) {
             int empty;
             const int r = in_bucket(bk, k, empty);
             if (r >= 0) return r;
@@ -1484,6 +1486,14 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_ABL
                 if (A.ablate == 1 || A.ablate >= 8) return;  // expansion only
 #endif
+                // a partition already past its key limit is redone split: the
+                // rest of its sweep does nothing (a badly overfull table made
+                // every new key probe the whole table)
+                if (__hip_atomic_load(&S.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
+                    __hip_atomic_load(&S.n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > limit) {
+                    if ((threadIdx.x & 63u) == 0) S.overflow = 1;
+                    return;
+                }
                 const uint32_t h0 = k0.hash(), h1 = k1.hash();
                 // home buckets of both k-mers in flight together
                 int e0_, e1_;
@@ -1649,6 +1659,7 @@ DEV void bin_body(const BinArgs& A) {
             PROF_MARK(2);
             if (S.overflow || S.n_keys > limit) {  // uniform: split this partition in two and redo both
                 PROF_CNT(9, 1);
+                PROF_CNT(10, omode ? 1000000u + (ohi - olo) * 1000u + Lv : 0u);  // (diagnostic: offset-range overflows)
                 if (tid == 0) {
                     if (Lv >= 20 || S.sp + 2 > BIN_STACK) {
                         atomicOr(A.status, ST_PROBE_LIMIT);
@@ -2208,7 +2219,7 @@ void bins_prof_report(hipStream_t s) {
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bin_prof), sizeof(h));
     static const char* nm[16] = {"bin records", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
-                                 "partitions", "overflows", "big lists", "bins", "slowest-bin-occ", "slowest-bin-cycles",
+                                 "partitions", "overflows", "omode-ovf(1e6*n+1e3*width+Lv)", "bins", "slowest-bin-occ", "slowest-bin-cycles",
                                  "occ", "records expanded"};
     fprintf(stderr, "[bin_prof]");
     for (int i = 0; i < 16; i++)
