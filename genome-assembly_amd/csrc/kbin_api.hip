@@ -1389,7 +1389,7 @@ static void offset_cuts(int K, int M, uint8_t (&cut)[5][17]) {
     std::vector<uint32_t> cs(L);
     const uint32_t full = (1u << (2 * M)) - 1u;
     uint64_t x = 0x243F6A8885A308D3ull;
-    for (int read = 0; read < 2000; read++) {
+    for (int read = 0; read < 400; read++) {  // (~50 K occurrences: once per context, in its first finalize)
         for (int i = 0; i < L; i++) {
             x += 0x9E3779B97F4A7C15ull;
             uint64_t z = x;
