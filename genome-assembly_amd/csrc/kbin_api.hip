@@ -1490,7 +1490,9 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     const bool few_bins = c->nbins_hint && c->nbins_hint < 3u * (uint32_t)std::max(1, cus);
     // offset partitions (bin_body) make a light bin of depth 3-4 cheaper than
     // flat lists for one-word keys
-    const int opart = std::min(4, std::max(0, env_int("KB_BIN_OPART", 4)));
+    // (one-word keys only: two-word bins expand through the ring, which
+    // would still walk every k-mer of the bin per range)
+    const int opart = KW == 1 ? std::min(4, std::max(0, env_int("KB_BIN_OPART", 4))) : 0;
     const uint32_t flat_l =
         (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", few_bins ? 4 : (KW == 1 && opart >= 4) ? 5 : 3));
     if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(KW * N, 1)));
