@@ -439,6 +439,46 @@ def test_split_bins(genome, flat_l, ts_log2, K, engine, monkeypatch):
             np.testing.assert_array_equal(res.first >> np.uint64(16), last.astype(np.uint64))
 
 
+@pytest.mark.parametrize("genome,ts_log2,fill,osplit,track", [(200000, 13, 50, 0, 0), (200000, 11, 50, 0, 1),
+                                                               (200000, 10, 85, 0, 0), (3000, 11, 50, 0, 0),
+                                                               (3000, 12, 85, 0, 1), (200000, 11, 50, 1, 0),
+                                                               (3000, 11, 50, 1, 1)])
+def test_offset_partitions(genome, ts_log2, fill, osplit, track, engine, monkeypatch):
+    """light bins partitioned by the signature's offset inside the k-mer
+    (bin_body): small tables push bins to depths 1-4, a
+    high light-bin load (85 %) and high coverage (3 kbp genome) overfill
+    ranges so they split by hash on top (the sweep stops inserting once past
+    the key limit), and KB_BIN_OSPLIT=1 bins big ranges on any block; with
+    and without first-occurrence tracking (the global sweep-2 path)"""
+    import torch
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    monkeypatch.setenv("KB_BIN_TS_LOG2", str(ts_log2))
+    monkeypatch.setenv("KB_BIN_FILL_LIGHT_PCT", str(fill))
+    monkeypatch.setenv("KB_BIN_OSPLIT", str(osplit))
+    if osplit:
+        monkeypatch.setenv("KB_BIN_SPLIT_DIV", "1000000")
+    n, L, K = 40000, 150, 31
+    wpr = (L + 31) // 32
+    words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, genome, 5000, 13)
+    torch.cuda.synchronize()
+    bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n, wpr, n * L)
+    ora = oracle.bin_reads(bases, hl, K, 7, 1, True)
+    flags = kbin.KB_TRACK_FIRST if track else 0
+    with kbin.Engine(K, 7, cutoff=1, max_read_len=L, flags=flags) as eng:
+        for _ in range(2):  # the second pass runs with the learned density
+            eng.reset()
+            eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
+            eng.finalize(True)
+            res = eng.export()
+            assert_same(res, ora)
+            if track:
+                last = res.ids[res.offset[1:].astype(np.int64) - 1]
+                np.testing.assert_array_equal(res.first >> np.uint64(16), last.astype(np.uint64))
+
+
 def test_alphabet_rejected():
     """bytes outside ACGT are rejected loudly (alphabet): kb_submit
     returns before the pack kernel has run, so the error surfaces at the next
