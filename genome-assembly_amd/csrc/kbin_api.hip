@@ -51,11 +51,13 @@ struct DevBuf {
     uint64_t cap = 0;
     hipError_t ensure(uint64_t n) {
         if (n <= cap && p) return hipSuccess;
-        // 1/8 headroom, so passes whose sizes wander by a few percent (the
-        // partitioned passes of one job) do not free and map tens of GB each
-        // time (fresh device memory is cleared at roughly 20-25 GB/s)
+        // A first allocation is exact (peak HBM per context stays at what the
+        // pass needs).  A regrowth takes 1/8 headroom, so passes whose sizes
+        // wander by a few percent (the partitioned passes of one job) regrow
+        // once rather than freeing and mapping tens of GB every pass (fresh
+        // device memory is cleared at roughly 20-25 GB/s)
         uint64_t want = std::max<uint64_t>(n, 1);
-        want += want / 8;
+        if (p) want += want / 8;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -76,24 +78,41 @@ struct DevBuf {
     }
 };
 
-// pinned host buffer (page-locked: full-rate DMA both ways), grown on demand
+// host buffer, grown on demand: page-locked (full-rate DMA both ways) up to
+// PIN_MAX_BYTES, else -- or when the pinned allocation fails -- pageable
+// malloc memory (hipMemcpyAsync into it then completes synchronously).  Pinning
+// only affects the copy rate, never the result.
+constexpr uint64_t PIN_MAX_BYTES = 8ull << 30;
 template <typename T>
 struct PinBuf {
     T* p = nullptr;
     uint64_t cap = 0;
+    bool pinned = false;
     hipError_t ensure(uint64_t n) {
         if (n <= cap && p) return hipSuccess;
         release();
         const uint64_t want = std::max<uint64_t>(n, 1) + std::max<uint64_t>(n, 1) / 8;
-        hipError_t e = hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault);
-        if (e == hipSuccess) cap = want;
-        else p = nullptr;
-        return e;
+        if (want * sizeof(T) <= PIN_MAX_BYTES &&
+            hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault) == hipSuccess) {
+            pinned = true;
+            cap = want;
+            return hipSuccess;
+        }
+        (void)hipGetLastError();  // (a failed pinned allocation is not sticky)
+        p = static_cast<T*>(malloc(want * sizeof(T)));
+        if (!p) return hipErrorOutOfMemory;
+        pinned = false;
+        cap = want;
+        return hipSuccess;
     }
     void release() {
-        if (p) (void)hipHostFree(p);
+        if (p) {
+            if (pinned) (void)hipHostFree(p);
+            else free(p);
+        }
         p = nullptr;
         cap = 0;
+        pinned = false;
     }
 };
 
@@ -225,6 +244,7 @@ struct kb_ctx {
     DevBuf<uint32_t> bcount, bmmer, bocc;  // bin descriptors (with starts); bocc: k-mers
     DevBuf<uint32_t> flat_list, flat_next, flat_l0, flat_off, flat_cur, flat_chunk, pool_bin, chunk_bin;  // heavy bins published for phase 1
     DevBuf<unsigned long long> flat_sbase, flat_obase, flat_n;  // flat_n[0] bins, [1] offset pool
+    DevBuf<unsigned long long> pstat;  // [KB_PSTAT] path counters of the bin kernels (BinArgs::pstat)
     DevBuf<uint64_t> regions;  // local bucket regions (pay layout)
     DevBuf<unsigned long long> bfill;  // records per bucket
     DevBuf<uint64_t> bbase;  // [NB + 1] bucket output bases (bucket_bases_kernel)
@@ -284,7 +304,7 @@ static int set_device(kb_ctx* c) {
     return KB_OK;
 }
 
-extern "C" int kb_abi_version(void) { return 1; }
+extern "C" int kb_abi_version(void) { return 2; }  // 2: kb_timing path counters
 
 extern "C" const char* kb_last_error(void) { return g_err.c_str(); }
 
@@ -321,7 +341,7 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     }
     e = hipHostMalloc((void**)&c->h_misc, 16 * sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
-    e = hipHostMalloc((void**)&c->h_totals, 16 * sizeof(uint64_t), hipHostMallocDefault);
+    e = hipHostMalloc((void**)&c->h_totals, 32 * sizeof(uint64_t), hipHostMallocDefault);  // [16..23] path counters
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
     e = hipHostMalloc((void**)&c->h_alpha, 2 * sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_ENOMEM, "hipHostMalloc"); }
@@ -735,6 +755,10 @@ extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
     if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
     int rc = set_device(c);
     if (rc) return rc;
+    // every host batch routed from here must be ACGT: records built from an
+    // invalid read would otherwise reach the peers, whose finalize succeeds
+    rc = ingest_check(c, true);
+    if (rc) return rc;
     if (binned_applies(c) && c->KW == 1) return route_plan_binned(c, n_dest, h_counts);
     c->route_binned = false;
     std::vector<uint64_t> tot(n_dest, 0);
@@ -812,6 +836,8 @@ static int scatter_regions(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions, uint
     if (region_cap && !d_regions) return fail(KB_EINVAL, "null regions");
     if (region_cap >= 0xFFFFFFFFull) return fail(KB_EINVAL, "region_cap must be below 2^32 records");
     int rc = set_device(c);
+    if (rc) return rc;
+    rc = ingest_check(c, true);  // (as kb_route_plan: nothing invalid leaves this context)
     if (rc) return rc;
     bool affine = false;
     int64_t id_c = 0;
@@ -1452,11 +1478,13 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     while (NB < (uint32_t)std::min(1024, std::max(64, env_int("KB_BIN_NB", 1024)))) NB <<= 1;
     // every counter of this finalize's first attempt zeroed in one launch
     HIPCHK(c->flat_n.ensure(8));
+    HIPCHK(c->pstat.ensure(KB_PSTAT));
     {
         ClearList cl{};
         cl.add(c->totals.p, 16 * sizeof(uint64_t));
         cl.add(c->misc.p, 6 * sizeof(uint32_t));  // (status words, the list kernels' queue lengths)
         cl.add(c->flat_n.p, 8 * sizeof(unsigned long long));
+        cl.add(c->pstat.p, KB_PSTAT * sizeof(unsigned long long));
         if (bucketed) {
             HIPCHK(c->bfill.ensure(NB));
             cl.add(c->bfill.p, NB * sizeof(unsigned long long));
@@ -1713,6 +1741,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             a.rho_tab = c->rho_tab > 0.f ? c->rho_tab : a.rho;
             a.tab_keys = reinterpret_cast<unsigned long long*>(c->totals.p + 11);
         }
+        if (attempt) HIPCHK(hipMemsetAsync(c->pstat.p, 0, KB_PSTAT * sizeof(unsigned long long), c->s));
+        a.pstat = c->pstat.p;
         HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr));
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
@@ -1745,6 +1775,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
 #endif
         REC(5);
         HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 14 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        HIPCHK(hipMemcpyAsync(c->h_totals + 16, c->pstat.p, KB_PSTAT * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         if (R && !bucketed)
             HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
@@ -1811,6 +1842,19 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(hipEventElapsedTime(&c->tm.emit_ms, c->ev[4], c->ev[5]));
         HIPCHK(hipEventElapsedTime(&c->tm.total_ms, c->ev[0], c->ev[5]));
         HIPCHK(hipEventElapsedTime(&c->tm.bin_kernel_ms, c->ev[6], c->ev[7]));
+    }
+    {
+        const uint64_t* ps = c->h_totals + 16;  // (BinArgs::pstat)
+        c->tm.heavy_bins = (uint32_t)ps[0];
+        c->tm.split_bins = (uint32_t)ps[1];
+        c->tm.partitions = ps[2];
+        c->tm.overflow_redos = (uint32_t)ps[3];
+        c->tm.max_depth = (uint32_t)ps[4];
+        c->tm.prefiltered = ps[5];
+        c->tm.offset_partitions = ps[6];
+        c->tm.flat_partitions = ps[7];
+        c->tm.long_lists = c->h_misc[4];
+        c->tm.clustered_lists = c->h_misc[5];
     }
     c->tm.table_slots = 1ull << ts_log2;
     c->tm.n_bins = (uint32_t)c->h_totals[2];

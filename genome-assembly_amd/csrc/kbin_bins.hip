@@ -1400,6 +1400,7 @@ DEV void bin_body(const BinArgs& A) {
             __syncthreads();
             for (uint32_t k = tid; k < nch; k += BIN_THREADS) A.chunk_bin[S.i0 + k] = b;
             if (tid == 0) {
+                if (A.pstat) atomicAdd(&A.pstat[flat ? 0 : 1], 1ull);
                 if (fsl) atomicAdd(&A.flat_n[6], 1ull);  // (LDS-staged lists)
                 A.flat_obase[b] = S.e0;
                 A.flat_sbase[b] = S.stage_base;
@@ -1661,6 +1662,7 @@ DEV void bin_body(const BinArgs& A) {
                 PROF_CNT(9, 1);
                 PROF_CNT(10, omode ? 1000000u + (ohi - olo) * 1000u + Lv : 0u);  // (diagnostic: offset-range overflows)
                 if (tid == 0) {
+                    if (A.pstat) atomicAdd(&A.pstat[3], 1ull);
                     if (Lv >= 20 || S.sp + 2 > BIN_STACK) {
                         atomicOr(A.status, ST_PROBE_LIMIT);
                     } else {
@@ -1690,6 +1692,13 @@ DEV void bin_body(const BinArgs& A) {
                 const uint32_t ne = (uint32_t)tot, ni = (uint32_t)(tot >> 32);
                 atomicAdd(&A.gcount[2], (unsigned long long)(S.n_keys + S.n_single));  // distinct before prune
                 if (A.tab_keys) atomicAdd(A.tab_keys, (unsigned long long)S.n_keys);
+                if (A.pstat) {
+                    atomicAdd(&A.pstat[2], 1ull);
+                    atomicMax(&A.pstat[4], (unsigned long long)(Lv + (omode ? l0 : 0u)));
+                    if (S.n_single) atomicAdd(&A.pstat[5], (unsigned long long)S.n_single);
+                    if (omode) atomicAdd(&A.pstat[6], 1ull);
+                    if (PHASE == 1 && flat) atomicAdd(&A.pstat[7], 1ull);
+                }
                 // entries and ids from ONE packed counter (entries << 32 | ids; both
                 // totals < 2^32): consecutive entries own consecutive id ranges,
                 // so offset[e + 1] ends entry e's list (the CSR contract)

@@ -255,7 +255,14 @@ struct BinArgs {
     uint32_t fs_lds;           // 1: heavy bins with 9..2048 partitions write their lists LDS-staged
     float rho_tab;             // expected table keys per occurrence under the pre-filter
     unsigned long long* tab_keys;  // (zeroed) keys that entered a table
+    // (zeroed) path counters for kb_timing, one atomic per bin or partition:
+    // [0] heavy bins published as flat lists [1] split bins published
+    // [2] partitions swept to their prune [3] partitions redone split (overflow)
+    // [4] deepest partition depth (max) [5] keys kept out by the pre-filter
+    // [6] offset-range partitions [7] partitions swept from flat lists
+    unsigned long long* pstat;
 };
+constexpr int KB_PSTAT = 8;
 
 struct ListArgs {
     const uint64_t* totals;    // totals[0] = entries

@@ -71,7 +71,12 @@ class kb_timing(C.Structure):
                 ("runs_ms", C.c_float), ("emit_ms", C.c_float), ("total_ms", C.c_float),
                 ("scan_insert_launches", C.c_uint32), ("sort_passes", C.c_uint32),
                 ("table_slots", C.c_uint64), ("engine", C.c_uint32), ("n_bins", C.c_uint32),
-                ("n_superkmers", C.c_uint64), ("bin_kernel_ms", C.c_float)]
+                ("n_superkmers", C.c_uint64), ("bin_kernel_ms", C.c_float),
+                # path counters (kbin.h): which bin-phase paths the finalize took
+                ("heavy_bins", C.c_uint32), ("split_bins", C.c_uint32), ("partitions", C.c_uint64),
+                ("offset_partitions", C.c_uint64), ("flat_partitions", C.c_uint64),
+                ("max_depth", C.c_uint32), ("overflow_redos", C.c_uint32), ("prefiltered", C.c_uint64),
+                ("long_lists", C.c_uint32), ("clustered_lists", C.c_uint32)]
 
 
 _lib = None

@@ -112,6 +112,19 @@ typedef struct {
     uint64_t n_superkmers;  /* binned: super-k-mer records                       */
     float bin_kernel_ms;    /* binned: bin_kernel alone (runs_ms also holds the
                                heavy-bin kernels and bins_final)                */
+    /* binned: which paths the last finalize took (filled with or without
+     * timing; tests assert on them) */
+    uint32_t heavy_bins;    /* bins turned into flat per-partition lists       */
+    uint32_t split_bins;    /* light bins split across workgroups              */
+    uint64_t partitions;    /* LDS-table partitions swept to their prune       */
+    uint64_t offset_partitions; /* of those, split by minimizer offset range   */
+    uint64_t flat_partitions;   /* of those, swept from a heavy bin's flat list */
+    uint32_t max_depth;     /* deepest split of one bin (log2 of its tables)   */
+    uint32_t overflow_redos;/* partitions redone split after overflowing       */
+    uint64_t prefiltered;   /* keys seen once, counted but kept out of the
+                               tables by the singleton pre-filter              */
+    uint32_t long_lists;    /* lists of 257..4096 ids (bucketed list sort)     */
+    uint32_t clustered_lists; /* of those, lists sorted by the full network    */
 } kb_timing;
 
 /* Create a context (kb_create replaces zcreate_hash_table for the level-1

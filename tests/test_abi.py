@@ -51,7 +51,29 @@ def test_host_exports_reference_surface():
 
 
 def test_abi_version():
-    assert kbin.load_library().kb_abi_version() == 1
+    assert kbin.load_library().kb_abi_version() == 2
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """the ctypes mirrors of kb_params / kb_csr / kb_timing have the C layout
+    of include/kbin.h (size and every field offset, compiled here with gcc)"""
+    structs = {"kb_params": kbin.kb_params, "kb_csr": kbin.kb_csr, "kb_timing": kbin.kb_timing}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "kbin.h"', "int main(void) {"]
+    for name, cls in structs.items():
+        lines.append(f'printf("{name} %zu\\n", sizeof({name}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{name}.{f} %zu\\n", offsetof({name}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(kbin.INCLUDE_DIR), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                  check=True).stdout.splitlines())
+    for name, cls in structs.items():
+        assert int(got[name]) == C.sizeof(cls), name
+        for f, _ in cls._fields_:
+            assert int(got[f"{name}.{f}"]) == getattr(cls, f).offset, f"{name}.{f}"
 
 
 @pytest.mark.parametrize("K,M,code", [(10, 6, kbin.KB_EINVAL), (64, 7, kbin.KB_EINVAL),

@@ -500,6 +500,28 @@ def test_alphabet_rejected():
         assert_same(eng.export(), oracle.bin_reads(b"".join(reads), [len(r) for r in reads], 11, 4, 1, True))
 
 
+@pytest.mark.parametrize("how", ["scatter", "split", "plan"])
+def test_alphabet_rejected_before_routing(how):
+    """a batch with a byte outside ACGT never leaves the context: kb_route_scatter,
+    kb_split_passes and kb_route_plan check the pack status first (KB_EALPHABET),
+    so no record built from the invalid read reaches a peer or a pass"""
+    import torch
+    with kbin.Engine(31, 7, max_read_len=150) as eng:
+        eng.submit([b"ACGT" * 20 + b"N" + b"ACGT" * 10])  # returns before the pack has run
+        cap = 1024
+        buf = torch.zeros(4 * cap * eng.record_words(), dtype=torch.int64, device="cuda")
+        with pytest.raises(kbin.KbError) as ei:
+            if how == "scatter":
+                eng.route_scatter(4, buf.data_ptr(), cap)
+            elif how == "split":
+                eng.split_passes(4, buf.data_ptr(), cap)
+            else:
+                eng.route_plan(4)
+        assert ei.value.code == kbin.KB_EALPHABET
+        torch.cuda.synchronize()
+        assert int(buf.abs().sum()) == 0  # nothing was written
+
+
 def test_streaming_submits_reuse_buffer():
     """kb_submit copies in and returns without waiting (double-buffered pinned
     staging, pooled device batches): 40 batches of varying size, each written
