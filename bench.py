@@ -282,6 +282,167 @@ def load_traffic(tag: str, kernel: str):
         return None
 
 
+def single_gpu_runner(K, M, L, cutoff, n, wpr, P, local, reads, pass_log, scan_once=True):
+    """The single-GPU step of a workload: (engine, step(digest=False)).  P > 1:
+    one super-k-mer pass over the reads (kb_split_passes) fills the P passes'
+    regions and each pass bins its region (no rescans) -- or, when the regions
+    would not fit beside the passes' buffers (or scan_once is off), every pass
+    rescans the reads with kb_set_partition.  step() appends (export_device,
+    timing, None) of every pass to pass_log and returns the digest summed over
+    the passes when asked."""
+    eng = kbin.Engine(K, M, cutoff=cutoff, max_read_len=L, device=local)
+    # Super-k-mers per read: about 2 (L - K + 1) / (K - M + 2) (a sticky
+    # signature holds for half a window on average; ~10 at 150 bp K31 M7,
+    # ~7 at 250 bp K63 M7), with a margin; the partition hash splits them
+    # evenly, and a short region is retried bigger.  Gated on the HBM: the
+    # regions sit beside the pass's own buffers
+    per_read = 2.0 * max(1, L - K + 1) / (K - M + 2) * 1.25 + 1.0
+    split = {"cap": int(n * per_read / P * 1.1) + 4096, "buf": None, "counts": None}
+    split_bytes = P * split["cap"] * (1 + (2 * K - M + 31) // 32) * 8
+    scan_once = (P > 1 and scan_once
+                 and split_bytes < 0.15 * torch.cuda.get_device_properties(local).total_memory)
+    sender = kbin.Engine(K, M, cutoff=cutoff, max_read_len=L, device=local) if scan_once else None
+    rw = eng.record_words()
+
+    def scan():
+        sender.reset()
+        w, ln = reads()
+        sender.submit_packed_device(w.data_ptr(), ln.data_ptr(), n, wpr, first_id=0)
+        for _ in range(3):
+            need = P * split["cap"] * rw
+            if split["buf"] is None or split["buf"].numel() < need:
+                split["buf"] = None  # (free the old one first)
+                split["buf"] = torch.empty(need, dtype=torch.int64, device="cuda")
+            ok, counts = sender.split_passes(P, split["buf"].data_ptr(), split["cap"])
+            if ok:
+                split["counts"] = [int(c) for c in counts]
+                return
+            split["cap"] = int(int(counts.max()) * 1.1) + 1024
+        raise RuntimeError("kb_split_passes: region capacity not converging")
+
+    def step(digest=False):
+        pass_log.clear()
+        dig = [0, 0, 0, 0]
+        if scan_once:
+            scan()
+        for p in range(P):
+            eng.reset()
+            if scan_once:
+                eng.set_partition(p, P)
+                eng.submit_superkmers_device(split["buf"][p * split["cap"] * rw:].data_ptr(),
+                                             split["counts"][p])
+            else:
+                w, ln = reads()
+                eng.submit_packed_device(w.data_ptr(), ln.data_ptr(), n, wpr, first_id=0)
+                if P > 1:
+                    eng.set_partition(p, P)
+            eng.finalize(prune=True)
+            pass_log.append((eng.export_device(), eng.timing(), None))
+            if digest:
+                dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
+        return dig
+
+    return eng, step
+
+
+def roofline(passes, L, K, world, kmers_scanned_per_s, tag):
+    """roofline of the dominant kernel: SURVEY.md 8(d)'s algorithmic bytes per
+    k-mer occurrence x the occurrences one launch processes / the launch's
+    device time (HIP events on the engine stream, inside the timed loop).
+    Binned: bin_kernel alone (events right around it) while it does most of
+    the bin phase (light bins, C2); when heavy bins dominate (C3) it only
+    publishes them, and the roofline kernel is the whole bin phase (runs_ms:
+    bin_kernel, the heavy-bin kernels, bins_final)."""
+    tim = [t for _, t in passes]
+    bpk = algorithmic_bytes_per_read(L, K) / max(1, L - K + 1)
+    binned = int(tim[-1]["engine"]) == kbin.KB_ENG_BINNED
+    kname = "bin_kernel" if binned else ("scan_insert_kernel<1>" if K <= 31 else "scan_insert_kernel<2>")
+    bin_alone = binned and all(0 < t.get("bin_kernel_ms", 0) and t["bin_kernel_ms"] >= 0.5 * t["runs_ms"]
+                               for t in tim)
+    if binned and not bin_alone:
+        kname = "bin phase (bin_kernel + heavy-bin kernels)"
+    launch_ms = [(t["bin_kernel_ms"] if bin_alone else t["runs_ms"]) if binned
+                 else t["scan_insert_ms"] / max(1, t["scan_insert_launches"]) for t in tim]
+    avg_kernel_ms = float(np.mean(launch_ms))
+    kmers_per_launch = float(np.mean([int(d["n_kmers"]) for d, _ in passes]))
+    achieved = kmers_per_launch * bpk / (avg_kernel_ms * 1e-3) / 1e9  # GB/s, per launch
+    traffic = load_traffic(tag, kname)
+    return {"bound": "hbm", "kernel": kname,
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+            **({"traffic_cold_launch": traffic["cold_bytes"], "traffic_source": traffic["source"]}
+               if traffic else {}),
+            "kernel_ms": round(avg_kernel_ms, 4),
+            "kmers_per_launch": int(kmers_per_launch),
+            "bytes_per_kmer": round(bpk, 3),
+            "path_frac": round(kmers_scanned_per_s * bpk / (world * HBM_PEAK_GBS * 1e9), 4)}
+
+
+def path_counters(passes):
+    """which bin-phase paths the passes took (kb_timing path counters, summed)"""
+    keys = ("n_bins", "split_mmers", "heavy_bins", "split_bins", "partitions", "offset_partitions",
+            "flat_partitions", "overflow_redos", "prefiltered", "long_lists", "clustered_lists")
+    out = {k: int(sum(int(t.get(k, 0)) for _, t in passes)) for k in keys}
+    out["max_depth"] = int(max(int(t.get("max_depth", 0)) for _, t in passes))
+    return out
+
+
+# C3's digest over its 4 passes (kb_digest summed), unchanged since round 1
+# (DESIGN.md section 9): entries, ids, key sum, list sum
+C3_DIGEST = ("0x55e59a7", "0x2c09aea31", "0x970d0f0c5efb1b3", "0x1b44773986421548")
+
+
+def capacity_leg(local, steps=2, warmup=1):
+    """SURVEY 8(d) C3 on one GPU (the largest single-GPU BASELINE config:
+    100M x 150 bp, 12 G k-mer occurrences, P = 4 mmer-partitioned passes, one
+    super-k-mer scan for all passes): ms per step, the bin phase's roofline, the
+    paths taken, and the full result's digest checked against the committed
+    one.  Not the bench value (the headline is C2)."""
+    wl = WORKLOADS["c3"]
+    n, L, K, M, P = wl["reads"], wl["read_len"], wl["K"], wl["M"], wl["parts"]
+    wpr = (L + 31) // 32
+    w = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    ln = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(w.data_ptr(), ln.data_ptr(), n, L, wl["genome"], wl["err_ppm"],
+                               gen_seed(wl["seed"]), device=local, read_base=0)
+    torch.cuda.synchronize()
+    pass_log = []
+    eng, step = single_gpu_runner(K, M, L, 1, n, wpr, P, local, lambda off=0: (w, ln), pass_log)
+    eng.set_timing(True)
+    tc = time.perf_counter()
+    step()
+    torch.cuda.synchronize()
+    cold_ms = (time.perf_counter() - tc) * 1e3
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    log = []
+    for _ in range(steps):
+        step()
+        log.extend((d, t) for d, t, _ in pass_log)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    kmers = n * (L - K + 1)
+    dig = tuple(hex(x) for x in step(digest=True))
+    torch.cuda.synchronize()
+    del eng, step
+    out = {"workload": f"C3: {n} x {L}bp reads, genome {wl['genome']} bp, {wl['err_ppm'] / 1e4:.2f}% "
+                       f"substitutions, seed {wl['seed']}, K={K} M={M}, prune cutoff 1, {P} mmer-partitioned "
+                       f"passes (one super-k-mer scan)",
+           "value": round(kmers / dt, 1), "unit": "k-mers/s", "ms_per_step": round(dt * 1e3, 3),
+           "steps": steps, "cold_first_step_ms": round(cold_ms, 1),
+           "roofline": roofline(log, L, K, 1, kmers / dt, f"n{n}_L{L}_K{K}_M{M}_P{P}"),
+           "phases_ms": {k: round(float(sum(t[k] for _, t in log)) / steps, 3)
+                         for k in ("scan_insert_ms", "sort_ms", "runs_ms", "emit_ms", "total_ms")},
+           "paths": path_counters(log[-P:]),
+           "digest": list(dig), "digest_expected": list(C3_DIGEST), "digest_ok": dig == C3_DIGEST}
+    if not out["digest_ok"]:
+        print(f"capacity leg: C3 digest {dig} != committed {C3_DIGEST}", file=sys.stderr)
+    return out
+
+
 def main():
     # stdout carries exactly ONE JSON line (rank 0): native libraries print to
     # fd 1 (RCCL's version banner, gloo's connection notes), so fd 1 points at
@@ -317,9 +478,12 @@ def main():
                     help="fresh: every step bins new reads of the same genome (all sets generated before "
                          "timing); replay: the same reads every step; auto: fresh when the sets fit in "
                          "5%% of the HBM")
-    ap.add_argument("--host-input", action="store_true",
-                    help="N=1: also time the host-ingest path (kb_submit of host ASCII, finalize, "
-                         "kb_export) with H2D and D2H reported separately")
+    ap.add_argument("--no-host-input", dest="host_input", action="store_false",
+                    help="N=1: skip the host-ingest leg (kb_submit of host ASCII, finalize, kb_export, "
+                         "H2D and D2H reported separately; on by default)")
+    ap.add_argument("--no-capacity", dest="capacity", action="store_false",
+                    help="N=1: skip the C3 capacity leg (100M x 150 bp in 4 passes, digest-checked; on by "
+                         "default)")
     ap.add_argument("--dropin", action="store_true",
                     help="N=1: also time the reference surface (kbin_main: fgets + process_read loop, "
                          "prune_data with materialised zhash tables) on the workload's reads")
@@ -441,63 +605,19 @@ def main():
             while pending:
                 runner.wait(pending.pop())
     else:
-        eng = kbin.Engine(K, M, cutoff=args.cutoff, max_read_len=L, device=local)
-        # P > 1: one super-k-mer pass over the reads (kb_split_passes) fills the
-        # passes' regions; each pass then bins its region (no rescans).
-        # Super-k-mers per read: about 2 (L - K + 1) / (K - M + 2) (a sticky
-        # signature holds for half a window on average; ~10 at 150 bp K31 M7,
-        # ~7 at 250 bp K63 M7), with a margin; the partition hash splits them
-        # evenly, and a short region is retried bigger.  Gated on the HBM: the
-        # regions sit beside the pass's own buffers
-        per_read = 2.0 * max(1, L - K + 1) / (K - M + 2) * 1.25 + 1.0
-        split = {"cap": int(n * per_read / P * 1.1) + 4096, "buf": None, "counts": None}
-        split_bytes = P * split["cap"] * (1 + (2 * K - M + 31) // 32) * 8
-        scan_once = (P > 1 and not args.no_scan_once
-                     and split_bytes < 0.15 * torch.cuda.get_device_properties(local).total_memory)
-        sender = kbin.Engine(K, M, cutoff=args.cutoff, max_read_len=L, device=local) if scan_once else None
-        rw = eng.record_words()
+        eng, step = single_gpu_runner(K, M, L, args.cutoff, n, wpr, P, local, reads, pass_log,
+                                      scan_once=not args.no_scan_once)
 
         def drain():
             pass
 
-        def scan():
-            sender.reset()
-            w, ln = reads()
-            sender.submit_packed_device(w.data_ptr(), ln.data_ptr(), n, wpr, first_id=0)
-            for _ in range(3):
-                need = P * split["cap"] * rw
-                if split["buf"] is None or split["buf"].numel() < need:
-                    split["buf"] = None  # (free the old one first)
-                    split["buf"] = torch.empty(need, dtype=torch.int64, device="cuda")
-                ok, counts = sender.split_passes(P, split["buf"].data_ptr(), split["cap"])
-                if ok:
-                    split["counts"] = [int(c) for c in counts]
-                    return
-                split["cap"] = int(int(counts.max()) * 1.1) + 1024
-            raise RuntimeError("kb_split_passes: region capacity not converging")
+    if world == 1 and not args.routed:
+        _step1 = step
 
         def step(digest=False):
-            pass_log.clear()
-            dig = [0, 0, 0, 0]
-            if scan_once:
-                scan()
-            for p in range(P):
-                eng.reset()
-                if scan_once:
-                    eng.set_partition(p, P)
-                    eng.submit_superkmers_device(split["buf"][p * split["cap"] * rw:].data_ptr(),
-                                                 split["counts"][p])
-                else:
-                    w, ln = reads()
-                    eng.submit_packed_device(w.data_ptr(), ln.data_ptr(), n, wpr, first_id=0)
-                    if P > 1:
-                        eng.set_partition(p, P)
-                eng.finalize(prune=True)
-                pass_log.append((eng.export_device(), eng.timing(), None))
-                if digest:
-                    dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
+            d = _step1(digest)
             cur[0] += 1
-            return dig
+            return d
 
     def barrier():
         if dist is not None:
@@ -543,41 +663,10 @@ def main():
     total_scanned = scanned * world
     value = total_scanned * args.steps / elapsed
 
-    # roofline of the dominant kernel: SURVEY.md 8(d)'s algorithmic bytes per
-    # k-mer occurrence x the occurrences one launch processes / the launch's
-    # device time (HIP events on the engine stream, inside the timed loop)
     passes = [pt for st in steps_log for pt in st]
     tim = [t for _, t in passes]
-    bpr = algorithmic_bytes_per_read(L, K)
-    bpk = bpr / max(1, L - K + 1)
-    binned = int(tim[-1]["engine"]) == kbin.KB_ENG_BINNED
-    kname = "bin_kernel" if binned else ("scan_insert_kernel<1>" if K <= 31 else "scan_insert_kernel<2>")
-    # binned: bin_kernel alone (events right around it) while it does most of
-    # the bin phase (light bins, C2); when heavy bins dominate (C3) it only
-    # publishes them, and the roofline kernel is the whole bin phase (runs_ms:
-    # bin_kernel, the heavy-bin kernels, bins_final)
-    bin_alone = binned and all(0 < t.get("bin_kernel_ms", 0) and t["bin_kernel_ms"] >= 0.5 * t["runs_ms"]
-                               for t in tim)
-    if binned and not bin_alone:
-        kname = "bin phase (bin_kernel + heavy-bin kernels)"
-    launch_ms = [(t["bin_kernel_ms"] if bin_alone else t["runs_ms"]) if binned
-                 else t["scan_insert_ms"] / max(1, t["scan_insert_launches"]) for t in tim]
-    avg_kernel_ms = float(np.mean(launch_ms))
-    kmers_per_launch = float(np.mean([int(d["n_kmers"]) for d, _ in passes]))
-    achieved = kmers_per_launch * bpk / (avg_kernel_ms * 1e-3) / 1e9  # GB/s, per launch
     tag = f"n{n}_L{L}_K{K}_M{M}" + (f"_P{args.parts}" if args.parts > 1 else "")
-    traffic = load_traffic(tag, kname)
-    roof = {"bound": "hbm", "kernel": kname,
-            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
-            **({"traffic_cold_launch": traffic["cold_bytes"], "traffic_source": traffic["source"]}
-               if traffic else {}),
-            "kernel_ms": round(avg_kernel_ms, 4),
-            "kmers_per_launch": int(kmers_per_launch),
-            "bytes_per_kmer": round(bpk, 3),
-            "path_frac": round(total_scanned * args.steps / elapsed * bpk
-                               / (world * HBM_PEAK_GBS * 1e9), 4)}
+    roof = roofline(passes, L, K, world, total_scanned * args.steps / elapsed, tag)
     # device time per step (all passes of a step added up)
     phases = {k: round(float(np.mean([sum(t[k] for _, t in st) for st in steps_log])), 4)
               for k in ("scan_insert_ms", "sort_ms", "runs_ms", "emit_ms", "total_ms")}
@@ -628,6 +717,7 @@ def main():
                   **({"replay": replay} if replay else {})},
         "roofline": roof,
         "phases_ms": phases,
+        "paths": path_counters(steps_log[-1]),
         **({"route_ms": {k: round(float(np.mean([r[k] for r in route_t])), 4) for k in route_t[0]}}
            if route_t else {}),
         "result": {**({"digest": digest} if digest else {}),
@@ -637,8 +727,10 @@ def main():
                    "engine": {1: "table", 2: "binned"}.get(int(tim[-1]["engine"]), "?"),
                    "bins": int(tim[-1]["n_bins"]), "superkmers": int(tim[-1]["n_superkmers"])},
     }
-    if rank == 0 and world == 1 and args.host_input and P == 1:
+    if world == 1 and args.host_input and P == 1:
         out["host_input"] = host_input_leg(sets[0][0], sets[0][1], n, wpr, L, K, M, args.cutoff, local)
+    if world == 1 and args.capacity and args.workload == "c2" and not args.routed:
+        out["capacity"] = capacity_leg(local)
     if rank == 0 and world == 1 and args.dropin and P == 1:
         out["dropin"] = dropin_leg(sets[0][0], sets[0][1], n, wpr, L, K, M, args.cutoff, local)
     if rank == 0 and world == 1 and args.cpu_sample > 0:

@@ -11,12 +11,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <queue>
 #include <string>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -264,17 +267,19 @@ struct kb_ctx {
     uint32_t part = 0, part_n = 1;  // kb_set_partition: this pass's mmer partition
     // balanced local buckets: records per canonical mmer seen in earlier passes,
     // and one device map (mmer -> bucket) per (part, part_n) key
-    std::vector<uint32_t> mmer_w;
+    std::vector<uint32_t> mmer_w;  // records per canonical mmer (all its sub-bins)
+    std::vector<uint64_t> mmer_o;  // k-mer occurrences per canonical mmer
+    std::unordered_map<uint64_t, uint32_t> sub_w;  // (mmer << 16 | sub-bin) -> records, split mmers of the last pass
     struct BucketMap {
         uint64_t key = 0;
         uint32_t nb = 0;
         bool stale = false;
-        bool spread = false;  // some mmer has a run of buckets
         uint64_t want_max = 0;  // the largest bucket load the packing expects (records)
         uint64_t want_tot = 0;
-        DevBuf<uint16_t> map;
-        DevBuf<uint16_t> run;  // [nb] spread runs (bucket_kernel's brun)
-        DevBuf<uint32_t> run_mmer;  // [nb] the mmer of a run's head
+        uint32_t split = 0;     // mmers split into context sub-bins
+        std::vector<uint32_t> h_map;  // host copy of map
+        DevBuf<uint32_t> map;   // per canonical mmer (bm_* in kbin_internal.h)
+        DevBuf<uint16_t> sub;   // buckets of the split mmers' sub-bins
     };
     std::vector<BucketMap> bmaps;
     uint64_t* h_totals = nullptr;
@@ -394,7 +399,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
     c->misc.release(); c->totals.release(); c->first.release(); c->e_first.release();
-    for (auto& m : c->bmaps) { m.map.release(); m.run.release(); m.run_mmer.release(); }
+    for (auto& m : c->bmaps) { m.map.release(); m.sub.release(); }
     c->flat_list.release(); c->flat_next.release(); c->flat_l0.release(); c->flat_off.release();
     c->flat_cur.release(); c->flat_chunk.release(); c->pool_bin.release(); c->chunk_bin.release();
     c->flat_sbase.release(); c->flat_obase.release(); c->flat_n.release(); c->hll.release();
@@ -637,6 +642,18 @@ static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
 }
+
+// KB_DEBUG=1: one stderr line per host-side event of a finalize (diagnostics)
+static double now_ms() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+#define KB_DBG(...)                                             \
+    do {                                                        \
+        static const bool _on = env_int("KB_DEBUG", 0) != 0;    \
+        if (_on) fprintf(stderr, "[kb] " __VA_ARGS__);          \
+    } while (0)
 
 // the binned engine (kbin_bins.hip) serves K <= 63 unless the table engine is
 // forced (flag, or KB_ENGINE=table).  Two-word k-mers (K > 31) take only its
@@ -1118,70 +1135,86 @@ static kb_ctx::BucketMap* bmap_find(kb_ctx* c, uint32_t NB) {
     return nullptr;
 }
 
-static int bmap_build(kb_ctx* c, uint32_t NB) {
+// Context sub-bins (kbin_internal.h): an mmer whose expected distinct keys
+// exceed one LDS table at the light load (few mmers per rank at N GPUs, high
+// coverage), or whose records exceed 1.5 buckets' fair share, is split into
+// 4^b + 1 sub-bins, b the smallest depth that brings each under both.  Each
+// sub-bin is then an item of its own in the packing below, placed on any
+// bucket -- a light bin of its own in bin_kernel: no flat lists, no
+// re-expansion per partition, finer longest-first scheduling.
+static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
+    const int bmax = std::min<int>((int)SUB_MAX_B, std::max(0, env_int("KB_BIN_SUB", (int)SUB_MAX_B)));
+    const double ts = c->KW == 1 ? 8192.0 : 4096.0;
+    const double cap = ts * std::min(0.85, std::max(0.2, env_int("KB_BIN_SUB_FILL_PCT", 50) / 100.0));
+    uint32_t b = 0;
+    while ((int)b < bmax && (keys / (double)(1u << (2 * b)) > cap || w / (double)(1u << (2 * b)) > 1.5 * mean)) b++;
+    return b;
+}
+
+static int bmap_build(kb_ctx* c, uint32_t NB, double rho) {
     const int M = c->p.M;
     const uint32_t half = 1u << (2 * M - 1);
-    std::vector<std::pair<uint32_t, uint32_t>> items;  // (records, mmer)
-    std::vector<uint16_t> h(half);
+    struct Item {
+        double w;
+        uint32_t mm, sub;  // sub: ~0 for an unsplit mmer
+    };
+    std::vector<Item> items;
+    std::vector<uint32_t> h(half);
+    uint64_t tot_w = 0;
+    for (uint32_t i = 0; i < half && i < c->mmer_w.size(); i++) tot_w += c->mmer_w[i];
+    const double mean = std::max(1.0, (double)tot_w / NB);
+    std::vector<uint16_t> subs;
+    uint32_t n_split = 0;
     for (uint32_t i = 0; i < half; i++) {
         const uint32_t mm = half + i;
-        if (c->part_n > 1 && sk_hash_dest(mm, c->part_n, 0x9E3779B97F4A7C15ull) != c->part) {
-            h[i] = (uint16_t)sk_hash_dest(mm, NB, sk_bucket_salt());  // another pass's mmer: never seen here
+        h[i] = (uint32_t)sk_hash_dest(mm, NB, sk_bucket_salt());  // unseen (or another pass's): hash
+        if (c->part_n > 1 && sk_hash_dest(mm, c->part_n, 0x9E3779B97F4A7C15ull) != c->part) continue;
+        const double w = i < c->mmer_w.size() ? (double)c->mmer_w[i] : 0.0;
+        if (w <= 0) continue;
+        const double occ = i < c->mmer_o.size() && c->mmer_o[i] ? (double)c->mmer_o[i] : 12.0 * w;
+        const uint32_t b = sub_depth(c, w, occ * rho, mean);
+        if (!b) {
+            items.push_back({w, mm, ~0u});
             continue;
         }
-        if (i < c->mmer_w.size() && c->mmer_w[i]) items.push_back({c->mmer_w[i], mm});
-        else h[i] = (uint16_t)sk_hash_dest(mm, NB, sk_bucket_salt());  // unseen: hash
+        // sub-bin 0, the edge, holds a few percent; the contexts share the
+        // rest -- or, when the last pass split this mmer as deep, as measured
+        const uint32_t nsub = sub_count(b);
+        const kb_ctx::BucketMap* old = bmap_find(c, NB);
+        const bool same = old && !old->h_map.empty() && (old->h_map[i] & BM_SPLIT) &&
+                          ((old->h_map[i] >> 28) & 7u) == b;
+        h[i] = BM_SPLIT | (b << 28) | (uint32_t)subs.size();
+        for (uint32_t s2 = 0; s2 < nsub; s2++) {
+            double ws = s2 ? w / (double)(nsub - 1) : 0.04 * w + 1.0;
+            if (same) {
+                auto f = c->sub_w.find(((uint64_t)mm << 16) | s2);
+                ws = f != c->sub_w.end() ? (double)f->second : 1.0;
+            }
+            items.push_back({ws, mm, s2});
+        }
+        subs.resize(subs.size() + nsub, 0);
+        n_split++;
     }
-    std::sort(items.begin(), items.end(), [](const std::pair<uint32_t, uint32_t>& a,
-                                             const std::pair<uint32_t, uint32_t>& b) { return a.first > b.first; });
-    // Spread: an mmer above twice the mean bucket load gets a run of k
-    // consecutive buckets of its own (from the front, at most 3/4 of them);
-    // its records pick one by hash and the run's regions are laid out
-    // contiguously, one bin (few mmers per rank: one workgroup ordering a whole
-    // mmer set bucket_kernel's time)
-    uint64_t tot_w = 0;
-    for (auto& it : items) tot_w += it.first;
-    const double mean = (double)tot_w / NB;
-    std::vector<uint16_t> run(NB, 0);
-    std::vector<uint32_t> run_mm(NB, 0);
-    uint32_t next = 0;
-    uint64_t spread_max_load = 0;
-    const uint32_t spread_cap = env_int("KB_BIN_SPREAD", 1) ? NB * 3 / 4 : 0;
-    std::vector<bool> placed(items.size(), false);
-    for (size_t i = 0; i < items.size() && NB <= 1024; i++) {
-        const double w = items[i].first;
-        if (w <= 2.0 * mean || next + 2 > spread_cap) break;  // (sorted: the rest are smaller)
-        uint32_t k = (uint32_t)std::min(63.0, std::ceil(w / mean));
-        k = std::min(k, spread_cap - next);
-        h[items[i].second - half] = (uint16_t)(next | (k << 10));
-        run[next] = (uint16_t)k;
-        run_mm[next] = items[i].second;
-        for (uint32_t j = 1; j < k; j++) run[next + j] = BK_RUN_CONT;
-        spread_max_load = std::max<uint64_t>(spread_max_load, (uint64_t)(w / k) + 1);
-        next += k;
-        placed[i] = true;
-    }
-    // least-loaded bucket first; at most 128 mmers per bucket (bucket_kernel maps 256)
-    using Slot = std::pair<uint64_t, uint32_t>;  // (load, bucket)
+    std::sort(items.begin(), items.end(), [](const Item& a, const Item& b) { return a.w > b.w; });
+    // longest processing time first onto the least loaded bucket; at most 128
+    // bins per bucket (bucket_kernel maps 256)
+    using Slot = std::pair<double, uint32_t>;  // (load, bucket)
     std::priority_queue<Slot, std::vector<Slot>, std::greater<Slot>> pq;
     std::vector<uint32_t> nm(NB, 0);
-    for (uint32_t b = next; b < NB; b++) pq.push({0, b});
-    for (size_t i = 0; i < items.size(); i++) {
-        if (placed[i]) continue;
-        auto& it = items[i];
+    for (uint32_t b = 0; b < NB; b++) pq.push({0.0, b});
+    for (const Item& it : items) {
         Slot sl = pq.top();
         pq.pop();
         while (nm[sl.second] >= 128 && !pq.empty()) {  // full: retire it
             sl = pq.top();
             pq.pop();
         }
-        h[it.second - half] = (uint16_t)sl.second;
+        if (it.sub == ~0u) h[it.mm - half] = sl.second;
+        else subs[(h[it.mm - half] & 0x0FFFFFFFu) + it.sub] = (uint16_t)sl.second;
         nm[sl.second]++;
-        pq.push({sl.first + it.first, sl.second});
+        pq.push({sl.first + it.w, sl.second});
     }
-    uint64_t want_max = spread_max_load, want_tot = 0;
-    for (size_t i = 0; i < items.size(); i++)
-        if (placed[i]) want_tot += items[i].first;
+    double want_max = 0, want_tot = 0;
     while (!pq.empty()) {
         want_max = std::max(want_max, pq.top().first);
         want_tot += pq.top().first;
@@ -1195,55 +1228,125 @@ static int bmap_build(kb_ctx* c, uint32_t NB) {
         m->nb = NB;
     }
     HIPCHK(m->map.ensure(half));
-    HIPCHK(hipMemcpyAsync(m->map.p, h.data(), half * sizeof(uint16_t), hipMemcpyHostToDevice, c->s));
-    m->spread = next > 0;
-    if (m->spread) {
-        HIPCHK(m->run.ensure(NB));
-        HIPCHK(m->run_mmer.ensure(NB));
-        HIPCHK(hipMemcpyAsync(m->run.p, run.data(), NB * sizeof(uint16_t), hipMemcpyHostToDevice, c->s));
-        HIPCHK(hipMemcpyAsync(m->run_mmer.p, run_mm.data(), NB * sizeof(uint32_t), hipMemcpyHostToDevice, c->s));
-    }
-    HIPCHK(hipStreamSynchronize(c->s));  // h is a local
+    HIPCHK(hipMemcpyAsync(m->map.p, h.data(), half * sizeof(uint32_t), hipMemcpyHostToDevice, c->s));
+    m->h_map = h;
+    HIPCHK(m->sub.ensure(std::max<size_t>(subs.size(), 1)));
+    if (!subs.empty())
+        HIPCHK(hipMemcpyAsync(m->sub.p, subs.data(), subs.size() * sizeof(uint16_t), hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));  // h and subs are locals
     m->stale = false;
-    m->want_max = want_max;
-    m->want_tot = want_tot;
+    m->split = n_split;
+    m->want_max = (uint64_t)want_max + 1;
+    m->want_tot = (uint64_t)want_tot + 1;
     // the region stride the next map-routed pass starts with (one pass when
     // the packing holds; a larger bucket reruns it bigger)
-    c->bucket_cap = std::max<uint64_t>(c->bucket_cap, want_max + want_max / 4 + 1024);
+    c->bucket_cap = std::max<uint64_t>(c->bucket_cap, m->want_max + m->want_max / 4 + 1024);
     return KB_OK;
 }
 
-// after a bucketed pass: learn records per mmer from the bin descriptors and
-// (re)build this key's map when it is missing or the pass found it unbalanced
-static int bmap_learn(kb_ctx* c, uint32_t NB, uint64_t R, uint64_t nbins) {
+// after a bucketed pass: learn records and occurrences per mmer from the bin
+// descriptors (a split mmer's sub-bins add up) and (re)build this key's map
+// when it is missing or the pass found it unbalanced
+static int bmap_learn(kb_ctx* c, uint32_t NB, uint64_t R, uint64_t nbins, double rho) {
     if (!env_int("KB_BIN_BALANCE", 1) || R < (uint64_t)std::max(0, env_int("KB_BIN_BALANCE_MIN", 1 << 18)))
         return KB_OK;
     kb_ctx::BucketMap* m = bmap_find(c, NB);
     if (m && !m->stale) return KB_OK;
-    std::vector<uint32_t> mm(nbins), cnt(nbins);
+    std::vector<uint32_t> mm(nbins), cnt(nbins), occ(nbins);
     HIPCHK(hipMemcpyAsync(mm.data(), c->bmmer.p, nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipMemcpyAsync(cnt.data(), c->bcount.p, nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipMemcpyAsync(occ.data(), c->bocc.p, nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     const uint32_t half = 1u << (2 * c->p.M - 1);
-    if (c->mmer_w.size() != half) c->mmer_w.assign(half, 0);
-    for (uint64_t b = 0; b < nbins; b++)
-        if (mm[b] >= half && mm[b] < 2 * half) c->mmer_w[mm[b] - half] = std::max(cnt[b], 1u);
-    return bmap_build(c, NB);
+    c->mmer_w.assign(half, 0);
+    c->mmer_o.assign(half, 0);
+    // a split mmer's sub-bins as measured (bmmer: the mmer | sub-bin << 16),
+    // which the packing uses while the mmer keeps its depth
+    c->sub_w.clear();
+    for (uint64_t b = 0; b < nbins; b++) {
+        const uint32_t mmer = mm[b] & 0xFFFFu, sub = mm[b] >> 16;
+        if (mmer < half || mmer >= 2 * half) continue;
+        c->mmer_w[mmer - half] += std::max(cnt[b], 1u);
+        c->mmer_o[mmer - half] += occ[b];
+        if (m && m->split) {
+            const uint32_t e = m->h_map.empty() ? 0u : m->h_map[mmer - half];
+            if (e & BM_SPLIT) c->sub_w[((uint64_t)mmer << 16) | sub] += std::max(cnt[b], 1u);
+        }
+    }
+    return bmap_build(c, NB, rho);
 }
 
 // ---- phase A, bucketed: records straight into NB local bucket regions
 // (hash of the mmer); the learned capacity grows (and the pass reruns) when a
 // bucket overflows.  Reads: the one-pass super-k-mer kernel in region mode;
 // received: the block-aggregated converter.  Returns R and N (one sync per try).
+// A context's first pass of a (part, part_n) key has no learned map.  Hashed
+// into the buckets, the records would be very uneven (the minimizer rule
+// makes mmer frequencies skewed: the largest hashed bucket holds ~8x the
+// mean), which took a counting pass to lay the regions out exactly.  Instead
+// the first pass packs the buckets by a PRIOR: on uniform sequence, a
+// canonical mmer with canonical score c is a window's leftmost maximum
+// (binning.c:972) about as often as all W - 1 other positions score below it,
+// i.e. in proportion to ((c - 2^(2M-1)) / 2^(2M-1))^(W-1) (W = K - M + 1
+// positions; each canonical score stands for two strings).  Packed by that
+// weight, buckets come out as even as packed by the true counts (simulated
+// at K31 M7: max/mean 1.85 either way, 6.4 hashed).  The records expected per
+// read, 2 (L - K + 1) / (K - M + 2), scale it.  The prior map is marked stale,
+// so the pass's own bins replace it.
+static int bmap_prior(kb_ctx* c, uint32_t NB) {
+    const int K = c->p.K, M = c->p.M, W = K - M + 1;
+    const uint32_t half = 1u << (2 * M - 1);
+    double R_est = 0;
+    for (auto& b : c->batches) {
+        if (b.routed || !b.n_reads) continue;
+        if (b.superkmers) {
+            R_est += (double)b.n_reads;
+        } else {
+            const double L = std::min(b.RW * 32.0, (double)c->p.max_read_len);
+            R_est += (double)b.n_reads * std::max(1.0, 2.0 * std::max(1.0, L - K + 1) / (K - M + 2));
+        }
+    }
+    const bool reads_part = c->part_n > 1 && std::none_of(c->batches.begin(), c->batches.end(),
+                                                          [](const Batch& b) { return b.superkmers; });
+    std::vector<double> p(half);
+    double tot = 0, mine = 0;
+    for (uint32_t i = 0; i < half; i++) {
+        p[i] = std::pow((double)(i + 1) / half, W - 1);
+        tot += p[i];
+        if (c->part_n <= 1 || sk_hash_dest(half + i, c->part_n, 0x9E3779B97F4A7C15ull) == c->part) mine += p[i];
+    }
+    // reads scanned for one partition emit only its records; received ones are its own
+    const double R_part = reads_part ? R_est * mine / std::max(tot, 1e-300) : R_est;
+    c->mmer_w.assign(half, 0);
+    c->mmer_o.assign(half, 0);
+    for (uint32_t i = 0; i < half; i++) {
+        const double w = R_part * p[i] / std::max(mine, 1e-300);
+        c->mmer_w[i] = (uint32_t)std::min(4e9, std::ceil(w));
+    }
+    const int rc = bmap_build(c, NB, c->rho > 0.f ? (double)c->rho : 0.0);
+    if (rc) return rc;
+    kb_ctx::BucketMap* m = bmap_find(c, NB);
+    m->stale = true;  // (the pass learns the real one)
+    // a prior misses real data's skew more than a learned map: a wider stride
+    // (an overflowing bucket reruns the pass bigger)
+    c->bucket_cap = std::max<uint64_t>(c->bucket_cap, m->want_max + m->want_max / 2 + 1024);
+    return KB_OK;
+}
+
 static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, uint64_t& R, uint64_t& N) {
     const int M = c->p.M;
     kb_ctx::BucketMap* bm = bmap_find(c, NB);
-    const uint16_t* bmap = bm ? bm->map.p : nullptr;
-    // Without a learned map for this (part, part_n) key (a context's first
-    // pass, or a partition's first) the records are routed by hash and the
-    // buckets are uneven (the largest ~8x the mean): a counting pass first
-    // (capacity 0: every record counted, none written), then regions laid out
-    // exactly (rbase).  With a map, one pass into regions of the learned
+    if (!bm && env_int("KB_BIN_PRIOR", 1) && env_int("KB_BIN_BALANCE", 1)) {
+        const int rc = bmap_prior(c, NB);
+        if (rc) return rc;
+        bm = bmap_find(c, NB);
+    }
+    const uint32_t* bmap = bm ? bm->map.p : nullptr;
+    const uint16_t* bsub = bm ? bm->sub.p : nullptr;
+    // Without any map (KB_BIN_PRIOR=0) the records are routed by hash and the
+    // buckets are uneven: a counting pass first (capacity 0: every record
+    // counted, none written), then regions laid out exactly (rbase).  With a
+    // map (learned, or the prior), one pass into regions of the learned
     // capacity (stride), rerun bigger on overflow.
     const bool exact = bmap == nullptr;
     HIPCHK(c->bfill.ensure(NB));
@@ -1269,7 +1372,8 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
             if (b.routed || !b.n_reads) continue;
             if (received) {
                 if (!b.superkmers) continue;
-                HIPCHK(launch_sk_convert_buckets(b.recs, b.n_reads, rec_words(c), 2 * c->KW, M, NB, bmap, c->regions.p, cap,
+                HIPCHK(launch_sk_convert_buckets(b.recs, b.n_reads, rec_words(c), 2 * c->KW, M, NB, c->p.K, bmap, bsub,
+                                                 c->regions.p, cap,
                                                  use_base ? c->rbase.p : nullptr, c->bfill.p, c->misc.p,
                                                  reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
             } else {
@@ -1292,6 +1396,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
                 a.dest_salt = sk_bucket_salt();
                 a.rw = (int)RWD;  // header + span words
                 a.bucket_map = bmap;
+                a.sub_map = bsub;
                 a.binned_fmt = 1;
                 a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p);
                 HIPCHK(launch_sk(a, true, c->s));
@@ -1338,8 +1443,11 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
         // a map that no longer fits (largest bucket > 1.5x what the packing
         // expected, scaled to this pass's records): relearn it after this pass
         if (bm && R && bm->want_tot &&
-            (double)mx > 1.5 * (double)bm->want_max * (double)R / (double)bm->want_tot + 64.0)
+            (double)mx > 1.5 * (double)bm->want_max * (double)R / (double)bm->want_tot + 64.0) {
+            KB_DBG("map stale: bucket %llu vs expected %.0f\n", (unsigned long long)mx,
+                   (double)bm->want_max * (double)R / (double)bm->want_tot);
             bm->stale = true;
+        }
         if (use_base || mx <= cap) {
             c->rexact = use_base;
             c->bucket_cap_used = cap;  // the region stride of this pass (0: exact bases)
@@ -1354,6 +1462,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
         }
         // grow and rerun the pass; with headroom, so a later pass's slightly
         // larger bucket does not regrow (each growth maps the regions afresh)
+        KB_DBG("record pass rerun: bucket %llu > cap %llu\n", (unsigned long long)mx, (unsigned long long)cap);
         c->bucket_cap = mx + mx / 2 + 1024;
     }
     return fail(KB_EDEVICE, "internal: bucket capacity did not converge");
@@ -1498,7 +1607,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     if (rc) return rc;
     c->n_occ = N;
     REC(2);
-    const uint64_t max_bins = std::max<uint64_t>(1, std::min<uint64_t>(R, 1ull << (2 * M - 1)));
+    // bins: canonical mmers, or context sub-bins of the split ones
+    uint64_t bin_keys = 1ull << (2 * M - 1);
+    if (bucketed)
+        if (kb_ctx::BucketMap* bm = bmap_find(c, NB)) bin_keys += (uint64_t)bm->split * (sub_count(SUB_MAX_B) - 1);
+    const uint64_t max_bins = std::max<uint64_t>(1, std::min<uint64_t>(R, bin_keys));
     HIPCHK(c->starts.ensure(max_bins + 1));
     HIPCHK(c->bcount.ensure(max_bins));
     HIPCHK(c->bmmer.ensure(max_bins));
@@ -1541,8 +1654,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         ba.bbase = c->bbase.p;
         {
             kb_ctx::BucketMap* bm = bmap_find(c, NB);  // (the map the record pass used)
-            ba.brun = bm && bm->spread ? bm->run.p : nullptr;
-            ba.brun_mmer = bm && bm->spread ? bm->run_mmer.p : nullptr;
+            ba.bucket_map = bm && bm->split ? bm->map.p : nullptr;
+            ba.K = c->p.K;
         }
         ba.bin_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 2);
         ba.bstart = c->starts.p;
@@ -1592,12 +1705,19 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         h.w2 = KW == 2 ? c->srec.p + 3 * R : nullptr;
         h.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
         h.K = c->p.K;
-        HIPCHK(c->hll.ensure(4096));
-        HIPCHK(launch_hll(h, R, KW, c->hll.p, c->s));
-        std::vector<uint32_t> regs(4096);
-        HIPCHK(hipMemcpyAsync(regs.data(), c->hll.p, 4096 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        h.M = M;
+        // large passes estimate from the bins of 1/8 of the mmers (whole bins:
+        // the ratio of a sample of bins, 1/8 of the expansion work)
+        const uint32_t sample = R >= (1u << 20) && max_bins >= 256 ? (uint32_t)std::max(1, env_int("KB_BIN_HLL_SAMPLE", 8)) : 1u;
+        HIPCHK(c->hll.ensure(4096 + 2));
+        HIPCHK(launch_hll(h, R, KW, c->hll.p, sample, c->s));
+        std::vector<uint32_t> regs(4096 + 2);
+        HIPCHK(hipMemcpyAsync(regs.data(), c->hll.p, (4096 + 2) * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipStreamSynchronize(c->s));
-        c->rho = (float)std::min(1.0, std::max(1e-4, hll_estimate(regs.data()) / (double)N));
+        uint64_t occ_s = 0;
+        memcpy(&occ_s, regs.data() + 4096, sizeof(occ_s));
+        if (occ_s)
+            c->rho = (float)std::min(1.0, std::max(1e-4, hll_estimate(regs.data()) / (double)occ_s));
     }
     REC(3);
     // ---- one workgroup per bin.  Entry capacity: learned (or N/8), rerun once
@@ -1743,6 +1863,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         }
         if (attempt) HIPCHK(hipMemsetAsync(c->pstat.p, 0, KB_PSTAT * sizeof(unsigned long long), c->s));
         a.pstat = c->pstat.p;
+        a.ldsbar = (uint32_t)(env_int("KB_BIN_LDSBAR", 1) != 0);
+        a.ts_adapt = (uint32_t)(env_int("KB_BIN_TS_ADAPT", 1) != 0);
         HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr));
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
@@ -1787,7 +1909,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             for (size_t i = 0; i < c->bmaps.size(); i++)
                 if (c->bmaps[i].key == bmap_key(c) && c->bmaps[i].nb == NB) {
                     auto& m = c->bmaps[i];
-                    m.map.release(); m.run.release(); m.run_mmer.release();
+                    m.map.release(); m.sub.release();
                     c->bmaps.erase(c->bmaps.begin() + (long)i);
                     return finalize_binned(c, prune, affine, id_c, received);
                 }
@@ -1825,8 +1947,15 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     c->n_ids = c->h_totals[1];
     c->n_distinct = c->h_totals[6];
     if (bucketed) {
-        const int rc2 = bmap_learn(c, NB, R, std::min<uint64_t>(c->h_totals[2], max_bins));
+        const double rho_now = N ? (double)c->h_totals[6] / (double)N : 0.1;
+        const double t_l = now_ms();
+        const kb_ctx::BucketMap* bm0 = bmap_find(c, NB);
+        const bool relearn = !bm0 || bm0->stale;
+        const int rc2 = bmap_learn(c, NB, R, std::min<uint64_t>(c->h_totals[2], max_bins), rho_now);
         if (rc2) return rc2;
+        KB_DBG("learn part %u/%u: %s %.3f ms (bins %llu, R %llu)\n", c->part, c->part_n,
+               relearn ? "rebuilt" : "kept", now_ms() - t_l, (unsigned long long)c->h_totals[2],
+               (unsigned long long)R);
     }
     c->n_occ_entries_hint = c->n_entries;
     c->ecap_hint = c->n_entries + c->n_entries / 4 + 1024;
@@ -1855,6 +1984,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         c->tm.flat_partitions = ps[7];
         c->tm.long_lists = c->h_misc[4];
         c->tm.clustered_lists = c->h_misc[5];
+        const kb_ctx::BucketMap* bm = bucketed ? bmap_find(c, NB) : nullptr;  // (before this pass's learning)
+        c->tm.split_mmers = bm ? bm->split : 0u;
     }
     c->tm.table_slots = 1ull << ts_log2;
     c->tm.n_bins = (uint32_t)c->h_totals[2];

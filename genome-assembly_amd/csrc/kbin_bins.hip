@@ -151,10 +151,12 @@ DEV void put_record(const SkScanArgs& A, uint64_t* o, uint32_t ord, uint64_t lo,
     for (int w = 1; w < A.rw; w++) o[w] = window64(sw, (int)lo + 32 * (w - 1));
 }
 
-// destination region of a super-k-mer: its owner rank (routing) or its local
-// bucket (the balanced map when the host has one, else the hash)
-DEV uint32_t region_of(const SkScanArgs& A, uint32_t mmer, uint64_t rec) {
-    return A.bucket_map ? bucket_of(A.bucket_map[mmer - (1u << (2 * A.M - 1))], rec) : dest_of(mmer, A.G, A.dest_salt);
+// destination region of a super-k-mer (piece): its owner rank (routing) or
+// its local bucket (the balanced map when the host has one -- per context
+// sub-bin for a split mmer -- else the hash)
+DEV uint32_t region_of(const SkScanArgs& A, uint32_t mmer, uint32_t sub) {
+    return A.bucket_map ? bm_bucket(A.bucket_map[mmer - (1u << (2 * A.M - 1))], A.sub_map, sub)
+                        : dest_of(mmer, A.G, A.dest_salt);
 }
 
 // Add one record to a packed 16-bit LDS destination count (two per word) and
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
     const uint32_t halfM = 1u << (2 * M - 1);
     const bool one_word = K <= 31 && M <= 12;  // (scores < 2^24 keep 8 bits for the offset)
     const uint32_t tid = threadIdx.x;
-    uint64_t* stg = smem + SKT * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
+    uint64_t* stg = smem + SKT * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, region (routed) or mmer}
     __shared__ uint32_t span_end;
     __shared__ unsigned long long s_base;
     __shared__ uint32_t dcnt2[SK_MAX_DEST / 2];  // per-destination counts, 16 bits each (< SK_STAGE)
@@ -297,20 +299,40 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 }
                 if (WRITE) {
                     const uint64_t rev = bsm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
-                    const uint64_t e = (uint64_t)lo | (n << 16) | ((uint64_t)(sig - lo) << 22) | (rev << 28) |
-                                       ((uint64_t)tid << 29) | ((uint64_t)(uint32_t)best << 38);
-                    const uint64_t loc = alloc ? (uint64_t)atomicAdd(&span_end, 1u) : rbase + nseg - bfirst;
-                    if (loc < SK_STAGE) {
-                        stg[loc] = e;
-                    } else if (rounds) {
-                        break;  // stage full: resume at this record in the next round
-                    } else if (route) {  // many destinations: one record, its own slot
-                        const uint32_t d = region_of(A, (uint32_t)best, (r << 16) | (uint64_t)lo);
-                        const uint64_t i = atomicAdd(&A.dest_ctr[d], 1ull);
-                        if (i < region_room(A.region_base, A.region_cap, d))
-                            put_record(A, A.regions + (region_off(A.region_base, A.region_cap, d) + i) * (uint64_t)A.rw,
-                                       A.ord_base + (uint32_t)r, (uint64_t)lo, n, (uint64_t)(sig - lo), rev, sw);
-                    } else {  // ordered records beyond the staging area: direct (scattered) stores
+                    const int so = sig - lo;
+                    // a split mmer (local buckets): the record goes to its context
+                    // sub-bin, cut in two when its first k-mers lie in the edge
+                    const uint32_t sb = A.bucket_map ? bm_depth(A.bucket_map[(uint32_t)best - halfM]) : 0u;
+                    const int ne = sb ? sub_edge(so, (int)n, K, M, sb) : 0;
+                    const uint32_t np_ = (ne > 0 && ne < (int)n) ? 2u : 1u;
+                    const uint64_t wctx = sb ? window64(sw, sig + M) : 0ull;
+                    const uint64_t loc = alloc ? (uint64_t)atomicAdd(&span_end, np_) : rbase + nseg - bfirst;
+                    if (rounds && loc + np_ > SK_STAGE) {
+                        // stage full: resume at this record in the next round (a
+                        // slot reserved here holds no record: n = 0)
+                        if (loc < SK_STAGE) stg[loc] = 0;
+                        break;
+                    }
+                    for (uint32_t q = 0; q < np_; q++) {
+                        const int cut = q ? ne : 0;
+                        const uint64_t pn = np_ == 2 ? (q ? n - (uint64_t)ne : (uint64_t)ne) : n;
+                        const int plo = lo + cut, pso = so - cut;
+                        const uint32_t psub = sb ? sub_ctx(pso, K, M, sb, wctx, rev != 0) : 0u;
+                        // routed: the destination, computed once (the map
+                        // lookups stay out of the placement loops); else the mmer
+                        const uint32_t d = route ? region_of(A, (uint32_t)best, psub) : 0u;
+                        const uint64_t e = (uint64_t)plo | (pn << 16) | ((uint64_t)pso << 22) | (rev << 28) |
+                                           ((uint64_t)tid << 29) | ((uint64_t)(route ? d : (uint32_t)best) << 38);
+                        if (loc + q < SK_STAGE) {
+                            stg[loc + q] = e;
+                        } else if (route) {  // many destinations: one record, its own slot
+                            const uint64_t i = atomicAdd(&A.dest_ctr[d], 1ull);
+                            if (i < region_room(A.region_base, A.region_cap, d))
+                                put_record(A, A.regions + (region_off(A.region_base, A.region_cap, d) + i) * (uint64_t)A.rw,
+                                           A.ord_base + (uint32_t)r, (uint64_t)plo, pn, (uint64_t)pso, rev, sw);
+                        }
+                    }
+                    if (loc + np_ > SK_STAGE && !route && !alloc) {  // ordered records beyond the staging area: direct (scattered) stores
                         const uint64_t t = rbase + nseg;
                         A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)r) | (n << 32) |
                                            ((uint64_t)(sig - lo) << 38) | (rev << 44) | ((uint64_t)lo << 45);
@@ -336,11 +358,14 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 const bool agg = A.G <= 64;  // ranks, not local buckets: aggregate per wave
                 for (uint32_t i = tid; i < span; i += SKT) {
                     const uint64_t e = stg[i];
-                    const uint32_t d = region_of(A, (uint32_t)(e >> 38), ((r0 + ((e >> 29) & 0x1FFu)) << 16) | (e & 0xFFFFu));
-                    if (agg)
-                        wave_dest_add(dcnt2, d);
-                    else
+                    const bool none = !((e >> 16) & 63u);  // (a slot a full stage left empty)
+                    const uint32_t d = (uint32_t)(e >> 38);  // (the destination)
+                    if (agg) {
+                        if (!__ballot(!none)) continue;  // (wave-uniform)
+                        if (!none) wave_dest_add(dcnt2, d);
+                    } else if (!none) {
                         atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1)));
+                    }
                 }
                 __syncthreads();
                 for (uint32_t d = tid; d < A.G; d += SKT) {
@@ -354,7 +379,8 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 __syncthreads();
                 for (uint32_t i = tid; i < span; i += SKT) {
                     const uint64_t e = stg[i];
-                    const uint32_t d = region_of(A, (uint32_t)(e >> 38), ((r0 + ((e >> 29) & 0x1FFu)) << 16) | (e & 0xFFFFu));
+                    if (!((e >> 16) & 63u)) continue;  // (an empty slot: wave_dest_add lanes below skip it too)
+                    const uint32_t d = (uint32_t)(e >> 38);
                     const uint64_t slot =
                         (uint64_t)dbase[d] +
                         (agg ? wave_dest_add(dcnt2, d)
@@ -606,6 +632,7 @@ struct alignas(16) BinShared {
     uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, part0;
     uint32_t n_single;  // pre-filter: keys seen once in this partition
     uint32_t maxc;      // the partition's longest kept list (the LDS id windows)
+    uint32_t ts;        // LDS table slots of the next partition (<= the carved TS)
     unsigned long long wkey;  // LDS id windows: cursor << 32 | entry << 16 | scan index of the next window's start
     unsigned long long e0, i0, stage_base;
     uint32_t flat_idx, fa, fb, l0;
@@ -617,11 +644,13 @@ static_assert(sizeof(BinShared) % 16 == 0, "LDS carve must stay 16-B aligned (gu
 
 // block-wide exclusive scan of two u32 quantities packed in a u64 (each lane's
 // value < 2^32, totals < 2^32)
-DEV uint64_t block_excl_scan_u64(uint64_t v, uint64_t* red, uint64_t& total) {
+DEV void lds_barrier();
+DEV uint64_t block_excl_scan_u64(uint64_t v, uint64_t* red, uint64_t& total, bool lds_only = false) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t inc = wave_incl_scan(v, lane);
     if (lane == 63) red[wid] = inc;
-    __syncthreads();
+    if (lds_only) lds_barrier();
+    else __syncthreads();
     uint64_t wp = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < BIN_THREADS / 64; w++) {
@@ -629,7 +658,8 @@ DEV uint64_t block_excl_scan_u64(uint64_t v, uint64_t* red, uint64_t& total) {
         if (w < wid) wp += x;
         tot += x;
     }
-    __syncthreads();
+    if (lds_only) lds_barrier();
+    else __syncthreads();
     total = tot;
     return wp + inc - v;
 }
@@ -1072,6 +1102,21 @@ DEV uint32_t sk_cell(const TKey<2>& k, uint32_t cells) {
 }
 constexpr uint64_t M48 = (1ull << 48) - 1ull;
 
+// workgroup barrier ordering LDS accesses only (no wait for outstanding global
+// stores); the memory clobber keeps the compiler from moving memory ops across
+DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// bin_kernel's barriers that order LDS only (table, cursors, windows, shared
+// scalars): __syncthreads also waits for every outstanding global store of the
+// workgroup (the stage, the window's read ids, the entries), so a phase that
+// only needs the LDS would wait out the store latency of the one before.  The
+// barriers that publish global data to other waves stay full: before the id
+// windows read the stage and the entries back, and on an overflow redo (whose
+// stage stores must land before the redo rewrites the same slots)
+DEV void bar_lds(const BinArgs& A) {
+    if (A.ldsbar) lds_barrier();
+    else __syncthreads();
+}
+
 // LDS path of one partition, after its prune: the kept occurrences' ordinals
 // go to an LDS window at their list positions (cursor atomics on cnt), each
 // list is put in reverse call order there (binning.c:1065-1068 prepends:
@@ -1116,7 +1161,7 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
             // windows' cursors have reached their list ends, <= wlo)
             const uint32_t X = wlo + cap;
             if (tid == 0) S.wkey = 0;
-            __syncthreads();
+            bar_lds(A);
             unsigned long long best = 0;
             uint32_t e = e_mine;
             for (uint32_t k = 0; k < per; k++) {
@@ -1126,7 +1171,7 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
                 e++;
             }
             if (best) atomicMax(&S.wkey, best);
-            __syncthreads();
+            bar_lds(A);
             const unsigned long long w = S.wkey;
             whi = (uint32_t)(w >> 32);
             ehi = (uint32_t)(w >> 16) & 0xFFFFu;
@@ -1151,7 +1196,7 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
                 if (pos < PRUNED) wv[pos - wlo] = (uint32_t)v[u] + 1u;  // ordinal + 1 (0 pads the sorts)
             }
         }
-        __syncthreads();
+        bar_lds(A);
         PROF_MARK(4);
         // ---- every list in place: a wave takes 64 entries at a time
         for (uint32_t eb = elo + (tid & ~63u); eb < ehi; eb += BIN_THREADS) {
@@ -1182,7 +1227,7 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
                 wave_sync();
             }
         }
-        __syncthreads();
+        bar_lds(A);
         PROF_MARK(5);
         // ---- the window as read ids, 16-B stores where aligned
         const uint32_t nw = whi - wlo;
@@ -1197,7 +1242,7 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
         }
         for (uint32_t j = head + 4u * body + tid; j < nw; j += BIN_THREADS)
             A.ids_out[g0 + j] = id_of(wv[j] - 1u, A.read_ids, A.id_off);
-        __syncthreads();  // (the window is the next window's, then the next partition's table)
+        bar_lds(A);  // (the window is the next window's, then the next partition's table)
         PROF_MARK(6);
         wlo = whi;
         elo = ehi;
@@ -1210,7 +1255,7 @@ DEV void bin_body(const BinArgs& A) {
     constexpr uint32_t Q = bin_q<KW>();
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     BinShared& S = *reinterpret_cast<BinShared*>(smem);      // all LDS in one dynamic array
-    const uint32_t TS = 1u << A.ts_log2, bmask = TS / 4 - 1;  // buckets of four slots
+    const uint32_t TS = 1u << A.ts_log2;  // the carved table (buckets of four slots; a partition may use less)
     BinTable<KW> T;
     // cnt | claim words | low words | rings: after the prune everything past
     // cnt is dead, and the LDS path's id window takes it (win_cap ids)
@@ -1227,7 +1272,6 @@ DEV void bin_body(const BinArgs& A) {
     uint32_t* qo = reinterpret_cast<uint32_t*>(ring0 + KW * BIN_WAVES * Q) + wq;
     uint16_t* qp = reinterpret_cast<uint16_t*>(reinterpret_cast<uint32_t*>(ring0 + KW * BIN_WAVES * Q) +
                                                BIN_WAVES * Q) + wq;
-    const uint32_t limit = TS - TS / 4;
     const uint64_t nbins = min(A.totals[2], A.max_bins);
     const uint32_t tid = threadIdx.x;
 #ifdef KB_BIN_PROF
@@ -1245,7 +1289,7 @@ DEV void bin_body(const BinArgs& A) {
         // first.  Phase 1: the partitions of the heavy bins phase 0 turned into
         // flat lists, any block any partition (a giant bin is no longer one
         // workgroup's serial loop)
-        __syncthreads();
+        bar_lds(A);
         if (tid == 0) {
             if (PHASE == 0) {
                 S.item = (uint32_t)min(next_item, 0xFFFFFFFFull);
@@ -1266,7 +1310,7 @@ DEV void bin_body(const BinArgs& A) {
                 }
             }
         }
-        __syncthreads();
+        bar_lds(A);
         if (PHASE == 0 ? S.item >= nbins : S.item == 0xFFFFFFFFu) break;  // uniform
         if (PHASE == 1) {  // one flat partition of bin S.item
             const uint32_t b = S.item;
@@ -1276,7 +1320,7 @@ DEV void bin_body(const BinArgs& A) {
                 S.fa = A.flat_off[A.flat_obase[b] + S.part0];
                 S.fb = A.flat_off[A.flat_obase[b] + S.part0 + 1];
             }
-            __syncthreads();
+            bar_lds(A);
         }
         // phase 0 with descriptors (bucketed path): one 32-B load per bin --
         // bin, records, mmer, occurrences and stage base, in processing order
@@ -1291,14 +1335,14 @@ DEV void bin_body(const BinArgs& A) {
         const uint32_t b = have_desc ? d0.x : PHASE == 0 ? A.order[S.item] : S.item;
         const uint32_t lo = have_desc ? d0.y : A.bstart[b];
         const uint32_t hi = lo + (have_desc ? d0.z : A.bcount[b]);
-        const uint32_t mmer = have_desc ? d0.w : A.bmmer[b];
+        const uint32_t mmer = (have_desc ? d0.w : A.bmmer[b]) & 0xFFFFu;  // (a context sub-bin's index rides above)
 
         // occurrences of the bin -> first partition depth
         uint64_t occ_tot = 0;
         if (PHASE == 0 && have_desc && d1.x) {  // (0: a spread run's bin, counted below)
             occ_tot = d1.x;
             if (tid == 0) S.stage_base = (uint64_t)d1.y | ((uint64_t)d1.z << 32);
-            __syncthreads();
+            bar_lds(A);
         } else if (PHASE == 0) {
             // the bucket ordering counted them (its length rows), else a pass
             // over the record headers
@@ -1311,7 +1355,7 @@ DEV void bin_body(const BinArgs& A) {
             }
             // the bin's stage range (one slot per occurrence, reused per partition)
             if (tid == 0) S.stage_base = atomicAdd(A.stage_ctr, (unsigned long long)occ_tot);
-            __syncthreads();
+            bar_lds(A);
         }
         uint64_t* stage = A.stage + S.stage_base;  // (flat: moved to each partition's list)
         PROF_CNT(11, PHASE == 0);
@@ -1437,6 +1481,16 @@ DEV void bin_body(const BinArgs& A) {
             if (l1 <= A.opart && l1 > l0) l0 = l1;
         }
         const bool omode = (PHASE == 0 && !flat && !split && l0 >= 1 && l0 <= A.opart) || (PHASE == 1 && osplit);
+        // a light bin that fits one table takes the smallest table its keys
+        // fill to the light load (context sub-bins and small mmers: less to
+        // clear and to scan in the prune); one that overflows it retries on a
+        // table four times larger before it splits
+        uint32_t tsb = TS;
+        if (PHASE == 0 && A.ts_adapt && !flat && !split && l0 == 0) {
+            const double keys = (double)occ_tot * A.rho;
+            tsb = (uint32_t)BIN_THREADS;
+            while (tsb < TS && keys > (double)A.fill_light * tsb) tsb <<= 1;
+        }
         const uint32_t p_lo = PHASE == 0 ? 0u : S.part0, p_hi = PHASE == 0 ? (1u << l0) : S.part0 + 1u;
         for (uint32_t p0 = p_lo; p0 < p_hi; p0++) {
         const uint32_t olo = omode ? A.ocut[l0][p0] : 0u, ohi = omode ? A.ocut[l0][p0 + 1] : 64u;
@@ -1444,12 +1498,14 @@ DEV void bin_body(const BinArgs& A) {
             S.sp = 1;
             S.stack_p[0] = omode ? 0u : p0;
             S.stack_l[0] = omode ? 0u : l0;
+            S.ts = tsb;
         }
-        __syncthreads();
+        bar_lds(A);
         // flat: this partition's list is [fa, fb) of the bin's stage range
         const uint32_t fa = flat || split ? S.fa : 0u, fb = flat ? S.fb : 0u;
         stage = A.stage + S.stage_base + fa;
         while (true) {
+            const uint32_t ts = S.ts, bmask = ts / 4 - 1, limit = ts - ts / 4;  // (uniform)
             if (tid == 0) {
                 if (S.sp == 0) {
                     S.cur_l = 0xFFFFFFFFu;
@@ -1464,7 +1520,7 @@ DEV void bin_body(const BinArgs& A) {
                 S.n_single = 0;
                 S.maxc = 0;
             }
-            for (uint32_t i = tid; i < TS; i += BIN_THREADS) {
+            for (uint32_t i = tid; i < ts; i += BIN_THREADS) {
                 T.ca[i] = 0;
                 if constexpr (KW == 2) T.cb[i] = 0;
                 cnt[i] = 0;
@@ -1472,7 +1528,7 @@ DEV void bin_body(const BinArgs& A) {
             uint32_t* const sk = reinterpret_cast<uint32_t*>(ring0);  // (flat partitions use no rings)
             if (PHASE == 1 && pfb)
                 for (uint32_t i = tid; i < sk_words; i += BIN_THREADS) sk[i] = 0;
-            __syncthreads();
+            bar_lds(A);
             PROF_MARK(1);
             const uint32_t P = S.cur_p, Lv = S.cur_l;
             if (Lv == 0xFFFFFFFFu) break;  // uniform
@@ -1656,14 +1712,19 @@ DEV void bin_body(const BinArgs& A) {
                 if (singles && lane == 0) atomicAdd(&S.n_single, singles);
                 if (tid == 0) S.n_stage = nf;
             }
-            __syncthreads();
+            bar_lds(A);
             PROF_MARK(2);
             if (S.overflow || S.n_keys > limit) {  // uniform: split this partition in two and redo both
                 PROF_CNT(9, 1);
                 PROF_CNT(10, omode ? 1000000u + (ohi - olo) * 1000u + Lv : 0u);  // (diagnostic: offset-range overflows)
                 if (tid == 0) {
                     if (A.pstat) atomicAdd(&A.pstat[3], 1ull);
-                    if (Lv >= 20 || S.sp + 2 > BIN_STACK) {
+                    if (ts < TS) {  // a larger table first
+                        S.ts = min(TS, ts << 2);
+                        S.stack_p[S.sp] = P;
+                        S.stack_l[S.sp] = Lv;
+                        S.sp++;
+                    } else if (Lv >= 20 || S.sp + 2 > BIN_STACK) {
                         atomicOr(A.status, ST_PROBE_LIMIT);
                     } else {
                         S.stack_p[S.sp] = P;
@@ -1680,14 +1741,14 @@ DEV void bin_body(const BinArgs& A) {
             // slots t, t + 1024, ...: a wave's reads of the table are consecutive
             // words (owning 8 adjacent slots put 16 lanes on one LDS bank)
             uint64_t mine = 0;  // (ids << 32) | entries over this thread's slots
-            const uint32_t per = TS / BIN_THREADS;  // TS >= BIN_THREADS
+            const uint32_t per = ts / BIN_THREADS;  // ts >= BIN_THREADS
             for (uint32_t k = 0; k < per; k++) {
                 const uint32_t i = tid + k * BIN_THREADS;
                 const uint32_t c = cnt[i];
                 if (T.ca[i] && c > A.keep_gt) mine += ((uint64_t)c << 32) + 1ull;
             }
             uint64_t tot;
-            uint64_t ex = block_excl_scan_u64(mine, S.red, tot);
+            uint64_t ex = block_excl_scan_u64(mine, S.red, tot, A.ldsbar != 0);
             if (tid == 0) {
                 const uint32_t ne = (uint32_t)tot, ni = (uint32_t)(tot >> 32);
                 atomicAdd(&A.gcount[2], (unsigned long long)(S.n_keys + S.n_single));  // distinct before prune
@@ -1708,7 +1769,7 @@ DEV void bin_body(const BinArgs& A) {
                 S.i0 = got & 0xFFFFFFFFull;
                 if (S.e0 + ne > A.max_entries || S.i0 + ni > A.max_ids) atomicOr(A.status, ST_TABLE_FULL);
             }
-            __syncthreads();
+            bar_lds(A);
             const unsigned long long e0 = S.e0, i0 = S.i0;
             const bool room = !(e0 + (uint32_t)tot > A.max_entries || i0 + (uint32_t)(tot >> 32) > A.max_ids);
             uint32_t mc = 0;  // (the longest kept list: the LDS windows hold whole lists)
@@ -1753,7 +1814,7 @@ DEV void bin_body(const BinArgs& A) {
             // and two-word keys (C5: 624 -> 641 ms) keep the global path
             const bool win_phase = PHASE == 0 || (KW == 1 && A.win_heavy && !(flat && Lv > l0));
             if (win_phase && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
-                lds_lists<KW>(A, S, cnt, TS, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage,
+                lds_lists<KW>(A, S, cnt, ts, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage,
                               (uint32_t)ex PROF_ARGS);
                 PROF_MARK(4);
                 continue;
@@ -1817,7 +1878,7 @@ DEV void bin_body(const BinArgs& A) {
             }
         }
 #endif
-        __syncthreads();
+        bar_lds(A);
     }
 #ifdef KB_BIN_PROF
     if (tid == 0)
@@ -2238,10 +2299,6 @@ void bins_prof_report(hipStream_t s) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bin_prof), z, sizeof(z));
 }
 #endif
-
-// workgroup barrier ordering LDS accesses only (no wait for outstanding global
-// stores); the memory clobber keeps the compiler from moving memory ops across
-DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---------------------------------------------------------------------------
 // phase C: every list into reverse call order (binning.c:1061-1068 prepends,
@@ -2968,17 +3025,37 @@ DEV uint32_t order_class(uint32_t c) {
 constexpr int HLL_LOG2 = 12;
 constexpr int HLL_THREADS = 256;
 
+// Sampled (sample > 1): only the records of the canonical mmers with
+// dest_of(mmer, sample, HLL_SALT) == 0 -- whole bins, since keys of different
+// mmers never coincide, so distinct / occurrences of the sample estimates the
+// whole ratio -- at 1 / sample of the expansion work; occ_out counts the
+// sample's occurrences.
+constexpr uint64_t HLL_SALT = 0xD1B54A32D192ED03ull;
+
 template <int KW>
-__global__ __launch_bounds__(HLL_THREADS) void hll_kernel(BinArgs A, uint64_t R, uint32_t* __restrict__ regs) {
+__global__ __launch_bounds__(HLL_THREADS) void hll_kernel(BinArgs A, uint64_t R, uint32_t* __restrict__ regs,
+                                                          uint32_t sample, unsigned long long* occ_out) {
     __shared__ uint32_t reg[1 << HLL_LOG2];
+    __shared__ unsigned long long s_occ;
     for (int i = threadIdx.x; i < (1 << HLL_LOG2); i += HLL_THREADS) reg[i] = 0;
+    if (threadIdx.x == 0) s_occ = 0;
     __syncthreads();
+    const int M = A.M;
+    const uint32_t maskM = (1u << (2 * M)) - 1u;
+    uint64_t occ = 0;
     for (uint64_t r = (uint64_t)blockIdx.x * HLL_THREADS + threadIdx.x; r < R; r += (uint64_t)gridDim.x * HLL_THREADS) {
         const uint64_t hd = A.hdr[r];
         const int n = (int)((hd >> 32) & 63u);
         const uint64_t fl = 0ull - ((hd >> 44) & 1ull);
         Span<KW> sp;
         sp.load(A, (uint32_t)r);
+        if (sample > 1) {
+            const int so = (int)((hd >> 38) & 63u);
+            const uint32_t sm = (uint32_t)(span_window(A.w0[r], A.w1[r], 0ull, 0ull, so) >> (64 - 2 * M));
+            const uint32_t canon = ((hd >> 44) & 1u) ? maskM - sm : sm;
+            if (dest_of(canon, sample, HLL_SALT) != 0) continue;
+        }
+        occ += (uint64_t)n;
         for (int j = 0; j < n; j++) {
             uint64_t hi, lo;
             sp.key(A.K, fl).code(hi, lo);
@@ -2989,13 +3066,16 @@ __global__ __launch_bounds__(HLL_THREADS) void hll_kernel(BinArgs A, uint64_t R,
             atomicMax(&reg[ix], rank);
         }
     }
+    if (occ) atomicAdd(&s_occ, (unsigned long long)occ);
     __syncthreads();
     for (int i = threadIdx.x; i < (1 << HLL_LOG2); i += HLL_THREADS)
         if (reg[i]) atomicMax(&regs[i], reg[i]);
+    if (threadIdx.x == 0 && s_occ) atomicAdd(occ_out, s_occ);
 }
 
-hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(regs, 0, sizeof(uint32_t) << HLL_LOG2, s);
+// regs: 2^12 registers followed by a u64 occurrence count (zeroed here)
+hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, uint32_t sample, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(regs, 0, (sizeof(uint32_t) << HLL_LOG2) + sizeof(uint64_t), s);
     if (e != hipSuccess || !R) return e;
     int dev = 0, cus = 0;
     e = hipGetDevice(&dev);
@@ -3003,8 +3083,9 @@ hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, hipS
     if (e != hipSuccess) return e;
     const uint64_t want = (R + HLL_THREADS - 1) / HLL_THREADS;
     const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)std::max(1, cus) * 8));
-    if (KW == 1) hipLaunchKernelGGL(hll_kernel<1>, dim3(blocks), dim3(HLL_THREADS), 0, s, a, R, regs);
-    else hipLaunchKernelGGL(hll_kernel<2>, dim3(blocks), dim3(HLL_THREADS), 0, s, a, R, regs);
+    unsigned long long* occ = reinterpret_cast<unsigned long long*>(regs + (1 << HLL_LOG2));
+    if (KW == 1) hipLaunchKernelGGL(hll_kernel<1>, dim3(blocks), dim3(HLL_THREADS), 0, s, a, R, regs, sample, occ);
+    else hipLaunchKernelGGL(hll_kernel<2>, dim3(blocks), dim3(HLL_THREADS), 0, s, a, R, regs, sample, occ);
     return hipGetLastError();
 }
 
@@ -3127,9 +3208,10 @@ hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, co
 constexpr int BK_THREADS = 512;
 constexpr uint32_t BK_SLOTS = 256;  // mmers per bucket (a bucket with more is reported)
 
-DEV int bk_slot(uint32_t* keys, uint32_t mmer, bool insert) {
-    const uint32_t k = mmer + 1u;
-    uint32_t i = (uint32_t)((mix64((uint64_t)mmer) >> 32) & (BK_SLOTS - 1));
+// a bucket's bins: key (mmer << SUB_BITS | context sub-bin) + 1 in an LDS table
+DEV int bk_slot(uint32_t* keys, uint32_t bkey, bool insert) {
+    const uint32_t k = bkey + 1u;
+    uint32_t i = (uint32_t)((mix64((uint64_t)bkey) >> 32) & (BK_SLOTS - 1));
     for (uint32_t p = 0; p < BK_SLOTS; p++) {
         const uint32_t v = keys[i];
         if (v == k) return (int)i;
@@ -3144,13 +3226,23 @@ DEV int bk_slot(uint32_t* keys, uint32_t mmer, bool insert) {
 }
 
 // ROWS = k-mers per record rounded up to a power of two: n <= K - M + 1
-// (<= 31 for K <= 31, <= 57 for K <= 63); row ROWS - n puts longest first
+// (<= 31 for K <= 31, <= 57 for K <= 63); row ROWS - n puts longest first.
+// The bin key: canonical mmer << SUB_BITS | the piece's context sub-bin (0
+// unless the map splits the mmer; the record pass cut every piece to one side)
 template <int ROWS>
-DEV void bk_decode(uint64_t h, uint64_t a, uint64_t b, int M, uint32_t& canon, uint32_t& row) {
+DEV void bk_decode(uint64_t h, uint64_t a, uint64_t b, const BucketArgs& A, uint32_t& bkey, uint32_t& row) {
+    const int M = A.M;
     const uint32_t maskM = (1u << (2 * M)) - 1u;
     const int so = (int)((h >> 38) & 63u);
     const uint32_t sm = (uint32_t)(span_window(a, b, 0ull, 0ull, so) >> (64 - 2 * M));
-    canon = ((h >> 44) & 1u) ? maskM - sm : sm;
+    const bool rev = ((h >> 44) & 1u) != 0;
+    const uint32_t canon = rev ? maskM - sm : sm;
+    uint32_t sub = 0;
+    if (A.bucket_map) {
+        const uint32_t sb = bm_depth(A.bucket_map[canon - (1u << (2 * M - 1))]);
+        if (sb) sub = sub_ctx(so, A.K, M, sb, span_window(a, b, 0ull, 0ull, so + M), rev);
+    }
+    bkey = (canon << SUB_BITS) | sub;
     row = (uint32_t)ROWS - (uint32_t)((h >> 32) & 63u);
 }
 
@@ -3190,9 +3282,9 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (i0 + (uint64_t)u * BK_THREADS >= cnt) break;
-            uint32_t canon, row;
-            bk_decode<ROWS>(h[u], a[u], b[u], A.M, canon, row);
-            const int sl = bk_slot(keys, canon, true);
+            uint32_t bkey, row;
+            bk_decode<ROWS>(h[u], a[u], b[u], A, bkey, row);
+            const int sl = bk_slot(keys, bkey, true);
             if (sl < 0) s_full = 1;
             else atomicAdd(&hist[sl * ROWS + row], 1u);
         }
@@ -3224,7 +3316,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     uint64_t wp = 0;
     for (int w = 0; w < wid; w++) wp += red[w];
     uint32_t run = (uint32_t)(wp + inc - mine);
-    if (tid == 0) s_base = A.bbase[bk];  // exclusive prefix of the fills: a spread run is contiguous
+    if (tid == 0) s_base = A.bbase[bk];  // exclusive prefix of the fills
 #pragma unroll
     for (uint32_t k = 0; k < PER; k++) {
         const uint32_t c = loc[k];
@@ -3232,23 +3324,9 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
         run += c;
     }
     __syncthreads();
-    // count non-empty slots, reserve bin descriptors.  A spread mmer's run of
-    // buckets (that mmer only) gets one descriptor, from its first bucket --
-    // which may itself have drawn no record
-    const uint16_t brun = A.brun ? A.brun[bk] : (uint16_t)0;
-    if (brun != 0 && brun != BK_RUN_CONT && tid == 0) {
-        const uint64_t n = A.bbase[bk + brun] - A.bbase[bk];
-        if (n) {
-            const unsigned long long bi = atomicAdd(A.bin_ctr, 1ull);
-            if (bi < A.max_bins) {
-                A.bstart[bi] = (uint32_t)A.bbase[bk];
-                A.bcount[bi] = (uint32_t)n;
-                A.bmmer[bi] = A.brun_mmer[bk];
-                if (A.bocc) A.bocc[bi] = 0;  // (its buckets' counts are not summed: bin_kernel counts)
-            }
-        }
-    }
-    const bool has = brun == 0 && tid < BK_SLOTS && keys[tid] != 0;
+    // count non-empty slots, reserve bin descriptors (one per bin key: an
+    // mmer, or one context sub-bin of a split mmer)
+    const bool has = tid < BK_SLOTS && keys[tid] != 0;
     if (has) atomicAdd(&s_nb, 1u);
     __syncthreads();
     if (tid == 0) s_bin = s_nb ? atomicAdd(A.bin_ctr, (unsigned long long)s_nb) : 0ull;
@@ -3263,7 +3341,9 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
         if (bi < A.max_bins) {
             A.bstart[bi] = (uint32_t)s_base + first;
             A.bcount[bi] = last - first;
-            A.bmmer[bi] = keys[tid] - 1u;
+            // the mmer, and its context sub-bin above bit 16 (bin_kernel masks
+            // it off; the host learns each sub-bin's records from it)
+            A.bmmer[bi] = ((keys[tid] - 1u) >> SUB_BITS) | (((keys[tid] - 1u) & ((1u << SUB_BITS) - 1u)) << 16);
             if (A.bocc) A.bocc[bi] = socc[tid];
         }
     }
@@ -3287,9 +3367,9 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (i0 + (uint64_t)u * BK_THREADS >= cnt) break;
-            uint32_t canon, row;
-            bk_decode<ROWS>(h[u], a[u], b[u], A.M, canon, row);
-            const int sl = bk_slot(keys, canon, false);
+            uint32_t bkey, row;
+            bk_decode<ROWS>(h[u], a[u], b[u], A, bkey, row);
+            const int sl = bk_slot(keys, bkey, false);
             const uint64_t pos = base + atomicAdd(&hist[sl * ROWS + row], 1u);
             A.hdr[pos] = h[u];
             A.w0[pos] = a[u];
@@ -3335,11 +3415,14 @@ hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s) {
 }
 
 // received routed records -> local bucket regions (pay layout, ordinal = id,
-// 1 + spw words); a block reserves one range per bucket for its 256 x 8 records
+// 1 + spw words); a block reserves one range per bucket for its 256 x 8
+// records.  A split mmer's record goes to its context sub-bin's bucket, cut in
+// two (edge piece first) when its first k-mers lie in the edge.
 template <int SPW>
 __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t* __restrict__ recs, uint64_t n_rec,
-                                                                 int rw, int M, uint32_t NB,
-                                                                 const uint16_t* __restrict__ bucket_map,
+                                                                 int rw, int M, uint32_t NB, int K,
+                                                                 const uint32_t* __restrict__ bucket_map,
+                                                                 const uint16_t* __restrict__ sub_map,
                                                                  uint64_t* __restrict__ regions, uint64_t cap,
                                                                  const uint64_t* __restrict__ rbase,
                                                                  unsigned long long* bfill, uint32_t* status,
@@ -3353,12 +3436,15 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
     for (uint64_t k0 = (uint64_t)blockIdx.x * 256 * PERT; k0 < n_rec; k0 += (uint64_t)gridDim.x * 256 * PERT) {
         for (uint32_t d = threadIdx.x; d < NB; d += 256) cnt[d] = 0;
         __syncthreads();
-        uint32_t dst[PERT];
+        // per record: the destination of its (last) piece, and of its edge
+        // piece when it is cut (ne > 0 k-mers)
+        uint32_t dst[PERT], dst2[PERT], ne[PERT];
         uint64_t pay0[PERT], ps[PERT][SPW];
 #pragma unroll
         for (int j = 0; j < PERT; j++) {
             const uint64_t k = k0 + (uint64_t)j * 256 + threadIdx.x;
             dst[j] = 0xFFFFFFFFu;
+            ne[j] = 0;
             if (k >= n_rec) continue;
             const uint64_t* r = recs + k * (uint64_t)rw;
             const uint64_t h = r[0];
@@ -3373,8 +3459,27 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
             neg |= (int32_t)id < 0;
             kmers += n;
             pay0[j] = (uint64_t)id | (n << 32) | (so << 38) | ((uint64_t)rev << 44) | (lo << 45);
-            dst[j] = bucket_map ? bucket_of(bucket_map[canon - halfM], ((uint64_t)id << 16) | lo)
-                                : dest_of(canon, NB, BUCKET_SALT);
+            if (bucket_map) {
+                const uint32_t me = bucket_map[canon - halfM];
+                const uint32_t b = bm_depth(me);
+                uint32_t sub = 0;
+                if (b) {
+                    const int e = sub_edge((int)so, (int)n, K, M, b);
+                    // the context at so + M: past the first two span words
+                    // when a long (K > 31) record's first k-mers are its edge
+                    const uint64_t wc = span_window(ps[j][0], ps[j][1], SPW > 2 ? ps[j][SPW > 2 ? 2 : 0] : 0ull,
+                                                    SPW > 3 ? ps[j][SPW > 3 ? 3 : 0] : 0ull, (int)so + M);
+                    if (e > 0 && e < (int)n) {
+                        ne[j] = (uint32_t)e;
+                        dst2[j] = bm_bucket(me, sub_map, 0u);
+                        atomicAdd(&cnt[dst2[j]], 1u);
+                    }
+                    sub = sub_ctx((int)so - (int)ne[j], K, M, b, wc, rev);
+                }
+                dst[j] = bm_bucket(me, sub_map, sub);
+            } else {
+                dst[j] = dest_of(canon, NB, BUCKET_SALT);
+            }
             atomicAdd(&cnt[dst[j]], 1u);
         }
         __syncthreads();
@@ -3386,12 +3491,31 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
 #pragma unroll
         for (int j = 0; j < PERT; j++) {
             if (dst[j] == 0xFFFFFFFFu) continue;
+            const uint64_t h = pay0[j];
+            if (ne[j]) {  // the edge piece: the record's first ne k-mers, same span start
+                const uint64_t slot = base[dst2[j]] + atomicAdd(&cnt[dst2[j]], 1u);
+                if (slot < region_room(rbase, cap, dst2[j])) {
+                    uint64_t* o = regions + (region_off(rbase, cap, dst2[j]) + slot) * (1 + SPW);
+                    o[0] = (h & ~(63ull << 32)) | ((uint64_t)ne[j] << 32);
+#pragma unroll
+                    for (int w = 0; w < SPW; w++) o[1 + w] = ps[j][w];
+                }
+            }
             const uint64_t slot = base[dst[j]] + atomicAdd(&cnt[dst[j]], 1u);
             if (slot >= region_room(rbase, cap, dst[j])) continue;  // counted: the caller retries bigger
             uint64_t* o = regions + (region_off(rbase, cap, dst[j]) + slot) * (1 + SPW);
-            o[0] = pay0[j];
+            if (ne[j]) {  // the rest: k-mers ne.., span from base ne, signature ne closer
+                const uint64_t c = ne[j];
+                const uint64_t n = (h >> 32) & 63u, so = (h >> 38) & 63u, lo = (h >> 45) & 0xFFFFu;
+                o[0] = (h & 0xFFFFFFFFull) | ((n - c) << 32) | ((so - c) << 38) | (h & (1ull << 44)) | ((lo + c) << 45);
+                uint64_t sw[4] = {ps[j][0], ps[j][1], SPW > 2 ? ps[j][SPW > 2 ? 2 : 0] : 0ull, SPW > 3 ? ps[j][SPW > 3 ? 3 : 0] : 0ull};
 #pragma unroll
-            for (int w = 0; w < SPW; w++) o[1 + w] = ps[j][w];
+                for (int w = 0; w < SPW; w++) o[1 + w] = span_window(sw[0], sw[1], sw[2], sw[3], (int)c + 32 * w);
+            } else {
+                o[0] = h;
+#pragma unroll
+                for (int w = 0; w < SPW; w++) o[1 + w] = ps[j][w];
+            }
         }
         __syncthreads();
     }
@@ -3402,18 +3526,18 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
 }
 
 hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
-                                     const uint16_t* bucket_map, uint64_t* regions, uint64_t cap, const uint64_t* rbase,
-                                     unsigned long long* bfill,
+                                     int K, const uint32_t* bucket_map, const uint16_t* sub_map, uint64_t* regions,
+                                     uint64_t cap, const uint64_t* rbase, unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s) {
     if (!n_rec) return hipSuccess;
     if (NB < 1 || NB > SK_MAX_DEST || (spw != 2 && spw != 4)) return hipErrorInvalidValue;
     const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
     if (spw == 2)
         hipLaunchKernelGGL(sk_convert_buckets_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, bucket_map, regions, cap, rbase, bfill, status, n_kmers);
+                           NB, K, bucket_map, sub_map, regions, cap, rbase, bfill, status, n_kmers);
     else
         hipLaunchKernelGGL(sk_convert_buckets_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, bucket_map, regions, cap, rbase, bfill, status, n_kmers);
+                           NB, K, bucket_map, sub_map, regions, cap, rbase, bfill, status, n_kmers);
     return hipGetLastError();
 }
 

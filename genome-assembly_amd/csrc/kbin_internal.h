@@ -109,9 +109,12 @@ struct SkScanArgs {
     uint64_t dest_salt;
     int rw;
     int binned_fmt;
-    // local buckets only: canonical mmer - 2^(2M-1) -> bucket, balanced by the
-    // host from the bins of earlier passes (null: hash of the mmer)
-    const uint16_t* bucket_map;
+    // local buckets only: canonical mmer - 2^(2M-1) -> bucket map entry
+    // (bm_* below), balanced by the host from the bins of earlier passes (null:
+    // hash of the mmer); a split mmer's records are cut into their context
+    // sub-bins (at most two pieces each) on the way into the buckets
+    const uint32_t* bucket_map;
+    const uint16_t* sub_map;
     // partitioned passes (kb_set_partition): only super-k-mers whose mmer is in
     // partition part of part_n are emitted and counted (part_n <= 1: all)
     uint32_t part, part_n;
@@ -132,18 +135,17 @@ struct BucketArgs {
     uint64_t* w3;
     int spw;                   // span words per record: 2 (K <= 31) or 4 (K <= 63)
     uint64_t* bbase;           // [NB + 1] output base of each bucket (bucket_bases_kernel)
-    const uint16_t* brun;      // [NB] or null: spread runs (BK_RUN_CONT, or the run length at its head)
-    const uint32_t* brun_mmer; // [NB] the canonical mmer of a run's head bucket
+    const uint32_t* bucket_map;  // or null: the map the record pass used (a split mmer's
+                                 // records are grouped by (mmer, context sub-bin))
+    int K;
     uint32_t* bocc;            // [max_bins] k-mer occurrences of the bin (0: not counted), or null
     unsigned long long* bin_ctr;   // bins (zeroed; = totals[2])
     uint32_t* bstart;          // [max_bins] first record of bin
     uint32_t* bcount;          // [max_bins] records of bin
     uint32_t* bmmer;           // [max_bins] the bin's canonical mmer
     uint64_t max_bins;
-    uint32_t* status;          // ST_BUCKET_FULL: a bucket holds too many mmers
+    uint32_t* status;          // ST_BUCKET_FULL: a bucket holds too many bins
 };
-
-constexpr uint16_t BK_RUN_CONT = 0xFFFF;  // brun: a spread mmer's bucket after the first
 
 // region d of a record region set: fixed stride cap, or exact bases
 __device__ __forceinline__ uint64_t region_off(const uint64_t* base, uint64_t cap, uint32_t d) {
@@ -153,13 +155,46 @@ __device__ __forceinline__ uint64_t region_room(const uint64_t* base, uint64_t c
     return base ? base[d + 1] - base[d] : cap;
 }
 
-// Bucket map entry (u16 per canonical mmer): the bucket, or for a large mmer
-// spread over a run of k >= 2 consecutive buckets (each holding only it),
-// first | k << 10; the record picks one by a hash of (read, first k-mer).
-__device__ __forceinline__ uint32_t bucket_of(uint16_t m, uint64_t rec) {
-    const uint32_t k = m >> 10, first = m & 1023u;
-    if (k < 2) return first;
-    return first + (uint32_t)(((rec * 0x9E3779B97F4A7C15ull) >> 32) % k);
+// ---- context sub-bins.  The reference's level-1 key is the signature mmer
+// (binning.c:1045) and every (mmer, kmer) entry lives in one mmer bin, but a
+// bin can hold far more distinct keys than one LDS table (few mmers per rank
+// at N GPUs, high coverage).  A finer partition of a bin that is a function of
+// the KEY and constant along a super-k-mer: for the k-mer starting o bases
+// before its signature (o = sig - i; o is the first occurrence of the
+// canonical mmer string in the key's k-mer, bin_body), the b bases right
+// after the mmer lie inside the k-mer whenever o <= K - M - b, and they are
+// the read's bases sig + M .. sig + M + b - 1 for every k-mer of the record
+// (complemented with it, binning.c:1029-1040).  So sub-bin 1 + ctx holds the
+// keys with o <= K - M - b and context ctx (4^b of them), sub-bin 0 (the
+// "edge") the keys with o > K - M - b: a record is at most cut in two, its
+// first so - (K - M - b) k-mers into the edge.  (Measured on uniform reads at
+// K31 M7: b = 2 leaves 1.2 % of the occurrences in the edge and cuts 9.5 % of
+// the records; the 16 context sub-bins hold 0.76..1.10 x their mean.)
+constexpr uint32_t SUB_MAX_B = 4;                      // 257 sub-bins at most
+constexpr uint32_t SUB_BITS = 9;                       // sub-bin index bits
+__host__ __device__ inline uint32_t sub_count(uint32_t b) { return b ? (1u << (2 * b)) + 1u : 1u; }
+
+// Bucket map entry (u32 per canonical mmer - 2^(2M-1)):
+//   bit 31 clear: the mmer's one bin lives in bucket (entry & 1023)
+//   bit 31 set:   the mmer is split into sub_count(b) context sub-bins,
+//                 b = (entry >> 28) & 7 in 1..SUB_MAX_B; sub-bin s lives in
+//                 bucket sub_map[(entry & 0x0FFFFFFF) + s]
+constexpr uint32_t BM_SPLIT = 0x80000000u;
+__device__ __forceinline__ uint32_t bm_depth(uint32_t e) { return (e & BM_SPLIT) ? (e >> 28) & 7u : 0u; }
+__device__ __forceinline__ uint32_t bm_bucket(uint32_t e, const uint16_t* sub_map, uint32_t sub) {
+    return (e & BM_SPLIT) ? (uint32_t)sub_map[(e & 0x0FFFFFFFu) + sub] : (e & 1023u);
+}
+// k-mers of a record (sig offset so, n k-mers) in the edge of depth b: its first ones
+__device__ __forceinline__ int sub_edge(int so, int n, int K, int M, uint32_t b) {
+    const int e = so - (K - M - (int)b);
+    return e <= 0 ? 0 : (e < n ? e : n);
+}
+// sub-bin of a piece whose k-mers all lie on one side: w = 64-bit window of
+// the read (or span) at the signature + M, rev = the complement won
+__device__ __forceinline__ uint32_t sub_ctx(int so, int K, int M, uint32_t b, uint64_t w, bool rev) {
+    if (!b || so > K - M - (int)b) return 0u;
+    const uint32_t m = (1u << (2 * b)) - 1u;
+    return 1u + (((uint32_t)(w >> (64 - 2 * b)) ^ (rev ? m : 0u)) & m);
 }
 
 constexpr uint32_t KB_FLAT_MAX = 16384;  // partitions of one heavy bin's flat lists (kbin_bins.hip FLAT_MAX)
@@ -261,6 +296,8 @@ struct BinArgs {
     // [4] deepest partition depth (max) [5] keys kept out by the pre-filter
     // [6] offset-range partitions [7] partitions swept from flat lists
     unsigned long long* pstat;
+    uint32_t ts_adapt;         // 1: one-table light bins take the smallest table for their keys (KB_BIN_TS_ADAPT)
+    uint32_t ldsbar;           // 1: barriers that order LDS only skip the global-store drain (KB_BIN_LDSBAR)
 };
 constexpr int KB_PSTAT = 8;
 
@@ -308,9 +345,10 @@ hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t 
 hipError_t launch_bins_desc(const uint32_t* order, const uint32_t* bstart, const uint32_t* bcount,
                             const uint32_t* bmmer, const uint32_t* bocc, const uint64_t* totals, uint64_t max_bins,
                             uint4* desc, unsigned long long* stage_ctr, hipStream_t s);
-// HyperLogLog of the k-mers of the bin-ordered records (2^12 u32 registers,
-// zeroed here) and its estimate (host): the cold pass's distinct keys
-hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, hipStream_t s);
+// HyperLogLog of the k-mers of the bin-ordered records (2^12 u32 registers
+// and a u64 occurrence count, zeroed here; sample > 1: the bins of 1 / sample
+// of the mmers only) and its estimate (host): the cold pass's distinct keys
+hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, uint32_t sample, hipStream_t s);
 double hll_estimate(const uint32_t* regs);
 hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uint32_t* order, uint64_t max_bins,
                              hipStream_t s);
@@ -322,7 +360,7 @@ hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, co
                                 uint32_t* bcount, uint32_t* bmmer, uint64_t max_bins, hipStream_t s);
 // received records into local bucket regions (block-aggregated reservations)
 hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
-                                     const uint16_t* bucket_map,
+                                     int K, const uint32_t* bucket_map, const uint16_t* sub_map,
                                      uint64_t* regions, uint64_t cap, const uint64_t* rbase, unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s);
 size_t bins_lds_bytes(uint32_t ts_log2, int KW);

@@ -125,6 +125,9 @@ typedef struct {
                                tables by the singleton pre-filter              */
     uint32_t long_lists;    /* lists of 257..4096 ids (bucketed list sort)     */
     uint32_t clustered_lists; /* of those, lists sorted by the full network    */
+    uint32_t split_mmers;   /* mmers whose bins were split into context
+                               sub-bins (the bucket map the pass used)         */
+    uint32_t reserved0;
 } kb_timing;
 
 /* Create a context (kb_create replaces zcreate_hash_table for the level-1

@@ -115,15 +115,16 @@ def test_route_scatter(K, M, G, engine):
     assert union == ora
 
 
-@pytest.mark.parametrize("spread", ["1", "0"])
-def test_receiver_learned_map(spread, engine, monkeypatch):
+@pytest.mark.parametrize("sub", ["4", "0"])
+def test_receiver_learned_map(sub, engine, monkeypatch):
     """a receiver reused over passes learns its bucket map from its own bins
-    (few mmers per shard: large ones spread over runs of buckets) and converts
-    received records by it -- every pass equals the oracle's share"""
+    (few mmers per shard: large ones split into context sub-bins) and converts
+    received records by it, cutting them at the edge -- every pass equals the
+    oracle's share"""
     if engine != "binned":
         pytest.skip("binned engine only")
     monkeypatch.setenv("KB_BIN_BALANCE_MIN", "0")
-    monkeypatch.setenv("KB_BIN_SPREAD", spread)
+    monkeypatch.setenv("KB_BIN_SUB", sub)
     K, M, G = 31, 7, 4
     reads = _reads()
     bases, lens = kbin.pack_reads(reads)

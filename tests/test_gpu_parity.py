@@ -229,17 +229,18 @@ def test_partitioned_passes(P, radix, long_reads, K, M, engine, monkeypatch):
     assert tuple(dig) == kbin.result_digest(ora)  # digests add over partitions
 
 
-@pytest.mark.parametrize("K,M,spread", [(21, 5, "1"), (63, 7, "1"), (21, 5, "0")])
-def test_balanced_buckets(K, M, spread, engine, monkeypatch):
+@pytest.mark.parametrize("K,M,sub", [(21, 5, "4"), (63, 7, "4"), (21, 5, "0"), (31, 7, "1")])
+def test_balanced_buckets(K, M, sub, engine, monkeypatch):
     """after a pass the host packs the mmers into local buckets by their
-    record counts (largest first, least-loaded bucket; an mmer above twice the
-    mean load gets a run of buckets of its own, laid out as one bin); later
-    passes route records by that map, per partition key -- every pass equals
-    the oracle"""
+    record counts (largest first, least-loaded bucket; an mmer above 1.5 x the
+    mean load, or above one LDS table of keys, is split into context sub-bins,
+    each an item of its own); later passes route records by that map, cutting
+    a split mmer's records at the edge, per partition key -- every pass equals
+    the oracle, and the split happened where allowed"""
     if engine != "binned":
         pytest.skip("binned engine only")
     monkeypatch.setenv("KB_BIN_BALANCE_MIN", "0")
-    monkeypatch.setenv("KB_BIN_SPREAD", spread)
+    monkeypatch.setenv("KB_BIN_SUB", sub)
     rng = np.random.default_rng(K)
     genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20000)
     reads = []
@@ -249,6 +250,7 @@ def test_balanced_buckets(K, M, spread, engine, monkeypatch):
         reads.append(genome[s0:s0 + L].tobytes())
     bases, lens = kbin.pack_reads(reads)
     ora = oracle.bin_reads(bases, lens, K, M, 1, True)
+    splits = []
     with kbin.Engine(K, M, cutoff=1, max_read_len=300) as eng:
         for P in (1, 3):
             for _ in range(3):  # the first pass of a key learns its map, the next ones use it
@@ -259,7 +261,9 @@ def test_balanced_buckets(K, M, spread, engine, monkeypatch):
                     eng.set_partition(p, P)
                     eng.finalize(prune=True)
                     parts.append(eng.export())
+                    splits.append(eng.timing()["split_mmers"])
                 assert_same(kbin.Result.concat(parts), ora)
+        assert (max(splits) > 0) == (sub != "0"), splits
 
 
 def test_explicit_ids_nonmonotone():
@@ -501,11 +505,13 @@ def test_alphabet_rejected():
 
 
 @pytest.mark.parametrize("how", ["scatter", "split", "plan"])
-def test_alphabet_rejected_before_routing(how):
+def test_alphabet_rejected_before_routing(how, engine):
     """a batch with a byte outside ACGT never leaves the context: kb_route_scatter,
     kb_split_passes and kb_route_plan check the pack status first (KB_EALPHABET),
     so no record built from the invalid read reaches a peer or a pass"""
     import torch
+    if engine != "binned" and how != "plan":
+        pytest.skip("the one-pass senders are the binned engine's")
     with kbin.Engine(31, 7, max_read_len=150) as eng:
         eng.submit([b"ACGT" * 20 + b"N" + b"ACGT" * 10])  # returns before the pack has run
         cap = 1024
