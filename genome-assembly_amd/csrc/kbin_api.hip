@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <ctime>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -48,19 +49,29 @@ static int fail(int code, const char* fmt, ...) {
                         #expr, hipGetErrorString(_e), __FILE__, __LINE__);                \
     } while (0)
 
+static double g_alloc_ms = 0;  // (KB_DEBUG) host time in DevBuf allocations since the last report
+static double alloc_now_ms() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
     uint64_t cap = 0;
-    hipError_t ensure(uint64_t n) {
+    // Data-sized buffers (slack, the default) take 1/8 headroom, so passes
+    // whose sizes wander by a few percent (the partitioned passes of one job,
+    // records cut into sub-bins) do not free and map them afresh each pass: a
+    // re-mapped allocation is cleared by the driver at roughly 20-25 GB/s (a
+    // C3-sized stage regrown per pass cost seconds).  When the headroom does
+    // not fit, the allocation is exact (no KB_ENOMEM from the headroom).
+    // Fixed-size buffers (exact) allocate what they ask.
+    hipError_t ensure(uint64_t n, bool slack = true) {
         if (n <= cap && p) return hipSuccess;
-        // A first allocation is exact (peak HBM per context stays at what the
-        // pass needs).  A regrowth takes 1/8 headroom, so passes whose sizes
-        // wander by a few percent (the partitioned passes of one job) regrow
-        // once rather than freeing and mapping tens of GB every pass (fresh
-        // device memory is cleared at roughly 20-25 GB/s)
+        const double t0 = alloc_now_ms();
         uint64_t want = std::max<uint64_t>(n, 1);
-        if (p) want += want / 8;
+        if (slack) want += want / 8;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -72,8 +83,10 @@ struct DevBuf {
         }
         if (e == hipSuccess) cap = want;
         else p = nullptr;
+        g_alloc_ms += alloc_now_ms() - t0;
         return e;
     }
+    hipError_t ensure_exact(uint64_t n) { return ensure(n, false); }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -253,8 +266,7 @@ struct kb_ctx {
     DevBuf<uint64_t> bbase;  // [NB + 1] bucket output bases (bucket_bases_kernel)
     DevBuf<uint64_t> rbase;  // [NB + 1] exact region bases (a pass without a learned map)
     bool rexact = false;     // the regions of the last record pass use rbase
-    uint64_t bucket_cap = 0;   // learned region capacity (records per bucket)
-    uint64_t bucket_cap_used = 0;  // the capacity (region stride) the regions were written with
+    uint64_t bucket_cap_used = 0;  // the region stride (records per bucket) the regions were written with
     DevBuf<uint64_t> kpart;    // per-block k-mer sums of the count pass
     int ocut_km = -1;          // (K << 8 | M) the offset cut table was made for
     uint8_t ocut[5][17] = {};  // offset partitions' ranges (offset_cuts)
@@ -262,6 +274,7 @@ struct kb_ctx {
     float rho_tab = 0.f;       // learned table keys / occurrences under the singleton pre-filter
     DevBuf<uint32_t> hll;      // cold pass: HyperLogLog registers (launch_hll)
     bool bucket_failed = false;  // a bucket overflowed its mmer map: radix path from now on
+    bool prior_off = false;      // a prior map overflowed a bucket: hash routing for first passes
     uint64_t n_occ_entries_hint = 0;  // entries of the last finalize (lists grid)
     uint64_t ecap_hint = 0;    // entry capacity for the next binned finalize
     uint32_t part = 0, part_n = 1;  // kb_set_partition: this pass's mmer partition
@@ -276,8 +289,13 @@ struct kb_ctx {
         bool stale = false;
         uint64_t want_max = 0;  // the largest bucket load the packing expects (records)
         uint64_t want_tot = 0;
+        uint64_t cap = 0;       // region stride of this key's passes (records per bucket)
         uint32_t split = 0;     // mmers split into context sub-bins
         std::vector<uint32_t> h_map;  // host copy of map
+        // a pass's descriptors waiting to rebuild this map (bmap_apply)
+        bool pending = false;
+        std::vector<uint32_t> p_mm, p_cnt, p_occ;
+        double p_rho = 0;
         DevBuf<uint32_t> map;   // per canonical mmer (bm_* in kbin_internal.h)
         DevBuf<uint16_t> sub;   // buckets of the split mmers' sub-bins
     };
@@ -291,6 +309,10 @@ struct kb_ctx {
     PinBuf<uint32_t> h_mmer, h_cnt;  // pinned: kb_export's D2H at full rate
     PinBuf<uint64_t> h_hi, h_lo, h_off, h_first;
     PinBuf<int32_t> h_ids;
+    PinBuf<uint32_t> h_bins;  // a pass's bin descriptors for map learning (mmer | sub, records, occurrences)
+    PinBuf<uint8_t> map_stage;  // bucket map uploads (bmap_build)
+    hipEvent_t map_done = nullptr;
+    bool map_stage_used = false;
     bool exported = false;
 
     // timing
@@ -300,6 +322,7 @@ struct kb_ctx {
     // grid hints for kernels that usually have nothing to do (~0: not seen yet)
     uint64_t hint_heavy = ~0ull, hint_lq = ~0ull, hint_long[2] = {~0ull, ~0ull};
     uint64_t hint_entries = 0, hint_ids = 0;  // the last finalize's entries and ids (kb_reset keeps them)
+    double t_fin = 0;  // (KB_DEBUG) host time the finalize started
     bool alpha_dirty = false;  // a pack kernel may have set the sticky alphabet status since it was cleared
     hipEvent_t ev[8] = {};
 };
@@ -314,6 +337,8 @@ extern "C" int kb_abi_version(void) { return 2; }  // 2: kb_timing path counters
 extern "C" const char* kb_last_error(void) { return g_err.c_str(); }
 
 extern "C" void* kb_stream(kb_ctx* ctx) { return ctx ? (void*)ctx->s : nullptr; }
+
+static uint64_t bin_budget(const kb_ctx* c, uint32_t NB);
 
 extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     if (!params || !out) return fail(KB_EINVAL, "null argument");
@@ -355,9 +380,38 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
         e = hipEventCreateWithFlags(&sl.done, hipEventDisableTiming);
         if (e != hipSuccess) { kb_destroy(c); return fail(KB_EDEVICE, "hipEventCreate"); }
     }
-    if (c->misc.ensure(16) != hipSuccess || c->totals.ensure(16) != hipSuccess ||
+    e = hipEventCreateWithFlags(&c->map_done, hipEventDisableTiming);
+    if (e != hipSuccess) { kb_destroy(c); return fail(KB_EDEVICE, "hipEventCreate"); }
+    {
+        // the bucket maps' pinned staging (map upload, bin descriptors back):
+        // page-locking takes milliseconds, so here rather than inside a finalize
+        const uint64_t half = 1ull << (2 * p.M - 1), bins = bin_budget(c, 1024);
+        if (c->map_stage.ensure(half * sizeof(uint32_t) + bins * sizeof(uint16_t)) != hipSuccess ||
+            c->h_bins.ensure(3 * bins) != hipSuccess) {
+            kb_destroy(c);
+            return fail(KB_ENOMEM, "hipHostMalloc");
+        }
+        // The runtime sets up its host-to-device copy path for copies of this
+        // size on first use (milliseconds, once per process and device): a
+        // map-sized warm-up copy here keeps it out of the first finalize
+        static bool warm[64] = {};
+        if (p.device >= 0 && p.device < 64 && !warm[p.device]) {
+            DevBuf<uint8_t> t;
+            const uint64_t nb = half * sizeof(uint32_t);
+            if (t.ensure_exact(nb) == hipSuccess &&
+                hipMemcpyAsync(t.p, c->map_stage.p, nb, hipMemcpyHostToDevice, c->s) == hipSuccess &&
+                hipStreamSynchronize(c->s) == hipSuccess)
+                warm[p.device] = true;
+            t.release();
+        }
+    }
+    // (the zeroing goes up as a host-to-device copy: the context's first such
+    // copy sets up the copy path, here rather than inside a first finalize)
+    memset(c->h_totals, 0, 32 * sizeof(uint64_t));
+    if (c->misc.ensure_exact(16) != hipSuccess || c->totals.ensure_exact(16) != hipSuccess ||
         hipMemsetAsync(c->misc.p, 0, 16 * sizeof(uint32_t), c->s) != hipSuccess ||
-        hipMemsetAsync(c->totals.p, 0, 16 * sizeof(uint64_t), c->s) != hipSuccess) {
+        hipMemcpyAsync(c->totals.p, c->h_totals, 16 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s) != hipSuccess ||
+        hipStreamSynchronize(c->s) != hipSuccess) {
         kb_destroy(c);
         return fail(KB_ENOMEM, "device alloc");
     }
@@ -390,7 +444,8 @@ extern "C" void kb_destroy(kb_ctx* c) {
     }
     c->pool.release();
     c->h_mmer.release(); c->h_cnt.release(); c->h_hi.release(); c->h_lo.release(); c->h_off.release();
-    c->h_first.release(); c->h_ids.release();
+    c->h_first.release(); c->h_ids.release(); c->h_bins.release(); c->map_stage.release();
+    if (c->map_done) (void)hipEventDestroy(c->map_done);
     if (c->h_alpha) (void)hipHostFree(c->h_alpha);
     c->table.release(); c->occ_a.release();
     c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
@@ -1143,7 +1198,8 @@ static kb_ctx::BucketMap* bmap_find(kb_ctx* c, uint32_t NB) {
 // bucket -- a light bin of its own in bin_kernel: no flat lists, no
 // re-expansion per partition, finer longest-first scheduling.
 static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
-    const int bmax = std::min<int>((int)SUB_MAX_B, std::max(0, env_int("KB_BIN_SUB", (int)SUB_MAX_B)));
+    int bmax = std::min<int>((int)SUB_MAX_B, std::max(0, env_int("KB_BIN_SUB", (int)SUB_MAX_B)));
+    if (!sub_room(c->p.K, c->p.M, 2 * c->KW)) bmax = 0;  // (no spare span bits for the stamp)
     const double ts = c->KW == 1 ? 8192.0 : 4096.0;
     const double cap = ts * std::min(0.85, std::max(0.2, env_int("KB_BIN_SUB_FILL_PCT", 50) / 100.0));
     uint32_t b = 0;
@@ -1151,36 +1207,56 @@ static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
     return b;
 }
 
+// bins one finalize may describe: every canonical mmer once, plus the extra
+// sub-bins of the split ones (bmap_build keeps within it)
+static uint64_t bin_budget(const kb_ctx* c, uint32_t NB) {
+    const uint64_t half = 1ull << (2 * c->p.M - 1);
+    return half + (sub_room(c->p.K, c->p.M, 2 * c->KW) ? 48ull * NB : 0ull);
+}
+
 static int bmap_build(kb_ctx* c, uint32_t NB, double rho) {
+    const double tb0 = now_ms();
     const int M = c->p.M;
     const uint32_t half = 1u << (2 * M - 1);
     struct Item {
         double w;
         uint32_t mm, sub;  // sub: ~0 for an unsplit mmer
     };
-    std::vector<Item> items;
     std::vector<uint32_t> h(half);
     uint64_t tot_w = 0;
     for (uint32_t i = 0; i < half && i < c->mmer_w.size(); i++) tot_w += c->mmer_w[i];
     const double mean = std::max(1.0, (double)tot_w / NB);
+    // this pass's mmers, heaviest first: the split depths are handed out in
+    // that order within the bin budget
+    std::vector<std::pair<double, uint32_t>> seen;
+    for (uint32_t i = 0; i < half; i++) {
+        h[i] = (uint32_t)sk_hash_dest(half + i, NB, sk_bucket_salt());  // unseen (or another pass's): hash
+        if (c->part_n > 1 && sk_hash_dest(half + i, c->part_n, 0x9E3779B97F4A7C15ull) != c->part) continue;
+        const double w = i < c->mmer_w.size() ? (double)c->mmer_w[i] : 0.0;
+        // (a negligible mmer keeps its hash bucket: no packing item)
+        if (w > 0 && w >= mean / 512.0) seen.push_back({w, i});
+    }
+    std::sort(seen.begin(), seen.end(), [](const std::pair<double, uint32_t>& a,
+                                           const std::pair<double, uint32_t>& b) { return a.first > b.first; });
+    uint64_t extra = bin_budget(c, NB) - half;  // sub-bins beyond one per mmer
+    const kb_ctx::BucketMap* old = bmap_find(c, NB);
+    std::vector<Item> items;
     std::vector<uint16_t> subs;
     uint32_t n_split = 0;
-    for (uint32_t i = 0; i < half; i++) {
-        const uint32_t mm = half + i;
-        h[i] = (uint32_t)sk_hash_dest(mm, NB, sk_bucket_salt());  // unseen (or another pass's): hash
-        if (c->part_n > 1 && sk_hash_dest(mm, c->part_n, 0x9E3779B97F4A7C15ull) != c->part) continue;
-        const double w = i < c->mmer_w.size() ? (double)c->mmer_w[i] : 0.0;
-        if (w <= 0) continue;
+    for (const auto& sw : seen) {
+        const uint32_t i = sw.second, mm = half + i;
+        const double w = sw.first;
         const double occ = i < c->mmer_o.size() && c->mmer_o[i] ? (double)c->mmer_o[i] : 12.0 * w;
-        const uint32_t b = sub_depth(c, w, occ * rho, mean);
+        uint32_t b = sub_depth(c, w, occ * rho, mean);
+        while (b && sub_count(b) - 1 > extra) b--;
         if (!b) {
             items.push_back({w, mm, ~0u});
             continue;
         }
+        extra -= sub_count(b) - 1;
         // sub-bin 0, the edge, holds a few percent; the contexts share the
         // rest -- or, when the last pass split this mmer as deep, as measured
         const uint32_t nsub = sub_count(b);
-        const kb_ctx::BucketMap* old = bmap_find(c, NB);
         const bool same = old && !old->h_map.empty() && (old->h_map[i] & BM_SPLIT) &&
                           ((old->h_map[i] >> 28) & 7u) == b;
         h[i] = BM_SPLIT | (b << 28) | (uint32_t)subs.size();
@@ -1195,7 +1271,9 @@ static int bmap_build(kb_ctx* c, uint32_t NB, double rho) {
         subs.resize(subs.size() + nsub, 0);
         n_split++;
     }
+    const double tb1 = now_ms();
     std::sort(items.begin(), items.end(), [](const Item& a, const Item& b) { return a.w > b.w; });
+    const double tb2 = now_ms();
     // longest processing time first onto the least loaded bucket; at most 128
     // bins per bucket (bucket_kernel maps 256)
     using Slot = std::pair<double, uint32_t>;  // (load, bucket)
@@ -1220,6 +1298,7 @@ static int bmap_build(kb_ctx* c, uint32_t NB, double rho) {
         want_tot += pq.top().first;
         pq.pop();
     }
+    const double tb3 = now_ms();
     kb_ctx::BucketMap* m = bmap_find(c, NB);
     if (!m) {
         c->bmaps.emplace_back();
@@ -1227,51 +1306,67 @@ static int bmap_build(kb_ctx* c, uint32_t NB, double rho) {
         m->key = bmap_key(c);
         m->nb = NB;
     }
-    HIPCHK(m->map.ensure(half));
-    HIPCHK(hipMemcpyAsync(m->map.p, h.data(), half * sizeof(uint32_t), hipMemcpyHostToDevice, c->s));
-    m->h_map = h;
+    HIPCHK(m->map.ensure_exact(half));
     HIPCHK(m->sub.ensure(std::max<size_t>(subs.size(), 1)));
+    // uploaded from the context's pinned staging (a pageable copy stages
+    // through the runtime's bounce buffers: milliseconds on a context's first
+    // use); the last upload must have left it
+    const uint64_t need = half * sizeof(uint32_t) + subs.size() * sizeof(uint16_t);
+    if (c->map_stage_used) HIPCHK(hipEventSynchronize(c->map_done));
+    HIPCHK(c->map_stage.ensure(need));
+    memcpy(c->map_stage.p, h.data(), half * sizeof(uint32_t));
+    if (!subs.empty()) memcpy(c->map_stage.p + half * sizeof(uint32_t), subs.data(), subs.size() * sizeof(uint16_t));
+    HIPCHK(hipMemcpyAsync(m->map.p, c->map_stage.p, half * sizeof(uint32_t), hipMemcpyHostToDevice, c->s));
     if (!subs.empty())
-        HIPCHK(hipMemcpyAsync(m->sub.p, subs.data(), subs.size() * sizeof(uint16_t), hipMemcpyHostToDevice, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));  // h and subs are locals
+        HIPCHK(hipMemcpyAsync(m->sub.p, c->map_stage.p + half * sizeof(uint32_t), subs.size() * sizeof(uint16_t),
+                              hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipEventRecord(c->map_done, c->s));
+    c->map_stage_used = true;
+    KB_DBG("bmap_build: %zu items, setup %.3f sort %.3f pack %.3f upload %.3f ms\n", items.size(), tb1 - tb0,
+           tb2 - tb1, tb3 - tb2, now_ms() - tb3);
+    m->h_map = std::move(h);
     m->stale = false;
+    m->pending = false;
     m->split = n_split;
     m->want_max = (uint64_t)want_max + 1;
     m->want_tot = (uint64_t)want_tot + 1;
-    // the region stride the next map-routed pass starts with (one pass when
-    // the packing holds; a larger bucket reruns it bigger)
-    c->bucket_cap = std::max<uint64_t>(c->bucket_cap, m->want_max + m->want_max / 4 + 1024);
+    // the region stride (records per bucket) this key's next pass writes with:
+    // the largest bucket the packing expects plus a fifth (dense regions: a
+    // sparse stride spreads a block's scattered record stores over more
+    // pages), a larger bucket reruns the pass bigger
+    // (a rebuilt map keeps the stride its key's passes have needed so far:
+    // the packing's expectation runs some 10-25 % under the fullest bucket)
+    m->cap = std::max<uint64_t>(m->cap, m->want_max + m->want_max / 3 + 256);
     return KB_OK;
 }
 
-// after a bucketed pass: learn records and occurrences per mmer from the bin
-// descriptors (a split mmer's sub-bins add up) and (re)build this key's map
-// when it is missing or the pass found it unbalanced
-static int bmap_learn(kb_ctx* c, uint32_t NB, uint64_t R, uint64_t nbins, double rho) {
+// Learning a key's map from a bucketed pass: its bins' descriptors (records,
+// occurrences, mmer | sub-bin << 16) give the records and occurrences per
+// mmer (a split mmer's sub-bins add up) and each sub-bin's own records.  The
+// descriptors ride the finalize's last copy (bmap_stage); the map itself is
+// rebuilt when the key is next binned (bmap_apply), so no finalize waits on
+// the packing -- a one-shot caller never pays it.
+static bool bmap_wants(kb_ctx* c, uint32_t NB, uint64_t R) {
     if (!env_int("KB_BIN_BALANCE", 1) || R < (uint64_t)std::max(0, env_int("KB_BIN_BALANCE_MIN", 1 << 18)))
-        return KB_OK;
-    kb_ctx::BucketMap* m = bmap_find(c, NB);
-    if (m && !m->stale) return KB_OK;
-    std::vector<uint32_t> mm(nbins), cnt(nbins), occ(nbins);
-    HIPCHK(hipMemcpyAsync(mm.data(), c->bmmer.p, nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipMemcpyAsync(cnt.data(), c->bcount.p, nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipMemcpyAsync(occ.data(), c->bocc.p, nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
+        return false;
+    const kb_ctx::BucketMap* m = bmap_find(c, NB);
+    return !m || m->stale;
+}
+
+static int bmap_apply(kb_ctx* c, uint32_t NB, const uint32_t* mm, const uint32_t* cnt, const uint32_t* occ,
+                      uint64_t nbins, double rho) {
+    const kb_ctx::BucketMap* m = bmap_find(c, NB);
     const uint32_t half = 1u << (2 * c->p.M - 1);
     c->mmer_w.assign(half, 0);
     c->mmer_o.assign(half, 0);
-    // a split mmer's sub-bins as measured (bmmer: the mmer | sub-bin << 16),
-    // which the packing uses while the mmer keeps its depth
     c->sub_w.clear();
     for (uint64_t b = 0; b < nbins; b++) {
         const uint32_t mmer = mm[b] & 0xFFFFu, sub = mm[b] >> 16;
         if (mmer < half || mmer >= 2 * half) continue;
         c->mmer_w[mmer - half] += std::max(cnt[b], 1u);
         c->mmer_o[mmer - half] += occ[b];
-        if (m && m->split) {
-            const uint32_t e = m->h_map.empty() ? 0u : m->h_map[mmer - half];
-            if (e & BM_SPLIT) c->sub_w[((uint64_t)mmer << 16) | sub] += std::max(cnt[b], 1u);
-        }
+        if (m && m->split && !m->h_map.empty() && (m->h_map[mmer - half] & BM_SPLIT))
+            c->sub_w[((uint64_t)mmer << 16) | sub] += std::max(cnt[b], 1u);
     }
     return bmap_build(c, NB, rho);
 }
@@ -1323,23 +1418,35 @@ static int bmap_prior(kb_ctx* c, uint32_t NB) {
         const double w = R_part * p[i] / std::max(mine, 1e-300);
         c->mmer_w[i] = (uint32_t)std::min(4e9, std::ceil(w));
     }
-    const int rc = bmap_build(c, NB, c->rho > 0.f ? (double)c->rho : 0.0);
+    // (no density learned yet: a typical one -- splits then follow the keys as well as the loads)
+    const int rc = bmap_build(c, NB, c->rho > 0.f ? (double)c->rho : 0.1);
     if (rc) return rc;
     kb_ctx::BucketMap* m = bmap_find(c, NB);
     m->stale = true;  // (the pass learns the real one)
     // a prior misses real data's skew more than a learned map: a wider stride
     // (an overflowing bucket reruns the pass bigger)
-    c->bucket_cap = std::max<uint64_t>(c->bucket_cap, m->want_max + m->want_max / 2 + 1024);
+    m->cap = 3 * m->want_max + 1024;
     return KB_OK;
 }
 
 static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, uint64_t& R, uint64_t& N) {
     const int M = c->p.M;
     kb_ctx::BucketMap* bm = bmap_find(c, NB);
-    if (!bm && env_int("KB_BIN_PRIOR", 1) && env_int("KB_BIN_BALANCE", 1)) {
+    if (bm && bm->pending) {  // the last pass of this key left its bins: rebuild the map from them
+        const double t0 = now_ms();
+        const int rc = bmap_apply(c, NB, bm->p_mm.data(), bm->p_cnt.data(), bm->p_occ.data(), bm->p_mm.size(),
+                                  bm->p_rho);
+        if (rc) return rc;
+        bm = bmap_find(c, NB);
+        KB_DBG("map rebuilt part %u/%u: %.3f ms, %u split\n", c->part, c->part_n, now_ms() - t0, bm->split);
+    }
+    if (!bm && !c->prior_off && env_int("KB_BIN_PRIOR", 1) && env_int("KB_BIN_BALANCE", 1)) {
+        const double t0 = now_ms();
         const int rc = bmap_prior(c, NB);
         if (rc) return rc;
         bm = bmap_find(c, NB);
+        KB_DBG("prior map part %u/%u: %.3f ms (allocations %.3f), %u split, cap %llu\n", c->part, c->part_n,
+               now_ms() - t0, g_alloc_ms, bm->split, (unsigned long long)bm->cap);
     }
     const uint32_t* bmap = bm ? bm->map.p : nullptr;
     const uint16_t* bsub = bm ? bm->sub.p : nullptr;
@@ -1359,7 +1466,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
     for (int attempt = 0; attempt < 3; attempt++) {
         const bool counting = exact && attempt == 0;
         const bool use_base = exact && attempt > 0;
-        const uint64_t cap = exact ? 0 : c->bucket_cap;
+        const uint64_t cap = exact ? 0 : bm->cap;
         if (attempt > 0 || !zeroed) {  // (the finalize's first clear zeroed them for attempt 0)
             ClearList cl{};
             cl.add(c->bfill.p, NB * sizeof(unsigned long long));
@@ -1373,7 +1480,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
             if (received) {
                 if (!b.superkmers) continue;
                 HIPCHK(launch_sk_convert_buckets(b.recs, b.n_reads, rec_words(c), 2 * c->KW, M, NB, c->p.K, bmap, bsub,
-                                                 c->regions.p, cap,
+                                                 bm && bm->split ? 1 : 0, c->regions.p, cap,
                                                  use_base ? c->rbase.p : nullptr, c->bfill.p, c->misc.p,
                                                  reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
             } else {
@@ -1397,6 +1504,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
                 a.rw = (int)RWD;  // header + span words
                 a.bucket_map = bmap;
                 a.sub_map = bsub;
+                a.sub_stamp = bm && bm->split ? 1 : 0;
                 a.binned_fmt = 1;
                 a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p);
                 HIPCHK(launch_sk(a, true, c->s));
@@ -1418,6 +1526,9 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
             HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         }
         HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync (two without a map): R and N size the rest
+        KB_DBG("record pass attempt %d: %s cap %llu, %.3f ms since finalize (allocations %.3f ms)\n", attempt,
+               counting ? "counting" : use_base ? "exact" : "stride", (unsigned long long)cap, now_ms() - c->t_fin,
+               g_alloc_ms);
         if (!counting) c->h_misc[0] = (uint32_t)c->h_totals[14];
         if (c->h_misc[0] & ST_NEG_ID)
             return fail(KB_EINVAL, "routed read ids must be non-negative (they order the id lists)");
@@ -1451,7 +1562,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
         if (use_base || mx <= cap) {
             c->rexact = use_base;
             c->bucket_cap_used = cap;  // the region stride of this pass (0: exact bases)
-            if (!use_base) c->bucket_cap = std::max<uint64_t>(c->bucket_cap, mx + mx / 8 + 1024);  // next passes
+            if (!use_base && mx + mx / 16 > cap) bm->cap = mx + mx / 5 + 256;  // (close to full: next passes wider)
             if (N >= 0xFFFFFFFFull)
                 return fail(KB_EOVERFLOW, "%llu k-mer occurrences in one context (limit 2^32-1)",
                             (unsigned long long)N);
@@ -1463,7 +1574,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
         // grow and rerun the pass; with headroom, so a later pass's slightly
         // larger bucket does not regrow (each growth maps the regions afresh)
         KB_DBG("record pass rerun: bucket %llu > cap %llu\n", (unsigned long long)mx, (unsigned long long)cap);
-        c->bucket_cap = mx + mx / 2 + 1024;
+        bm->cap = mx + mx / 4 + 1024;
     }
     return fail(KB_EDEVICE, "internal: bucket capacity did not converge");
 }
@@ -1569,6 +1680,8 @@ static void offset_cuts(int K, int M, uint8_t (&cut)[5][17]) {
 
 static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool received) {
     const int M = c->p.M;
+    c->t_fin = now_ms();
+    g_alloc_ms = 0;
     c->tm.engine = KB_ENG_BINNED;
     REC(0);
     HIPCHK(c->totals.ensure(16));
@@ -1586,8 +1699,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     uint32_t NB = 1;
     while (NB < (uint32_t)std::min(1024, std::max(64, env_int("KB_BIN_NB", 1024)))) NB <<= 1;
     // every counter of this finalize's first attempt zeroed in one launch
-    HIPCHK(c->flat_n.ensure(8));
-    HIPCHK(c->pstat.ensure(KB_PSTAT));
+    HIPCHK(c->flat_n.ensure_exact(8));
+    HIPCHK(c->pstat.ensure_exact(KB_PSTAT));
     {
         ClearList cl{};
         cl.add(c->totals.p, 16 * sizeof(uint64_t));
@@ -1607,10 +1720,9 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     if (rc) return rc;
     c->n_occ = N;
     REC(2);
-    // bins: canonical mmers, or context sub-bins of the split ones
-    uint64_t bin_keys = 1ull << (2 * M - 1);
-    if (bucketed)
-        if (kb_ctx::BucketMap* bm = bmap_find(c, NB)) bin_keys += (uint64_t)bm->split * (sub_count(SUB_MAX_B) - 1);
+    // bins: canonical mmers, or context sub-bins of the split ones (a fixed
+    // budget: the buffers sized by it keep their size as maps change)
+    const uint64_t bin_keys = bucketed ? bin_budget(c, NB) : 1ull << (2 * M - 1);
     const uint64_t max_bins = std::max<uint64_t>(1, std::min<uint64_t>(R, bin_keys));
     HIPCHK(c->starts.ensure(max_bins + 1));
     HIPCHK(c->bcount.ensure(max_bins));
@@ -1653,9 +1765,10 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(c->bbase.ensure(NB + 1));
         ba.bbase = c->bbase.p;
         {
+            // records written by a map-routed pass carry their sub-bin (zero
+            // for an unsplit mmer); a hash-routed pass writes spans untouched
             kb_ctx::BucketMap* bm = bmap_find(c, NB);  // (the map the record pass used)
-            ba.bucket_map = bm && bm->split ? bm->map.p : nullptr;
-            ba.K = c->p.K;
+            ba.sub = bm && bm->split ? 1 : 0;
         }
         ba.bin_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 2);
         ba.bstart = c->starts.p;
@@ -1709,11 +1822,13 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         // large passes estimate from the bins of 1/8 of the mmers (whole bins:
         // the ratio of a sample of bins, 1/8 of the expansion work)
         const uint32_t sample = R >= (1u << 20) && max_bins >= 256 ? (uint32_t)std::max(1, env_int("KB_BIN_HLL_SAMPLE", 8)) : 1u;
-        HIPCHK(c->hll.ensure(4096 + 2));
+        HIPCHK(c->hll.ensure_exact(4096 + 2));
         HIPCHK(launch_hll(h, R, KW, c->hll.p, sample, c->s));
         std::vector<uint32_t> regs(4096 + 2);
         HIPCHK(hipMemcpyAsync(regs.data(), c->hll.p, (4096 + 2) * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipStreamSynchronize(c->s));
+        KB_DBG("hll (sample 1/%u): %.3f ms since finalize (allocations %.3f ms)\n", sample, now_ms() - c->t_fin,
+               g_alloc_ms);
         uint64_t occ_s = 0;
         memcpy(&occ_s, regs.data() + 4096, sizeof(occ_s));
         if (occ_s)
@@ -1728,6 +1843,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     uint64_t ecap = std::min<uint64_t>(N + 1, c->ecap_hint ? c->ecap_hint : N / 8 + 1024);
     if (const int forced = env_int("KB_BIN_ECAP0", 0)) ecap = (uint64_t)forced;  // tests: force the rerun
     BinArgs a{};
+    const bool learn = bucketed && bmap_wants(c, NB, R);  // (before the record pass's map may be replaced)
     for (int attempt = 0;; attempt++) {
         HIPCHK(c->e_mmer.ensure(ecap));
         HIPCHK(c->e_cnt.ensure(ecap));
@@ -1898,6 +2014,14 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         REC(5);
         HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 14 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         HIPCHK(hipMemcpyAsync(c->h_totals + 16, c->pstat.p, KB_PSTAT * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        if (learn) {  // the bins' descriptors for the map (bmap_apply), in the same copy batch
+            HIPCHK(c->h_bins.ensure(3 * max_bins));
+            HIPCHK(hipMemcpyAsync(c->h_bins.p, c->bmmer.p, max_bins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_bins.p + max_bins, c->bcount.p, max_bins * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_bins.p + 2 * max_bins, c->bocc.p, max_bins * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, c->s));
+        }
         HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         if (R && !bucketed)
             HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
@@ -1905,9 +2029,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(hipStreamSynchronize(c->s));
         if (c->h_misc[0] & ST_BUCKET_FULL) {  // a bucket held too many mmers
             c->finalized = false;
-            // a learned map packed them: forget it and rerun on the hash routing
+            // a learned (or prior) map packed them: forget it and rerun on the
+            // hash routing (no prior for this context from now on)
             for (size_t i = 0; i < c->bmaps.size(); i++)
                 if (c->bmaps[i].key == bmap_key(c) && c->bmaps[i].nb == NB) {
+                    c->prior_off = true;
                     auto& m = c->bmaps[i];
                     m.map.release(); m.sub.release();
                     c->bmaps.erase(c->bmaps.begin() + (long)i);
@@ -1948,14 +2074,24 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     c->n_distinct = c->h_totals[6];
     if (bucketed) {
         const double rho_now = N ? (double)c->h_totals[6] / (double)N : 0.1;
-        const double t_l = now_ms();
-        const kb_ctx::BucketMap* bm0 = bmap_find(c, NB);
-        const bool relearn = !bm0 || bm0->stale;
-        const int rc2 = bmap_learn(c, NB, R, std::min<uint64_t>(c->h_totals[2], max_bins), rho_now);
-        if (rc2) return rc2;
-        KB_DBG("learn part %u/%u: %s %.3f ms (bins %llu, R %llu)\n", c->part, c->part_n,
-               relearn ? "rebuilt" : "kept", now_ms() - t_l, (unsigned long long)c->h_totals[2],
-               (unsigned long long)R);
+        KB_DBG("bins done: %.3f ms since finalize (allocations %.3f ms)\n", now_ms() - c->t_fin, g_alloc_ms);
+        if (learn) {
+            const uint64_t nb = std::min<uint64_t>(c->h_totals[2], max_bins);
+            const uint32_t* hb = c->h_bins.p;
+            kb_ctx::BucketMap* bm0 = bmap_find(c, NB);
+            if (bm0) {  // rebuilt when this key is next binned
+                bm0->p_mm.assign(hb, hb + nb);
+                bm0->p_cnt.assign(hb + max_bins, hb + max_bins + nb);
+                bm0->p_occ.assign(hb + 2 * max_bins, hb + 2 * max_bins + nb);
+                bm0->p_rho = rho_now;
+                bm0->pending = true;
+            } else {  // (no map at all: KB_BIN_PRIOR=0) the next pass needs one now
+                const int rc2 = bmap_apply(c, NB, hb, hb + max_bins, hb + 2 * max_bins, nb, rho_now);
+                if (rc2) return rc2;
+            }
+            KB_DBG("learn part %u/%u: %s (bins %llu, R %llu)\n", c->part, c->part_n, bm0 ? "deferred" : "built",
+                   (unsigned long long)nb, (unsigned long long)R);
+        }
     }
     c->n_occ_entries_hint = c->n_entries;
     c->ecap_hint = c->n_entries + c->n_entries / 4 + 1024;

@@ -141,22 +141,51 @@ DEV int32_t id_of(uint32_t ord, const int32_t* read_ids, uint32_t id_off) {
 // routed one (read id), see SkScanArgs; then rw - 1 span words from base lo
 // (n + K - 1 <= 2K - M bases: 2 words for K <= 31, 4 for K <= 63)
 DEV void put_record(const SkScanArgs& A, uint64_t* o, uint32_t ord, uint64_t lo, uint64_t n, uint64_t so,
-                    uint64_t rev, const uint64_t* sw) {
+                    uint64_t rev, const uint64_t* sw, uint32_t sub = 0) {
     if (A.binned_fmt) {
         o[0] = (uint64_t)ord | (n << 32) | (so << 38) | (rev << 44) | (lo << 45);
     } else {
         const uint32_t id = (uint32_t)id_of(ord, A.read_ids, A.id_off);
         o[0] = (uint64_t)id | (lo << 32) | (n << 48) | (so << 54);
     }
-    for (int w = 1; w < A.rw; w++) o[w] = window64(sw, (int)lo + 32 * (w - 1));
+    for (int w = 1; w < A.rw; w++) {
+        uint64_t x = window64(sw, (int)lo + 32 * (w - 1));
+        if (A.sub_stamp && w + 1 == A.rw) x = (x & ~SUB_MASK) | sub;  // (a bucket record's sub-bin, sub_room)
+        o[w] = x;
+    }
 }
 
-// destination region of a super-k-mer (piece): its owner rank (routing) or
-// its local bucket (the balanced map when the host has one -- per context
-// sub-bin for a split mmer -- else the hash)
-DEV uint32_t region_of(const SkScanArgs& A, uint32_t mmer, uint32_t sub) {
-    return A.bucket_map ? bm_bucket(A.bucket_map[mmer - (1u << (2 * A.M - 1))], A.sub_map, sub)
-                        : dest_of(mmer, A.G, A.dest_salt);
+// The pieces of one record bound for destination regions: its owner rank or
+// local bucket, or -- a split mmer's record -- its context sub-bin's bucket,
+// cut in two (the first ne k-mers, the edge, then the rest) when its first
+// k-mers lie in the edge.  row: the read's LDS row (the context bases).
+// Returns the number of pieces; d[] their regions.
+DEV uint32_t record_pieces(const SkScanArgs& A, uint32_t canon, int lo, int n, int so, bool rev,
+                           const uint64_t* row, uint32_t (&d)[2], uint32_t (&sub)[2], int& ne) {
+    ne = 0;
+    sub[0] = sub[1] = 0;
+    if (!A.bucket_map) {
+        d[0] = dest_of(canon, A.G, A.dest_salt);
+        return 1;
+    }
+    const uint32_t me = A.bucket_map[canon - (1u << (2 * A.M - 1))];
+    const uint32_t b = bm_depth(me);
+    if (!b) {
+        d[0] = me & 1023u;
+        return 1;
+    }
+    const uint64_t w = window64(row, lo + so + A.M);  // the read's bases after the signature
+    const int e = sub_edge(so, n, A.K, A.M, b);
+    if (e > 0 && e < n) {
+        ne = e;
+        sub[1] = sub_ctx(so - e, A.K, A.M, b, w, rev);
+        d[0] = bm_bucket(me, A.sub_map, 0u);
+        d[1] = bm_bucket(me, A.sub_map, sub[1]);
+        return 2;
+    }
+    sub[0] = sub_ctx(so, A.K, A.M, b, w, rev);
+    d[0] = bm_bucket(me, A.sub_map, sub[0]);
+    return 1;
 }
 
 // Add one record to a packed 16-bit LDS destination count (two per word) and
@@ -222,7 +251,7 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
     const uint32_t halfM = 1u << (2 * M - 1);
     const bool one_word = K <= 31 && M <= 12;  // (scores < 2^24 keep 8 bits for the offset)
     const uint32_t tid = threadIdx.x;
-    uint64_t* stg = smem + SKT * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, region (routed) or mmer}
+    uint64_t* stg = smem + SKT * RS;  // WRITE: [SK_STAGE] {lo, n, so, rev, row, canon}
     __shared__ uint32_t span_end;
     __shared__ unsigned long long s_base;
     __shared__ uint32_t dcnt2[SK_MAX_DEST / 2];  // per-destination counts, 16 bits each (< SK_STAGE)
@@ -299,40 +328,28 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 }
                 if (WRITE) {
                     const uint64_t rev = bsm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
-                    const int so = sig - lo;
-                    // a split mmer (local buckets): the record goes to its context
-                    // sub-bin, cut in two when its first k-mers lie in the edge
-                    const uint32_t sb = A.bucket_map ? bm_depth(A.bucket_map[(uint32_t)best - halfM]) : 0u;
-                    const int ne = sb ? sub_edge(so, (int)n, K, M, sb) : 0;
-                    const uint32_t np_ = (ne > 0 && ne < (int)n) ? 2u : 1u;
-                    const uint64_t wctx = sb ? window64(sw, sig + M) : 0ull;
-                    const uint64_t loc = alloc ? (uint64_t)atomicAdd(&span_end, np_) : rbase + nseg - bfirst;
-                    if (rounds && loc + np_ > SK_STAGE) {
-                        // stage full: resume at this record in the next round (a
-                        // slot reserved here holds no record: n = 0)
-                        if (loc < SK_STAGE) stg[loc] = 0;
-                        break;
-                    }
-                    for (uint32_t q = 0; q < np_; q++) {
-                        const int cut = q ? ne : 0;
-                        const uint64_t pn = np_ == 2 ? (q ? n - (uint64_t)ne : (uint64_t)ne) : n;
-                        const int plo = lo + cut, pso = so - cut;
-                        const uint32_t psub = sb ? sub_ctx(pso, K, M, sb, wctx, rev != 0) : 0u;
-                        // routed: the destination, computed once (the map
-                        // lookups stay out of the placement loops); else the mmer
-                        const uint32_t d = route ? region_of(A, (uint32_t)best, psub) : 0u;
-                        const uint64_t e = (uint64_t)plo | (pn << 16) | ((uint64_t)pso << 22) | (rev << 28) |
-                                           ((uint64_t)tid << 29) | ((uint64_t)(route ? d : (uint32_t)best) << 38);
-                        if (loc + q < SK_STAGE) {
-                            stg[loc + q] = e;
-                        } else if (route) {  // many destinations: one record, its own slot
-                            const uint64_t i = atomicAdd(&A.dest_ctr[d], 1ull);
-                            if (i < region_room(A.region_base, A.region_cap, d))
-                                put_record(A, A.regions + (region_off(A.region_base, A.region_cap, d) + i) * (uint64_t)A.rw,
-                                           A.ord_base + (uint32_t)r, (uint64_t)plo, pn, (uint64_t)pso, rev, sw);
+                    const uint64_t e = (uint64_t)lo | (n << 16) | ((uint64_t)(sig - lo) << 22) | (rev << 28) |
+                                       ((uint64_t)tid << 29) | ((uint64_t)(uint32_t)best << 38);
+                    const uint64_t loc = alloc ? (uint64_t)atomicAdd(&span_end, 1u) : rbase + nseg - bfirst;
+                    if (loc < SK_STAGE) {
+                        stg[loc] = e;
+                    } else if (rounds) {
+                        break;  // stage full: resume at this record in the next round
+                    } else if (route) {  // many destinations: each piece its own slot
+                        uint32_t d[2], sub[2];
+                        int ne;
+                        const uint32_t np_ = record_pieces(A, (uint32_t)best, lo, (int)n, sig - lo, rev != 0, sw, d, sub, ne);
+                        for (uint32_t q = 0; q < np_; q++) {
+                            const int cut = q ? ne : 0;
+                            const uint64_t pn = np_ == 2 && q == 0 ? (uint64_t)ne : n - (uint64_t)cut;
+                            const uint64_t i = atomicAdd(&A.dest_ctr[d[q]], 1ull);
+                            if (i < region_room(A.region_base, A.region_cap, d[q]))
+                                put_record(A, A.regions + (region_off(A.region_base, A.region_cap, d[q]) + i) * (uint64_t)A.rw,
+                                           A.ord_base + (uint32_t)r, (uint64_t)(lo + cut), pn,
+                                           (uint64_t)(sig - lo - cut), rev, sw, sub[q]);
                         }
                     }
-                    if (loc + np_ > SK_STAGE && !route && !alloc) {  // ordered records beyond the staging area: direct (scattered) stores
+                    if (loc >= SK_STAGE && !route && !alloc) {  // ordered records beyond the staging area: direct (scattered) stores
                         const uint64_t t = rbase + nseg;
                         A.pay[3 * t + 0] = (uint64_t)(A.ord_base + (uint32_t)r) | (n << 32) |
                                            ((uint64_t)(sig - lo) << 38) | (rev << 44) | ((uint64_t)lo << 45);
@@ -358,13 +375,17 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 const bool agg = A.G <= 64;  // ranks, not local buckets: aggregate per wave
                 for (uint32_t i = tid; i < span; i += SKT) {
                     const uint64_t e = stg[i];
-                    const bool none = !((e >> 16) & 63u);  // (a slot a full stage left empty)
-                    const uint32_t d = (uint32_t)(e >> 38);  // (the destination)
-                    if (agg) {
-                        if (!__ballot(!none)) continue;  // (wave-uniform)
-                        if (!none) wave_dest_add(dcnt2, d);
-                    } else if (!none) {
-                        atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1)));
+                    const uint32_t row = (uint32_t)((e >> 29) & 0x1FFu);
+                    uint32_t d[2], sub[2];
+                    int ne;
+                    const uint32_t np_ = record_pieces(A, (uint32_t)(e >> 38), (int)(e & 0xFFFFu), (int)((e >> 16) & 63u),
+                                                       (int)((e >> 22) & 63u), ((e >> 28) & 1u) != 0, smem + row * RS, d,
+                                                       sub, ne);
+                    for (uint32_t q = 0; q < np_; q++) {
+                        if (agg)
+                            wave_dest_add(dcnt2, d[q]);
+                        else
+                            atomicAdd(&dcnt2[d[q] >> 1], 1u << (16 * (d[q] & 1)));
                     }
                 }
                 __syncthreads();
@@ -379,17 +400,25 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 __syncthreads();
                 for (uint32_t i = tid; i < span; i += SKT) {
                     const uint64_t e = stg[i];
-                    if (!((e >> 16) & 63u)) continue;  // (an empty slot: wave_dest_add lanes below skip it too)
-                    const uint32_t d = (uint32_t)(e >> 38);
-                    const uint64_t slot =
-                        (uint64_t)dbase[d] +
-                        (agg ? wave_dest_add(dcnt2, d)
-                             : ((atomicAdd(&dcnt2[d >> 1], 1u << (16 * (d & 1))) >> (16 * (d & 1))) & 0xFFFFu));
-                    if (slot >= region_room(A.region_base, A.region_cap, d)) continue;  // counted: the caller retries bigger
                     const uint32_t row = (uint32_t)((e >> 29) & 0x1FFu);
-                    put_record(A, A.regions + (region_off(A.region_base, A.region_cap, d) + slot) * (uint64_t)A.rw,
-                               A.ord_base + (uint32_t)(r0 + row), e & 0xFFFFu, (e >> 16) & 63u, (e >> 22) & 63u,
-                               (e >> 28) & 1u, smem + row * RS);
+                    const int lo = (int)(e & 0xFFFFu), n = (int)((e >> 16) & 63u), so = (int)((e >> 22) & 63u);
+                    uint32_t d[2], sub[2];
+                    int ne;
+                    const uint32_t np_ = record_pieces(A, (uint32_t)(e >> 38), lo, n, so, ((e >> 28) & 1u) != 0,
+                                                       smem + row * RS, d, sub, ne);
+                    for (uint32_t q = 0; q < np_; q++) {
+                        const uint32_t dq = d[q];
+                        const uint64_t slot =
+                            (uint64_t)dbase[dq] +
+                            (agg ? wave_dest_add(dcnt2, dq)
+                                 : ((atomicAdd(&dcnt2[dq >> 1], 1u << (16 * (dq & 1))) >> (16 * (dq & 1))) & 0xFFFFu));
+                        if (slot >= region_room(A.region_base, A.region_cap, dq)) continue;  // counted: the caller retries bigger
+                        const int cut = q ? ne : 0;
+                        const int pn = np_ == 2 && q == 0 ? ne : n - cut;
+                        put_record(A, A.regions + (region_off(A.region_base, A.region_cap, dq) + slot) * (uint64_t)A.rw,
+                                   A.ord_base + (uint32_t)(r0 + row), (uint64_t)(lo + cut), (uint64_t)pn,
+                                   (uint64_t)(so - cut), (e >> 28) & 1u, smem + row * RS, sub[q]);
+                    }
                 }
             } else {
                 if (alloc) {  // the block's staged records get one contiguous range
@@ -3230,18 +3259,14 @@ DEV int bk_slot(uint32_t* keys, uint32_t bkey, bool insert) {
 // The bin key: canonical mmer << SUB_BITS | the piece's context sub-bin (0
 // unless the map splits the mmer; the record pass cut every piece to one side)
 template <int ROWS>
-DEV void bk_decode(uint64_t h, uint64_t a, uint64_t b, const BucketArgs& A, uint32_t& bkey, uint32_t& row) {
+DEV void bk_decode(uint64_t h, uint64_t a, uint64_t b, uint64_t last, const BucketArgs& A, uint32_t& bkey,
+                   uint32_t& row) {
     const int M = A.M;
     const uint32_t maskM = (1u << (2 * M)) - 1u;
     const int so = (int)((h >> 38) & 63u);
     const uint32_t sm = (uint32_t)(span_window(a, b, 0ull, 0ull, so) >> (64 - 2 * M));
-    const bool rev = ((h >> 44) & 1u) != 0;
-    const uint32_t canon = rev ? maskM - sm : sm;
-    uint32_t sub = 0;
-    if (A.bucket_map) {
-        const uint32_t sb = bm_depth(A.bucket_map[canon - (1u << (2 * M - 1))]);
-        if (sb) sub = sub_ctx(so, A.K, M, sb, span_window(a, b, 0ull, 0ull, so + M), rev);
-    }
+    const uint32_t canon = ((h >> 44) & 1u) ? maskM - sm : sm;
+    const uint32_t sub = A.sub ? (uint32_t)(last & SUB_MASK) : 0u;  // (stamped by the record pass)
     bkey = (canon << SUB_BITS) | sub;
     row = (uint32_t)ROWS - (uint32_t)((h >> 32) & 63u);
 }
@@ -3269,7 +3294,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     __syncthreads();
     constexpr int U = SPW == 2 ? 4 : 2;  // records in flight per thread
     for (uint64_t i0 = tid; i0 < cnt; i0 += U * BK_THREADS) {
-        uint64_t h[U], a[U], b[U];
+        uint64_t h[U], a[U], b[U], z[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint64_t i = i0 + (uint64_t)u * BK_THREADS;
@@ -3277,13 +3302,14 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
                 h[u] = src[RWD * i];
                 a[u] = src[RWD * i + 1];
                 b[u] = src[RWD * i + 2];
+                z[u] = SPW == 2 ? b[u] : (A.sub ? src[RWD * i + SPW] : 0ull);
             }
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (i0 + (uint64_t)u * BK_THREADS >= cnt) break;
             uint32_t bkey, row;
-            bk_decode<ROWS>(h[u], a[u], b[u], A, bkey, row);
+            bk_decode<ROWS>(h[u], a[u], b[u], z[u], A, bkey, row);
             const int sl = bk_slot(keys, bkey, true);
             if (sl < 0) s_full = 1;
             else atomicAdd(&hist[sl * ROWS + row], 1u);
@@ -3368,7 +3394,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
         for (int u = 0; u < U; u++) {
             if (i0 + (uint64_t)u * BK_THREADS >= cnt) break;
             uint32_t bkey, row;
-            bk_decode<ROWS>(h[u], a[u], b[u], A, bkey, row);
+            bk_decode<ROWS>(h[u], a[u], b[u], SPW == 2 ? b[u] : d[u], A, bkey, row);
             const int sl = bk_slot(keys, bkey, false);
             const uint64_t pos = base + atomicAdd(&hist[sl * ROWS + row], 1u);
             A.hdr[pos] = h[u];
@@ -3422,7 +3448,7 @@ template <int SPW>
 __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t* __restrict__ recs, uint64_t n_rec,
                                                                  int rw, int M, uint32_t NB, int K,
                                                                  const uint32_t* __restrict__ bucket_map,
-                                                                 const uint16_t* __restrict__ sub_map,
+                                                                 const uint16_t* __restrict__ sub_map, int sub_stamp,
                                                                  uint64_t* __restrict__ regions, uint64_t cap,
                                                                  const uint64_t* __restrict__ rbase,
                                                                  unsigned long long* bfill, uint32_t* status,
@@ -3437,50 +3463,81 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
         for (uint32_t d = threadIdx.x; d < NB; d += 256) cnt[d] = 0;
         __syncthreads();
         // per record: the destination of its (last) piece, and of its edge
-        // piece when it is cut (ne > 0 k-mers)
-        uint32_t dst[PERT], dst2[PERT], ne[PERT];
+        // piece when it is cut (ne > 0 k-mers).  In phases, so that the
+        // record loads, then the map lookups, then the sub-bin lookups of all
+        // PERT records are in flight together (one record's chain of
+        // dependent global loads at a time left the kernel latency-bound)
+        uint32_t dst[PERT], dst2[PERT], ne[PERT], sub1[PERT];  // sub1: the (last) piece's sub-bin
+        uint32_t canon[PERT], me[PERT];
         uint64_t pay0[PERT], ps[PERT][SPW];
 #pragma unroll
         for (int j = 0; j < PERT; j++) {
             const uint64_t k = k0 + (uint64_t)j * 256 + threadIdx.x;
             dst[j] = 0xFFFFFFFFu;
             ne[j] = 0;
+            sub1[j] = 0;
+            me[j] = 0;
             if (k >= n_rec) continue;
             const uint64_t* r = recs + k * (uint64_t)rw;
-            const uint64_t h = r[0];
+            pay0[j] = r[0];
 #pragma unroll
             for (int w = 0; w < SPW; w++) ps[j][w] = w + 1 < rw ? r[w + 1] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < PERT; j++) {
+            if (k0 + (uint64_t)j * 256 + threadIdx.x >= n_rec) continue;
+            const uint64_t h = pay0[j];
             const uint32_t id = (uint32_t)h;
             const uint64_t lo = (h >> 32) & 0xFFFFu, n = (h >> 48) & 63u, so = (h >> 54) & 63u;
             // the signature (so <= 56) ends inside the first two span words
             const uint32_t sm = (uint32_t)(span_window(ps[j][0], ps[j][1], 0ull, 0ull, (int)so) >> (64 - 2 * M));
             const bool rev = sm < halfM;  // complement wins (binning.c:1029-1040)
-            const uint32_t canon = rev ? maskM - sm : sm;
+            canon[j] = rev ? maskM - sm : sm;
             neg |= (int32_t)id < 0;
             kmers += n;
             pay0[j] = (uint64_t)id | (n << 32) | (so << 38) | ((uint64_t)rev << 44) | (lo << 45);
-            if (bucket_map) {
-                const uint32_t me = bucket_map[canon - halfM];
-                const uint32_t b = bm_depth(me);
-                uint32_t sub = 0;
-                if (b) {
-                    const int e = sub_edge((int)so, (int)n, K, M, b);
-                    // the context at so + M: past the first two span words
-                    // when a long (K > 31) record's first k-mers are its edge
-                    const uint64_t wc = span_window(ps[j][0], ps[j][1], SPW > 2 ? ps[j][SPW > 2 ? 2 : 0] : 0ull,
-                                                    SPW > 3 ? ps[j][SPW > 3 ? 3 : 0] : 0ull, (int)so + M);
-                    if (e > 0 && e < (int)n) {
-                        ne[j] = (uint32_t)e;
-                        dst2[j] = bm_bucket(me, sub_map, 0u);
-                        atomicAdd(&cnt[dst2[j]], 1u);
-                    }
-                    sub = sub_ctx((int)so - (int)ne[j], K, M, b, wc, rev);
+            dst[j] = 0;
+        }
+        if (bucket_map) {
+#pragma unroll
+            for (int j = 0; j < PERT; j++)
+                if (dst[j] != 0xFFFFFFFFu) me[j] = bucket_map[canon[j] - halfM];
+#pragma unroll
+            for (int j = 0; j < PERT; j++) {
+                if (dst[j] == 0xFFFFFFFFu) continue;
+                const uint32_t b = bm_depth(me[j]);
+                if (!b) {
+                    dst[j] = me[j] & 1023u;
+                    continue;
                 }
-                dst[j] = bm_bucket(me, sub_map, sub);
-            } else {
-                dst[j] = dest_of(canon, NB, BUCKET_SALT);
+                const uint64_t h = pay0[j];
+                const int n = (int)((h >> 32) & 63u), so = (int)((h >> 38) & 63u);
+                const bool rev = ((h >> 44) & 1u) != 0;
+                const int e = sub_edge(so, n, K, M, b);
+                // the context at so + M: past the first two span words
+                // when a long (K > 31) record's first k-mers are its edge
+                const uint64_t wc = span_window(ps[j][0], ps[j][1], SPW > 2 ? ps[j][SPW > 2 ? 2 : 0] : 0ull,
+                                                SPW > 3 ? ps[j][SPW > 3 ? 3 : 0] : 0ull, so + M);
+                if (e > 0 && e < n) ne[j] = (uint32_t)e;
+                sub1[j] = sub_ctx(so - (int)ne[j], K, M, b, wc, rev);
             }
+#pragma unroll
+            for (int j = 0; j < PERT; j++) {
+                if (dst[j] == 0xFFFFFFFFu || !(me[j] & BM_SPLIT)) continue;
+                const uint32_t off = me[j] & 0x0FFFFFFFu;
+                dst[j] = sub_map[off + sub1[j]];
+                if (ne[j]) dst2[j] = sub_map[off];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < PERT; j++)
+                if (dst[j] != 0xFFFFFFFFu) dst[j] = dest_of(canon[j], NB, BUCKET_SALT);
+        }
+#pragma unroll
+        for (int j = 0; j < PERT; j++) {
+            if (dst[j] == 0xFFFFFFFFu) continue;
             atomicAdd(&cnt[dst[j]], 1u);
+            if (ne[j]) atomicAdd(&cnt[dst2[j]], 1u);
         }
         __syncthreads();
         for (uint32_t d = threadIdx.x; d < NB; d += 256) {
@@ -3492,13 +3549,15 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
         for (int j = 0; j < PERT; j++) {
             if (dst[j] == 0xFFFFFFFFu) continue;
             const uint64_t h = pay0[j];
-            if (ne[j]) {  // the edge piece: the record's first ne k-mers, same span start
+            // (a bucket record's last span word carries its sub-bin, sub_room)
+            const uint64_t stamp = sub_stamp ? SUB_MASK : 0ull;
+            if (ne[j]) {  // the edge piece (sub-bin 0): the record's first ne k-mers, same span start
                 const uint64_t slot = base[dst2[j]] + atomicAdd(&cnt[dst2[j]], 1u);
                 if (slot < region_room(rbase, cap, dst2[j])) {
                     uint64_t* o = regions + (region_off(rbase, cap, dst2[j]) + slot) * (1 + SPW);
                     o[0] = (h & ~(63ull << 32)) | ((uint64_t)ne[j] << 32);
 #pragma unroll
-                    for (int w = 0; w < SPW; w++) o[1 + w] = ps[j][w];
+                    for (int w = 0; w < SPW; w++) o[1 + w] = w + 1 == SPW ? ps[j][w] & ~stamp : ps[j][w];
                 }
             }
             const uint64_t slot = base[dst[j]] + atomicAdd(&cnt[dst[j]], 1u);
@@ -3510,11 +3569,14 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
                 o[0] = (h & 0xFFFFFFFFull) | ((n - c) << 32) | ((so - c) << 38) | (h & (1ull << 44)) | ((lo + c) << 45);
                 uint64_t sw[4] = {ps[j][0], ps[j][1], SPW > 2 ? ps[j][SPW > 2 ? 2 : 0] : 0ull, SPW > 3 ? ps[j][SPW > 3 ? 3 : 0] : 0ull};
 #pragma unroll
-                for (int w = 0; w < SPW; w++) o[1 + w] = span_window(sw[0], sw[1], sw[2], sw[3], (int)c + 32 * w);
+                for (int w = 0; w < SPW; w++) {
+                    const uint64_t x = span_window(sw[0], sw[1], sw[2], sw[3], (int)c + 32 * w);
+                    o[1 + w] = w + 1 == SPW ? (x & ~stamp) | (sub1[j] & stamp) : x;
+                }
             } else {
                 o[0] = h;
 #pragma unroll
-                for (int w = 0; w < SPW; w++) o[1 + w] = ps[j][w];
+                for (int w = 0; w < SPW; w++) o[1 + w] = w + 1 == SPW ? (ps[j][w] & ~stamp) | (sub1[j] & stamp) : ps[j][w];
             }
         }
         __syncthreads();
@@ -3526,18 +3588,18 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
 }
 
 hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
-                                     int K, const uint32_t* bucket_map, const uint16_t* sub_map, uint64_t* regions,
-                                     uint64_t cap, const uint64_t* rbase, unsigned long long* bfill,
+                                     int K, const uint32_t* bucket_map, const uint16_t* sub_map, int sub_stamp,
+                                     uint64_t* regions, uint64_t cap, const uint64_t* rbase, unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s) {
     if (!n_rec) return hipSuccess;
     if (NB < 1 || NB > SK_MAX_DEST || (spw != 2 && spw != 4)) return hipErrorInvalidValue;
     const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
     if (spw == 2)
         hipLaunchKernelGGL(sk_convert_buckets_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, K, bucket_map, sub_map, regions, cap, rbase, bfill, status, n_kmers);
+                           NB, K, bucket_map, sub_map, sub_stamp, regions, cap, rbase, bfill, status, n_kmers);
     else
         hipLaunchKernelGGL(sk_convert_buckets_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, K, bucket_map, sub_map, regions, cap, rbase, bfill, status, n_kmers);
+                           NB, K, bucket_map, sub_map, sub_stamp, regions, cap, rbase, bfill, status, n_kmers);
     return hipGetLastError();
 }
 

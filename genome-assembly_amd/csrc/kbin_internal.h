@@ -115,6 +115,7 @@ struct SkScanArgs {
     // sub-bins (at most two pieces each) on the way into the buckets
     const uint32_t* bucket_map;
     const uint16_t* sub_map;
+    int sub_stamp;             // the map splits mmers: bucket records carry their sub-bin (sub_room)
     // partitioned passes (kb_set_partition): only super-k-mers whose mmer is in
     // partition part of part_n are emitted and counted (part_n <= 1: all)
     uint32_t part, part_n;
@@ -135,9 +136,7 @@ struct BucketArgs {
     uint64_t* w3;
     int spw;                   // span words per record: 2 (K <= 31) or 4 (K <= 63)
     uint64_t* bbase;           // [NB + 1] output base of each bucket (bucket_bases_kernel)
-    const uint32_t* bucket_map;  // or null: the map the record pass used (a split mmer's
-                                 // records are grouped by (mmer, context sub-bin))
-    int K;
+    int sub;                   // records carry their context sub-bin (sub_room): group by (mmer, sub-bin)
     uint32_t* bocc;            // [max_bins] k-mer occurrences of the bin (0: not counted), or null
     unsigned long long* bin_ctr;   // bins (zeroed; = totals[2])
     uint32_t* bstart;          // [max_bins] first record of bin
@@ -184,6 +183,14 @@ __device__ __forceinline__ uint32_t bm_depth(uint32_t e) { return (e & BM_SPLIT)
 __device__ __forceinline__ uint32_t bm_bucket(uint32_t e, const uint16_t* sub_map, uint32_t sub) {
     return (e & BM_SPLIT) ? (uint32_t)sub_map[(e & 0x0FFFFFFFu) + sub] : (e & 1023u);
 }
+// A bucket record carries its sub-bin in the low SUB_BITS of its last span
+// word: the span holds n + K - 1 <= 2K - M bases of its 32 x spw, and those
+// bits (the last 4.5 base positions) lie past every k-mer the bin kernels
+// read.  Splitting needs that room (and the bucket ordering then groups the
+// records by (mmer, sub-bin) without the map).
+__host__ __device__ inline bool sub_room(int K, int M, int spw) { return 32 * spw - (2 * K - M) >= 5; }
+constexpr uint64_t SUB_MASK = (1ull << SUB_BITS) - 1ull;
+
 // k-mers of a record (sig offset so, n k-mers) in the edge of depth b: its first ones
 __device__ __forceinline__ int sub_edge(int so, int n, int K, int M, uint32_t b) {
     const int e = so - (K - M - (int)b);
@@ -360,7 +367,7 @@ hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, co
                                 uint32_t* bcount, uint32_t* bmmer, uint64_t max_bins, hipStream_t s);
 // received records into local bucket regions (block-aggregated reservations)
 hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int rw, int spw, int M, uint32_t NB,
-                                     int K, const uint32_t* bucket_map, const uint16_t* sub_map,
+                                     int K, const uint32_t* bucket_map, const uint16_t* sub_map, int sub_stamp,
                                      uint64_t* regions, uint64_t cap, const uint64_t* rbase, unsigned long long* bfill,
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s);
 size_t bins_lds_bytes(uint32_t ts_log2, int KW);
