@@ -1201,7 +1201,7 @@ static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
     int bmax = std::min<int>((int)SUB_MAX_B, std::max(0, env_int("KB_BIN_SUB", (int)SUB_MAX_B)));
     if (!sub_room(c->p.K, c->p.M, 2 * c->KW)) bmax = 0;  // (no spare span bits for the stamp)
     const double ts = c->KW == 1 ? 8192.0 : 4096.0;
-    const double cap = ts * std::min(0.85, std::max(0.2, env_int("KB_BIN_SUB_FILL_PCT", 50) / 100.0));
+    const double cap = ts * std::min(4.0, std::max(0.2, env_int("KB_BIN_SUB_FILL_PCT", 80) / 100.0));
     uint32_t b = 0;
     while ((int)b < bmax && (keys / (double)(1u << (2 * b)) > cap || w / (double)(1u << (2 * b)) > 1.5 * mean)) b++;
     return b;
