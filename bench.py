@@ -255,8 +255,10 @@ def dropin_leg(words, lens, n, wpr, L, K, M, cutoff, device):
     row["process_wall_ms"] = round(wall * 1e3, 1)
     row["kmers_per_s"] = round(row["kmers"] / row["total_ms"] * 1e3, 1)
     row["note"] = ("kbin_main: fgets + process_read loop (async batched kb_submit) -> prune_data "
-                   "(kb_finalize, kb_export, materialise zhash/ll_node tables, prune); process_wall_ms adds "
-                   "process start, HIP init and the file read")
+                   "(kb_finalize, kb_export, direct zhash layout: every table's insertion/rehash history "
+                   "replayed on integer codes, only surviving entries and their ll_node lists allocated); "
+                   "total_ms = read loop + prune_data; process_wall_ms adds process start, HIP init and "
+                   "the file read")
     return row
 
 

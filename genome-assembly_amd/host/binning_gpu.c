@@ -7,6 +7,7 @@
  * materialises the surviving (mmer, kmer) entries into the caller's level-1
  * table as reference-layout ZHashTable / ll_node structures.
  */
+#include <malloc.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -196,6 +197,8 @@ static uint64_t *first_order(const kb_csr *r)
 static long n_threads(void)
 {
     long nt = sysconf(_SC_NPROCESSORS_ONLN);
+    const char *env = getenv("KBH_THREADS");
+    if (env && atol(env) > 0) nt = atol(env);
     if (nt < 1) nt = 1;
     return nt > 16 ? 16 : nt;
 }
@@ -259,10 +262,13 @@ static void *fill_tables(void *arg)
     return NULL;
 }
 
-/* Rebuild the reference's two-level table from the CSR: level 1 (mmer ->
- * level-2 table) in the order the reference creates its entries (the first
- * occurrence of any key of that mmer), then every level-2 table as above. */
-static void materialise(struct ZHashTable *level1, const kb_csr *r, int prune)
+/* REPLAY: rebuild the reference's two-level table from the CSR by calling
+ * zhash_set in the reference's insertion order -- level 1 (mmer -> level-2
+ * table) in the order the reference creates its entries (the first occurrence
+ * of any key of that mmer), then every level-2 table as above.  Used when the
+ * caller's table already holds entries, and by the tests as the check on the
+ * direct layout below (kbh_materialise_csr). */
+static void materialise_replay(struct ZHashTable *level1, const kb_csr *r, int prune)
 {
     char ms[17];
     const uint64_t n = r->n_entries;
@@ -313,6 +319,443 @@ static void materialise(struct ZHashTable *level1, const kb_csr *r, int prune)
     free(gid);
     free(l2);
     free(order);
+}
+
+
+/* DIRECT layout (the default): the final shape of every table -- size step,
+ * bucket chains and their order -- is a function of the keys' insertion order
+ * alone, so it is computed on integer codes and only the SURVIVING entries are
+ * allocated and linked; no strings are hashed, no table is ever rehashed in
+ * memory and pruned keys cost no allocation.
+ *
+ *   bucket (zhash.c:171-182): h = fold (17 h + c) mod m over the key's chars,
+ *     i.e. the key's base-17 value P mod m; P is split into 15-char chunks
+ *     (each < 2^64 for chars <= 'T'), h = sum_t (chunk_t mod m)(17^15t mod m)
+ *     mod m;
+ *   zhash_set (zhash.c:53-76): push on the chain head; after the insert, if
+ *     entry_count > m / 2 rehash to the next ladder step;
+ *   zhash_rehash (zhash.c:184-214): walk the old buckets 0..m-1, each chain
+ *     head to tail, pushing every entry onto the head of its new chain;
+ *   the prune (binning.c:1085-1144) unlinks entries through iterators, which
+ *     never resize: survivors keep their relative chain order, a level-2
+ *     table left empty is dropped from level 1, and level 1 keeps the size of
+ *     its full history.
+ * Each table's history is replayed on int32 chains (the ladder steps it
+ * passes through), then its final chains are walked once to allocate and link
+ * the survivors.  Tables are independent: worker threads take them largest
+ * first. */
+#define CHUNK_CHARS 15
+#define MAX_CHUNKS 5 /* K <= 63 */
+#define LADDER_TOP 23
+
+static uint64_t g_pw[LADDER_TOP][MAX_CHUNKS]; /* 17^(15 t) mod m_s */
+
+static void init_powers(void)
+{
+    for (int s = 0; s < LADDER_TOP; s++) {
+        const uint64_t m = LADDER[s];
+        uint64_t p15 = 1;
+        for (int i = 0; i < CHUNK_CHARS; i++) p15 = p15 * 17 % m;
+        uint64_t p = 1 % m;
+        for (int t = 0; t < MAX_CHUNKS; t++) {
+            g_pw[s][t] = p;
+            p = p * p15 % m;
+        }
+    }
+}
+
+/* base-17 chunks of the key string for the 2-bit code (char j of the string
+ * is code bits 2(n-1-j)); chunk t holds powers 17^(15t .. 15t+14) */
+static int key_chunks(uint64_t hi, uint64_t lo, int n, uint64_t *ch)
+{
+    const int nc = (n + CHUNK_CHARS - 1) / CHUNK_CHARS;
+    for (int t = 0; t < nc; t++) ch[t] = 0;
+    for (int p = n - 1; p >= 0; p--) { /* p = power of 17 = distance from the end */
+        const unsigned c2 = p >= 32 ? (unsigned)(hi >> (2 * (p - 32))) & 3u : (unsigned)(lo >> (2 * p)) & 3u;
+        uint64_t *a = &ch[p / CHUNK_CHARS];
+        *a = *a * 17 + (unsigned char)BP[c2];
+    }
+    return nc;
+}
+
+static inline uint32_t bucket_at(const uint64_t *ch, int nc, int s)
+{
+    const uint64_t m = LADDER[s];
+    uint64_t h = 0;
+    for (int t = 0; t < nc; t++) h += (ch[t] % m) * g_pw[s][t];
+    return (uint32_t)(h % m);
+}
+
+static int final_step(uint64_t n)
+{
+    int s = 0;
+    for (uint64_t c = 1; c <= n; c++)
+        if (c > LADDER[s] / 2 && s + 1 < LADDER_TOP) s++;
+    return s;
+}
+
+/* per-thread scratch of the replay */
+typedef struct {
+    uint64_t *ch;   /* [n * nc] key chunks */
+    int32_t *next;  /* [n] chain links */
+    int32_t *head, *nhead;
+    uint64_t cap_n, cap_m;
+} replay_buf;
+
+static void replay_reserve(replay_buf *b, uint64_t n, int nc, uint64_t m)
+{
+    if (n > b->cap_n) {
+        free(b->ch);
+        free(b->next);
+        b->cap_n = n + n / 2;
+        b->ch = xmalloc(b->cap_n * MAX_CHUNKS * sizeof(uint64_t));
+        b->next = xmalloc(b->cap_n * sizeof(int32_t));
+    }
+    if (m > b->cap_m) {
+        free(b->head);
+        free(b->nhead);
+        b->cap_m = m;
+        b->head = xmalloc(m * sizeof(int32_t));
+        b->nhead = xmalloc((m + 1) * sizeof(int32_t));
+    }
+    (void)nc;
+}
+
+/* Replays n inserts (key i's chunks at ch + i*nc); returns the final step and
+ * leaves the final chains in b->head[0..m) / b->next (-1 terminated). */
+static int replay(replay_buf *b, uint64_t n, int nc)
+{
+    int s = 0;
+    uint64_t m = LADDER[0];
+    memset(b->head, 0xFF, m * sizeof(int32_t));
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t h = bucket_at(b->ch + i * nc, nc, s);
+        b->next[i] = b->head[h];
+        b->head[h] = (int32_t)i;
+        if (i + 1 > m / 2 && s + 1 < LADDER_TOP) {
+            const uint64_t nm = LADDER[s + 1];
+            memset(b->nhead, 0xFF, nm * sizeof(int32_t));
+            for (uint64_t bk = 0; bk < m; bk++) {
+                for (int32_t j = b->head[bk]; j >= 0;) {
+                    const int32_t nx = b->next[j];
+                    const uint32_t h2 = bucket_at(b->ch + (uint64_t)j * nc, nc, s + 1);
+                    b->next[j] = b->nhead[h2];
+                    b->nhead[h2] = j;
+                    j = nx;
+                }
+            }
+            int32_t *t = b->head;
+            b->head = b->nhead;
+            b->nhead = t;
+            s++;
+            m = nm;
+        }
+    }
+    return s;
+}
+
+static struct ZHashTable *new_table(int s, uint64_t count)
+{
+    struct ZHashTable *t = xmalloc(sizeof *t);
+    t->size_index = (size_t)s;
+    t->entry_count = count;
+    t->entries = calloc(LADDER[s], sizeof(struct ZHashEntry *));
+    if (!t->entries) exit(EXIT_FAILURE);
+    return t;
+}
+
+static struct ZHashEntry *new_entry(const char *key, size_t klen, void *val)
+{
+    struct ZHashEntry *e = xmalloc(sizeof *e);
+    e->key = xmalloc(klen + 1);
+    memcpy(e->key, key, klen + 1);
+    e->val = val;
+    e->next = NULL;
+    return e;
+}
+
+/* an entry as the replay and the linking need it, gathered once by the
+ * grouping scatter (sequential reads of the CSR): insertion stamp, list start
+ * with the survivor flag in bit 63, list length, k-mer code */
+typedef struct {
+    uint64_t first, o0, len, lo, hi;
+} key_rec;
+#define REC_ALIVE (1ull << 63)
+
+typedef struct {
+    const kb_csr *r;
+    key_rec *grouped;         /* entries grouped by mmer */
+    const uint64_t *gstart;   /* [nm + 1] */
+    const uint32_t *work;     /* mmers, largest group first */
+    struct ZHashTable **l2;   /* [nm] out: level-2 table (NULL: none survives) */
+    uint64_t *gfirst;         /* [nm] out: first sight of the mmer */
+    uint64_t n_work, next, nodes, kept;
+} direct_job;
+
+/* in-place sort of a group by insertion stamp (stamps are distinct) */
+static void sort_recs(key_rec *a, int64_t n)
+{
+    while (n > 24) {
+        const uint64_t x = a[0].first, y = a[n / 2].first, z = a[n - 1].first;
+        const uint64_t piv = x < y ? (y < z ? y : (x < z ? z : x)) : (x < z ? x : (y < z ? z : y));
+        int64_t i = 0, k = n - 1;
+        for (;;) {
+            while (a[i].first < piv) i++;
+            while (a[k].first > piv) k--;
+            if (i >= k) break;
+            const key_rec t = a[i];
+            a[i++] = a[k];
+            a[k--] = t;
+        }
+        /* [0, k] <= piv <= [k + 1, n): recurse on the smaller side */
+        if (k + 1 < n - k - 1) {
+            sort_recs(a, k + 1);
+            a += k + 1;
+            n -= k + 1;
+        } else {
+            sort_recs(a + k + 1, n - k - 1);
+            n = k + 1;
+        }
+    }
+    for (int64_t i = 1; i < n; i++) {
+        const key_rec t = a[i];
+        int64_t k = i;
+        for (; k > 0 && a[k - 1].first > t.first; k--) a[k] = a[k - 1];
+        a[k] = t;
+    }
+}
+
+static void *direct_tables(void *arg)
+{
+    direct_job *j = arg;
+    const kb_csr *r = j->r;
+    const int nc = (g_K + CHUNK_CHARS - 1) / CHUNK_CHARS;
+    replay_buf b = {0};
+    uint64_t nodes = 0, kept = 0;
+    char ks[129];
+    for (;;) {
+        const uint64_t w = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+        if (w >= j->n_work) break;
+        const uint32_t mm = j->work[w];
+        const uint64_t g0 = j->gstart[mm], n = j->gstart[mm + 1] - g0;
+        key_rec *fk = j->grouped + g0;
+        uint64_t alive = 0;
+        for (uint64_t i = 0; i < n; i++) alive += fk[i].o0 >> 63;
+        sort_recs(fk, (int64_t)n); /* insertion order */
+        j->gfirst[mm] = fk[0].first;
+        if (!alive) continue; /* the prune drops the whole table */
+        replay_reserve(&b, n, nc, LADDER[final_step(n)]);
+        for (uint64_t i = 0; i < n; i++) key_chunks(fk[i].hi, fk[i].lo, g_K, b.ch + i * nc);
+        const int s = replay(&b, n, nc);
+        struct ZHashTable *t = new_table(s, alive);
+        /* survivors in chain order, per bucket (in the scratch the replay
+         * no longer needs: the chunks and the spare head array) */
+        int32_t *ord = (int32_t *)b.ch, q = 0;
+        uint32_t *bstart = (uint32_t *)b.nhead;
+        for (uint64_t bk = 0; bk < LADDER[s]; bk++) {
+            bstart[bk] = (uint32_t)q;
+            for (int32_t i = b.head[bk]; i >= 0; i = b.next[i])
+                if (fk[i].o0 & REC_ALIVE) ord[q++] = i;
+        }
+        bstart[LADDER[s]] = (uint32_t)q;
+        for (uint64_t bk = 0; bk < LADDER[s]; bk++) {
+            struct ZHashEntry **tail = &t->entries[bk];
+            for (uint32_t p = bstart[bk]; p < bstart[bk + 1]; p++) {
+                const key_rec *kr = &fk[ord[p]];
+                if (p + 4 < (uint32_t)q) __builtin_prefetch(&r->ids[fk[ord[p + 4]].o0 & ~REC_ALIVE]);
+                const uint64_t o0 = kr->o0 & ~REC_ALIVE, o1 = o0 + kr->len;
+                ll_node *head = NULL, **lt = &head;
+                for (uint64_t k = o0; k < o1; k++) {
+                    ll_node *nd = xmalloc(sizeof *nd); /* create_node_num, llist.c:6-11 */
+                    nd->next = NULL;
+                    nd->read_id = r->ids[k];
+                    *lt = nd;
+                    lt = &nd->next;
+                }
+                nodes += o1 - o0;
+                code_to_str(kr->hi, kr->lo, g_K, ks);
+                *tail = new_entry(ks, (size_t)g_K, head);
+                tail = &(*tail)->next;
+            }
+        }
+        kept += alive;
+        j->l2[mm] = t;
+    }
+    free(b.ch);
+    free(b.next);
+    free(b.head);
+    free(b.nhead);
+    __atomic_fetch_add(&j->nodes, nodes, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&j->kept, kept, __ATOMIC_RELAXED);
+    return NULL;
+}
+
+typedef struct {
+    const kb_csr *r;
+    uint64_t lo, hi;
+    uint64_t *cnt; /* [nm] this slice's histogram, then its scatter cursors */
+    key_rec *grouped;
+    int prune;
+} group_slice;
+
+static void *slice_count(void *arg)
+{
+    group_slice *g = arg;
+    for (uint64_t e = g->lo; e < g->hi; e++) g->cnt[g->r->mmer[e]]++;
+    return NULL;
+}
+
+/* survivor test of the prune (binning.c:1093-1102: fewer than cutoff + 1
+ * list nodes) */
+static void *slice_scatter(void *arg)
+{
+    group_slice *g = arg;
+    const kb_csr *r = g->r;
+    for (uint64_t e = g->lo; e < g->hi; e++) {
+        key_rec *k = &g->grouped[g->cnt[r->mmer[e]]++];
+        const int alive = !g->prune ||
+                          ((int)r->count[e] > g_cutoff && (int64_t)(r->offset[e + 1] - r->offset[e]) > g_cutoff);
+        k->first = r->first ? r->first[e] : e;
+        k->o0 = r->offset[e] | (alive ? REC_ALIVE : 0);
+        k->len = r->offset[e + 1] - r->offset[e];
+        k->lo = r->kmer_lo[e];
+        k->hi = r->kmer_hi[e];
+    }
+    return NULL;
+}
+
+static void run_slices(void *(*fn)(void *), group_slice *sl, long nt)
+{
+    pthread_t th[16];
+    int started[16] = {0};
+    for (long t = 1; t < nt; t++) started[t] = pthread_create(&th[t], NULL, fn, &sl[t]) == 0;
+    fn(&sl[0]);
+    for (long t = 1; t < nt; t++)
+        if (started[t]) pthread_join(th[t], NULL);
+        else fn(&sl[t]);
+}
+
+static const uint64_t *g_sort_first; /* level-1 order: qsort has no context argument */
+static int cmp_mmer_first(const void *a, const void *b)
+{
+    const uint64_t x = g_sort_first[*(const uint32_t *)a], y = g_sort_first[*(const uint32_t *)b];
+    return x < y ? -1 : x > y;
+}
+
+static const uint64_t *g_sort_size;
+static int cmp_mmer_size(const void *a, const void *b)
+{
+    const uint64_t x = g_sort_size[*(const uint32_t *)a], y = g_sort_size[*(const uint32_t *)b];
+    return x > y ? -1 : x < y;
+}
+
+static void materialise_direct(struct ZHashTable *level1, const kb_csr *r, int prune)
+{
+    static pthread_once_t once = PTHREAD_ONCE_INIT;
+    pthread_once(&once, init_powers);
+    const uint64_t n = r->n_entries;
+    const uint32_t nm = 1u << (2 * g_M);
+    const long nt = n_threads();
+    double t = now_ms();
+    /* 1. entries grouped by mmer: per-slice histograms, then a stable scatter */
+    group_slice sl[16];
+    key_rec *grouped = xmalloc((n ? n : 1) * sizeof(key_rec));
+    uint64_t *gstart = calloc((size_t)nm + 1, sizeof(uint64_t));
+    if (!gstart) exit(EXIT_FAILURE);
+    for (long s = 0; s < nt; s++) {
+        sl[s].r = r;
+        sl[s].lo = n * (uint64_t)s / (uint64_t)nt;
+        sl[s].hi = n * (uint64_t)(s + 1) / (uint64_t)nt;
+        sl[s].cnt = calloc(nm, sizeof(uint64_t));
+        if (!sl[s].cnt) exit(EXIT_FAILURE);
+        sl[s].grouped = grouped;
+        sl[s].prune = prune;
+    }
+    run_slices(slice_count, sl, nt);
+    uint64_t run = 0;
+    for (uint32_t m = 0; m < nm; m++) {
+        gstart[m] = run;
+        for (long s = 0; s < nt; s++) {
+            const uint64_t c = sl[s].cnt[m];
+            sl[s].cnt[m] = run;
+            run += c;
+        }
+    }
+    gstart[nm] = run;
+    run_slices(slice_scatter, sl, nt);
+    for (long s = 0; s < nt; s++) free(sl[s].cnt);
+    uint32_t *work = xmalloc(nm * sizeof(uint32_t)), nw = 0;
+    uint64_t *gsize = xmalloc(nm * sizeof(uint64_t));
+    for (uint32_t m = 0; m < nm; m++) {
+        gsize[m] = gstart[m + 1] - gstart[m];
+        if (gsize[m]) work[nw++] = m;
+    }
+    g_sort_size = gsize;
+    qsort(work, nw, sizeof(uint32_t), cmp_mmer_size);
+    g_times.order_ms = now_ms() - t;
+    /* 2. level-2 tables (worker threads) */
+    t = now_ms();
+    direct_job j = {r, grouped, gstart, work, calloc(nm, sizeof(struct ZHashTable *)),
+                    xmalloc(nm * sizeof(uint64_t)), nw, 0, 0, 0};
+    if (!j.l2) exit(EXIT_FAILURE);
+    /* ~10^8 small blocks: grow the arenas in 64 MB steps, not 128 KB ones
+     * (each growth is a syscall under the process's address-space lock,
+     * which the page faults of the other workers also take); restored to
+     * glibc's default after */
+    mallopt(M_TOP_PAD, 64 << 20);
+    run_workers(direct_tables, &j, nt);
+    mallopt(M_TOP_PAD, 128 << 10);
+    g_times.fill_ms = now_ms() - t;
+    g_times.nodes += j.nodes;
+    /* 3. level 1: every mmer in first-sight order, survivors linked */
+    t = now_ms();
+    g_sort_first = j.gfirst;
+    qsort(work, nw, sizeof(uint32_t), cmp_mmer_first);
+    replay_buf b = {0};
+    replay_reserve(&b, nw ? nw : 1, 1, LADDER[final_step(nw)]);
+    for (uint32_t i = 0; i < nw; i++) key_chunks(0, work[i], g_M, b.ch + i);
+    const int s1 = replay(&b, nw, 1);
+    uint64_t kept1 = 0;
+    for (uint32_t i = 0; i < nw; i++) kept1 += j.l2[work[i]] != NULL;
+    free(level1->entries);
+    level1->size_index = (size_t)s1;
+    level1->entry_count = kept1;
+    level1->entries = calloc(LADDER[s1], sizeof(struct ZHashEntry *));
+    if (!level1->entries) exit(EXIT_FAILURE);
+    char ms[17];
+    for (uint64_t bk = 0; bk < LADDER[s1]; bk++) {
+        struct ZHashEntry **tail = &level1->entries[bk];
+        for (int32_t i = b.head[bk]; i >= 0; i = b.next[i]) {
+            struct ZHashTable *l2 = j.l2[work[i]];
+            if (!l2) continue;
+            code_to_str(0, work[i], g_M, ms);
+            *tail = new_entry(ms, (size_t)g_M, l2);
+            tail = &(*tail)->next;
+        }
+    }
+    free(b.ch);
+    free(b.next);
+    free(b.head);
+    free(b.nhead);
+    g_times.group_ms = now_ms() - t;
+    free(j.l2);
+    free(j.gfirst);
+    free(work);
+    free(gsize);
+    free(gstart);
+    free(grouped);
+}
+
+/* direct layout for a fresh table (the reference path: prune_data on the
+ * table process_read filled), replay otherwise */
+static int materialise(struct ZHashTable *level1, const kb_csr *r, int prune)
+{
+    if (level1->entry_count == 0 && level1->size_index == 0 && g_M <= CHUNK_CHARS && getenv("KBH_REPLAY") == NULL) {
+        materialise_direct(level1, r, prune);
+        return 1; /* already pruned */
+    }
+    materialise_replay(level1, r, prune);
+    return 0;
 }
 
 /* prune_kmers / prune_data semantics on the materialised table
@@ -401,14 +844,69 @@ static struct ZHashTable *finish(struct ZHashTable *hash_table, int prune)
     g_times.entries = r.n_entries;
     g_times.ids = r.n_ids;
     t = now_ms();
-    materialise(hash_table, &r, prune);
+    const int done = materialise(hash_table, &r, prune);
     g_times.materialise_ms = now_ms() - t;
     t = now_ms();
-    if (prune) prune_materialised(hash_table, g_cutoff);
+    if (prune && !done) prune_materialised(hash_table, g_cutoff);
     g_times.prune_ms = now_ms() - t;
+    t = now_ms();
     kbh_release(hash_table);
+    g_times.release_ms = now_ms() - t;
     g_times.total_ms = now_ms() - t0;
     return hash_table;
+}
+
+int kbh_materialise_csr(struct ZHashTable *hash_table, const kb_csr *r, int prune, int replay_only)
+{
+    if (!hash_table || !r) return KB_EINVAL;
+    memset(&g_times, 0, sizeof g_times);
+    int done;
+    if (replay_only) {
+        materialise_replay(hash_table, r, prune);
+        done = 0;
+    } else {
+        done = materialise(hash_table, r, prune);
+    }
+    if (prune && !done) prune_materialised(hash_table, g_cutoff);
+    return KB_OK;
+}
+
+static uint64_t mix64(uint64_t x)
+{
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+static uint64_t str_hash(const char *s)
+{
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    for (; *s; s++) h = mix64(h ^ (unsigned char)*s);
+    return h;
+}
+
+uint64_t kbh_layout_digest(struct ZHashTable *level1)
+{
+    uint64_t h = mix64(level1->size_index * 1000003u + level1->entry_count);
+    const size_t m1 = LADDER[level1->size_index];
+    for (size_t b1 = 0; b1 < m1; b1++) {
+        for (struct ZHashEntry *me = level1->entries[b1]; me; me = me->next) {
+            struct ZHashTable *level2 = me->val;
+            h = mix64(h ^ b1 ^ str_hash(me->key));
+            h = mix64(h ^ (level2->size_index << 40) ^ level2->entry_count);
+            const size_t m2 = LADDER[level2->size_index];
+            for (size_t b2 = 0; b2 < m2; b2++) {
+                for (struct ZHashEntry *ke = level2->entries[b2]; ke; ke = ke->next) {
+                    h = mix64(h ^ (b2 << 1) ^ str_hash(ke->key));
+                    for (ll_node *t = ke->val; t; t = t->next) h = mix64(h ^ (uint32_t)t->read_id);
+                    h = mix64(h + 1);
+                }
+            }
+        }
+    }
+    return h;
 }
 
 /* binning.c:1130 */

@@ -61,10 +61,10 @@ int main(int argc, char **argv)
                 "{\"reads\": %d, \"kmers\": %lld, \"read_loop_ms\": %.3f, \"finalize_ms\": %.3f, "
                 "\"export_ms\": %.3f, \"materialise_ms\": %.3f, \"prune_ms\": %.3f, \"total_ms\": %.3f, "
                 "\"entries\": %llu, \"ids\": %llu, \"nodes\": %llu, \"materialise_order_ms\": %.3f, "
-                "\"materialise_group_ms\": %.3f, \"materialise_fill_ms\": %.3f}\n",
+                "\"materialise_group_ms\": %.3f, \"materialise_fill_ms\": %.3f, \"release_ms\": %.3f}\n",
                 read_id, kmers, loop, t.finalize_ms, t.export_ms, t.materialise_ms, t.prune_ms, loop + t.total_ms,
                 (unsigned long long)t.entries, (unsigned long long)t.ids, (unsigned long long)t.nodes, t.order_ms,
-                t.group_ms, t.fill_ms);
+                t.group_ms, t.fill_ms, t.release_ms);
     }
     if (!(denv && *denv == '1')) kbh_dump_table(hash_table, stdout);
     return 0;

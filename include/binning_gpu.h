@@ -30,6 +30,7 @@
 #include <stdio.h>
 
 #include "kb_zhash.h"
+#include "kbin.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -54,11 +55,23 @@ typedef struct {
     uint64_t entries;       /* keys materialised (all, before the prune) */
     uint64_t ids;           /* ids exported */
     uint64_t nodes;         /* ll_nodes allocated (kept keys only when pruning) */
-    double order_ms;        /* materialise: first-occurrence order (radix sort) */
-    double group_ms;        /* materialise: level 1 + grouping by mmer (one thread) */
+    double order_ms;        /* materialise: entries grouped by mmer (direct layout;
+                               replay: first-occurrence radix sort) */
+    double group_ms;        /* materialise: level 1 */
     double fill_ms;         /* materialise: level-2 tables and lists (worker threads) */
+    double release_ms;      /* kbh_release: the engine context's device and pinned memory */
 } kbh_times;
 int kbh_last_times(kbh_times *out);
+
+/* Materialise a CSR (kb_export layout, `first` = insertion order) into
+ * hash_table exactly as prune_data does (prune: the cutoff set by
+ * kbh_configure).  replay_only: build it by zhash_set in insertion order (the
+ * slow, obviously-reference path) instead of the direct layout -- the two
+ * must give identical tables (kbh_layout_digest). */
+int kbh_materialise_csr(struct ZHashTable *hash_table, const kb_csr *r, int prune, int replay_only);
+/* digest of a two-level table's exact layout: size steps, counts, bucket
+ * index and chain order of every entry, keys, list contents and order */
+uint64_t kbh_layout_digest(struct ZHashTable *hash_table);
 
 /* drop the engine context bound to hash_table (the tables stay) */
 void kbh_release(struct ZHashTable *hash_table);

@@ -1,0 +1,71 @@
+"""The drop-in's DIRECT table layout (binning_gpu.c materialise_direct: the
+zhash history replayed on integer codes, survivors only allocated) against the
+REPLAY (zhash_set of every key in first-occurrence order, then the prune's
+unlinks, zhash.c:53-76/184-214, binning.c:1085-1144) on synthetic CSRs:
+identical size steps, bucket chains, chain order, keys and lists
+(kbh_layout_digest).  No GPU: the CSR is host memory built here."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import kbin
+
+
+def host_lib():
+    lib = C.CDLL(str(kbin.HOST_LIB_PATH))
+    lib.zcreate_hash_table.restype = C.c_void_p
+    lib.kbh_materialise_csr.argtypes = [C.c_void_p, C.POINTER(kbin.kb_csr), C.c_int, C.c_int]
+    lib.kbh_layout_digest.argtypes = [C.c_void_p]
+    lib.kbh_layout_digest.restype = C.c_uint64
+    lib.kbh_dump_table.argtypes = [C.c_void_p, C.c_void_p]
+    return lib
+
+
+def synthetic_csr(rng, n, K, M, heavy=0):
+    """n distinct (mmer, kmer) keys with unique first-occurrence stamps,
+    counts 1..4 (a third at 1: pruned at cutoff 1), `heavy` keys piled on one
+    mmer (a table that climbs many ladder steps)"""
+    nm = 1 << (2 * M)
+    mmer = rng.integers(0, nm, n, dtype=np.uint64).astype(np.uint32)
+    mmer[:heavy] = 5 % nm
+    bits = 2 * K
+    lo = rng.integers(0, 2**63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    hi = rng.integers(0, 2**63, n, dtype=np.uint64)
+    if bits < 64:
+        lo &= np.uint64((1 << bits) - 1)
+        hi[:] = 0
+    elif bits < 128:
+        hi &= np.uint64((1 << (bits - 64)) - 1)
+    lo[:] = lo ^ np.arange(n, dtype=np.uint64) << np.uint64(min(bits, 64) - 24)  # distinct keys
+    if bits < 64:
+        lo &= np.uint64((1 << bits) - 1)
+    key = np.stack([mmer.astype(np.uint64), hi, lo], 1)
+    assert len(np.unique(key, axis=0)) == n
+    count = rng.choice([1, 1, 2, 3, 4], n).astype(np.uint32)
+    offset = np.zeros(n + 1, np.uint64)
+    offset[1:] = np.cumsum(count)
+    ids = rng.integers(0, 1 << 30, int(offset[-1])).astype(np.int32)
+    first = (rng.permutation(n).astype(np.uint64) << np.uint64(16)) | rng.integers(0, 300, n, dtype=np.uint64)
+    arrays = dict(mmer=mmer, kmer_hi=hi, kmer_lo=lo, count=count, offset=offset, ids=ids, first=first)
+    c = kbin.kb_csr()
+    c.n_entries, c.n_ids = n, int(offset[-1])
+    for f, a in arrays.items():
+        setattr(c, f, a.ctypes.data_as(dict(kbin.kb_csr._fields_)[f]))
+    return c, arrays
+
+
+@pytest.mark.parametrize("n,K,M,heavy", [(0, 31, 7, 0), (1, 31, 7, 0), (3000, 31, 7, 0), (40000, 21, 3, 0),
+                                         (20000, 31, 7, 12000), (20000, 63, 7, 3000), (5000, 32, 4, 0),
+                                         (30000, 27, 6, 30000)])
+@pytest.mark.parametrize("prune", [1, 0])
+def test_direct_layout_equals_replay(n, K, M, heavy, prune):
+    lib = host_lib()
+    rng = np.random.default_rng(n + K + M + heavy)
+    csr, keep = synthetic_csr(rng, n, K, M, heavy)
+    assert lib.kbh_configure(K, M, 1, 0) == 0
+    a, b = lib.zcreate_hash_table(), lib.zcreate_hash_table()
+    assert lib.kbh_materialise_csr(a, C.byref(csr), prune, 1) == 0
+    assert lib.kbh_materialise_csr(b, C.byref(csr), prune, 0) == 0
+    assert lib.kbh_layout_digest(a) == lib.kbh_layout_digest(b)
+    del keep
