@@ -103,7 +103,7 @@ static void pack_code(const char *s, int n, uint64_t *hi, uint64_t *lo)
 
 /* process_read restated (binning.c:902-1076).  Emits one record per k-mer. */
 static int scan_read(const char *read, int read_len, int K, int M, uint32_t ord,
-                     recvec_t *out, int *alphabet_ok)
+                     const uint8_t *mmer_mask, recvec_t *out, uint64_t *n_kmers, int *alphabet_ok)
 {
     const char *kmer = read;
     const char *signature = NULL; /* binning.c:906 */
@@ -181,9 +181,12 @@ static int scan_read(const char *read, int read_len, int K, int M, uint32_t ord,
         uint64_t mh, ml;
         pack_code(signature_cpy, M, &mh, &ml);
         r.mmer = (uint32_t)ml;
-        pack_code(kmer_key, K, &r.hi, &r.lo);
-        r.ord = ord;
-        if (push(out, r)) return -1;
+        (*n_kmers)++;
+        if (!mmer_mask || mmer_mask[r.mmer]) { /* test-side partition filter */
+            pack_code(kmer_key, K, &r.hi, &r.lo);
+            r.ord = ord;
+            if (push(out, r)) return -1;
+        }
         kmer++;                                                /* binning.c:1072 */
     }
     return 0;
@@ -205,18 +208,26 @@ int kbo_bin(const char *bases, const uint64_t *read_off, uint64_t n_reads,
             const int32_t *read_ids, int K, int M, int cutoff, int prune,
             kbo_result *out)
 {
+    return kbo_bin_masked(bases, read_off, n_reads, read_ids, K, M, cutoff, prune, NULL, out);
+}
+
+int kbo_bin_masked(const char *bases, const uint64_t *read_off, uint64_t n_reads,
+                   const int32_t *read_ids, int K, int M, int cutoff, int prune,
+                   const uint8_t *mmer_mask, kbo_result *out)
+{
     memset(out, 0, sizeof(*out));
     if (K < 1 || K > 64 || M < 1 || M > 8 || M > K) return KBO_EINVAL;
     recvec_t v = {0};
     int alphabet_ok = 1;
+    uint64_t n_kmers = 0;
     for (uint64_t r = 0; r < n_reads; r++) {
         int len = (int)(read_off[r + 1] - read_off[r]);
-        if (scan_read(bases + read_off[r], len, K, M, (uint32_t)r, &v, &alphabet_ok)) {
+        if (scan_read(bases + read_off[r], len, K, M, (uint32_t)r, mmer_mask, &v, &n_kmers, &alphabet_ok)) {
             free(v.r);
             return KBO_ENOMEM;
         }
     }
-    out->n_kmers = v.n;
+    out->n_kmers = n_kmers;
     out->alphabet_ok = alphabet_ok;
     if (v.n) qsort(v.r, v.n, sizeof(rec_t), cmp_rec);
 

@@ -23,6 +23,12 @@ typedef struct {
 int kbo_bin(const char *bases, const uint64_t *read_off, uint64_t n_reads,
             const int32_t *read_ids, int K, int M, int cutoff, int prune,
             kbo_result *out);
+/* kbo_bin restricted to the keys whose canonical mmer code m has
+ * mmer_mask[m] != 0 (4^M bytes; NULL = all): checks one partition of a large
+ * input without sorting the rest.  n_kmers still counts every k-mer. */
+int kbo_bin_masked(const char *bases, const uint64_t *read_off, uint64_t n_reads,
+                   const int32_t *read_ids, int K, int M, int cutoff, int prune,
+                   const uint8_t *mmer_mask, kbo_result *out);
 void kbo_free(kbo_result *r);
 int kbo_write_dump(const kbo_result *r, int K, int M, const char *path);
 int kbo_read_fgets(const char *path, int read_length, char **bases_out,

@@ -39,6 +39,10 @@ def lib() -> C.CDLL:
         l.kbo_bin.argtypes = [C.c_char_p, C.POINTER(C.c_uint64), C.c_uint64, C.POINTER(C.c_int32),
                               C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(kbo_result)]
         l.kbo_bin.restype = C.c_int
+        l.kbo_bin_masked.argtypes = [C.c_char_p, C.POINTER(C.c_uint64), C.c_uint64, C.POINTER(C.c_int32),
+                                     C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8),
+                                     C.POINTER(kbo_result)]
+        l.kbo_bin_masked.restype = C.c_int
         l.kbo_free.argtypes = [C.POINTER(kbo_result)]
         l.kbo_free.restype = None
         l.kbo_read_fgets.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.POINTER(C.c_char)),
@@ -64,8 +68,9 @@ class OracleResult:
 
 
 def bin_reads(bases: bytes, lens, K: int, M: int, cutoff: int = 1, prune: bool = True,
-              ids=None) -> OracleResult:
-    """Run the oracle on concatenated reads."""
+              ids=None, mmer_mask=None) -> OracleResult:
+    """Run the oracle on concatenated reads (mmer_mask: uint8 per canonical
+    mmer code, keys of unmasked mmers dropped -- one partition of a big input)."""
     l = lib()
     lens = np.asarray(lens, dtype=np.uint64)
     off = np.zeros(len(lens) + 1, dtype=np.uint64)
@@ -75,8 +80,13 @@ def bin_reads(bases: bytes, lens, K: int, M: int, cutoff: int = 1, prune: bool =
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         idp = ids.ctypes.data_as(C.POINTER(C.c_int32))
     r = kbo_result()
-    rc = l.kbo_bin(bases, off.ctypes.data_as(C.POINTER(C.c_uint64)), len(lens), idp, K, M, cutoff,
-                   1 if prune else 0, C.byref(r))
+    maskp = None
+    if mmer_mask is not None:
+        mmer_mask = np.ascontiguousarray(mmer_mask, dtype=np.uint8)
+        assert mmer_mask.size == 1 << (2 * M)
+        maskp = mmer_mask.ctypes.data_as(C.POINTER(C.c_uint8))
+    rc = l.kbo_bin_masked(bases, off.ctypes.data_as(C.POINTER(C.c_uint64)), len(lens), idp, K, M, cutoff,
+                          1 if prune else 0, maskp, C.byref(r))
     if rc:
         raise RuntimeError(f"kbo_bin failed: {rc}")
     n = int(r.n_entries)

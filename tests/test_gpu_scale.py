@@ -66,7 +66,7 @@ def test_c2_full_vs_oracle():
         eng.set_timing(True)
         eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
         eng.finalize(True)
-        assert eng.timing()["engine"] == kbin.KB_ENG_BINNED
+        t = eng.timing()
         dig = eng.digest()
         res = eng.export()
     bases, hl = _unpack(words, lens, n, wpr, L)
@@ -75,6 +75,11 @@ def test_c2_full_vs_oracle():
     assert ora.n_entries > 5_000_000  # the workload really is C2-sized
     assert_same(res, ora)
     assert tuple(dig) == kbin.result_digest(ora)
+    # the default path at C2: context sub-bins for the big mmers, offset
+    # partitions for the bins still over one table
+    assert t["engine"] == kbin.KB_ENG_BINNED
+    assert t["split_mmers"] > 100 and t["n_bins"] > 2500, t
+    assert t["offset_partitions"] > 0, t
 
 
 @pytest.mark.timeout(600)
