@@ -101,3 +101,25 @@ def test_oracle_vs_reference_binary(tmp_path, K, M, rl):
         bases, lens = oracle.read_fgets(p, rl)
         res = oracle.bin_reads(bases, lens, K, M, 1, bool(prune))
         assert dump_bytes(res, K, M) == ref
+
+
+@pytest.mark.parametrize("K,M,prune", [(31, 7, True), (63, 7, False), (21, 5, True)])
+def test_masked_oracle_is_a_partition(K, M, prune):
+    """kbo_bin_masked (the capacity tests' partition filter) returns exactly
+    the full result's entries whose mmer is in the mask, lists included, and
+    still counts every k-mer"""
+    rng = np.random.default_rng(K)
+    n, L = 3000, 150
+    genome = rng.integers(0, 4, 20000)
+    st = rng.integers(0, len(genome) - L, n)
+    raw = np.frombuffer(b"TGCA", dtype=np.uint8)[genome[st[:, None] + np.arange(L)]].reshape(-1)
+    lens = np.full(n, L, np.uint32)
+    full = oracle.bin_reads(raw.tobytes(), lens, K, M, 1, prune)
+    mask = (rng.random(1 << (2 * M)) < 0.3).astype(np.uint8)
+    part = oracle.bin_reads(raw.tobytes(), lens, K, M, 1, prune, mmer_mask=mask)
+    keep = mask[full.mmer].astype(bool)
+    assert part.n_kmers == full.n_kmers and 0 < part.n_entries == int(keep.sum()) < full.n_entries
+    for f in ("mmer", "kmer_hi", "kmer_lo", "count"):
+        np.testing.assert_array_equal(getattr(part, f), getattr(full, f)[keep])
+    lists = [full.ids[full.offset[e]:full.offset[e + 1]] for e in np.flatnonzero(keep)]
+    np.testing.assert_array_equal(part.ids, np.concatenate(lists))
