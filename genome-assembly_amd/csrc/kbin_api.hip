@@ -280,6 +280,7 @@ struct kb_ctx {
     uint32_t part = 0, part_n = 1;  // kb_set_partition: this pass's mmer partition
     // balanced local buckets: records per canonical mmer seen in earlier passes,
     // and one device map (mmer -> bucket) per (part, part_n) key
+    std::vector<double> prior_p;   // bmap_prior's weight shape ((i + 1) / half)^(K - M) per canonical mmer
     std::vector<uint32_t> mmer_w;  // records per canonical mmer (all its sub-bins)
     std::vector<uint64_t> mmer_o;  // k-mer occurrences per canonical mmer
     std::unordered_map<uint64_t, uint32_t> sub_w;  // (mmer << 16 | sub-bin) -> records, split mmers of the last pass
@@ -383,6 +384,11 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     e = hipEventCreateWithFlags(&c->map_done, hipEventDisableTiming);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_EDEVICE, "hipEventCreate"); }
     {
+        {
+            const uint32_t hm = 1u << (2 * p.M - 1);
+            c->prior_p.resize(hm);
+            for (uint32_t i = 0; i < hm; i++) c->prior_p[i] = std::pow((double)(i + 1) / hm, p.K - p.M);
+        }
         // the bucket maps' pinned staging (map upload, bin descriptors back):
         // page-locking takes milliseconds, so here rather than inside a finalize
         const uint64_t half = 1ull << (2 * p.M - 1), bins = bin_budget(c, 1024);
@@ -393,14 +399,16 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
         }
         // The runtime sets up its host-to-device copy path for copies of this
         // size on first use (milliseconds, once per process and device): a
-        // map-sized warm-up copy here keeps it out of the first finalize
+        // map-sized warm-up copy here keeps it out of the first finalize; so
+        // does resolving the kernels (load_bin_kernels)
         static bool warm[64] = {};
         if (p.device >= 0 && p.device < 64 && !warm[p.device]) {
             DevBuf<uint8_t> t;
             const uint64_t nb = half * sizeof(uint32_t);
             if (t.ensure_exact(nb) == hipSuccess &&
                 hipMemcpyAsync(t.p, c->map_stage.p, nb, hipMemcpyHostToDevice, c->s) == hipSuccess &&
-                hipStreamSynchronize(c->s) == hipSuccess)
+                hipStreamSynchronize(c->s) == hipSuccess &&
+                (getenv("KB_PRELOAD") && atoi(getenv("KB_PRELOAD")) == 0 ? true : load_bin_kernels() == hipSuccess))
                 warm[p.device] = true;
             t.release();
         }
@@ -1211,7 +1219,8 @@ static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
 // sub-bins of the split ones (bmap_build keeps within it)
 static uint64_t bin_budget(const kb_ctx* c, uint32_t NB) {
     const uint64_t half = 1ull << (2 * c->p.M - 1);
-    return half + (sub_room(c->p.K, c->p.M, 2 * c->KW) ? 48ull * NB : 0ull);
+    const uint64_t per_bucket = (uint64_t)std::min(120, std::max(0, env_int("KB_BIN_SUB_EXTRA", 48)));
+    return half + (sub_room(c->p.K, c->p.M, 2 * c->KW) ? per_bucket * NB : 0ull);
 }
 
 static int bmap_build(kb_ctx* c, uint32_t NB, double rho) {
@@ -1236,8 +1245,14 @@ static int bmap_build(kb_ctx* c, uint32_t NB, double rho) {
         // (a negligible mmer keeps its hash bucket: no packing item)
         if (w > 0 && w >= mean / 512.0) seen.push_back({w, i});
     }
-    std::sort(seen.begin(), seen.end(), [](const std::pair<double, uint32_t>& a,
-                                           const std::pair<double, uint32_t>& b) { return a.first > b.first; });
+    // (a prior's weights rise with the mmer score: ascending already)
+    const auto desc = [](const std::pair<double, uint32_t>& a, const std::pair<double, uint32_t>& b) {
+        return a.first > b.first;
+    };
+    if (std::is_sorted(seen.begin(), seen.end(), [&](const auto& a, const auto& b) { return desc(b, a); }))
+        std::reverse(seen.begin(), seen.end());
+    else if (!std::is_sorted(seen.begin(), seen.end(), desc))
+        std::sort(seen.begin(), seen.end(), desc);
     uint64_t extra = bin_budget(c, NB) - half;  // sub-bins beyond one per mmer
     const kb_ctx::BucketMap* old = bmap_find(c, NB);
     std::vector<Item> items;
@@ -1275,28 +1290,42 @@ static int bmap_build(kb_ctx* c, uint32_t NB, double rho) {
     std::sort(items.begin(), items.end(), [](const Item& a, const Item& b) { return a.w > b.w; });
     const double tb2 = now_ms();
     // longest processing time first onto the least loaded bucket; at most 128
-    // bins per bucket (bucket_kernel maps 256)
-    using Slot = std::pair<double, uint32_t>;  // (load, bucket)
-    std::priority_queue<Slot, std::vector<Slot>, std::greater<Slot>> pq;
+    // bins per bucket (bucket_kernel maps 256).  A binary min-heap of packed
+    // (load in 1/16 records << 11 | bucket) words: one compare per level, the
+    // top replaced in place (no pop + push)
+    std::vector<uint64_t> heap(NB);
     std::vector<uint32_t> nm(NB, 0);
-    for (uint32_t b = 0; b < NB; b++) pq.push({0.0, b});
-    for (const Item& it : items) {
-        Slot sl = pq.top();
-        pq.pop();
-        while (nm[sl.second] >= 128 && !pq.empty()) {  // full: retire it
-            sl = pq.top();
-            pq.pop();
+    for (uint32_t b = 0; b < NB; b++) heap[b] = b;  // (all loads 0: already a heap)
+    uint32_t hn = NB;
+    auto sift = [&](uint32_t i) {
+        const uint64_t v = heap[i];
+        for (;;) {
+            uint32_t c2 = 2 * i + 1;
+            if (c2 >= hn) break;
+            if (c2 + 1 < hn && heap[c2 + 1] < heap[c2]) c2++;
+            if (heap[c2] >= v) break;
+            heap[i] = heap[c2];
+            i = c2;
         }
-        if (it.sub == ~0u) h[it.mm - half] = sl.second;
-        else subs[(h[it.mm - half] & 0x0FFFFFFFu) + it.sub] = (uint16_t)sl.second;
-        nm[sl.second]++;
-        pq.push({sl.first + it.w, sl.second});
+        heap[i] = v;
+    };
+    for (const Item& it : items) {
+        while (hn > 1 && nm[heap[0] & 2047u] >= 128) {  // full: retire it
+            std::swap(heap[0], heap[--hn]);  // (kept past the heap: its load still counts)
+            sift(0);
+        }
+        const uint32_t b = (uint32_t)(heap[0] & 2047u);
+        if (it.sub == ~0u) h[it.mm - half] = b;
+        else subs[(h[it.mm - half] & 0x0FFFFFFFu) + it.sub] = (uint16_t)b;
+        nm[b]++;
+        heap[0] += (uint64_t)std::llround(std::min(it.w, 1e12) * 16.0) << 11;
+        sift(0);
     }
     double want_max = 0, want_tot = 0;
-    while (!pq.empty()) {
-        want_max = std::max(want_max, pq.top().first);
-        want_tot += pq.top().first;
-        pq.pop();
+    for (uint32_t i = 0; i < NB; i++) {
+        const double ld = (double)(heap[i] >> 11) / 16.0;
+        want_max = std::max(want_max, ld);
+        want_tot += ld;
     }
     const double tb3 = now_ms();
     kb_ctx::BucketMap* m = bmap_find(c, NB);
@@ -1403,10 +1432,9 @@ static int bmap_prior(kb_ctx* c, uint32_t NB) {
     }
     const bool reads_part = c->part_n > 1 && std::none_of(c->batches.begin(), c->batches.end(),
                                                           [](const Batch& b) { return b.superkmers; });
-    std::vector<double> p(half);
+    const std::vector<double>& p = c->prior_p;  // (kb_create: the shape depends on K and M only)
     double tot = 0, mine = 0;
     for (uint32_t i = 0; i < half; i++) {
-        p[i] = std::pow((double)(i + 1) / half, W - 1);
         tot += p[i];
         if (c->part_n <= 1 || sk_hash_dest(half + i, c->part_n, 0x9E3779B97F4A7C15ull) == c->part) mine += p[i];
     }
@@ -1808,6 +1836,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(launch_bins_desc(c->border.p, c->starts.p, c->bcount.p, c->bmmer.p, c->bocc.p, c->totals.p, max_bins,
                                 c->bdesc.p, reinterpret_cast<unsigned long long*>(c->totals.p + 10), c->s));
     }
+    float* rho_dev = nullptr;
     if (c->rho <= 0.f && N && env_int("KB_BIN_HLL", 1)) {
         // the context's first finalize: distinct keys per occurrence from one
         // HyperLogLog over the records (no learned density yet)
@@ -1822,17 +1851,14 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         // large passes estimate from the bins of 1/8 of the mmers (whole bins:
         // the ratio of a sample of bins, 1/8 of the expansion work)
         const uint32_t sample = R >= (1u << 20) && max_bins >= 256 ? (uint32_t)std::max(1, env_int("KB_BIN_HLL_SAMPLE", 8)) : 1u;
-        HIPCHK(c->hll.ensure_exact(4096 + 2));
+        // (registers, the u64 occurrence count, then the estimate: read by the
+        // bin kernel from device memory -- the host never waits for it; the
+        // finalize's own distinct count replaces it afterwards)
+        HIPCHK(c->hll.ensure_exact(4096 + 3));
         HIPCHK(launch_hll(h, R, KW, c->hll.p, sample, c->s));
-        std::vector<uint32_t> regs(4096 + 2);
-        HIPCHK(hipMemcpyAsync(regs.data(), c->hll.p, (4096 + 2) * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
-        HIPCHK(hipStreamSynchronize(c->s));
-        KB_DBG("hll (sample 1/%u): %.3f ms since finalize (allocations %.3f ms)\n", sample, now_ms() - c->t_fin,
-               g_alloc_ms);
-        uint64_t occ_s = 0;
-        memcpy(&occ_s, regs.data() + 4096, sizeof(occ_s));
-        if (occ_s)
-            c->rho = (float)std::min(1.0, std::max(1e-4, hll_estimate(regs.data()) / (double)occ_s));
+        rho_dev = reinterpret_cast<float*>(c->hll.p + 4096 + 2);
+        HIPCHK(launch_hll_finish(c->hll.p, rho_dev, c->s));
+        KB_DBG("hll (sample 1/%u) queued: %.3f ms since finalize\n", sample, now_ms() - c->t_fin);
     }
     REC(3);
     // ---- one workgroup per bin.  Entry capacity: learned (or N/8), rerun once
@@ -1914,6 +1940,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.keep_gt = prune ? (uint32_t)c->p.cutoff : 0u;
         a.ts_log2 = (uint32_t)ts_log2;
         a.rho = c->rho > 0.f ? c->rho : 0.25f;
+        a.rho_dev = rho_dev;
         a.fill = (float)std::min(0.85, std::max(0.3, env_int("KB_BIN_FILL_PCT", 60) / 100.0));
         a.ablate = env_int("KB_BIN_ABLATE", 0);
         a.ringfree = (uint32_t)(env_int("KB_BIN_RINGFREE", 1) != 0);

@@ -1285,6 +1285,7 @@ DEV void bin_body(const BinArgs& A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     BinShared& S = *reinterpret_cast<BinShared*>(smem);      // all LDS in one dynamic array
     const uint32_t TS = 1u << A.ts_log2;  // the carved table (buckets of four slots; a partition may use less)
+    const float rho = A.rho_dev ? *A.rho_dev : A.rho;  // (cold pass: the device's HLL estimate)
     BinTable<KW> T;
     // cnt | claim words | low words | rings: after the prune everything past
     // cnt is dead, and the LDS path's id window takes it (win_cap ids)
@@ -1395,7 +1396,7 @@ DEV void bin_body(const BinArgs& A) {
 #endif
         uint32_t l0 = 0;  // uniform: initial partition depth from the expected distinct keys
         if (PHASE == 0) {
-            const double want = (double)occ_tot * A.rho / ((double)A.fill * TS);
+            const double want = (double)occ_tot * rho / ((double)A.fill * TS);
             while ((double)(1u << l0) < want && l0 < 16) l0++;
         } else {
             l0 = S.l0 & 0xFFu;
@@ -1414,7 +1415,7 @@ DEV void bin_body(const BinArgs& A) {
         bool osplit = PHASE == 1 && !flat && (S.l0 & OSPLIT_BIT);
         if (PHASE == 0 && A.osplit && A.opart && A.flat_l && l0 < A.flat_l &&
             ((A.big_occ && l0 >= 1 && occ_tot > A.big_occ) || (A.split_occ && occ_tot > A.split_occ))) {
-            const double want = (double)occ_tot * A.rho / ((double)A.fill_light * TS);
+            const double want = (double)occ_tot * rho / ((double)A.fill_light * TS);
             uint32_t l1 = 0;
             while ((double)(1u << l1) < want && l1 < 16) l1++;
             while (l1 < A.opart && A.big_occ && (occ_tot >> l1) > A.big_occ) l1++;
@@ -1441,7 +1442,7 @@ DEV void bin_body(const BinArgs& A) {
         bool pfb = PHASE == 1 ? flat && (S.l0 & PF_BIT) : false;
         if (PHASE == 0 && flat && A.pf) {
             const double want_t = (double)occ_tot * A.rho_tab / ((double)A.fill * TS);
-            const double want_s = (double)occ_tot * A.rho / (PF_LOAD * (double)sk_cells);
+            const double want_s = (double)occ_tot * rho / (PF_LOAD * (double)sk_cells);
             const double want = want_t > want_s ? want_t : want_s;
             l0 = 0;
             while ((double)(1u << l0) < want && l0 < 16) l0++;
@@ -1504,7 +1505,7 @@ DEV void bin_body(const BinArgs& A) {
         // table load (fill_light: fewer second probe rounds) where that depth
         // stays offset-partitioned
         if (PHASE == 0 && !flat && !split && A.opart) {
-            const double want = (double)occ_tot * A.rho / ((double)A.fill_light * TS);
+            const double want = (double)occ_tot * rho / ((double)A.fill_light * TS);
             uint32_t l1 = 0;
             while ((double)(1u << l1) < want && l1 < 16) l1++;
             if (l1 <= A.opart && l1 > l0) l0 = l1;
@@ -1516,7 +1517,7 @@ DEV void bin_body(const BinArgs& A) {
         // table four times larger before it splits
         uint32_t tsb = TS;
         if (PHASE == 0 && A.ts_adapt && !flat && !split && l0 == 0) {
-            const double keys = (double)occ_tot * A.rho;
+            const double keys = (double)occ_tot * rho;
             tsb = (uint32_t)BIN_THREADS;
             while (tsb < TS && keys > (double)A.fill_light * tsb) tsb <<= 1;
         }
@@ -3118,6 +3119,42 @@ hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, uint
     return hipGetLastError();
 }
 
+// hll_estimate on the device: one block reduces the registers (sum of 2^-r,
+// zero registers) and writes distinct / occurrences
+__global__ __launch_bounds__(256) void hll_finish_kernel(const uint32_t* __restrict__ regs, float* __restrict__ rho) {
+    __shared__ double s_sum[256];
+    __shared__ int s_zero[256];
+    double sum = 0.0;
+    int zeros = 0;
+    for (int i = threadIdx.x; i < (1 << HLL_LOG2); i += 256) {
+        sum += ldexp(1.0, -(int)regs[i]);
+        zeros += regs[i] == 0;
+    }
+    s_sum[threadIdx.x] = sum;
+    s_zero[threadIdx.x] = zeros;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            s_sum[threadIdx.x] += s_sum[threadIdx.x + w];
+            s_zero[threadIdx.x] += s_zero[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double m = (double)(1 << HLL_LOG2);
+        double est = 0.7213 / (1.0 + 1.079 / m) * m * m / s_sum[0];
+        if (est <= 2.5 * m && s_zero[0]) est = m * log(m / (double)s_zero[0]);  // small range: linear counting
+        const unsigned long long occ = *reinterpret_cast<const unsigned long long*>(regs + (1 << HLL_LOG2));
+        const double r = occ ? est / (double)occ : 0.25;
+        *rho = (float)(r < 1e-4 ? 1e-4 : (r > 1.0 ? 1.0 : r));
+    }
+}
+
+hipError_t launch_hll_finish(const uint32_t* regs, float* rho, hipStream_t s) {
+    hipLaunchKernelGGL(hll_finish_kernel, dim3(1), dim3(256), 0, s, regs, rho);
+    return hipGetLastError();
+}
+
 double hll_estimate(const uint32_t* regs) {
     const double m = (double)(1 << HLL_LOG2);
     double sum = 0.0;
@@ -3720,4 +3757,31 @@ hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, 
     return hipGetLastError();
 }
 
+// The runtime resolves a kernel (and loads the code object holding it) at its
+// first launch in the process: milliseconds spread over a context's first
+// finalize.  kb_create resolves the binned path's kernels once per process and
+// device instead (hipFuncGetAttributes), with the other one-time setup.
+hipError_t load_bin_kernels() {
+    const void* k[] = {
+        (const void*)sk_thread_kernel<true>, (const void*)sk_thread_kernel<false>,
+        (const void*)sk_kmers_total_kernel, (const void*)sk_convert_buckets_kernel<2>,
+        (const void*)sk_convert_buckets_kernel<4>, (const void*)bucket_kernel<2>, (const void*)bucket_kernel<4>,
+        (const void*)bucket_bases_kernel, (const void*)bucket_stats_kernel, (const void*)bins_order_kernel,
+        (const void*)bins_desc_kernel, (const void*)hll_kernel<1>, (const void*)hll_kernel<2>,
+        (const void*)hll_finish_kernel, (const void*)bin_kernel<1>, (const void*)bin_kernel<2>,
+        (const void*)flat_count_kernel<1>, (const void*)flat_count_kernel<2>, (const void*)flat_scan_kernel,
+        (const void*)flat_scatter_kernel<1>, (const void*)flat_scatter_kernel<2>,
+        (const void*)flat_scatter_lds_kernel<1>, (const void*)flat_scatter_lds_kernel<2>,
+        (const void*)bin_parts_kernel<1>, (const void*)bin_parts_kernel<2>, (const void*)bins_final_kernel,
+        (const void*)lists_kernel, (const void*)lists_bucket_kernel, (const void*)lists_long_kernel,
+        (const void*)clear_kernel};
+    for (const void* f : k) {
+        hipFuncAttributes at;
+        const hipError_t e = hipFuncGetAttributes(&at, f);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 }  // namespace kb
+

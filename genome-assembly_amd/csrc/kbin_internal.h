@@ -253,6 +253,7 @@ struct BinArgs {
     uint32_t keep_gt;
     uint32_t ts_log2;
     float rho;                 // expected distinct keys per occurrence
+    const float* rho_dev;      // cold pass: rho estimated on the device (hll_finish_kernel); else null
     float fill;                // target table load when choosing the partition depth
     uint32_t ringfree;         // unpartitioned bins expand without the per-wave ring (KB_BIN_RINGFREE)
     // offset partitions: a light bin of initial depth 1 <= l <= opart is split by
@@ -357,6 +358,11 @@ hipError_t launch_bins_desc(const uint32_t* order, const uint32_t* bstart, const
 // of the mmers only) and its estimate (host): the cold pass's distinct keys
 hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, uint32_t sample, hipStream_t s);
 double hll_estimate(const uint32_t* regs);
+// resolve the binned path's kernels (kb_create: once per process and device)
+hipError_t load_bin_kernels();
+// distinct / occurrences from launch_hll's registers, on the device (no host
+// round trip): written to *rho (clamped to [1e-4, 1]; 0.25 with no occurrences)
+hipError_t launch_hll_finish(const uint32_t* regs, float* rho, hipStream_t s);
 hipError_t launch_bins_order(const uint32_t* bcount, const uint64_t* totals, uint32_t* order, uint64_t max_bins,
                              hipStream_t s);
 hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s);

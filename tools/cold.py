@@ -18,6 +18,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c5")
 ap.add_argument("--steps", type=int, default=2)
 ap.add_argument("--reads", type=int, default=None)
+ap.add_argument("--prewarm", type=int, default=0, help="first bin this many reads on a throw-away context")
 a = ap.parse_args()
 wl = bench.WORKLOADS[a.workload]
 n, L, K, M, P = a.reads or wl["reads"], wl["read_len"], wl["K"], wl["M"], wl["parts"]
@@ -26,7 +27,16 @@ w = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
 ln = torch.empty(n, dtype=torch.int32, device="cuda")
 kbin.generate_reads_device(w.data_ptr(), ln.data_ptr(), n, L, wl["genome"], wl["err_ppm"], bench.gen_seed(wl["seed"]))
 torch.cuda.synchronize()
+if a.prewarm:
+    with kbin.Engine(K, M, cutoff=1, max_read_len=L) as tmp:
+        t0 = time.perf_counter()
+        tmp.submit_packed_device(w.data_ptr(), ln.data_ptr(), a.prewarm, wpr, 0)
+        tmp.finalize(True)
+        torch.cuda.synchronize()
+        print(f"prewarm {a.prewarm} reads: {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
+tcr = time.perf_counter()
 with kbin.Engine(K, M, cutoff=1, max_read_len=L) as eng:
+    print(f"create: {(time.perf_counter() - tcr) * 1e3:.2f} ms", flush=True)
     eng.set_timing(True)
     for s in range(a.steps):
         eng.reset()
