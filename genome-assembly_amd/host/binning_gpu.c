@@ -853,6 +853,13 @@ static struct ZHashTable *finish(struct ZHashTable *hash_table, int prune)
     kbh_release(hash_table);
     g_times.release_ms = now_ms() - t;
     g_times.total_ms = now_ms() - t0;
+    if (getenv("KBH_TRACE")) /* (the drop-in binaries: no caller reads kbh_last_times) */
+        fprintf(stderr,
+                "{\"prune_data_ms\": %.3f, \"finalize_ms\": %.3f, \"export_ms\": %.3f, \"materialise_ms\": %.3f, "
+                "\"release_ms\": %.3f, \"entries\": %llu, \"ids\": %llu, \"nodes\": %llu}\n",
+                g_times.total_ms, g_times.finalize_ms, g_times.export_ms, g_times.materialise_ms,
+                g_times.release_ms, (unsigned long long)g_times.entries, (unsigned long long)g_times.ids,
+                (unsigned long long)g_times.nodes);
     return hash_table;
 }
 

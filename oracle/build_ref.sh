@@ -31,25 +31,36 @@ REF=${KB_REFERENCE_DIR:-/root/reference}
 HERE="$(cd "$(dirname "$0")" && pwd)"
 REPO="$(cd "$HERE/.." && pwd)"
 OUT="$HERE/_ref"
+RL=${KB_REF_READ_LENGTH:+_rl$KB_REF_READ_LENGTH}
 case $MODE in
-  harness) BIN="$OUT/ref_k${K}_m${M}_c${C}" ;;
-  g)       BIN="$OUT/refg_k${K}_m${M}_c${C}" ;;
-  full)    BIN="$OUT/full_k${K}_m${M}_c${C}" ;;
-  dropin)  BIN="$OUT/dropin_k${K}_m${M}_c${C}" ;;
+  harness) BIN="$OUT/ref_k${K}_m${M}_c${C}$RL" ;;
+  g)       BIN="$OUT/refg_k${K}_m${M}_c${C}$RL" ;;
+  full)    BIN="$OUT/full_k${K}_m${M}_c${C}$RL" ;;
+  dropin)  BIN="$OUT/dropin_k${K}_m${M}_c${C}$RL" ;;
 esac
 if [ ! -f "$REF/binning.c" ]; then
   echo "reference not present at $REF; skipping" >&2
   exit 0
 fi
 mkdir -p "$OUT"
-if [ -x "$BIN" ]; then exit 0; fi
+# (a drop-in binary links the shim: rebuilt whenever the shim or the engine
+# library is newer than it)
+if [ -x "$BIN" ]; then
+  if [ "$MODE" != dropin ]; then exit 0; fi
+  if [ ! "$REPO/genome-assembly_amd/host/binning_gpu.c" -nt "$BIN" ] && \
+     [ ! "$REPO/genome-assembly_amd/lib/libkbin.so" -nt "$BIN" ]; then exit 0; fi
+fi
 TMP="$(mktemp -d)"
 trap 'rm -rf "$TMP"' EXIT
 sed -e 's/^#define MMER_SIZE \(.*\)$/#ifndef MMER_SIZE\n#define MMER_SIZE \1\n#endif/' \
     -e 's/^#define KMER_SIZE \(.*\)$/#ifndef KMER_SIZE\n#define KMER_SIZE \1\n#endif/' \
     -e 's/^#define ABUNDANCE_CUTOFF \(.*\)$/#ifndef ABUNDANCE_CUTOFF\n#define ABUNDANCE_CUTOFF \1\n#endif/' \
+    -e 's/^#define READ_LENGTH \(.*\)$/#ifndef READ_LENGTH\n#define READ_LENGTH \1\n#endif/' \
     "$REF/binning.c" > "$TMP/binning_guarded.c"
 DEFS="-DKMER_SIZE=$K -DMMER_SIZE=$M -DABUNDANCE_CUTOFF=$C"
+# KB_REF_READ_LENGTH=<n>: the fgets chunk size (binning.c:13, 101 as shipped);
+# the binary name then ends in _rl<n>
+if [ -n "${KB_REF_READ_LENGTH:-}" ]; then DEFS="$DEFS -DREAD_LENGTH=$KB_REF_READ_LENGTH"; fi
 case $MODE in
   harness)
     gcc -O2 -w -I"$REF" $DEFS -Dmain=binning_main -c "$TMP/binning_guarded.c" -o "$TMP/binning.o"
