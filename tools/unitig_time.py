@@ -34,10 +34,14 @@ def run(exe, path, timeout, env=None):
     p = subprocess.Popen([str(exe), str(path)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)
     h, nbytes = hashlib.sha256(), 0
     deadline = t0 + timeout
+    beat = t0
     while True:
         b = p.stdout.read(1 << 20)
         if not b:
             break
+        if time.perf_counter() - beat > 20:  # (a heartbeat: the box kills runs silent for 3 min)
+            beat = time.perf_counter()
+            print(f"  {exe.name}: {nbytes >> 20} MiB out, {beat - t0:.0f} s", file=sys.stderr, flush=True)
         h.update(b)
         nbytes += len(b)
         if time.perf_counter() > deadline:
