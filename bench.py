@@ -322,11 +322,18 @@ def single_gpu_runner(K, M, L, cutoff, n, wpr, P, local, reads, pass_log, scan_o
             split["cap"] = int(int(counts.max()) * 1.1) + 1024
         raise RuntimeError("kb_split_passes: region capacity not converging")
 
+    dbg = os.environ.get("BENCH_DEBUG") == "1"
+
     def step(digest=False):
         pass_log.clear()
         dig = [0, 0, 0, 0]
+        t0 = time.perf_counter()
         if scan_once:
             scan()
+            if dbg:
+                torch.cuda.synchronize()
+                print(f"[bench] scan {1e3 * (time.perf_counter() - t0):.1f} ms (cap {split['cap']})",
+                      file=sys.stderr, flush=True)
         for p in range(P):
             eng.reset()
             if scan_once:
@@ -339,6 +346,9 @@ def single_gpu_runner(K, M, L, cutoff, n, wpr, P, local, reads, pass_log, scan_o
                 if P > 1:
                     eng.set_partition(p, P)
             eng.finalize(prune=True)
+            if dbg:
+                print(f"[bench] pass {p} done at {1e3 * (time.perf_counter() - t0):.1f} ms", file=sys.stderr,
+                      flush=True)
             pass_log.append((eng.export_device(), eng.timing(), None))
             if digest:
                 dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
