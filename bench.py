@@ -176,7 +176,11 @@ def cpu_baseline(words, lens, n_avail, n_sample, wpr, L, K, M, cutoff, ref_sampl
             "sample": f"{cores} independent reference processes (gcc -O2) run at once on {cores} disjoint "
                       f"shards of {sh} reads of the bench workload ({kms} k-mers): the slowest one's "
                       f"fgets + process_read + prune_data took {slow:.2f} s (process wall {wall:.2f} s); "
-                      f"the shards' tables are never merged (an upper bound); "
+                      f"the shards' tables are never merged, and a {sh}-read shard keeps each "
+                      f"process's tables far smaller than one table over the whole workload (faster "
+                      f"zhash chains, fewer rehashes): the shard size is part of why this is an upper "
+                      f"bound (one core on the first {m} reads: {rows['ref_1core_O2']['value'] / 1e6:.2f} M "
+                      f"k-mers/s); "
                       f"host nproc={os.cpu_count()}",
             "rows": rows, "port": port}
 
