@@ -1418,7 +1418,7 @@ static int bmap_apply(kb_ctx* c, uint32_t NB, const uint32_t* mm, const uint32_t
 // read, 2 (L - K + 1) / (K - M + 2), scale it.  The prior map is marked stale,
 // so the pass's own bins replace it.
 static int bmap_prior(kb_ctx* c, uint32_t NB) {
-    const int K = c->p.K, M = c->p.M, W = K - M + 1;
+    const int K = c->p.K, M = c->p.M;
     const uint32_t half = 1u << (2 * M - 1);
     double R_est = 0;
     for (auto& b : c->batches) {
@@ -1550,7 +1550,9 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
             HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
             HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         } else {  // R, the largest bucket and the status word folded next to N: one copy
-            HIPCHK(launch_bucket_stats(c->bfill.p, NB, c->misc.p, c->totals.p, c->s));
+            HIPCHK(c->bbase.ensure(NB + 1));
+            HIPCHK(launch_bucket_stats(c->bfill.p, NB, c->misc.p, c->totals.p, cap, use_base ? c->rbase.p : nullptr,
+                                       c->bbase.p, c->s));
             HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         }
         HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync (two without a map): R and N size the rest
@@ -1714,6 +1716,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     REC(0);
     HIPCHK(c->totals.ensure(16));
     c->tm.scan_insert_launches = 0;
+    c->tm.tail_reruns = 0;
     uint64_t R = 0, N = 0;
     // bucketed (default): records into local bucket regions, one workgroup
     // orders each bucket; radix: flat records, a global sort by (mmer, n)
@@ -1792,6 +1795,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         ba.spw = 2 * KW;
         HIPCHK(c->bbase.ensure(NB + 1));
         ba.bbase = c->bbase.p;
+        ba.bases_ready = 1;  // (bucket_stats_kernel, after the record pass that made these regions)
         {
             // records written by a map-routed pass carry their sub-bin (zero
             // for an unsplit mmer); a hash-routed pass writes spans untouched
@@ -1829,12 +1833,13 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(launch_sk_gather(c->sorted, c->pay.p, R, c->srec.p, c->s));
     }
     HIPCHK(c->border.ensure(max_bins));
-    HIPCHK(launch_bins_order(c->bcount.p, c->totals.p, c->border.p, max_bins, c->s));
     const bool use_desc = bucketed && env_int("KB_BIN_DESC", 1);
     if (use_desc) {  // (bocc: the bucket ordering counted every bin's occurrences)
         HIPCHK(c->bdesc.ensure(2 * max_bins));
-        HIPCHK(launch_bins_desc(c->border.p, c->starts.p, c->bcount.p, c->bmmer.p, c->bocc.p, c->totals.p, max_bins,
+        HIPCHK(launch_bins_plan(c->starts.p, c->bcount.p, c->bmmer.p, c->bocc.p, c->totals.p, max_bins, c->border.p,
                                 c->bdesc.p, reinterpret_cast<unsigned long long*>(c->totals.p + 10), c->s));
+    } else {
+        HIPCHK(launch_bins_order(c->bcount.p, c->totals.p, c->border.p, max_bins, c->s));
     }
     float* rho_dev = nullptr;
     if (c->rho <= 0.f && N && env_int("KB_BIN_HLL", 1)) {
@@ -2008,7 +2013,15 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.pstat = c->pstat.p;
         a.ldsbar = (uint32_t)(env_int("KB_BIN_LDSBAR", 1) != 0);
         a.ts_adapt = (uint32_t)(env_int("KB_BIN_TS_ADAPT", 1) != 0);
-        HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr));
+        // The tail kernels -- the heavy bins' list builds and partitions, the
+        // list kernels -- have work only when bin_kernel publishes a heavy bin
+        // or queues a list, and cost ~4.5 us per empty launch (8 of them: 2 %
+        // of a C2 step).  Where the last finalize needed none they are left
+        // out, and launched after all (full grids) only if this finalize's
+        // totals say bin_kernel published or queued something
+        const bool defer = attempt == 0 && c->hint_heavy == 0 && c->hint_lq == 0 && a.lq_items &&
+                           env_int("KB_BIN_DEFER_TAIL", 1) != 0;
+        HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr, !defer));
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
 #endif
@@ -2034,7 +2047,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         la.lq_hint = attempt ? ~0ull : c->hint_lq;
         la.long_hint[0] = attempt ? ~0ull : c->hint_long[0];
         la.long_hint[1] = attempt ? ~0ull : c->hint_long[1];
-        HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : ecap, c->s));
+        if (!defer) HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : ecap, c->s));
 #ifdef KB_BIN_PROF
         lists_prof_report(c->s);
 #endif
@@ -2054,6 +2067,24 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         else c->h_misc[8] = 0;
         HIPCHK(hipStreamSynchronize(c->s));
+        if (defer && (c->h_totals[12] || c->h_totals[13])) {
+            // the tail after all (a heavy bin published, or lists queued):
+            // full grids, then the totals again
+            c->tm.tail_reruns++;
+            a.heavy_hint = ~0ull;
+            HIPCHK(launch_bins_heavy(a, KW, c->s));
+            HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries,
+                                     flat_l ? c->flat_n.p : nullptr, a.lq_n, c->s));
+            la.lq_hint = ~0ull;
+            la.long_hint[0] = la.long_hint[1] = ~0ull;
+            HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : ecap, c->s));
+            REC(5);
+            HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 14 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_totals + 16, c->pstat.p, KB_PSTAT * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                  c->s));
+            HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipStreamSynchronize(c->s));
+        }
         if (c->h_misc[0] & ST_BUCKET_FULL) {  // a bucket held too many mmers
             c->finalized = false;
             // a learned (or prior) map packed them: forget it and rerun on the

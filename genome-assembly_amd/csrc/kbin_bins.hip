@@ -3242,6 +3242,87 @@ hipError_t launch_bins_desc(const uint32_t* order, const uint32_t* bstart, const
     return hipGetLastError();
 }
 
+// bins_order_kernel and bins_desc_kernel in one launch: the class histogram,
+// the processing order (kept in LDS up to PLAN_LDS bins, else re-read from
+// `order`), then the descriptors in rounds of 1024 processing slots (a block
+// scan of the occurrences per round carries the stage base) -- coalesced
+// descriptor stores and independent gathers, where bins_desc_kernel walked
+// each thread's range of slots one dependent load after another
+constexpr uint32_t PLAN_LDS = 8192;
+__global__ __launch_bounds__(1024) void bins_plan_kernel(const uint32_t* __restrict__ bstart,
+                                                         const uint32_t* __restrict__ bcount,
+                                                         const uint32_t* __restrict__ bmmer,
+                                                         const uint32_t* __restrict__ bocc,
+                                                         const uint64_t* __restrict__ totals, uint64_t max_bins,
+                                                         uint32_t* __restrict__ order, uint4* __restrict__ desc,
+                                                         unsigned long long* stage_ctr) {
+    constexpr uint32_t NC = 256;
+    __shared__ uint32_t hist[NC];
+    __shared__ uint32_t ordl[PLAN_LDS];
+    __shared__ uint64_t red[16];
+    const uint32_t t = threadIdx.x;
+    const int lane = (int)(t & 63u), wid = (int)(t >> 6);
+    const uint32_t nbins = (uint32_t)min(totals[2], max_bins);
+    if (t < NC) hist[t] = 0;
+    __syncthreads();
+    for (uint32_t b = t; b < nbins; b += 1024) atomicAdd(&hist[order_class(bcount[b])], 1u);
+    __syncthreads();
+    // exclusive offsets, largest class first: thread t < 256 holds class 255 - t
+    {
+        const uint32_t h = t < NC ? hist[NC - 1u - t] : 0u;
+        const uint64_t inc = wave_incl_scan((uint64_t)h, lane);
+        if (lane == 63 && wid < 4) red[wid] = inc;
+        __syncthreads();
+        uint64_t wp = 0;
+        for (int w = 0; w < wid && w < 4; w++) wp += red[w];
+        if (t < NC) hist[NC - 1u - t] = (uint32_t)(wp + inc - h);
+        __syncthreads();
+    }
+    const bool in_lds = nbins <= PLAN_LDS;
+    for (uint32_t b = t; b < nbins; b += 1024) {
+        const uint32_t pos = atomicAdd(&hist[order_class(bcount[b])], 1u);
+        order[pos] = b;
+        if (in_lds) ordl[pos] = b;
+    }
+    __threadfence_block();
+    __syncthreads();
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < nbins; base += 1024) {
+        const uint32_t i = base + t;
+        const bool v = i < nbins;
+        const uint32_t b = v ? (in_lds ? ordl[i] : order[i]) : 0u;
+        const uint32_t occ = v ? bocc[b] : 0u;
+        const uint4 d0 = v ? make_uint4(b, bstart[b], bcount[b], bmmer[b]) : make_uint4(0u, 0u, 0u, 0u);
+        const uint64_t inc = wave_incl_scan((uint64_t)occ, lane);
+        if (lane == 63) red[wid] = inc;
+        __syncthreads();
+        uint64_t wp = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            if (w < wid) wp += red[w];
+            tot += red[w];
+        }
+        const uint64_t run = carry + wp + inc - occ;
+        if (v) {
+            desc[2 * (uint64_t)i] = d0;
+            desc[2 * (uint64_t)i + 1] = make_uint4(occ, (uint32_t)run, (uint32_t)(run >> 32), 0u);
+        }
+        carry += tot;
+        __syncthreads();  // (red is the next round's)
+    }
+    // bins without a count (bocc 0) take their stage ranges from the stage
+    // counter, after every described range
+    if (t == 0) *stage_ctr = carry;
+}
+
+hipError_t launch_bins_plan(const uint32_t* bstart, const uint32_t* bcount, const uint32_t* bmmer,
+                            const uint32_t* bocc, const uint64_t* totals, uint64_t max_bins, uint32_t* order,
+                            uint4* desc, unsigned long long* stage_ctr, hipStream_t s) {
+    hipLaunchKernelGGL(bins_plan_kernel, dim3(1), dim3(1024), 0, s, bstart, bcount, bmmer, bocc, totals, max_bins,
+                       order, desc, stage_ctr);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void bins_describe_kernel(const uint64_t* __restrict__ keys,
                                                             const uint32_t* __restrict__ starts,
                                                             const uint64_t* __restrict__ totals,
@@ -3467,7 +3548,8 @@ __global__ __launch_bounds__(1024) void bucket_bases_kernel(const unsigned long 
 hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s) {
     if (!NB) return hipSuccess;
     if (NB > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(bucket_bases_kernel, dim3(1), dim3(1024), 0, s, a.bfill, a.cap, a.rbase, NB, a.bbase);
+    if (!a.bases_ready)
+        hipLaunchKernelGGL(bucket_bases_kernel, dim3(1), dim3(1024), 0, s, a.bfill, a.cap, a.rbase, NB, a.bbase);
     if (a.spw == 2)
         hipLaunchKernelGGL(bucket_kernel<2>, dim3(NB), dim3(BK_THREADS), 0, s, a);
     else if (a.spw == 4)
@@ -3647,35 +3729,41 @@ size_t bins_lds_bytes(uint32_t ts_log2, int KW) {
            (size_t)BIN_WAVES * Q * (KW * sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint16_t));
 }
 
+// the bin kernel's blocks (every CU, as many as fit) and the per-launch split
+// thresholds derived from them
 template <int KW>
-static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_t s, hipEvent_t* ev_bin) {
+static hipError_t bins_grid(const BinArgs& a, uint64_t& blocks, int& cus, size_t& lds, BinArgs& a2) {
     const uint32_t TS = 1u << a.ts_log2;
-    const size_t lds = bins_lds_bytes(a.ts_log2, KW);
+    lds = bins_lds_bytes(a.ts_log2, KW);
     if (TS < (uint32_t)BIN_THREADS || lds > 160 * 1024) return hipErrorInvalidValue;  // (the prune loop)
-    int dev = 0, cus = 0, per_cu = 0;
+    int dev = 0, per_cu = 0;
+    cus = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel<KW>, BIN_THREADS, lds);
     if (e != hipSuccess) return e;
-    const uint64_t blocks = (uint64_t)std::max(1, cus) * std::max(1, per_cu);
+    blocks = (uint64_t)std::max(1, cus) * std::max(1, per_cu);
     // split a light bin above 1/split_div of an even per-block share of the occurrences
-    BinArgs a2 = a;
+    a2 = a;
     a2.split_occ = a.flat_l && a.split_div ? a.n_occ / ((uint64_t)blocks * a.split_div) + 1 : 0;
     a2.big_occ = a.flat_l && a.big_div ? a.n_occ / ((uint64_t)blocks * a.big_div) + 1 : 0;
-    if (ev_bin) {
-        e = hipEventRecord(ev_bin[0], s);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS), lds, s,
-                       a2);
-    e = hipGetLastError();
-    if (e == hipSuccess && ev_bin) e = hipEventRecord(ev_bin[1], s);
-    if (e != hipSuccess || !a.flat_l) return e;
-    // the published bins: counts, offsets, flat lists -- every kernel exits at
-    // once without any -- then their partitions, spread over every CU
-    // (grids: small when the last finalize published no such bin -- an empty
-    // launch then costs its dispatch only; every kernel strides over its work,
-    // so a surprise heavy bin is still binned, more slowly, once)
+    return hipSuccess;
+}
+
+// the published bins: counts, offsets, flat lists -- every kernel exits at
+// once without any -- then their partitions, spread over every CU (grids:
+// small when the last finalize published no such bin -- an empty launch then
+// costs its dispatch only; every kernel strides over its work, so a surprise
+// heavy bin is still binned, more slowly, once)
+template <int KW>
+static hipError_t launch_heavy_kw(const BinArgs& a, hipStream_t s) {
+    if (!a.flat_l) return hipSuccess;
+    uint64_t blocks = 0;
+    int cus = 0;
+    size_t lds = 0;
+    BinArgs a2;
+    hipError_t e = bins_grid<KW>(a, blocks, cus, lds, a2);
+    if (e != hipSuccess) return e;
     const bool few = a.heavy_hint == 0;
     const size_t fb_lds = (size_t)FLAT_MAX * sizeof(uint32_t);
     const unsigned fb_blocks = few ? 32u : (unsigned)std::max(1, cus) * 8u;
@@ -3689,9 +3777,33 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     return hipGetLastError();
 }
 
-hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin) {
+template <int KW>
+static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_t s, hipEvent_t* ev_bin, bool heavy) {
+    uint64_t blocks = 0;
+    int cus = 0;
+    size_t lds = 0;
+    BinArgs a2;
+    hipError_t e = bins_grid<KW>(a, blocks, cus, lds, a2);
+    if (e != hipSuccess) return e;
+    if (ev_bin) {
+        e = hipEventRecord(ev_bin[0], s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS), lds, s,
+                       a2);
+    e = hipGetLastError();
+    if (e == hipSuccess && ev_bin) e = hipEventRecord(ev_bin[1], s);
+    if (e != hipSuccess || !heavy) return e;
+    return launch_heavy_kw<KW>(a, s);
+}
+
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin, bool heavy) {
     if (!max_bins) return hipSuccess;
-    return KW == 1 ? launch_bins_kw<1>(a, max_bins, s, ev_bin) : launch_bins_kw<2>(a, max_bins, s, ev_bin);
+    return KW == 1 ? launch_bins_kw<1>(a, max_bins, s, ev_bin, heavy) : launch_bins_kw<2>(a, max_bins, s, ev_bin, heavy);
+}
+
+hipError_t launch_bins_heavy(const BinArgs& a, int KW, hipStream_t s) {
+    return KW == 1 ? launch_heavy_kw<1>(a, s) : launch_heavy_kw<2>(a, s);
 }
 
 __global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
@@ -3715,32 +3827,53 @@ __global__ __launch_bounds__(1024) void clear_kernel(ClearList l) {
         for (uint32_t i = threadIdx.x; i < l.words[k]; i += 1024) l.p[k][i] = 0u;
 }
 
-__global__ __launch_bounds__(1024) void bucket_stats_kernel(const unsigned long long* bfill, uint32_t NB,
-                                                            const uint32_t* misc, uint64_t* totals) {
-    __shared__ unsigned long long s_sum, s_max;
-    if (threadIdx.x == 0) {
-        s_sum = 0;
-        s_max = 0;
-    }
+// After the record pass: R (records), the largest bucket and the status word
+// next to N for the host's one mid-finalize copy, and the exclusive prefix of
+// the bucket fills (clamped to the capacity) -> bbase[NB + 1], which the bucket
+// ordering reads (one launch where a stats kernel and a bases kernel were two)
+__global__ __launch_bounds__(1024) void bucket_stats_kernel(const unsigned long long* __restrict__ bfill, uint32_t NB,
+                                                            const uint32_t* misc, uint64_t* totals, uint64_t cap,
+                                                            const uint64_t* __restrict__ rbase,
+                                                            uint64_t* __restrict__ bbase) {
+    __shared__ uint64_t red[16];
+    __shared__ uint32_t mxw[16];
+    const uint32_t t = threadIdx.x;
+    const int lane = (int)(t & 63u), wid = (int)(t >> 6);
+    const uint64_t f = t < NB ? bfill[t] : 0ull;  // (NB <= 1024)
+    const uint64_t v = t < NB ? min<uint64_t>(f, region_room(rbase, cap, t)) : 0ull;
+    const uint64_t inc = wave_incl_scan(v, lane);
+    // fills < 2^32 (a region's capacity); a larger one is clamped for the max
+    const uint32_t m = wave_max_u32((uint32_t)min<uint64_t>(f, 0xFFFFFFFFull));
+    uint64_t fs = f;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) fs += (uint64_t)__shfl_xor((long long)fs, off, 64);
+    if (lane == 63) red[wid] = inc;
+    if (lane == 0) mxw[wid] = m;
+    __shared__ uint64_t fsum[16];
+    if (lane == 0) fsum[wid] = fs;
     __syncthreads();
-    unsigned long long sum = 0, mx = 0;
-    for (uint32_t d = threadIdx.x; d < NB; d += 1024) {
-        sum += bfill[d];
-        mx = max(mx, bfill[d]);
+    uint64_t wp = 0, tot = 0, sum = 0;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        if (w < wid) wp += red[w];
+        tot += red[w];
+        sum += fsum[w];
+        mx = max(mx, mxw[w]);
     }
-    atomicAdd(&s_sum, sum);
-    atomicMax(&s_max, mx);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        totals[12] = s_sum;
-        totals[13] = s_max;
+    if (t < NB) bbase[t] = wp + inc - v;
+    if (t == 0) {
+        bbase[NB] = tot;
+        totals[12] = sum;
+        totals[13] = mx;
         totals[14] = misc[0];
     }
 }
 
 hipError_t launch_bucket_stats(const unsigned long long* bfill, uint32_t NB, const uint32_t* misc, uint64_t* totals,
-                               hipStream_t s) {
-    hipLaunchKernelGGL(bucket_stats_kernel, dim3(1), dim3(1024), 0, s, bfill, NB, misc, totals);
+                               uint64_t cap, const uint64_t* rbase, uint64_t* bbase, hipStream_t s) {
+    if (NB > 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bucket_stats_kernel, dim3(1), dim3(1024), 0, s, bfill, NB, misc, totals, cap, rbase, bbase);
     return hipGetLastError();
 }
 
@@ -3767,7 +3900,7 @@ hipError_t load_bin_kernels() {
         (const void*)sk_kmers_total_kernel, (const void*)sk_convert_buckets_kernel<2>,
         (const void*)sk_convert_buckets_kernel<4>, (const void*)bucket_kernel<2>, (const void*)bucket_kernel<4>,
         (const void*)bucket_bases_kernel, (const void*)bucket_stats_kernel, (const void*)bins_order_kernel,
-        (const void*)bins_desc_kernel, (const void*)hll_kernel<1>, (const void*)hll_kernel<2>,
+        (const void*)bins_desc_kernel, (const void*)bins_plan_kernel, (const void*)hll_kernel<1>, (const void*)hll_kernel<2>,
         (const void*)hll_finish_kernel, (const void*)bin_kernel<1>, (const void*)bin_kernel<2>,
         (const void*)flat_count_kernel<1>, (const void*)flat_count_kernel<2>, (const void*)flat_scan_kernel,
         (const void*)flat_scatter_kernel<1>, (const void*)flat_scatter_kernel<2>,

@@ -136,6 +136,7 @@ struct BucketArgs {
     uint64_t* w3;
     int spw;                   // span words per record: 2 (K <= 31) or 4 (K <= 63)
     uint64_t* bbase;           // [NB + 1] output base of each bucket (bucket_bases_kernel)
+    int bases_ready;           // bbase already written (bucket_stats_kernel after the record pass)
     int sub;                   // records carry their context sub-bin (sub_room): group by (mmer, sub-bin)
     uint32_t* bocc;            // [max_bins] k-mer occurrences of the bin (0: not counted), or null
     unsigned long long* bin_ctr;   // bins (zeroed; = totals[2])
@@ -349,7 +350,15 @@ hipError_t launch_sk_kmers_total(const unsigned long long* part, uint64_t n, uns
 hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t R, uint64_t* srec,
                             hipStream_t s);
 // ev_bin[2]: recorded right before and right after bin_kernel (timing), or null
-hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin = nullptr);
+// heavy: also the published bins' kernels (flat lists, partitions); without,
+// launch_bins_heavy runs them later (a finalize that expected none)
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin = nullptr,
+                       bool heavy = true);
+hipError_t launch_bins_heavy(const BinArgs& a, int KW, hipStream_t s);
+// launch_bins_order + launch_bins_desc in one launch (bucketed path)
+hipError_t launch_bins_plan(const uint32_t* bstart, const uint32_t* bcount, const uint32_t* bmmer,
+                            const uint32_t* bocc, const uint64_t* totals, uint64_t max_bins, uint32_t* order,
+                            uint4* desc, unsigned long long* stage_ctr, hipStream_t s);
 hipError_t launch_bins_desc(const uint32_t* order, const uint32_t* bstart, const uint32_t* bcount,
                             const uint32_t* bmmer, const uint32_t* bocc, const uint64_t* totals, uint64_t max_bins,
                             uint4* desc, unsigned long long* stage_ctr, hipStream_t s);
@@ -399,7 +408,7 @@ hipError_t launch_clear(const ClearList& l, hipStream_t s);
 // totals[12] = sum of the NB bucket fills (records), totals[13] = the largest,
 // totals[14] = status word misc[0]: the record pass's results in one copy
 hipError_t launch_bucket_stats(const unsigned long long* bfill, uint32_t NB, const uint32_t* misc, uint64_t* totals,
-                               hipStream_t s);
+                               uint64_t cap, const uint64_t* rbase, uint64_t* bbase, hipStream_t s);
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                              uint64_t max_entries, const unsigned long long* flat_n, const unsigned long long* lq_n,
                              hipStream_t s);

@@ -127,7 +127,9 @@ typedef struct {
     uint32_t clustered_lists; /* of those, lists sorted by the full network    */
     uint32_t split_mmers;   /* mmers whose bins were split into context
                                sub-bins (the bucket map the pass used)         */
-    uint32_t reserved0;
+    uint32_t tail_reruns;   /* binned: 1 when this finalize left the tail kernels
+                               out (the last one needed none) and then ran them
+                               after all (a heavy bin published, lists queued) */
 } kb_timing;
 
 /* Create a context (kb_create replaces zcreate_hash_table for the level-1

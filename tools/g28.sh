@@ -1,0 +1,13 @@
+# round 3b: tail deferral + fused bins plan + fused bucket stats (product) vs
+# the r03 library (lib/ab_old), alternating; then the -m gpu suite
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r3b1; mkdir -p $O
+NOX="--cpu-sample 0 --no-capacity --no-host-input --steps 30 --warmup 5"
+for i in 1 2; do
+  timeout -k 10 200 python -u bench.py $NOX > $O/new$i.json 2> $O/new$i.err || exit 1
+  KB_LIB_PATH=genome-assembly_amd/lib/ab_old/libkbin.so timeout -k 10 200 python -u bench.py $NOX > $O/old$i.json 2> $O/old$i.err || exit 1
+done
+timeout -k 10 1500 python -u -m pytest -x -v -m gpu --timeout 900 --timeout-method thread tests > $O/gpu_tests.txt 2>&1 || exit 1
+echo rc=$?
