@@ -373,6 +373,8 @@ def roofline(passes, L, K, world, kmers_scanned_per_s, tag):
     bpk = algorithmic_bytes_per_read(L, K) / max(1, L - K + 1)
     binned = int(tim[-1]["engine"]) == kbin.KB_ENG_BINNED
     kname = "bin_kernel" if binned else ("scan_insert_kernel<1>" if K <= 31 else "scan_insert_kernel<2>")
+    # (runs_ms 0: the pass ran with bin_kernel's events only -- a light-bin
+    # workload, see main)
     bin_alone = binned and all(0 < t.get("bin_kernel_ms", 0) and t["bin_kernel_ms"] >= 0.5 * t["runs_ms"]
                                for t in tim)
     if binned and not bin_alone:
@@ -509,6 +511,9 @@ def main():
                          "one kb_split_passes scan into the passes' regions")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: no overlap of the next unit's record exchange with this unit's binning")
+    ap.add_argument("--timing-all", action="store_true",
+                    help="every phase event in the timed steps too (by default light-bin workloads record only "
+                         "bin_kernel's two events there)")
     ap.add_argument("--routed", action="store_true",
                     help="N=1 through the multi-GPU path (route, all-to-all over a 1-rank group, "
                          "receive): measures the routing overhead on one GPU")
@@ -653,6 +658,16 @@ def main():
         else:
             step()
     drain()
+    # Every phase event idles the GPU for ~5 us (seven per finalize: ~35 us of
+    # a 2-ms C2 step).  The phases come from the last warmup step; where
+    # bin_kernel is the bin phase (light bins) the timed steps record only the
+    # two events around it (the roofline's kernel time); heavy-bin workloads
+    # keep every event (their roofline kernel is the whole bin phase)
+    phase_log = [(d, t) for d, t, _ in pass_log] if args.warmup else []
+    light = bool(phase_log) and not args.timing_all and all(int(t["engine"]) == kbin.KB_ENG_BINNED and t["bin_kernel_ms"] > 0
+                                    and t["bin_kernel_ms"] >= 0.5 * t["runs_ms"] for _, t in phase_log)
+    if light:
+        eng.set_timing("kernel")
 
     steps_log = []  # per step: [(export_device, timing)] of each finalize (pass)
     barrier()
@@ -684,9 +699,11 @@ def main():
     tim = [t for _, t in passes]
     tag = f"n{n}_L{L}_K{K}_M{M}" + (f"_P{args.parts}" if args.parts > 1 else "")
     roof = roofline(passes, L, K, world, total_scanned * args.steps / elapsed, tag)
-    # device time per step (all passes of a step added up)
-    phases = {k: round(float(np.mean([sum(t[k] for _, t in st) for st in steps_log])), 4)
+    # device time per step (all passes of a step added up): the timed steps',
+    # or -- timed with bin_kernel's events only -- the last warmup step's
+    phases = {k: round(float(np.mean([sum(t[k] for _, t in st) for st in ([phase_log] if light else steps_log)])), 4)
               for k in ("scan_insert_ms", "sort_ms", "runs_ms", "emit_ms", "total_ms")}
+    phases["source"] = "last warmup step (all phase events)" if light else "timed steps"
     replay = None
     if fresh and args.steps:
         # the same number of steps replaying one set (round 1's headline mode)

@@ -317,7 +317,7 @@ struct kb_ctx {
     bool exported = false;
 
     // timing
-    bool timing = false;
+    int timing = 0;  // KB_TIMING_ALL / KB_TIMING_KERNEL (kb_set_timing)
     kb_timing tm{};
     uint32_t nbins_hint = 0;  // bins of the last binned finalize (flat-list threshold)
     // grid hints for kernels that usually have nothing to do (~0: not seen yet)
@@ -685,7 +685,8 @@ static uint64_t next_pow2(uint64_t x) {
 
 extern "C" int kb_set_timing(kb_ctx* c, int enable) {
     if (!c) return fail(KB_EINVAL, "null ctx");
-    c->timing = enable != 0;
+    if (enable < 0 || enable > KB_TIMING_KERNEL) return fail(KB_EINVAL, "timing mode %d", enable);
+    c->timing = enable;
     return KB_OK;
 }
 
@@ -695,8 +696,14 @@ extern "C" int kb_get_timing(kb_ctx* c, kb_timing* out) {
     return KB_OK;
 }
 
+// phase events: every mode on the table engine; the binned engine's
+// KB_TIMING_KERNEL records only the two events around bin_kernel (each event
+// record leaves the GPU idle some 5 us: seven of them cost ~35 us per C2 step)
 #define REC(i) \
-    do { if (c->timing) HIPCHK(hipEventRecord(c->ev[i], c->s)); } while (0)
+    do {                                                                                     \
+        if (c->timing == KB_TIMING_ALL || (c->timing && c->tm.engine == KB_ENG_TABLE))      \
+            HIPCHK(hipEventRecord(c->ev[i], c->s));                                          \
+    } while (0)
 
 // words per routed super-k-mer record: header + span of n + K - 1 <= 2K - M bases
 static int rec_words(const kb_ctx* c) { return 1 + (2 * c->p.K - c->p.M + 31) / 32; }
@@ -1808,6 +1815,13 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         ba.bmmer = c->bmmer.p;
         ba.bocc = c->bocc.p;
         ba.max_bins = max_bins;
+#ifdef KB_BIN_ABL
+        {   // (diagnostic: from a context's third finalize on, so the records
+            // the bin kernel reads are the last pass's -- replay input only)
+            static int abl_calls = 0;
+            ba.ablate = abl_calls++ >= 2 ? env_int("KB_BK_ABLATE", 0) : 0;
+        }
+#endif
         ba.status = c->misc.p;
         HIPCHK(launch_bucket_sort(ba, NB, c->s));
         c->tm.sort_passes = 0;
@@ -2158,14 +2172,16 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     // else the kept keys plus a margin for sketch collisions and counts 2..cutoff
     if (N) c->rho_tab = a.pf ? (float)((double)c->h_totals[11] / (double)N * 1.05)
                              : std::min(c->rho, (float)((double)c->n_entries / (double)N * 1.3 + 0.01));
-    if (c->timing) {
+    if (c->timing == KB_TIMING_ALL) {
         HIPCHK(hipEventElapsedTime(&c->tm.scan_insert_ms, c->ev[1], c->ev[2]));
         HIPCHK(hipEventElapsedTime(&c->tm.sort_ms, c->ev[2], c->ev[3]));
         HIPCHK(hipEventElapsedTime(&c->tm.runs_ms, c->ev[3], c->ev[4]));
         HIPCHK(hipEventElapsedTime(&c->tm.emit_ms, c->ev[4], c->ev[5]));
         HIPCHK(hipEventElapsedTime(&c->tm.total_ms, c->ev[0], c->ev[5]));
-        HIPCHK(hipEventElapsedTime(&c->tm.bin_kernel_ms, c->ev[6], c->ev[7]));
+    } else {
+        c->tm.scan_insert_ms = c->tm.sort_ms = c->tm.runs_ms = c->tm.emit_ms = c->tm.total_ms = 0.f;
     }
+    if (c->timing) HIPCHK(hipEventElapsedTime(&c->tm.bin_kernel_ms, c->ev[6], c->ev[7]));
     {
         const uint64_t* ps = c->h_totals + 16;  // (BinArgs::pstat)
         c->tm.heavy_bins = (uint32_t)ps[0];

@@ -24,6 +24,8 @@
 #include <cmath>
 #include <cstdio>
 
+#include <hip/hip_ext.h>
+
 #include "kbin_internal.h"
 #include "kbin_device.h"
 
@@ -188,6 +190,39 @@ DEV uint32_t record_pieces(const SkScanArgs& A, uint32_t canon, int lo, int n, i
     return 1;
 }
 
+// The record pass's count loop plans each staged record once -- its pieces'
+// destinations from the map entry me (bucket_map[canon - 2^(2M-1)], loaded by
+// the caller) -- and caches the plan in the staged entry, so the placement
+// loop repeats no map lookups.  Staged entry bits: lo 0..15 (< 512 for the
+// thread kernel's reads), n 16..21, so 22..27, rev 28, row 29..37, canon
+// 38..63; planned: canon -> d0 | d1 << 10 | ne << 20 | (pieces - 1) << 25, and
+// the sub-bin depth b in bits 9..11.
+DEV uint64_t record_plan(const SkScanArgs& A, uint64_t e, uint32_t me, const uint64_t* row) {
+    const uint32_t canon = (uint32_t)(e >> 38);
+    const int lo = (int)(e & 0x1FFu), n = (int)((e >> 16) & 63u), so = (int)((e >> 22) & 63u);
+    const bool rev = ((e >> 28) & 1u) != 0;
+    uint32_t d0 = 0, d1 = 0, b = 0, two = 0;
+    int ne = 0;
+    if (!A.bucket_map) {
+        d0 = dest_of(canon, A.G, A.dest_salt);
+    } else if (!(b = bm_depth(me))) {
+        d0 = me & 1023u;
+    } else {
+        const uint64_t w = window64(row, lo + so + A.M);  // the read's bases after the signature
+        const int ec = sub_edge(so, n, A.K, A.M, b);
+        if (ec > 0 && ec < n) {
+            ne = ec;
+            two = 1;
+            d0 = bm_bucket(me, A.sub_map, 0u);
+            d1 = bm_bucket(me, A.sub_map, sub_ctx(so - ec, A.K, A.M, b, w, rev));
+        } else {
+            d0 = bm_bucket(me, A.sub_map, sub_ctx(so, A.K, A.M, b, w, rev));
+        }
+    }
+    const uint64_t pk = (uint64_t)d0 | ((uint64_t)d1 << 10) | ((uint64_t)ne << 20) | ((uint64_t)two << 25);
+    return (e & 0x3FFFFF01FFull) | ((uint64_t)b << 9) | (pk << 38);
+}
+
 // Add one record to a packed 16-bit LDS destination count (two per word) and
 // return the count before it, aggregated over the wave: lanes bound for the
 // same destination share one atomic (the lowest lane's) and take their
@@ -240,6 +275,21 @@ constexpr uint32_t SK_STAGE = 4992;   // (two blocks per CU)
 static_assert(SKT <= 512, "a staged record keeps its row in 9 bits");
 constexpr uint32_t SK_MAX_DEST = 1024;  // destination regions (ranks or buckets)
 
+#ifdef KB_BIN_PROF
+// record pass phases (thread 0's clock at the block's barriers, summed over
+// blocks): row loads, walk, per-destination counts + reservations, placement
+__device__ unsigned long long g_sk_prof[8];
+#define SKPROF(ph)                                        \
+    do {                                                  \
+        if (tid == 0) {                                   \
+            const unsigned long long t1_ = clock64();     \
+            atomicAdd(&g_sk_prof[ph], t1_ - skt_);        \
+            skt_ = t1_;                                   \
+        }                                                 \
+    } while (0)
+#else
+#define SKPROF(ph) do {} while (0)
+#endif
 template <bool WRITE>
 __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -260,6 +310,9 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
     const bool alloc = WRITE && (A.rec_ctr || route);  // records placed by block allocation
     const bool rounds = alloc && !(route && A.G > 64);  // see the walk below
     uint64_t kmers = 0;
+#ifdef KB_BIN_PROF
+    unsigned long long skt_ = clock64();
+#endif
     for (uint64_t r0 = (uint64_t)blockIdx.x * SKT; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * SKT) {
         const uint32_t nrows = (uint32_t)min<uint64_t>(SKT, A.n_reads - r0);
         __syncthreads();
@@ -271,6 +324,7 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
             for (int w = RW; w < RS; w++) smem[tid * RS + w] = 0;
         if (tid == 0) span_end = 0;
         __syncthreads();
+        SKPROF(0);
         const uint64_t bfirst = WRITE && !alloc ? A.rec_base[r0] : 0;
         // Block allocation onto few counters (ranks, or the one record counter)
         // runs in rounds: a walk whose record finds the stage full stops there
@@ -330,7 +384,21 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                     const uint64_t rev = bsm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
                     const uint64_t e = (uint64_t)lo | (n << 16) | ((uint64_t)(sig - lo) << 22) | (rev << 28) |
                                        ((uint64_t)tid << 29) | ((uint64_t)(uint32_t)best << 38);
-                    const uint64_t loc = alloc ? (uint64_t)atomicAdd(&span_end, 1u) : rbase + nseg - bfirst;
+                    // one stage slot per record: one atomic per wave (the lanes
+                    // still walking take consecutive slots) -- 512 lanes' atomics
+                    // on the one LDS word serialised every segment round
+                    uint64_t loc;
+                    if (alloc) {
+                        const uint64_t am = __ballot(1);
+                        const int lead = __builtin_ctzll(am);
+                        uint32_t wb = 0;
+                        if ((int)(tid & 63u) == lead) wb = atomicAdd(&span_end, (uint32_t)__popcll(am));
+                        wb = (uint32_t)__shfl((int)wb, lead, 64);
+                        loc = (uint64_t)wb + __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+                    } else {
+                        loc = rbase + nseg - bfirst;
+                    }
                     if (loc < SK_STAGE) {
                         stg[loc] = e;
                     } else if (rounds) {
@@ -367,25 +435,40 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 atomicMax(&span_end, (uint32_t)min<uint64_t>(rbase + nseg - bfirst, SK_STAGE));
             if (!WRITE) break;
             __syncthreads();
+            SKPROF(1);
             const uint32_t span = min(span_end, SK_STAGE);
             if (route) {
                 // per destination: count, reserve a range, place (LDS cursors)
                 for (uint32_t d = tid; d < (A.G + 1) / 2; d += SKT) dcnt2[d] = 0;
                 __syncthreads();
                 const bool agg = A.G <= 64;  // ranks, not local buckets: aggregate per wave
-                for (uint32_t i = tid; i < span; i += SKT) {
-                    const uint64_t e = stg[i];
-                    const uint32_t row = (uint32_t)((e >> 29) & 0x1FFu);
-                    uint32_t d[2], sub[2];
-                    int ne;
-                    const uint32_t np_ = record_pieces(A, (uint32_t)(e >> 38), (int)(e & 0xFFFFu), (int)((e >> 16) & 63u),
-                                                       (int)((e >> 22) & 63u), ((e >> 28) & 1u) != 0, smem + row * RS, d,
-                                                       sub, ne);
-                    for (uint32_t q = 0; q < np_; q++) {
-                        if (agg)
-                            wave_dest_add(dcnt2, d[q]);
-                        else
-                            atomicAdd(&dcnt2[d[q] >> 1], 1u << (16 * (d[q] & 1)));
+                const uint32_t half = 1u << (2 * M - 1);
+                // two records per trip: both map loads in flight together
+                for (uint32_t i0 = tid; i0 < span; i0 += 2 * SKT) {
+                    const uint32_t i1 = i0 + SKT;
+                    const bool v1 = i1 < span;
+                    const uint64_t e0 = stg[i0], e1 = v1 ? stg[i1] : e0;
+                    uint32_t me0 = 0, me1 = 0;
+                    if (A.bucket_map) {
+                        me0 = A.bucket_map[(uint32_t)(e0 >> 38) - half];
+                        me1 = A.bucket_map[(uint32_t)(e1 >> 38) - half];
+                    }
+                    const uint64_t p0 = record_plan(A, e0, me0, smem + ((e0 >> 29) & 0x1FFu) * RS);
+                    const uint64_t p1 = record_plan(A, e1, me1, smem + ((e1 >> 29) & 0x1FFu) * RS);
+                    stg[i0] = p0;
+                    if (v1) stg[i1] = p1;
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        const uint64_t pl = u ? p1 : p0;
+                        if (u && !v1) break;
+                        const uint32_t np_ = 1u + (uint32_t)((pl >> 63) & 1u);
+                        for (uint32_t q = 0; q < np_; q++) {
+                            const uint32_t dq = (uint32_t)(pl >> (38 + 10 * q)) & 1023u;
+                            if (agg)
+                                wave_dest_add(dcnt2, dq);
+                            else
+                                atomicAdd(&dcnt2[dq >> 1], 1u << (16 * (dq & 1)));
+                        }
                     }
                 }
                 __syncthreads();
@@ -398,16 +481,24 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 __syncthreads();
                 for (uint32_t d = tid; d < (A.G + 1) / 2; d += SKT) dcnt2[d] = 0;
                 __syncthreads();
+                SKPROF(2);
                 for (uint32_t i = tid; i < span; i += SKT) {
-                    const uint64_t e = stg[i];
+                    const uint64_t e = stg[i];  // (planned)
                     const uint32_t row = (uint32_t)((e >> 29) & 0x1FFu);
-                    const int lo = (int)(e & 0xFFFFu), n = (int)((e >> 16) & 63u), so = (int)((e >> 22) & 63u);
-                    uint32_t d[2], sub[2];
-                    int ne;
-                    const uint32_t np_ = record_pieces(A, (uint32_t)(e >> 38), lo, n, so, ((e >> 28) & 1u) != 0,
-                                                       smem + row * RS, d, sub, ne);
+                    const int lo = (int)(e & 0x1FFu), n = (int)((e >> 16) & 63u), so = (int)((e >> 22) & 63u);
+                    const bool rev = ((e >> 28) & 1u) != 0;
+                    const uint32_t b = (uint32_t)((e >> 9) & 7u), np_ = 1u + (uint32_t)((e >> 63) & 1u);
+                    const int ne = (int)((e >> 58) & 31u);
+                    const uint64_t* rw_ = smem + row * RS;
+                    // the pieces' sub-bins (the stamp), from the read's bases in LDS
+                    uint32_t sub[2] = {0u, 0u};
+                    if (A.sub_stamp && b) {
+                        const uint64_t w = window64(rw_, lo + so + M);
+                        if (np_ == 2) sub[1] = sub_ctx(so - ne, K, M, b, w, rev);
+                        else sub[0] = sub_ctx(so, K, M, b, w, rev);
+                    }
                     for (uint32_t q = 0; q < np_; q++) {
-                        const uint32_t dq = d[q];
+                        const uint32_t dq = (uint32_t)(e >> (38 + 10 * q)) & 1023u;
                         const uint64_t slot =
                             (uint64_t)dbase[dq] +
                             (agg ? wave_dest_add(dcnt2, dq)
@@ -417,7 +508,7 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                         const int pn = np_ == 2 && q == 0 ? ne : n - cut;
                         put_record(A, A.regions + (region_off(A.region_base, A.region_cap, dq) + slot) * (uint64_t)A.rw,
                                    A.ord_base + (uint32_t)(r0 + row), (uint64_t)(lo + cut), (uint64_t)pn,
-                                   (uint64_t)(so - cut), (e >> 28) & 1u, smem + row * RS, sub[q]);
+                                   (uint64_t)(so - cut), rev ? 1u : 0u, rw_, sub[q]);
                     }
                 }
             } else {
@@ -440,6 +531,10 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 }
             }
             // another round while a walk stopped at the full stage
+#ifdef KB_BIN_PROF
+            __syncthreads();
+            SKPROF(3);
+#endif
             if (!rounds || !__syncthreads_or(lo < nK)) break;
             if (tid == 0) span_end = 0;
             __syncthreads();
@@ -2318,6 +2413,13 @@ void bins_prof_report(hipStream_t s) {
     unsigned long long h[16];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bin_prof), sizeof(h));
+    {
+        unsigned long long g[8];
+        (void)hipMemcpyFromSymbol(g, HIP_SYMBOL(g_sk_prof), sizeof(g));
+        fprintf(stderr, "[sk_prof] rows=%llu walk=%llu counts=%llu place=%llu\n", g[0], g[1], g[2], g[3]);
+        unsigned long long z8[8] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sk_prof), z8, sizeof(z8));
+    }
     static const char* nm[16] = {"bin records", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
                                  "partitions", "overflows", "omode-ovf(1e6*n+1e3*width+Lv)", "bins", "slowest-bin-occ", "slowest-bin-cycles",
                                  "occ", "records expanded"};
@@ -3493,6 +3595,9 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     }
     __syncthreads();
     const uint64_t base = s_base;
+#ifdef KB_BIN_ABL
+    if (A.ablate == 2) return;
+#endif
     for (uint64_t i0 = tid; i0 < cnt; i0 += U * BK_THREADS) {
         uint64_t h[U], a[U], b[U], c[U], d[U];
 #pragma unroll
@@ -3515,6 +3620,12 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
             bk_decode<ROWS>(h[u], a[u], b[u], SPW == 2 ? b[u] : d[u], A, bkey, row);
             const int sl = bk_slot(keys, bkey, false);
             const uint64_t pos = base + atomicAdd(&hist[sl * ROWS + row], 1u);
+#ifdef KB_BIN_ABL
+            if (A.ablate == 1) {
+                if (pos == ~0ull) A.hdr[0] = h[u] ^ a[u] ^ b[u];  // (keeps the loads alive)
+                continue;
+            }
+#endif
             A.hdr[pos] = h[u];
             A.w0[pos] = a[u];
             A.w1[pos] = b[u];
@@ -3785,14 +3896,11 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     BinArgs a2;
     hipError_t e = bins_grid<KW>(a, blocks, cus, lds, a2);
     if (e != hipSuccess) return e;
-    if (ev_bin) {
-        e = hipEventRecord(ev_bin[0], s);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS), lds, s,
-                       a2);
+    // timing: the kernel's own start and stop (hipExtLaunchKernelGGL) -- an
+    // event recorded on the stream before and after it idled the GPU ~6 us each
+    hipExtLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS),
+                          (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr, ev_bin ? ev_bin[1] : nullptr, 0u, a2);
     e = hipGetLastError();
-    if (e == hipSuccess && ev_bin) e = hipEventRecord(ev_bin[1], s);
     if (e != hipSuccess || !heavy) return e;
     return launch_heavy_kw<KW>(a, s);
 }

@@ -144,6 +144,8 @@ struct BucketArgs {
     uint32_t* bcount;          // [max_bins] records of bin
     uint32_t* bmmer;           // [max_bins] the bin's canonical mmer
     uint64_t max_bins;
+    int ablate;                // KB_BIN_ABL builds: KB_BK_ABLATE (1: no placement stores, 2: no
+                               // placement pass) -- results wrong by design
     uint32_t* status;          // ST_BUCKET_FULL: a bucket holds too many bins
 };
 

@@ -365,8 +365,11 @@ class Engine:
         (kbin.h: partitioned passes; the read batches are kept)"""
         _check(self.lib, self.lib.kb_set_partition(self._h, int(part), int(n_parts)))
 
-    def set_timing(self, on: bool = True) -> None:
-        _check(self.lib, self.lib.kb_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on=True) -> None:
+        """True / 1: every phase event; "kernel" / 2: only bin_kernel's (binned
+        engine: no idle gaps from the phase events); False / 0: off"""
+        mode = 2 if on == "kernel" else int(on)
+        _check(self.lib, self.lib.kb_set_timing(self._h, mode))
 
     def timing(self) -> dict:
         t = kb_timing()

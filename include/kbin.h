@@ -187,7 +187,12 @@ int kb_digest(kb_ctx *ctx, uint64_t out[4]);
 /* Drop all submitted reads and results; keeps allocations for reuse. */
 int kb_reset(kb_ctx *ctx);
 
-/* Per-phase timing of the last finalize (enable before kb_finalize). */
+/* Per-phase timing of the last finalize (enable before kb_finalize):
+ * 0 off, KB_TIMING_ALL every phase event, KB_TIMING_KERNEL (binned engine)
+ * only the two events around bin_kernel (bin_kernel_ms; the phase fields read
+ * 0) -- each event record idles the GPU for a few microseconds. */
+#define KB_TIMING_ALL 1
+#define KB_TIMING_KERNEL 2
 int kb_set_timing(kb_ctx *ctx, int enable);
 int kb_get_timing(kb_ctx *ctx, kb_timing *out);
 

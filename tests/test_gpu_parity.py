@@ -105,6 +105,33 @@ def test_binned_engine_selected(engine):
         assert t["n_superkmers"] > 0 and t["n_bins"] > 0
 
 
+def test_timing_modes(engine):
+    """kb_set_timing: every phase (1), bin_kernel's two events only (2: the
+    phase fields read 0 on the binned engine; the table engine keeps them), off
+    (0); anything else is KB_EINVAL.  The result does not depend on it."""
+    rng = np.random.default_rng(4)
+    reads = [rng.choice(np.frombuffer(b"ACGT", np.uint8), 150).tobytes() for _ in range(2000)]
+    bases, lens = kbin.pack_reads(reads)
+    ora = oracle.bin_reads(bases, lens, 31, 7, 1, True)
+    with kbin.Engine(31, 7, cutoff=1, max_read_len=150) as eng:
+        with pytest.raises(kbin.KbError):
+            kbin._check(eng.lib, eng.lib.kb_set_timing(eng._h, 3))
+        for mode in (True, "kernel", False):
+            eng.reset()
+            eng.set_timing(mode)
+            eng.submit(bases=bases, lens=lens, first_id=0)
+            eng.finalize(prune=True)
+            assert_same(eng.export(), ora)
+            t = eng.timing()
+            binned = t["engine"] == kbin.KB_ENG_BINNED
+            if mode is True:
+                assert t["total_ms"] > 0 and (t["bin_kernel_ms"] > 0 or not binned), t
+            elif mode == "kernel":
+                assert t["total_ms"] == 0 if binned else t["total_ms"] > 0, t
+                if binned:
+                    assert t["bin_kernel_ms"] > 0, t
+
+
 @pytest.mark.parametrize("K,M", [(63, 7), (33, 7), (32, 8), (45, 1), (63, 1), (40, 6)])
 def test_binned_two_word_kmers(K, M, engine, monkeypatch):
     """K > 31: the binned engine with two-word table keys (LDS claim word +
@@ -481,6 +508,50 @@ def test_offset_partitions(genome, ts_log2, fill, osplit, track, engine, monkeyp
             if track:
                 last = res.ids[res.offset[1:].astype(np.int64) - 1]
                 np.testing.assert_array_equal(res.first >> np.uint64(16), last.astype(np.uint64))
+
+
+@pytest.mark.parametrize("second", ["heavy", "lists"])
+def test_deferred_tail_surprise(second, engine, monkeypatch):
+    """a finalize after one that needed no tail kernels (no heavy bins, no
+    queued lists) leaves them out; when its own bins publish a heavy bin
+    (small forced tables) or queue long lists (2000x coverage) it runs them
+    after all -- kb_timing.tail_reruns says so -- and the result still equals
+    the oracle's"""
+    import torch
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    L, K, M = 150, 31, 7
+    wpr = (L + 31) // 32
+
+    def reads(n, genome, seed):
+        words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+        lens = torch.empty(n, dtype=torch.int32, device="cuda")
+        kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, genome, 1000, seed)
+        torch.cuda.synchronize()
+        return words, lens
+
+    w1, l1 = reads(20000, 2_000_000, 5)  # ~1.5x coverage: light bins, short lists
+    w2, l2 = reads(40000, 3000, 9)       # ~2000x: lists of thousands of ids
+    with kbin.Engine(K, M, cutoff=1, max_read_len=L) as eng:
+        eng.submit_packed_device(w1.data_ptr(), l1.data_ptr(), 20000, wpr, 0)
+        eng.finalize(True)
+        t = eng.timing()
+        assert t["heavy_bins"] == 0 and t["long_lists"] == 0 and t["tail_reruns"] == 0, t
+        if second == "heavy":
+            monkeypatch.setenv("KB_BIN_TS_LOG2", "10")
+            monkeypatch.setenv("KB_BIN_FLAT_L", "1")
+        eng.reset()
+        eng.submit_packed_device(w2.data_ptr(), l2.data_ptr(), 40000, wpr, 0)
+        eng.finalize(True)
+        t = eng.timing()
+        assert t["tail_reruns"] == 1, t
+        if second == "heavy":
+            assert t["heavy_bins"] > 0, t
+        else:
+            assert t["long_lists"] > 0, t
+        res = eng.export()
+    bases, hl = kbin.unpack_reads_to_host(w2.data_ptr(), l2.data_ptr(), 40000, wpr, 40000 * L)
+    assert_same(res, oracle.bin_reads(bases, hl, K, M, 1, True))
 
 
 def test_alphabet_rejected():
