@@ -1794,10 +1794,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         ba.rbase = c->rexact ? c->rbase.p : nullptr;
         ba.bfill = c->bfill.p;
         ba.M = M;
-        ba.hdr = c->srec.p;
-        ba.w0 = c->srec.p + R;
+        ba.hdr = c->srec.p;  // ((header, word 0) pairs, then word 1 / (word 1, word 2) pairs + word 3)
         ba.w1 = c->srec.p + 2 * R;
-        ba.w2 = KW == 2 ? c->srec.p + 3 * R : nullptr;
         ba.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
         ba.spw = 2 * KW;
         HIPCHK(c->bbase.ensure(NB + 1));
@@ -1860,10 +1858,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         // the context's first finalize: distinct keys per occurrence from one
         // HyperLogLog over the records (no learned density yet)
         BinArgs h{};
-        h.hdr = c->srec.p;
-        h.w0 = c->srec.p + R;
+        h.hdr = c->srec.p;  // ((header, word 0) pairs, then word 1 / (word 1, word 2) pairs + word 3)
         h.w1 = c->srec.p + 2 * R;
-        h.w2 = KW == 2 ? c->srec.p + 3 * R : nullptr;
         h.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
         h.K = c->p.K;
         h.M = M;
@@ -1906,10 +1902,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             REC(3);
         }
         a = BinArgs{};
-        a.hdr = c->srec.p;
-        a.w0 = c->srec.p + R;
+        a.hdr = c->srec.p;  // ((header, word 0) pairs, then word 1 / (word 1, word 2) pairs + word 3)
         a.w1 = c->srec.p + 2 * R;
-        a.w2 = KW == 2 ? c->srec.p + 3 * R : nullptr;
         a.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
         a.bstart = c->starts.p;
         a.bcount = c->bcount.p;

@@ -600,9 +600,9 @@ __global__ __launch_bounds__(256) void sk_gather_kernel(const uint64_t* __restri
                                                         uint64_t* __restrict__ srec) {
     for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < R; k += (uint64_t)gridDim.x * 256) {
         const uint64_t t = (uint32_t)keys[k];
-        const uint64_t hd = pay[3 * t];
-        srec[k] = hd;
-        srec[R + k] = pay[3 * t + 1];
+        const uint64_t hd = pay[3 * t], w0 = pay[3 * t + 1];
+        reinterpret_cast<uint4*>(srec)[k] = make_uint4((uint32_t)hd, (uint32_t)(hd >> 32), (uint32_t)w0,
+                                                        (uint32_t)(w0 >> 32));  // (header, word 0) pairs
         srec[2 * R + k] = pay[3 * t + 2];
     }
 }
@@ -837,13 +837,29 @@ struct TKey<2> {
 // a record's span bases in registers, advanced one base per k-mer
 template <int KW>
 struct Span;
+// Bin-ordered records (bucket_kernel, sk_gather_kernel): (header, span word
+// 0) pairs at hdr[2r], hdr[2r + 1] -- one 16-B access -- then span word 1
+// (K <= 31: w1[r]) or (word 1, word 2) pairs at w1[2r], w1[2r + 1] and word 3
+// at w3[r] (K <= 63).  (Three 8-B SoA arrays made bucket_kernel's placement a
+// scattered store per word: 0.145 of its 0.23 ms at C2.)
+DEV uint64_t rec_hdr(const BinArgs& A, uint64_t r) { return A.hdr[2 * r]; }
+DEV uint64_t u64_of(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
 template <>
 struct Span<1> {
     uint64_t w, x;
     DEV void load(const BinArgs& A, uint32_t r) {
-        w = A.w0[r];
+        w = A.hdr[2 * (uint64_t)r + 1];
         x = A.w1[r];
     }
+    // the header and the span together: one 16-B load and one 8-B load
+    DEV void load_rec(const BinArgs& A, uint32_t r, uint64_t& hd) {
+        const uint4 q = reinterpret_cast<const uint4*>(A.hdr)[r];
+        hd = u64_of(q.x, q.y);
+        w = u64_of(q.z, q.w);
+        x = A.w1[r];
+    }
+    DEV uint64_t word0() const { return w; }
+    DEV uint64_t word1() const { return x; }
     // fl = all ones when the complement wins (binning.c:1029-1040), else 0
     DEV TKey<1> key(int K, uint64_t fl) const { return TKey<1>{((w ^ fl) >> (64 - 2 * K)) + 1ull}; }
     DEV void step() {
@@ -861,11 +877,23 @@ template <>
 struct Span<2> {
     uint64_t s0, s1, s2, s3;
     DEV void load(const BinArgs& A, uint32_t r) {
-        s0 = A.w0[r];
-        s1 = A.w1[r];
-        s2 = A.w2[r];
+        s0 = A.hdr[2 * (uint64_t)r + 1];
+        const uint4 p = reinterpret_cast<const uint4*>(A.w1)[r];
+        s1 = u64_of(p.x, p.y);
+        s2 = u64_of(p.z, p.w);
         s3 = A.w3[r];
     }
+    DEV void load_rec(const BinArgs& A, uint32_t r, uint64_t& hd) {
+        const uint4 q = reinterpret_cast<const uint4*>(A.hdr)[r];
+        const uint4 p = reinterpret_cast<const uint4*>(A.w1)[r];
+        hd = u64_of(q.x, q.y);
+        s0 = u64_of(q.z, q.w);
+        s1 = u64_of(p.x, p.y);
+        s2 = u64_of(p.z, p.w);
+        s3 = A.w3[r];
+    }
+    DEV uint64_t word0() const { return s0; }
+    DEV uint64_t word1() const { return s1; }
     // complement without reversal (binning.c:1029-1040) = every code bit
     // flipped: fl = all ones when the complement wins, else 0
     DEV TKey<2> key(int K, uint64_t fl) const {
@@ -1041,8 +1069,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
 #endif
     Span<KW> nsp{};
     if (base + lane < hi) {
-        nhd = A.hdr[base + lane];
-        nsp.load(A, base + lane);
+        nsp.load_rec(A, base + lane, nhd);
     }
     for (; base < hi; base += BIN_THREADS) {
         const uint64_t hd = nhd;
@@ -1050,8 +1077,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
         const uint32_t nxt = base + BIN_THREADS + lane;
         nhd = 0;
         if (nxt < hi) {  // prefetch the next chunk
-            nhd = A.hdr[nxt];
-            nsp.load(A, nxt);
+            nsp.load_rec(A, nxt, nhd);
         }
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
@@ -1159,8 +1185,7 @@ DEV void expand_bin(const BinArgs& A, uint32_t lo, uint32_t hi, G&& g) {
     uint64_t nhd = 0;
     Span<KW> nsp{};
     if (base + lane < hi) {
-        nhd = A.hdr[base + lane];
-        nsp.load(A, base + lane);
+        nsp.load_rec(A, base + lane, nhd);
     }
     for (; base < hi; base += NT) {
         const uint64_t hd = nhd;
@@ -1168,8 +1193,7 @@ DEV void expand_bin(const BinArgs& A, uint32_t lo, uint32_t hi, G&& g) {
         const uint32_t nxt = base + NT + lane;
         nhd = 0;
         if (nxt < hi) {
-            nhd = A.hdr[nxt];
-            nsp.load(A, nxt);
+            nsp.load_rec(A, nxt, nhd);
         }
         const int n = (int)((hd >> 32) & 63u);
         const uint32_t ord = (uint32_t)hd;
@@ -1475,7 +1499,7 @@ DEV void bin_body(const BinArgs& A) {
             if (!occ_tot) {
                 uint64_t occ = 0;
                 for (uint32_t rec = lo + tid; rec < hi; rec += BIN_THREADS)
-                    occ += (A.hdr[rec] >> 32) & 63u;
+                    occ += (rec_hdr(A, rec) >> 32) & 63u;
                 (void)block_excl_scan_u64(occ, S.red, occ_tot);
             }
             // the bin's stage range (one slot per occurrence, reused per partition)
@@ -2071,7 +2095,7 @@ __global__ __launch_bounds__(FB_THREADS) void flat_count_kernel(BinArgs A) {
             // run inside every range, from its header alone
             uint32_t acc[16] = {};
             for (uint32_t r = lo + threadIdx.x; r < hi; r += FB_THREADS) {
-                const uint64_t hd = A.hdr[r];
+                const uint64_t hd = rec_hdr(A, r);
                 const int n = (int)((hd >> 32) & 63u), so = (int)((hd >> 38) & 63u);
 #pragma unroll
                 for (uint32_t q = 0; q < 16; q++) {
@@ -2226,8 +2250,7 @@ __global__ __launch_bounds__(FB_THREADS) void flat_scatter_kernel(BinArgs A) {
             uint64_t nhd = 0;
             Span<KW> nsp{};
             if (base + (uint32_t)lane < hi) {
-                nhd = A.hdr[base + lane];
-                nsp.load(A, base + lane);
+                nsp.load_rec(A, base + lane, nhd);
             }
             for (; base < hi; base += FB_THREADS) {  // (next record's loads first)
                 const uint64_t hd = nhd;
@@ -2235,8 +2258,7 @@ __global__ __launch_bounds__(FB_THREADS) void flat_scatter_kernel(BinArgs A) {
                 const uint32_t nxt = base + FB_THREADS + (uint32_t)lane;
                 nhd = 0;
                 if (nxt < hi) {
-                    nhd = A.hdr[nxt];
-                    nsp.load(A, nxt);
+                    nsp.load_rec(A, nxt, nhd);
                 }
                 const int n = (int)((hd >> 32) & 63u);
                 const uint32_t ord = (uint32_t)hd;
@@ -2326,7 +2348,7 @@ __global__ __launch_bounds__(FSL_THREADS) void flat_scatter_lds_kernel(BinArgs A
             // ---- this segment: the longest record run from lo within E entries
             {
                 const uint32_t r = lo + tid;
-                const uint32_t n = r < c_hi ? (uint32_t)((A.hdr[r] >> 32) & 63u) : 0u;
+                const uint32_t n = r < c_hi ? (uint32_t)((rec_hdr(A, r) >> 32) & 63u) : 0u;
                 const uint32_t inc = wave_incl_scan(n, lane);
                 if (lane == 63) red[wid] = inc;
                 __syncthreads();
@@ -3176,14 +3198,14 @@ __global__ __launch_bounds__(HLL_THREADS) void hll_kernel(BinArgs A, uint64_t R,
     const uint32_t maskM = (1u << (2 * M)) - 1u;
     uint64_t occ = 0;
     for (uint64_t r = (uint64_t)blockIdx.x * HLL_THREADS + threadIdx.x; r < R; r += (uint64_t)gridDim.x * HLL_THREADS) {
-        const uint64_t hd = A.hdr[r];
+        uint64_t hd;
+        Span<KW> sp;
+        sp.load_rec(A, (uint32_t)r, hd);
         const int n = (int)((hd >> 32) & 63u);
         const uint64_t fl = 0ull - ((hd >> 44) & 1ull);
-        Span<KW> sp;
-        sp.load(A, (uint32_t)r);
         if (sample > 1) {
             const int so = (int)((hd >> 38) & 63u);
-            const uint32_t sm = (uint32_t)(span_window(A.w0[r], A.w1[r], 0ull, 0ull, so) >> (64 - 2 * M));
+            const uint32_t sm = (uint32_t)(span_window(sp.word0(), sp.word1(), 0ull, 0ull, so) >> (64 - 2 * M));
             const uint32_t canon = ((hd >> 44) & 1u) ? maskM - sm : sm;
             if (dest_of(canon, sample, HLL_SALT) != 0) continue;
         }
@@ -3626,11 +3648,13 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
                 continue;
             }
 #endif
-            A.hdr[pos] = h[u];
-            A.w0[pos] = a[u];
-            A.w1[pos] = b[u];
-            if constexpr (SPW == 4) {
-                A.w2[pos] = c[u];
+            reinterpret_cast<uint4*>(A.hdr)[pos] = make_uint4((uint32_t)h[u], (uint32_t)(h[u] >> 32), (uint32_t)a[u],
+                                                              (uint32_t)(a[u] >> 32));
+            if constexpr (SPW == 2) {
+                A.w1[pos] = b[u];
+            } else {
+                reinterpret_cast<uint4*>(A.w1)[pos] = make_uint4((uint32_t)b[u], (uint32_t)(b[u] >> 32), (uint32_t)c[u],
+                                                                 (uint32_t)(c[u] >> 32));
                 A.w3[pos] = d[u];
             }
         }

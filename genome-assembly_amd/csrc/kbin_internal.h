@@ -129,11 +129,9 @@ struct BucketArgs {
     const uint64_t* rbase;     // [NB + 1] or null: region d at rbase[d], rbase[d+1]-rbase[d] records
     const unsigned long long* bfill;  // [NB] records per bucket
     int M;
-    uint64_t* hdr;             // [R] SoA output, bins contiguous, longest records first
-    uint64_t* w0;
-    uint64_t* w1;
-    uint64_t* w2;              // K > 31 (spw = 4): span bases 64..127
-    uint64_t* w3;
+    uint64_t* hdr;             // [2R] output (header, span word 0) pairs, bins contiguous, longest first
+    uint64_t* w1;              // [R] span word 1 (K <= 31), or [2R] (word 1, word 2) pairs (spw = 4)
+    uint64_t* w3;              // [R] span word 3 (spw = 4)
     int spw;                   // span words per record: 2 (K <= 31) or 4 (K <= 63)
     uint64_t* bbase;           // [NB + 1] output base of each bucket (bucket_bases_kernel)
     int bases_ready;           // bbase already written (bucket_stats_kernel after the record pass)
@@ -210,11 +208,9 @@ __device__ __forceinline__ uint32_t sub_ctx(int so, int K, int M, uint32_t b, ui
 constexpr uint32_t KB_FLAT_MAX = 16384;  // partitions of one heavy bin's flat lists (kbin_bins.hip FLAT_MAX)
 
 struct BinArgs {
-    const uint64_t* hdr;       // [R] bin-ordered record headers (see SkScanArgs::pay)
-    const uint64_t* w0;        // [R] span bases 0..31
-    const uint64_t* w1;        // [R] span bases 32..63
-    const uint64_t* w2;        // [R] span bases 64..95   (K > 31: two-word k-mers)
-    const uint64_t* w3;        // [R] span bases 96..127
+    const uint64_t* hdr;       // [2R] bin-ordered (header, span bases 0..31) pairs (header: SkScanArgs::pay)
+    const uint64_t* w1;        // [R] span bases 32..63, or [2R] (32..63, 64..95) pairs (K > 31)
+    const uint64_t* w3;        // [R] span bases 96..127 (K > 31: two-word k-mers)
     const uint32_t* bstart;    // [nbins] first record of bin
     const uint32_t* bcount;    // [nbins] records of bin
     const uint32_t* bmmer;     // [nbins] canonical mmer of bin
