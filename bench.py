@@ -353,7 +353,9 @@ def single_gpu_runner(K, M, L, cutoff, n, wpr, P, local, reads, pass_log, scan_o
             if dbg:
                 print(f"[bench] pass {p} done at {1e3 * (time.perf_counter() - t0):.1f} ms", file=sys.stderr,
                       flush=True)
-            pass_log.append((eng.export_device(), eng.timing(), None))
+            # (one pass: its export is the same shape every step -- read once
+            # after the timed steps; the timing struct converted after them too)
+            pass_log.append((eng.export_device() if P > 1 else None, eng.timing_raw(), None))
             if digest:
                 dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
         return dig
@@ -440,7 +442,7 @@ def capacity_leg(local, steps=2, warmup=1):
     log = []
     for _ in range(steps):
         step()
-        log.extend((d, t) for d, t, _ in pass_log)
+        log.extend((d, kbin.timing_dict(t)) for d, t, _ in pass_log)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     kmers = n * (L - K + 1)
@@ -615,7 +617,7 @@ def main():
                 else:
                     w, ln = reads()
                     runner.step(w, ln, n, wpr, first_id=rank * n, part=p, n_parts=P)
-                pass_log.append((eng.export_device(), eng.timing(), runner.last_times))
+                pass_log.append((eng.export_device() if P > 1 else None, eng.timing_raw(), runner.last_times))
                 if digest:
                     dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
             cur[0] += 1
@@ -659,13 +661,17 @@ def main():
             step()
     drain()
     # Every phase event idles the GPU for ~5 us (seven per finalize: ~35 us of
-    # a 2-ms C2 step).  The phases come from the last warmup step; where
-    # bin_kernel is the bin phase (light bins) the timed steps record only the
-    # two events around it (the roofline's kernel time); heavy-bin workloads
-    # keep every event (their roofline kernel is the whole bin phase)
-    phase_log = [(d, t) for d, t, _ in pass_log] if args.warmup else []
+    # a 2-ms C2 step).  Where bin_kernel is the bin phase (light bins) the
+    # timed steps record only its two events (the roofline's kernel time) and
+    # the phases come from one more step after them; heavy-bin workloads keep
+    # every event (their roofline kernel is the whole bin phase)
+    phase_log = [(d, kbin.timing_dict(t)) for d, t, _ in pass_log] if args.warmup else []
     light = bool(phase_log) and not args.timing_all and all(int(t["engine"]) == kbin.KB_ENG_BINNED and t["bin_kernel_ms"] > 0
                                     and t["bin_kernel_ms"] >= 0.5 * t["runs_ms"] for _, t in phase_log)
+    if dist is not None:  # (every rank takes the same branch: the phase step runs collectives)
+        lt = torch.tensor([1 if light else 0], dtype=torch.int32, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(lt, op=dist.ReduceOp.MIN)
+        light = bool(lt.item())
     if light:
         eng.set_timing("kernel")
 
@@ -675,7 +681,7 @@ def main():
     route_t = []
     for _ in range(args.steps):
         step()
-        steps_log.append([(d, t) for d, t, _ in pass_log])
+        steps_log.append([(d, t) for d, t, _ in pass_log])  # (converted after the timed steps)
         if world > 1 or args.routed:
             rts = [r for _, _, r in pass_log]
             route_t.append({k: sum(r[k] for r in rts) for k in rts[0]})
@@ -688,6 +694,16 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    # the Python side of the timed steps kept raw structs: convert them now, and
+    # read a one-pass step's export (the same shape every step) from the last
+    ex_last = eng.export_device()
+    if light:  # the phases: one untimed step with every phase event
+        eng.set_timing(True)
+        step()
+        drain()
+        phase_log = [(d, kbin.timing_dict(t)) for d, t, _ in pass_log]
+        eng.set_timing("kernel")
+    steps_log = [[(d if d is not None else ex_last, kbin.timing_dict(t)) for d, t in st] for st in steps_log]
     last = steps_log[-1]  # the passes of the last step, added up
     dev = {k: sum(int(d[k]) for d, _ in last) for k in ("n_kmers", "n_entries", "n_ids", "n_distinct")}
     n_kmers = dev["n_kmers"]               # occurrences this rank inserted (owned)
@@ -703,7 +719,7 @@ def main():
     # or -- timed with bin_kernel's events only -- the last warmup step's
     phases = {k: round(float(np.mean([sum(t[k] for _, t in st) for st in ([phase_log] if light else steps_log)])), 4)
               for k in ("scan_insert_ms", "sort_ms", "runs_ms", "emit_ms", "total_ms")}
-    phases["source"] = "last warmup step (all phase events)" if light else "timed steps"
+    phases["source"] = "one untimed step after the timed ones (all phase events)" if light else "timed steps"
     replay = None
     if fresh and args.steps:
         # the same number of steps replaying one set (round 1's headline mode)

@@ -242,6 +242,8 @@ struct kb_ctx {
     DevBuf<uint32_t> starts;
     DevBuf<uint32_t> e_mmer, e_cnt;
     DevBuf<uint64_t> e_hi, e_lo, e_off;
+    const uint64_t* e_hi_zeroed = nullptr;  // e_hi is all zero (one-word keys: bin_kernel leaves it alone)
+    uint64_t e_hi_zeroed_cap = 0;           // (an allocation may come back at the same address)
     DevBuf<uint64_t> first, e_first;  // KB_TRACK_FIRST
     DevBuf<int32_t> ids_out;
     DevBuf<uint64_t> scratch;
@@ -459,7 +461,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
     c->regions.release(); c->bfill.release(); c->bbase.release(); c->rbase.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
-    c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release();
+    c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release(); c->e_hi_zeroed = nullptr;
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
     c->misc.release(); c->totals.release(); c->first.release(); c->e_first.release();
     for (auto& m : c->bmaps) { m.map.release(); m.sub.release(); }
@@ -1889,6 +1891,13 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(c->e_mmer.ensure(ecap));
         HIPCHK(c->e_cnt.ensure(ecap));
         HIPCHK(c->e_hi.ensure(ecap));
+        if (KW == 1 && (c->e_hi_zeroed != c->e_hi.p || c->e_hi_zeroed_cap != c->e_hi.cap)) {
+            // K <= 31: every key's high code word is 0; zeroed once per
+            // allocation instead of 8 B per entry from bin_kernel each finalize
+            HIPCHK(hipMemsetAsync(c->e_hi.p, 0, c->e_hi.cap * sizeof(uint64_t), c->s));
+            c->e_hi_zeroed = c->e_hi.p;
+            c->e_hi_zeroed_cap = c->e_hi.cap;
+        }
         HIPCHK(c->e_lo.ensure(ecap));
         HIPCHK(c->e_off.ensure(ecap));
         if (attempt) {  // the bin kernel's counters and status start again
@@ -2358,6 +2367,7 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     HIPCHK(c->e_mmer.ensure(ne_cap));
     HIPCHK(c->e_cnt.ensure(ne_cap));
     HIPCHK(c->e_hi.ensure(ne_cap));
+    c->e_hi_zeroed = nullptr;  // (the table engine writes it)
     HIPCHK(c->e_lo.ensure(ne_cap));
     HIPCHK(c->e_off.ensure(ne_cap));
     if (track_first) HIPCHK(c->e_first.ensure(ne_cap));

@@ -1937,7 +1937,7 @@ DEV void bin_body(const BinArgs& A) {
                             uint64_t khi, klo;
                             key.code(khi, klo);
                             A.e_mmer[ge] = mmer;
-                            A.e_hi[ge] = khi;
+                            if constexpr (KW == 2) A.e_hi[ge] = khi;  // (one-word keys: kept zero, finalize_binned)
                             A.e_lo[ge] = klo;
                             A.e_cnt[ge] = c;
                             A.e_off[ge] = i0 + off;

@@ -371,10 +371,14 @@ class Engine:
         mode = 2 if on == "kernel" else int(on)
         _check(self.lib, self.lib.kb_set_timing(self._h, mode))
 
-    def timing(self) -> dict:
+    def timing_raw(self) -> "kb_timing":
+        """the kb_timing struct itself (one call; timing_dict() converts it)"""
         t = kb_timing()
         _check(self.lib, self.lib.kb_get_timing(self._h, C.byref(t)))
-        return {f: getattr(t, f) for f, _ in kb_timing._fields_ if f != "reserved"}
+        return t
+
+    def timing(self) -> dict:
+        return timing_dict(self.timing_raw())
 
     def stream(self) -> int:
         return self.lib.kb_stream(self._h) or 0
@@ -400,6 +404,10 @@ class Engine:
         _check(self.lib, self.lib.kb_export_device(self._h, C.byref(c)))
         return {f: (getattr(c, f) if f.startswith("n_") else C.cast(getattr(c, f), C.c_void_p).value)
                 for f, _ in kb_csr._fields_}
+
+
+def timing_dict(t: "kb_timing") -> dict:
+    return {f: getattr(t, f) for f, _ in kb_timing._fields_ if f != "reserved"}
 
 
 def generate_reads_device(words_ptr: int, lens_ptr: int, n_reads: int, read_len: int,

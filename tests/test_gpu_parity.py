@@ -256,8 +256,9 @@ def test_partitioned_passes(P, radix, long_reads, K, M, engine, monkeypatch):
     assert tuple(dig) == kbin.result_digest(ora)  # digests add over partitions
 
 
-@pytest.mark.parametrize("K,M,sub", [(21, 5, "4"), (63, 7, "4"), (21, 5, "0"), (31, 7, "1")])
-def test_balanced_buckets(K, M, sub, engine, monkeypatch):
+@pytest.mark.parametrize("K,M,sub,prior", [(21, 5, "4", "1"), (63, 7, "4", "1"), (21, 5, "0", "1"), (31, 7, "1", "1"),
+                                           (31, 7, "4", "0"), (63, 7, "4", "0")])
+def test_balanced_buckets(K, M, sub, prior, engine, monkeypatch):
     """after a pass the host packs the mmers into local buckets by their
     record counts (largest first, least-loaded bucket; an mmer above 1.5 x the
     mean load, or above one LDS table of keys, is split into context sub-bins,
@@ -268,6 +269,7 @@ def test_balanced_buckets(K, M, sub, engine, monkeypatch):
         pytest.skip("binned engine only")
     monkeypatch.setenv("KB_BIN_BALANCE_MIN", "0")
     monkeypatch.setenv("KB_BIN_SUB", sub)
+    monkeypatch.setenv("KB_BIN_PRIOR", prior)  # 0: a first pass without a map counts, then lays regions out exactly
     rng = np.random.default_rng(K)
     genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20000)
     reads = []
