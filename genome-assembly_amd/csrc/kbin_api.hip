@@ -254,6 +254,8 @@ struct kb_ctx {
     DevBuf<uint64_t> pay;      // super-k-mer records, call order (3 words each)
     DevBuf<uint64_t> srec;     // the same, bin order, structure of arrays
     DevBuf<uint64_t> stage;    // per-occurrence (slot, ordinal) staging
+    DevBuf<uint32_t> stage_ord;   // light bins: the stage as ordinals ...
+    DevBuf<uint16_t> stage_slot;  // ... and LDS slots (6 B per occurrence)
     DevBuf<uint64_t> kstage;   // heavy bins: per-occurrence k-mer code + 1
     DevBuf<uint32_t> long_q;   // entries with 257..4096 ids (lists_long_kernel)
     DevBuf<uint64_t> lq;       // list items for lists_kernel (BinArgs::lq_items); [0] the counter
@@ -458,7 +460,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->map_done) (void)hipEventDestroy(c->map_done);
     if (c->h_alpha) (void)hipHostFree(c->h_alpha);
     c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->stage_ord.release(); c->stage_slot.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
     c->regions.release(); c->bfill.release(); c->bbase.release(); c->rbase.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release(); c->e_hi_zeroed = nullptr;
@@ -1771,6 +1773,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     HIPCHK(c->srec.ensure(RWD * R));
     HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));  // ids by ordinal (+ radix ping-pong)
     HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
+    const bool stage6 = env_int("KB_BIN_STAGE6", 1) != 0;
+    if (stage6) {
+        HIPCHK(c->stage_ord.ensure(std::max<uint64_t>(N, 1)));
+        HIPCHK(c->stage_slot.ensure(std::max<uint64_t>(N, 1)));
+    }
     // heavy bins' flat k-mer lists (touched only when a bin needs many tables)
     // Few, large bins (the last finalize had fewer than three per CU: the
     // mmer-sharded receivers of N ranks, high coverage): bins above 1/32 of a
@@ -1924,6 +1931,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.bdesc = use_desc ? c->bdesc.p : nullptr;
         a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
         a.stage = c->stage.p;
+        a.stage_ord = stage6 ? c->stage_ord.p : nullptr;
+        a.stage_slot = stage6 ? c->stage_slot.p : nullptr;
         a.kstage = flat_l ? c->kstage.p : nullptr;
         a.flat_l = flat_l;
         a.n_occ = N;

@@ -1279,10 +1279,12 @@ DEV void sort_lists_lane(uint32_t* p, uint32_t n);
 template <int R>
 DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane);
 
+// (so, ss: the split stage of a light bin -- ordinals and slots -- or null:
+// the 8-B stage entries)
 template <int KW>
 DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, uint32_t* win, uint32_t win_cap,
                    uint32_t ns, unsigned long long e0, unsigned long long i0, uint32_t n_ent, uint32_t n_ids,
-                   const uint64_t* stage, uint32_t e_mine PROF_PARAMS) {
+                   const uint64_t* stage, const uint32_t* so, const uint16_t* ss, uint32_t e_mine PROF_PARAMS) {
     const uint32_t tid = threadIdx.x;
     const int lane = (int)(tid & 63u);
     const uint32_t per = TS / BIN_THREADS;
@@ -1332,7 +1334,8 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint32_t i = i0s + (uint32_t)u * BIN_THREADS;
-                v[u] = i < ns ? stage[i] : 0ull;
+                if (so) v[u] = i < ns ? ((uint64_t)ss[i] << 48) | so[i] : 0ull;
+                else v[u] = i < ns ? stage[i] : 0ull;
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -1653,6 +1656,11 @@ DEV void bin_body(const BinArgs& A) {
         // flat: this partition's list is [fa, fb) of the bin's stage range
         const uint32_t fa = flat || split ? S.fa : 0u, fb = flat ? S.fb : 0u;
         stage = A.stage + S.stage_base + fa;
+        // the split stage (6 B per occurrence): light bins of phase 0 without
+        // first-occurrence tracking (their stage is written and read back by
+        // this block alone; flat lists and partitions keep the 8-B entries)
+        uint32_t* const sp_ord = PHASE == 0 && A.stage_ord && !A.e_first ? A.stage_ord + S.stage_base : nullptr;
+        uint16_t* const sp_slot = sp_ord ? A.stage_slot + S.stage_base : nullptr;
         while (true) {
             const uint32_t ts = S.ts, bmask = ts / 4 - 1, limit = ts - ts / 4;  // (uniform)
             if (tid == 0) {
@@ -1763,7 +1771,12 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_ABL
                         if (A.ablate != 2)
 #endif
-                        stage[s0] = ((uint64_t)(l0 + 1) << 48) | ((uint64_t)p0 << 32) | o0;
+                        if (PHASE == 0 && sp_ord) {
+                            sp_ord[s0] = o0;
+                            sp_slot[s0] = (uint16_t)(l0 + 1);
+                        } else {
+                            stage[s0] = ((uint64_t)(l0 + 1) << 48) | ((uint64_t)p0 << 32) | o0;
+                        }
                     }
                 }
                 if (v1) {
@@ -1774,7 +1787,12 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_ABL
                         if (A.ablate != 2)
 #endif
-                        stage[s1] = ((uint64_t)(l1 + 1) << 48) | ((uint64_t)p1 << 32) | o1;
+                        if (PHASE == 0 && sp_ord) {
+                            sp_ord[s1] = o1;
+                            sp_slot[s1] = (uint16_t)(l1 + 1);
+                        } else {
+                            stage[s1] = ((uint64_t)(l1 + 1) << 48) | ((uint64_t)p1 << 32) | o1;
+                        }
                     }
                 }
             };
@@ -1963,7 +1981,7 @@ DEV void bin_body(const BinArgs& A) {
             // and two-word keys (C5: 624 -> 641 ms) keep the global path
             const bool win_phase = PHASE == 0 || (KW == 1 && A.win_heavy && !(flat && Lv > l0));
             if (win_phase && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
-                lds_lists<KW>(A, S, cnt, ts, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage,
+                lds_lists<KW>(A, S, cnt, ts, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage, sp_ord, sp_slot,
                               (uint32_t)ex PROF_ARGS);
                 PROF_MARK(4);
                 continue;
@@ -1979,7 +1997,7 @@ DEV void bin_body(const BinArgs& A) {
                 const uint32_t pmask = (1u << Lv) - 1u;
                 for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
                     if (filt && (kst_load<KW>(kst, fa + i).part() & pmask) != P) continue;
-                    const uint64_t v = stage[i];
+                    const uint64_t v = sp_ord ? ((uint64_t)sp_slot[i] << 48) | sp_ord[i] : stage[i];
                     if (PHASE == 1 && !(v >> 48)) continue;  // a pre-filtered single (flat partitions only)
                     const uint32_t ls = (uint32_t)(v >> 48) - 1u;
                     // one returning atomic: a pruned key's cursor starts at PRUNED and

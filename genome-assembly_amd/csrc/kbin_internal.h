@@ -222,6 +222,10 @@ struct BinArgs {
                                // {occurrences, stage base lo, hi, 0} (bins_desc_kernel)
     unsigned long long* work;  // work counter (zeroed)
     uint64_t* stage;           // [N] (LDS slot << 48 | position << 32 | ordinal) per occurrence
+    // light bins of the first phase without first-occurrence tracking: the
+    // stage as two arrays, 6 B per occurrence (null: the 8-B stage everywhere)
+    uint32_t* stage_ord;       // [N] ordinal
+    uint16_t* stage_slot;      // [N] LDS slot + 1 (0: not in the table)
     uint64_t* kstage;          // [KW N] heavy bins: the k-mer's table key per occurrence, parallel to stage
     uint32_t flat_l;           // heavy bin: initial partition depth >= flat_l (0 = never)
     // heavy bins, two launches: phase 0 bins every light bin and turns each heavy
