@@ -1656,11 +1656,12 @@ DEV void bin_body(const BinArgs& A) {
         // flat: this partition's list is [fa, fb) of the bin's stage range
         const uint32_t fa = flat || split ? S.fa : 0u, fb = flat ? S.fb : 0u;
         stage = A.stage + S.stage_base + fa;
-        // the split stage (6 B per occurrence): light bins of phase 0 without
-        // first-occurrence tracking (their stage is written and read back by
-        // this block alone; flat lists and partitions keep the 8-B entries)
-        uint32_t* const sp_ord = PHASE == 0 && A.stage_ord && !A.e_first ? A.stage_ord + S.stage_base : nullptr;
-        uint16_t* const sp_slot = sp_ord ? A.stage_slot + S.stage_base : nullptr;
+        // the split stage (6 B per occurrence: ordinals, slots) without
+        // first-occurrence tracking; a flat list's ordinals are in it already
+        // (flat_scatter), so its sweep 1 writes the slots only
+        uint32_t* const sp_ord = A.stage_ord && !A.e_first ? A.stage_ord + S.stage_base + fa : nullptr;
+        uint16_t* const sp_slot = sp_ord ? A.stage_slot + S.stage_base + fa : nullptr;
+        const bool sp_ord_w = !(PHASE == 1 && flat);
         while (true) {
             const uint32_t ts = S.ts, bmask = ts / 4 - 1, limit = ts - ts / 4;  // (uniform)
             if (tid == 0) {
@@ -1771,8 +1772,8 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_ABL
                         if (A.ablate != 2)
 #endif
-                        if (PHASE == 0 && sp_ord) {
-                            sp_ord[s0] = o0;
+                        if (sp_ord) {
+                            if (sp_ord_w) sp_ord[s0] = o0;
                             sp_slot[s0] = (uint16_t)(l0 + 1);
                         } else {
                             stage[s0] = ((uint64_t)(l0 + 1) << 48) | ((uint64_t)p0 << 32) | o0;
@@ -1787,8 +1788,8 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_ABL
                         if (A.ablate != 2)
 #endif
-                        if (PHASE == 0 && sp_ord) {
-                            sp_ord[s1] = o1;
+                        if (sp_ord) {
+                            if (sp_ord_w) sp_ord[s1] = o1;
                             sp_slot[s1] = (uint16_t)(l1 + 1);
                         } else {
                             stage[s1] = ((uint64_t)(l1 + 1) << 48) | ((uint64_t)p1 << 32) | o1;
@@ -1835,11 +1836,11 @@ DEV void bin_body(const BinArgs& A) {
                 uint64_t ne0 = 0, ne1 = 0;
                 if (c0 + lane < nf) {
                     n0 = kst_load<KW>(kst, fa + c0 + lane);
-                    ne0 = stage[c0 + lane];
+                    ne0 = sp_ord ? (uint64_t)sp_ord[c0 + lane] : stage[c0 + lane];
                 }
                 if (c0 + 64u + lane < nf) {
                     n1 = kst_load<KW>(kst, fa + c0 + 64u + lane);
-                    ne1 = stage[c0 + 64u + lane];
+                    ne1 = sp_ord ? (uint64_t)sp_ord[c0 + 64u + lane] : stage[c0 + 64u + lane];
                 }
                 for (; c0 < nf; c0 += BIN_THREADS * 2) {
                     const uint32_t i0 = c0 + lane, i1 = c0 + 64u + lane;
@@ -1849,11 +1850,11 @@ DEV void bin_body(const BinArgs& A) {
                     const uint32_t c1 = c0 + BIN_THREADS * 2;
                     if (c1 + lane < nf) {
                         n0 = kst_load<KW>(kst, fa + c1 + lane);
-                        ne0 = stage[c1 + lane];
+                        ne0 = sp_ord ? (uint64_t)sp_ord[c1 + lane] : stage[c1 + lane];
                     }
                     if (c1 + 64u + lane < nf) {
                         n1 = kst_load<KW>(kst, fa + c1 + 64u + lane);
-                        ne1 = stage[c1 + 64u + lane];
+                        ne1 = sp_ord ? (uint64_t)sp_ord[c1 + 64u + lane] : stage[c1 + 64u + lane];
                     }
                     if (Lv > l0) {
                         v0 = v0 && (k0.part() & pmask) == P;
@@ -1866,7 +1867,10 @@ DEV void bin_body(const BinArgs& A) {
                         singles += (uint32_t)__popcll(__ballot(s0)) + (uint32_t)__popcll(__ballot(s1));
                         // after an overflow a redo may find a slot field from the
                         // parent's attempt: clear it
-                        if (Lv > l0) {
+                        if (sp_ord) {  // (the split slots start unwritten: every single's is set)
+                            if (s0) sp_slot[i0] = 0;
+                            if (s1) sp_slot[i1] = 0;
+                        } else if (Lv > l0) {
                             if (s0) stage[i0] = e0;
                             if (s1) stage[i1] = e1;
                         }
@@ -2254,6 +2258,8 @@ __global__ __launch_bounds__(FB_THREADS) void flat_scatter_kernel(BinArgs A) {
         const uint64_t sb = A.flat_sbase[b];
         uint64_t* kst = A.kstage + KW * sb;
         uint64_t* stage = A.stage + sb;
+        // (the split stage: the list's ordinals alone, bin_body writes the slots)
+        uint32_t* const sord = A.stage_ord && !A.e_first ? A.stage_ord + sb : nullptr;
         if (packed) {
             uint32_t wb[8];  // this wave's next entry per partition (wave-uniform)
 #pragma unroll
@@ -2296,7 +2302,8 @@ __global__ __launch_bounds__(FB_THREADS) void flat_scatter_kernel(BinArgs A) {
                     }
                     if (j < n) {
                         kst_store<KW>(kst, i, key);
-                        stage[i] = ((uint64_t)(rlo + (uint32_t)j) << 32) | ord;
+                        if (sord) sord[i] = ord;
+                        else stage[i] = ((uint64_t)(rlo + (uint32_t)j) << 32) | ord;
                     }
                 }
             }
@@ -2304,7 +2311,8 @@ __global__ __launch_bounds__(FB_THREADS) void flat_scatter_kernel(BinArgs A) {
             expand_bin<KW, FB_THREADS>(A, lo, hi, [&](const TKey<KW>& key, uint32_t ord, uint32_t pos) {
                 const uint32_t i = atomicAdd(&hist[key.part() & pm], 1u);
                 kst_store<KW>(kst, i, key);
-                stage[i] = ((uint64_t)pos << 32) | ord;
+                if (sord) sord[i] = ord;
+                else stage[i] = ((uint64_t)pos << 32) | ord;
             });
         }
     }
@@ -2362,6 +2370,8 @@ __global__ __launch_bounds__(FSL_THREADS) void flat_scatter_lds_kernel(BinArgs A
         const uint64_t sb = A.flat_sbase[b];
         uint64_t* kst = A.kstage + KW * sb;
         uint64_t* stage = A.stage + sb;
+        // (the split stage: the list's ordinals alone, bin_body writes the slots)
+        uint32_t* const sord = A.stage_ord && !A.e_first ? A.stage_ord + sb : nullptr;
         for (uint32_t lo = c_lo; lo < c_hi;) {
             // ---- this segment: the longest record run from lo within E entries
             {
@@ -2441,7 +2451,8 @@ __global__ __launch_bounds__(FSL_THREADS) void flat_scatter_lds_kernel(BinArgs A
                     kst[2 * (uint64_t)g] = skey[2 * i];
                     kst[2 * (uint64_t)g + 1] = skey[2 * i + 1];
                 }
-                stage[g] = sval[i];
+                if (sord) sord[g] = (uint32_t)sval[i];
+                else stage[g] = sval[i];
             }
             lo = hi;
         }
