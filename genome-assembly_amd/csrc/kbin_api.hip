@@ -1772,8 +1772,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     if (bucketed) HIPCHK(c->bocc.ensure(max_bins));
     HIPCHK(c->srec.ensure(RWD * R));
     HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));  // ids by ordinal (+ radix ping-pong)
-    HIPCHK(c->stage.ensure(std::max<uint64_t>(N, 1)));
-    const bool stage6 = env_int("KB_BIN_STAGE6", 1) != 0;
+    // the stage: 4-B ordinals + 2-B slots (KB_BIN_STAGE6, default), or 8-B
+    // entries -- also with first-occurrence tracking, whose entries carry the
+    // k-mer's position (the 8-B array is then the only one touched)
+    const bool stage6 = env_int("KB_BIN_STAGE6", 1) != 0 && !(c->p.flags & KB_TRACK_FIRST);
+    HIPCHK(c->stage.ensure(stage6 ? 1 : std::max<uint64_t>(N, 1)));
     if (stage6) {
         HIPCHK(c->stage_ord.ensure(std::max<uint64_t>(N, 1)));
         HIPCHK(c->stage_slot.ensure(std::max<uint64_t>(N, 1)));
