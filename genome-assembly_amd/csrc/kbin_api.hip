@@ -83,7 +83,11 @@ struct DevBuf {
         }
         if (e == hipSuccess) cap = want;
         else p = nullptr;
-        g_alloc_ms += alloc_now_ms() - t0;
+        const double dt = alloc_now_ms() - t0;
+        g_alloc_ms += dt;
+        static const bool dbg = getenv("KB_DEBUG") && atoi(getenv("KB_DEBUG")) != 0;
+        if (dbg && want * sizeof(T) >= (64u << 20))
+            fprintf(stderr, "[kb] alloc %.1f MB in %.2f ms\n", (double)(want * sizeof(T)) / 1e6, dt);
         return e;
     }
     hipError_t ensure_exact(uint64_t n) { return ensure(n, false); }
