@@ -745,7 +745,10 @@ __device__ unsigned long long g_bin_prof[16];
 #ifndef KB_BIN_THREADS
 #define KB_BIN_THREADS 1024
 #endif
-constexpr int BIN_THREADS = KB_BIN_THREADS;  // (A/B builds: -DKB_BIN_THREADS=512 with KB_BIN_TS_LOG2=12)
+constexpr int BIN_THREADS = KB_BIN_THREADS;
+#ifndef KB_WIN_LOADS
+#define KB_WIN_LOADS 4  // stage loads in flight per thread in the id windows (8: more spills, measured slower)
+#endif  // (A/B builds: -DKB_BIN_THREADS=512 with KB_BIN_TS_LOG2=12)
 constexpr int BIN_STACK = 32;
 
 DEV uint64_t lds_load_u64(const uint64_t* p) {
@@ -1328,23 +1331,30 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
             shi = (uint32_t)w & 0xFFFFu;
         }
         // ---- this window's occurrences into LDS at their list positions
-        // (the claim words and rings are dead); four stage loads in flight
-        for (uint32_t i0s = tid; i0s < ns; i0s += 4u * BIN_THREADS) {
-            uint64_t v[4];
+        // (the claim words and rings are dead); WL stage loads in flight
+        constexpr int WL = KB_WIN_LOADS;
+        for (uint32_t i0s = tid; i0s < ns; i0s += (uint32_t)WL * BIN_THREADS) {
+            uint32_t vo[WL], vs[WL];  // ordinal, slot + 1 (0: a pre-filtered single, or nothing)
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < WL; u++) {
                 const uint32_t i = i0s + (uint32_t)u * BIN_THREADS;
-                if (so) v[u] = i < ns ? ((uint64_t)ss[i] << 48) | so[i] : 0ull;
-                else v[u] = i < ns ? stage[i] : 0ull;
+                if (so) {
+                    vo[u] = i < ns ? so[i] : 0u;
+                    vs[u] = i < ns ? (uint32_t)ss[i] : 0u;
+                } else {
+                    const uint64_t x = i < ns ? stage[i] : 0ull;
+                    vo[u] = (uint32_t)x;
+                    vs[u] = (uint32_t)(x >> 48);
+                }
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (!(v[u] >> 48)) continue;  // (a pre-filtered single, or nothing)
-                const uint32_t ls = (uint32_t)(v[u] >> 48) - 1u;
+            for (int u = 0; u < WL; u++) {
+                if (!vs[u]) continue;
+                const uint32_t ls = vs[u] - 1u;
                 const uint32_t o = (ls & (BIN_THREADS - 1u)) * per + ls / BIN_THREADS;  // (scan order)
                 if (o - slo >= shi - slo) continue;  // another window's list
                 const uint32_t pos = atomicAdd(&cnt[ls], 1u);
-                if (pos < PRUNED) wv[pos - wlo] = (uint32_t)v[u] + 1u;  // ordinal + 1 (0 pads the sorts)
+                if (pos < PRUNED) wv[pos - wlo] = vo[u] + 1u;  // ordinal + 1 (0 pads the sorts)
             }
         }
         bar_lds(A);
