@@ -344,6 +344,8 @@ static int set_device(kb_ctx* c) {
 extern "C" int kb_abi_version(void) { return 2; }  // 2: kb_timing path counters
 
 extern "C" const char* kb_last_error(void) { return g_err.c_str(); }
+// (kbin_group.hip: a group call's failure is this thread's last error too)
+void kb::set_last_error(const char* msg) { g_err = msg; }
 
 extern "C" void* kb_stream(kb_ctx* ctx) { return ctx ? (void*)ctx->s : nullptr; }
 
@@ -2063,6 +2065,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.pstat = c->pstat.p;
         a.ldsbar = (uint32_t)(env_int("KB_BIN_LDSBAR", 1) != 0);
         a.ts_adapt = (uint32_t)(env_int("KB_BIN_TS_ADAPT", 1) != 0);
+        a.corrupt = (uint32_t)(env_int("KB_DIAG_CORRUPT", 0) != 0);
         // The tail kernels -- the heavy bins' list builds and partitions, the
         // list kernels -- have work only when bin_kernel publishes a heavy bin
         // or queues a list, and cost ~4.5 us per empty launch (8 of them: 2 %
@@ -2177,6 +2180,14 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     if (c->h_misc[0] & ST_NEG_ID)
         return fail(KB_EINVAL, "routed read ids must be non-negative (they order the id lists)");
     if (bst & ST_PROBE_LIMIT) return fail(KB_ENOMEM, "a bin exceeded the partition depth");
+    // result invariants (a wrong result must not come back as KB_OK): every
+    // k-mer of the pass counted exactly once before the prune, and kept
+    // entries <= distinct keys <= k-mers
+    if (c->h_totals[5] != N || c->h_totals[0] > c->h_totals[6] || c->h_totals[6] > N)
+        return fail(KB_EDEVICE,
+                    "internal: result invariant violated (counted %llu of %llu k-mers, %llu entries, %llu distinct)",
+                    (unsigned long long)c->h_totals[5], (unsigned long long)N, (unsigned long long)c->h_totals[0],
+                    (unsigned long long)c->h_totals[6]);
     c->n_entries = c->h_totals[0];
     c->n_ids = c->h_totals[1];
     c->n_distinct = c->h_totals[6];
@@ -2422,6 +2433,11 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     if (c->h_totals[3])
         return fail(KB_EDEVICE, "internal: %llu runs > %llu distinct keys", (unsigned long long)c->h_totals[3],
                     (unsigned long long)ne_cap);
+    // result invariants: kept entries <= distinct keys (runs) <= k-mers, ids <= k-mers
+    if (c->h_totals[0] > c->h_totals[2] || c->h_totals[2] > N || c->h_totals[1] > N)
+        return fail(KB_EDEVICE, "internal: result invariant violated (%llu entries, %llu distinct, %llu ids, %llu k-mers)",
+                    (unsigned long long)c->h_totals[0], (unsigned long long)c->h_totals[2],
+                    (unsigned long long)c->h_totals[1], (unsigned long long)N);
     c->n_entries = c->h_totals[0];
     c->n_ids = c->h_totals[1];
     if (c->timing) {

@@ -759,6 +759,7 @@ struct alignas(16) BinShared {
     uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, part0;
     uint32_t n_single;  // pre-filter: keys seen once in this partition
     uint32_t maxc;      // the partition's longest kept list (the LDS id windows)
+    uint32_t sumc;      // the partition's occurrences counted in its table (the finalize's invariant)
     uint32_t ts;        // LDS table slots of the next partition (<= the carved TS)
     unsigned long long wkey;  // LDS id windows: cursor << 32 | entry << 16 | scan index of the next window's start
     unsigned long long e0, i0, stage_base;
@@ -1687,6 +1688,7 @@ DEV void bin_body(const BinArgs& A) {
                 S.n_stage = 0;
                 S.n_single = 0;
                 S.maxc = 0;
+                S.sumc = 0;
             }
             for (uint32_t i = tid; i < ts; i += BIN_THREADS) {
                 T.ca[i] = 0;
@@ -1893,6 +1895,12 @@ DEV void bin_body(const BinArgs& A) {
                 if (singles && lane == 0) atomicAdd(&S.n_single, singles);
                 if (tid == 0) S.n_stage = nf;
             }
+            if (A.corrupt && blockIdx.x == 0 && tid == 0)  // (diagnostic: one count + 1)
+                for (uint32_t i = 0; i < ts; i++)
+                    if (T.ca[i]) {
+                        atomicAdd(&cnt[i], 1u);
+                        break;
+                    }
             bar_lds(A);
             PROF_MARK(2);
             if (S.overflow || S.n_keys > limit) {  // uniform: split this partition in two and redo both
@@ -1922,17 +1930,26 @@ DEV void bin_body(const BinArgs& A) {
             // slots t, t + 1024, ...: a wave's reads of the table are consecutive
             // words (owning 8 adjacent slots put 16 lanes on one LDS bank)
             uint64_t mine = 0;  // (ids << 32) | entries over this thread's slots
+            uint32_t allc = 0;  // every key's count, kept or not
             const uint32_t per = ts / BIN_THREADS;  // ts >= BIN_THREADS
             for (uint32_t k = 0; k < per; k++) {
                 const uint32_t i = tid + k * BIN_THREADS;
                 const uint32_t c = cnt[i];
-                if (T.ca[i] && c > A.keep_gt) mine += ((uint64_t)c << 32) + 1ull;
+                if (T.ca[i]) {
+                    allc += c;
+                    if (c > A.keep_gt) mine += ((uint64_t)c << 32) + 1ull;
+                }
             }
+            allc = wave_sum_u32(allc);
+            if ((tid & 63u) == 0 && allc) atomicAdd(&S.sumc, allc);
             uint64_t tot;
             uint64_t ex = block_excl_scan_u64(mine, S.red, tot, A.ldsbar != 0);
             if (tid == 0) {
                 const uint32_t ne = (uint32_t)tot, ni = (uint32_t)(tot >> 32);
                 atomicAdd(&A.gcount[2], (unsigned long long)(S.n_keys + S.n_single));  // distinct before prune
+                // occurrences counted (pre-filtered singles count once each): the
+                // finalize checks the sum against the pass's k-mers
+                atomicAdd(&A.gcount[1], (unsigned long long)S.sumc + S.n_single);
                 if (A.tab_keys) atomicAdd(A.tab_keys, (unsigned long long)S.n_keys);
                 if (A.pstat) {
                     atomicAdd(&A.pstat[2], 1ull);

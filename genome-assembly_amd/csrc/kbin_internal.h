@@ -309,6 +309,8 @@ struct BinArgs {
     unsigned long long* pstat;
     uint32_t ts_adapt;         // 1: one-table light bins take the smallest table for their keys (KB_BIN_TS_ADAPT)
     uint32_t ldsbar;           // 1: barriers that order LDS only skip the global-store drain (KB_BIN_LDSBAR)
+    uint32_t corrupt;          // diagnostic (KB_DIAG_CORRUPT=1): block 0 adds one to a count, so the
+                               // finalize's invariant (sum of pre-prune counts == k-mers) must fail
 };
 constexpr int KB_PSTAT = 8;
 
@@ -371,6 +373,8 @@ hipError_t launch_hll(const BinArgs& a, uint64_t R, int KW, uint32_t* regs, uint
 double hll_estimate(const uint32_t* regs);
 // resolve the binned path's kernels (kb_create: once per process and device)
 hipError_t load_bin_kernels();
+// this thread's kb_last_error() message (kbin_group.hip's failures)
+void set_last_error(const char* msg);
 // distinct / occurrences from launch_hll's registers, on the device (no host
 // round trip): written to *rho (clamped to [1e-4, 1]; 0.25 with no occurrences)
 hipError_t launch_hll_finish(const uint32_t* regs, float* rho, hipStream_t s);

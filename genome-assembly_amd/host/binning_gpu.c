@@ -7,9 +7,11 @@
  * materialises the surviving (mmer, kmer) entries into the caller's level-1
  * table as reference-layout ZHashTable / ll_node structures.
  */
-#include <malloc.h>
 #include <pthread.h>
 #include <stdio.h>
+#if defined(__GLIBC__)
+#include <malloc.h> /* mallopt (heap_pad_begin) */
+#endif
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -44,6 +46,10 @@ static const size_t LADDER[23] = {
     217645177, 512927357, 1000000007};
 
 static int g_K = KMER_SIZE, g_M = MMER_SIZE, g_cutoff = ABUNDANCE_CUTOFF, g_device = 0;
+/* multi-GPU (kbh_configure_gpus, else KBH_GPUS in the environment: a count
+ * "8" or a device list "0,1,2,3"): one kb_group over these devices */
+#define KBH_MAX_GPUS 64
+static int g_ngpus = 0, g_gpus[KBH_MAX_GPUS], g_gpus_set = 0;
 static kbh_times g_times;
 
 static double now_ms(void)
@@ -60,10 +66,11 @@ int kbh_last_times(kbh_times *out)
     return KB_OK;
 }
 
-/* one engine context per level-1 table the caller uses */
+/* one engine context (or multi-GPU group) per level-1 table the caller uses */
 typedef struct {
     struct ZHashTable *table;
     kb_ctx *ctx;
+    kb_group *grp;          /* G > 1: the reads stay here until prune_data */
     char *bases;
     uint32_t *lens;
     int32_t *ids;
@@ -95,6 +102,40 @@ int kbh_configure(int K, int M, int cutoff, int device)
     return 0;
 }
 
+int kbh_configure_gpus(int n_gpus, const int *devices)
+{
+    if (n_gpus < 1 || n_gpus > KBH_MAX_GPUS) return KB_EINVAL;
+    g_ngpus = n_gpus;
+    for (int i = 0; i < n_gpus; i++) g_gpus[i] = devices ? devices[i] : i;
+    g_gpus_set = 1;
+    return KB_OK;
+}
+
+/* KBH_GPUS: "<count>" (devices 0 .. count-1) or "<d0>,<d1>,..." (a device may
+ * repeat: virtual shards on one GPU) */
+static void gpus_from_env(void)
+{
+    const char *e = getenv("KBH_GPUS");
+    if (g_gpus_set || !e || !*e) return;
+    g_gpus_set = 1;
+    if (!strchr(e, ',')) {
+        const int n = atoi(e);
+        if (n > 1 && n <= KBH_MAX_GPUS) {
+            g_ngpus = n;
+            for (int i = 0; i < n; i++) g_gpus[i] = i;
+        }
+        return;
+    }
+    int n = 0;
+    for (const char *q = e; *q && n < KBH_MAX_GPUS;) {
+        g_gpus[n++] = atoi(q);
+        q = strchr(q, ',');
+        if (!q) break;
+        q++;
+    }
+    g_ngpus = n;
+}
+
 static binding_t *binding(struct ZHashTable *t, int create)
 {
     binding_t *free_slot = NULL;
@@ -115,7 +156,12 @@ static binding_t *binding(struct ZHashTable *t, int create)
     p.max_read_len = 65535;
     p.device = g_device;
     p.flags = KB_TRACK_FIRST;
-    if (kb_create(&p, &free_slot->ctx) != KB_OK) die("kb_create");
+    gpus_from_env();
+    if (g_ngpus > 1) {
+        if (kb_group_create(&p, g_ngpus, g_gpus, &free_slot->grp) != KB_OK) die("kb_group_create");
+    } else if (kb_create(&p, &free_slot->ctx) != KB_OK) {
+        die("kb_create");
+    }
     free_slot->table = t;
     free_slot->cap_reads = 4096;
     free_slot->cap_bytes = 1 << 20;
@@ -154,7 +200,8 @@ struct ZHashTable *process_read(struct ZHashTable *hash_table, char *read, int r
     b->lens[b->n] = (uint32_t)len;
     b->ids[b->n] = read_id;
     b->n++;
-    if (b->n >= KBH_BATCH_READS || b->nbytes >= KBH_BATCH_BYTES) flush(b);
+    /* (a group splits the reads into contiguous per-GPU ranges at prune_data) */
+    if (!b->grp && (b->n >= KBH_BATCH_READS || b->nbytes >= KBH_BATCH_BYTES)) flush(b);
     return hash_table; /* binning.c:1075 */
 }
 
@@ -201,6 +248,28 @@ static long n_threads(void)
     if (env && atol(env) > 0) nt = atol(env);
     if (nt < 1) nt = 1;
     return nt > 16 ? 16 : nt;
+}
+
+/* The tables and lists are ~10^8-10^9 small malloc blocks built by several
+ * threads: grow the arenas in 64 MB steps rather than 128 KB ones (each
+ * growth is a syscall under the process's address-space lock, which the
+ * other workers' page faults also take), then put glibc's default pad back.
+ * Side effect (glibc): any M_TOP_PAD call also switches off the dynamic
+ * mmap threshold for the rest of the process, so later large blocks
+ * (>= 128 KiB) are always mmapped -- allocation speed only, never results.
+ * KBH_NO_TOP_PAD=1 leaves malloc's tuning untouched. */
+static void heap_pad_begin(void)
+{
+#if defined(__GLIBC__) && defined(M_TOP_PAD)
+    if (!getenv("KBH_NO_TOP_PAD")) mallopt(M_TOP_PAD, 64 << 20);
+#endif
+}
+
+static void heap_pad_end(void)
+{
+#if defined(__GLIBC__) && defined(M_TOP_PAD)
+    if (!getenv("KBH_NO_TOP_PAD")) mallopt(M_TOP_PAD, 128 << 10);
+#endif
 }
 
 /* run fn(arg) on up to 16 threads (the caller is one of them) */
@@ -698,13 +767,9 @@ static void materialise_direct(struct ZHashTable *level1, const kb_csr *r, int p
     direct_job j = {r, grouped, gstart, work, calloc(nm, sizeof(struct ZHashTable *)),
                     xmalloc(nm * sizeof(uint64_t)), nw, 0, 0, 0};
     if (!j.l2) exit(EXIT_FAILURE);
-    /* ~10^8 small blocks: grow the arenas in 64 MB steps, not 128 KB ones
-     * (each growth is a syscall under the process's address-space lock,
-     * which the page faults of the other workers also take); restored to
-     * glibc's default after */
-    mallopt(M_TOP_PAD, 64 << 20);
+    heap_pad_begin();
     run_workers(direct_tables, &j, nt);
-    mallopt(M_TOP_PAD, 128 << 10);
+    heap_pad_end();
     g_times.fill_ms = now_ms() - t;
     g_times.nodes += j.nodes;
     /* 3. level 1: every mmer in first-sight order, survivors linked */
@@ -828,18 +893,102 @@ static void prune_materialised(struct ZHashTable *level1, int cutoff)
     }
 }
 
+/* Multi-GPU: the reads of the whole loop, cut into G contiguous ranges (rank
+ * g's reads all precede rank g+1's, so arrival order at every receiver is the
+ * call order), each submitted with its call ORDINALS as ids -- lists then come
+ * out in reverse call order whatever ids the caller used, and first
+ * occurrences carry call ordinals as on one GPU.  After the group's exchange
+ * and binning, the G disjoint results are concatenated into one host CSR and
+ * ordinals mapped back to the caller's ids. */
+typedef struct {
+    uint32_t *mmer, *count;
+    uint64_t *hi, *lo, *offset, *first;
+    int32_t *ids;
+} merged_csr;
+
+static void group_finish(binding_t *b, kb_csr *r, merged_csr *m)
+{
+    int G = 0, nl = 0;
+    if (kb_group_info(b->grp, &G, &nl, NULL, NULL) != KB_OK) die("kb_group_info");
+    uint64_t byte0 = 0, r0 = 0;
+    int32_t *ord = xmalloc((b->n ? b->n : 1) * sizeof(int32_t));
+    for (uint64_t i = 0; i < b->n; i++) ord[i] = (int32_t)i;
+    for (int g = 0; g < nl; g++) {
+        const uint64_t r1 = b->n * (uint64_t)(g + 1) / (uint64_t)nl;
+        uint64_t nb = 0;
+        for (uint64_t i = r0; i < r1; i++) nb += b->lens[i];
+        if (r1 > r0 && kb_group_submit_ids(b->grp, g, b->bases + byte0, b->lens + r0, r1 - r0, ord + r0) != KB_OK)
+            die("kb_group_submit_ids");
+        byte0 += nb;
+        r0 = r1;
+    }
+    /* every key, pruned ones included, takes part in the insertion history */
+    if (kb_group_finalize(b->grp, 0) != KB_OK) die("kb_group_finalize");
+    free(ord);
+    kb_csr part[KBH_MAX_GPUS];
+    uint64_t ne = 0, ni = 0, nk = 0, nd = 0;
+    for (int g = 0; g < nl; g++) {
+        if (kb_export(kb_group_ctx(b->grp, g), &part[g]) != KB_OK) die("kb_export");
+        ne += part[g].n_entries;
+        ni += part[g].n_ids;
+        nk += part[g].n_kmers;
+        nd += part[g].n_distinct;
+    }
+    m->mmer = xmalloc((ne + 1) * sizeof(uint32_t));
+    m->count = xmalloc((ne + 1) * sizeof(uint32_t));
+    m->hi = xmalloc((ne + 1) * sizeof(uint64_t));
+    m->lo = xmalloc((ne + 1) * sizeof(uint64_t));
+    m->first = xmalloc((ne + 1) * sizeof(uint64_t));
+    m->offset = xmalloc((ne + 1) * sizeof(uint64_t));
+    m->ids = xmalloc((ni + 1) * sizeof(int32_t));
+    uint64_t e0 = 0, i0 = 0;
+    for (int g = 0; g < nl; g++) {
+        const kb_csr *q = &part[g];
+        const uint64_t n = q->n_entries;
+        memcpy(m->mmer + e0, q->mmer, n * sizeof(uint32_t));
+        memcpy(m->count + e0, q->count, n * sizeof(uint32_t));
+        memcpy(m->hi + e0, q->kmer_hi, n * sizeof(uint64_t));
+        memcpy(m->lo + e0, q->kmer_lo, n * sizeof(uint64_t));
+        if (q->first) memcpy(m->first + e0, q->first, n * sizeof(uint64_t));
+        else die("group result without first occurrences");
+        for (uint64_t e = 0; e < n; e++) m->offset[e0 + e] = i0 + q->offset[e];
+        for (uint64_t k = 0; k < q->n_ids; k++) m->ids[i0 + k] = b->ids[q->ids[k]]; /* ordinal -> caller id */
+        e0 += n;
+        i0 += q->n_ids;
+    }
+    m->offset[ne] = ni;
+    memset(r, 0, sizeof *r);
+    r->n_entries = ne;
+    r->n_ids = ni;
+    r->n_kmers = nk;
+    r->n_distinct = nd;
+    r->mmer = m->mmer;
+    r->kmer_hi = m->hi;
+    r->kmer_lo = m->lo;
+    r->count = m->count;
+    r->offset = m->offset;
+    r->ids = m->ids;
+    r->first = m->first;
+}
+
 static struct ZHashTable *finish(struct ZHashTable *hash_table, int prune)
 {
     binding_t *b = binding(hash_table, 1);
     memset(&g_times, 0, sizeof g_times);
     double t = now_ms(), t0 = t;
-    flush(b);
-    /* every key, pruned ones included, takes part in the insertion history */
-    if (kb_finalize(b->ctx, 0) != KB_OK) die("kb_finalize");
-    g_times.finalize_ms = now_ms() - t;
-    t = now_ms();
     kb_csr r;
-    if (kb_export(b->ctx, &r) != KB_OK) die("kb_export");
+    merged_csr m = {0};
+    if (b->grp) {
+        group_finish(b, &r, &m);
+        g_times.finalize_ms = now_ms() - t;
+    } else {
+        flush(b);
+        /* every key, pruned ones included, takes part in the insertion history */
+        if (kb_finalize(b->ctx, 0) != KB_OK) die("kb_finalize");
+        g_times.finalize_ms = now_ms() - t;
+        t = now_ms();
+        if (kb_export(b->ctx, &r) != KB_OK) die("kb_export");
+    }
     g_times.export_ms = now_ms() - t;
     g_times.entries = r.n_entries;
     g_times.ids = r.n_ids;
@@ -851,6 +1000,13 @@ static struct ZHashTable *finish(struct ZHashTable *hash_table, int prune)
     g_times.prune_ms = now_ms() - t;
     t = now_ms();
     kbh_release(hash_table);
+    free(m.mmer);
+    free(m.count);
+    free(m.hi);
+    free(m.lo);
+    free(m.first);
+    free(m.offset);
+    free(m.ids);
     g_times.release_ms = now_ms() - t;
     g_times.total_ms = now_ms() - t0;
     if (getenv("KBH_TRACE")) /* (the drop-in binaries: no caller reads kbh_last_times) */
@@ -919,6 +1075,94 @@ uint64_t kbh_layout_digest(struct ZHashTable *level1)
 /* binning.c:1130 */
 struct ZHashTable *prune_data(struct ZHashTable *hash_table) { return finish(hash_table, 1); }
 
+/* expand_read_id_list (binning.c:857-888): every kmer entry's id list becomes
+ * a list of strlen(key) list nodes (create_node_item, llist.c:13-18) whose
+ * items are the original list followed by strlen(key) - 1 fresh copies of it
+ * (duplicate_llist, llist.c:83-99).  The result depends on each entry alone,
+ * so the level-2 tables are expanded by worker threads, largest first.  Every
+ * node stays an individual malloc block, as the reference's are: downstream
+ * reference code frees and relinks them (merge_lists / free_llist at
+ * binning.c:174-181, llist.c:101-108).  The reference walks the tables with
+ * its static-cursor iterators (binning.c:298-460) to the end, which leaves
+ * them reset; this walk does not touch them. */
+typedef struct {
+    struct ZHashTable **tabs;
+    uint64_t n, next, nodes;
+} expand_job;
+
+static void *expand_tables(void *arg)
+{
+    expand_job *j = arg;
+    uint64_t nodes = 0;
+    for (;;) {
+        const uint64_t w = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+        if (w >= j->n) break;
+        struct ZHashTable *level2 = j->tabs[w];
+        const size_t m2 = LADDER[level2->size_index];
+        for (size_t b2 = 0; b2 < m2; b2++) {
+            for (struct ZHashEntry *ke = level2->entries[b2]; ke; ke = ke->next) {
+                ll_node *const list = ke->val;
+                const size_t klen = strlen(ke->key);
+                ll_node *outer = NULL, **ot = &outer;
+                for (size_t i = 0; i < klen; i++) {
+                    ll_node *copy = list;
+                    if (i) { /* duplicate_llist */
+                        ll_node **ct = &copy;
+                        for (const ll_node *s = list; s; s = s->next) {
+                            ll_node *nd = xmalloc(sizeof *nd);
+                            nd->next = NULL;
+                            nd->read_id = s->read_id;
+                            *ct = nd;
+                            ct = &nd->next;
+                            nodes++;
+                        }
+                        *ct = NULL;
+                        if (!list) copy = NULL;
+                    }
+                    ll_node *o = xmalloc(sizeof *o); /* create_node_item */
+                    o->next = NULL;
+                    o->item = copy;
+                    *ot = o;
+                    ot = &o->next;
+                    nodes++;
+                }
+                if (klen) ke->val = outer; /* (an empty key: the reference reads an unset pointer) */
+            }
+        }
+    }
+    __atomic_fetch_add(&j->nodes, nodes, __ATOMIC_RELAXED);
+    return NULL;
+}
+
+static int cmp_table_size(const void *a, const void *b)
+{
+    const size_t x = (*(struct ZHashTable *const *)a)->entry_count, y = (*(struct ZHashTable *const *)b)->entry_count;
+    return x > y ? -1 : x < y;
+}
+
+void expand_read_id_list(struct ZHashTable *hashtable)
+{
+    double t = now_ms();
+    const size_t m1 = LADDER[hashtable->size_index];
+    uint64_t nt2 = 0;
+    for (size_t b1 = 0; b1 < m1; b1++)
+        for (struct ZHashEntry *me = hashtable->entries[b1]; me; me = me->next) nt2 += me->val != NULL;
+    expand_job j = {xmalloc((nt2 + 1) * sizeof(struct ZHashTable *)), 0, 0, 0};
+    for (size_t b1 = 0; b1 < m1; b1++)
+        for (struct ZHashEntry *me = hashtable->entries[b1]; me; me = me->next)
+            if (me->val) j.tabs[j.n++] = me->val;
+    qsort(j.tabs, j.n, sizeof(struct ZHashTable *), cmp_table_size);
+    heap_pad_begin();
+    run_workers(expand_tables, &j, n_threads());
+    heap_pad_end();
+    free(j.tabs);
+    g_times.expand_ms = now_ms() - t;
+    g_times.expand_nodes = j.nodes;
+    if (getenv("KBH_TRACE"))
+        fprintf(stderr, "{\"expand_ms\": %.3f, \"expand_nodes\": %llu}\n", g_times.expand_ms,
+                (unsigned long long)j.nodes);
+}
+
 struct ZHashTable *kbh_finish_unpruned(struct ZHashTable *hash_table) { return finish(hash_table, 0); }
 
 void kbh_release(struct ZHashTable *hash_table)
@@ -926,6 +1170,7 @@ void kbh_release(struct ZHashTable *hash_table)
     binding_t *b = binding(hash_table, 0);
     if (!b) return;
     kb_destroy(b->ctx);
+    kb_group_destroy(b->grp);
     free(b->bases);
     free(b->lens);
     free(b->ids);

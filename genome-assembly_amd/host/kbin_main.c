@@ -4,7 +4,10 @@
  * chunking, process_read per chunk, prune_data, then the canonical dump of the
  * materialised two-level table (instead of the reference's unitig steps).
  *
- *   kbin_main <reads-file> <K> <M> <READ_LENGTH> <cutoff> <prune 0|1> [device]
+ *   kbin_main <reads-file> <K> <M> <READ_LENGTH> <cutoff> <prune 0|1> [device] [--gpus N|d0,d1,..]
+ *
+ * --gpus: bin on several GPUs through one multi-GPU group (mmer-sharded,
+ * records exchanged over RCCL; kbh_configure_gpus); the dump is identical.
  *
  * KBH_TIMING=1 in the environment: one JSON line of wall-clock phases on
  * stderr (read loop = fgets + process_read; then prune_data's phases);
@@ -19,14 +22,32 @@
 
 int main(int argc, char **argv)
 {
-    if (argc < 7) {
-        fprintf(stderr, "usage: %s <reads> <K> <M> <READ_LENGTH> <cutoff> <prune 0|1> [device]\n",
+    /* (--gpus anywhere after the positional arguments) */
+    int gpus[64], ng = 0, pos = argc;
+    for (int i = 1; i < argc; i++)
+        if (!strcmp(argv[i], "--gpus")) {
+            if (i + 1 >= argc) return 2;
+            const char *q = argv[i + 1];
+            if (!strchr(q, ',')) {
+                ng = atoi(q);
+                for (int g = 0; g < ng && g < 64; g++) gpus[g] = g;
+            } else {
+                for (; q && ng < 64; q = strchr(q, ',') ? strchr(q, ',') + 1 : NULL) gpus[ng++] = atoi(q);
+            }
+            if (pos == argc) pos = i;
+        }
+    if (pos < 7) {
+        fprintf(stderr, "usage: %s <reads> <K> <M> <READ_LENGTH> <cutoff> <prune 0|1> [device] [--gpus N|d0,d1,..]\n",
                 argv[0]);
         return 2;
     }
     const int K = atoi(argv[2]), M = atoi(argv[3]), rl = atoi(argv[4]);
     const int cutoff = atoi(argv[5]), prune = atoi(argv[6]);
-    kbh_configure(K, M, cutoff, argc > 7 ? atoi(argv[7]) : 0);
+    kbh_configure(K, M, cutoff, pos > 7 ? atoi(argv[7]) : 0);
+    if (ng > 1 && kbh_configure_gpus(ng, gpus) != 0) {
+        fprintf(stderr, "bad --gpus\n");
+        return 2;
+    }
 
     FILE *file = fopen(argv[1], "r");
     if (!file) {

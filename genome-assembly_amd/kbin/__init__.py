@@ -36,7 +36,11 @@ EXPORTED = [
     "kb_get_timing", "kb_generate_reads_device", "kb_generate_reads_device_at", "kb_unpack_reads_to_host", "kb_stream",
     "kb_last_error", "kb_abi_version", "kb_record_words", "kb_route_plan", "kb_route_pack",
     "kb_submit_superkmers_device", "kb_route_scatter", "kb_split_passes", "kb_set_partition", "kb_digest",
+    "kb_group_unique_id", "kb_group_create", "kb_group_create_rank", "kb_group_destroy", "kb_group_info",
+    "kb_group_submit_ids", "kb_group_submit_packed_device", "kb_group_set_partition", "kb_group_send",
+    "kb_group_receive", "kb_group_finalize", "kb_group_discard", "kb_group_reset", "kb_group_ctx",
 ]
+KB_TRANSPORT_RCCL, KB_TRANSPORT_LOCAL = 1, 2
 
 
 class KbError(RuntimeError):
@@ -129,8 +133,24 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_last_error.argtypes = []
     lib.kb_last_error.restype = C.c_char_p
     lib.kb_abi_version.restype = C.c_int
+    lib.kb_group_unique_id.argtypes = [vp, C.c_size_t]
+    lib.kb_group_create.argtypes = [C.POINTER(kb_params), C.c_int, C.POINTER(C.c_int), C.POINTER(vp)]
+    lib.kb_group_create_rank.argtypes = [C.POINTER(kb_params), C.c_int, C.c_int, vp, C.c_size_t, C.POINTER(vp)]
+    lib.kb_group_destroy.argtypes = [vp]
+    lib.kb_group_destroy.restype = None
+    lib.kb_group_info.argtypes = [vp] + [C.POINTER(C.c_int)] * 4
+    lib.kb_group_submit_ids.argtypes = [vp, C.c_int, C.c_char_p, C.POINTER(u32), u64, C.POINTER(i32)]
+    lib.kb_group_submit_packed_device.argtypes = [vp, C.c_int, vp, vp, u64, u32, i32]
+    lib.kb_group_set_partition.argtypes = [vp, u32, u32]
+    lib.kb_group_send.argtypes = [vp, C.POINTER(u64)]
+    lib.kb_group_receive.argtypes = [vp, C.c_int]
+    lib.kb_group_finalize.argtypes = [vp, C.c_int]
+    lib.kb_group_reset.argtypes = [vp]
+    lib.kb_group_discard.argtypes = [vp]
+    lib.kb_group_ctx.argtypes = [vp, C.c_int]
+    lib.kb_group_ctx.restype = vp
     for name in EXPORTED:
-        if name not in ("kb_destroy", "kb_stream", "kb_last_error"):
+        if name not in ("kb_destroy", "kb_stream", "kb_last_error", "kb_group_destroy", "kb_group_ctx"):
             getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
@@ -404,6 +424,121 @@ class Engine:
         _check(self.lib, self.lib.kb_export_device(self._h, C.byref(c)))
         return {f: (getattr(c, f) if f.startswith("n_") else C.cast(getattr(c, f), C.c_void_p).value)
                 for f, _ in kb_csr._fields_}
+
+
+class _CtxView(Engine):
+    """a context owned by something else (a group's receiver): the Engine
+    result/timing methods, no ownership"""
+
+    def __init__(self, lib, handle: int, K: int, M: int, cutoff: int):
+        self.lib, self._h = lib, C.c_void_p(handle)
+        self.K, self.M, self.cutoff = K, M, cutoff
+
+    def close(self) -> None:
+        self._h = None
+
+
+def group_unique_id() -> bytes:
+    """128-byte RCCL unique id for kb_group_create_rank (made once, by one
+    process, and handed to every rank by the caller)"""
+    lib = load_library()
+    buf = C.create_string_buffer(128)
+    _check(lib, lib.kb_group_unique_id(buf, 128))
+    return buf.raw
+
+
+class Group:
+    """A multi-GPU binning group (kbin.h "multi-GPU groups"): G ranks sharded
+    by canonical mmer; records exchanged over RCCL from C (or device copies
+    for virtual shards on one device).  devices: every rank in this process
+    (kb_group_create); rank/n_ranks/unique_id: this process is one rank
+    (kb_group_create_rank on `device`)."""
+
+    def __init__(self, K: int, M: int, cutoff: int = 1, max_read_len: int = 1024, *, devices=None,
+                 rank: int | None = None, n_ranks: int | None = None, unique_id: bytes | None = None,
+                 device: int = 0, flags: int = 0, lib_path=None):
+        self.lib = load_library(lib_path)
+        self.K, self.M, self.cutoff = K, M, cutoff
+        p = kb_params(K=K, M=M, cutoff=cutoff, max_read_len=max_read_len, device=device, flags=flags,
+                      table_slots=0)
+        h = C.c_void_p()
+        if rank is None:
+            devs = list(devices) if devices is not None else [device]
+            arr = (C.c_int * len(devs))(*devs)
+            _check(self.lib, self.lib.kb_group_create(C.byref(p), len(devs), arr, C.byref(h)))
+        else:
+            _check(self.lib, self.lib.kb_group_create_rank(C.byref(p), int(rank), int(n_ranks), unique_id,
+                                                           len(unique_id), C.byref(h)))
+        self._h = h
+        n, nl, r0, tr = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        _check(self.lib, self.lib.kb_group_info(self._h, C.byref(n), C.byref(nl), C.byref(r0), C.byref(tr)))
+        self.n_ranks, self.n_local, self.rank0, self.transport = n.value, nl.value, r0.value, tr.value
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.kb_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def submit(self, local: int, reads=None, *, bases: bytes | None = None, lens=None, ids=None,
+               first_id: int = 0) -> None:
+        if reads is not None:
+            bases, lens = pack_reads(reads)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = int(lens.shape[0])
+        if ids is None:
+            ids = np.arange(first_id, first_id + n, dtype=np.int32)
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        _check(self.lib, self.lib.kb_group_submit_ids(self._h, int(local), bases,
+                                                      lens.ctypes.data_as(C.POINTER(C.c_uint32)), n,
+                                                      ids.ctypes.data_as(C.POINTER(C.c_int32))))
+
+    def submit_packed_device(self, local: int, words_ptr: int, lens_ptr: int, n_reads: int,
+                             words_per_read: int, first_id: int = 0) -> None:
+        _check(self.lib, self.lib.kb_group_submit_packed_device(self._h, int(local), C.c_void_p(words_ptr),
+                                                                C.c_void_p(lens_ptr), n_reads, words_per_read,
+                                                                int(first_id)))
+
+    def set_partition(self, part: int, n_parts: int) -> None:
+        _check(self.lib, self.lib.kb_group_set_partition(self._h, int(part), int(n_parts)))
+
+    def send(self) -> np.ndarray:
+        """route + start the exchange; returns the G x G record counts"""
+        c = np.zeros(self.n_ranks * self.n_ranks, dtype=np.uint64)
+        _check(self.lib, self.lib.kb_group_send(self._h, c.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return c.reshape(self.n_ranks, self.n_ranks)
+
+    def receive(self, prune: bool = True) -> None:
+        _check(self.lib, self.lib.kb_group_receive(self._h, 1 if prune else 0))
+
+    def finalize(self, prune: bool = True) -> None:
+        _check(self.lib, self.lib.kb_group_finalize(self._h, 1 if prune else 0))
+
+    def reset(self) -> None:
+        """drop the submitted reads (units in flight keep their records)"""
+        _check(self.lib, self.lib.kb_group_reset(self._h))
+
+    def discard(self) -> None:
+        """wait for the oldest unit in flight and drop it unbinned"""
+        _check(self.lib, self.lib.kb_group_discard(self._h))
+
+    def ctx(self, local: int) -> Engine:
+        """local rank's receiver context (export / digest / timing)"""
+        h = self.lib.kb_group_ctx(self._h, int(local))
+        if not h:
+            raise KbError(KB_EINVAL, f"no local rank {local}")
+        return _CtxView(self.lib, h, self.K, self.M, self.cutoff)
 
 
 def timing_dict(t: "kb_timing") -> dict:

@@ -10,6 +10,14 @@ records (a run of consecutive k-mers of a read that share one signature,
 ~10 per 150-bp read at k31/m7 -- about 2 B per k-mer on the wire instead of
 a 12-16 B per-k-mer record) over RCCL (torch.distributed "nccl") / xGMI.
 
+Data path (one process per GPU, torch.distributed "nccl"): the exchange is
+the C-ABI's multi-GPU group (kbin.h kb_group_create_rank; kbin.Group):
+routing, the counts all-gather and the records' grouped ncclSend/ncclRecv
+all run in C (csrc/kbin_group.hip) on an RCCL communicator of its own, and
+torch.distributed only hands every rank the group's unique id.  The torch
+exchange below stays for the gloo rehearsal (KB_DIST_BACKEND=gloo: several
+ranks sharing a GPU, or CPU tests), where RCCL cannot run.
+
 Per step on every rank, wherever the binned engine applies (K <= 31 on any
 read length; K <= 63 on reads of <= 512 bp -- the default; kbin.h
 KB_ENGINE_BINNED):
@@ -33,7 +41,7 @@ import time
 import torch
 import torch.distributed as dist
 
-from . import Engine
+from . import Engine, Group, group_unique_id
 
 _MIX_SALT = 0x5851F42D4C957F2D
 _M64 = (1 << 64) - 1
@@ -143,10 +151,22 @@ def exchange_regions_async(regions: torch.Tensor, counts, cap: int, rec_words: i
 
 
 class ShardedBinner:
-    """One rank's share of a mmer-sharded binning job."""
+    """One rank's share of a mmer-sharded binning job.  transport "c" (the
+    default under an nccl process group): the C-ABI group does the routing
+    and the RCCL exchange; "torch": the exchange through torch.distributed
+    collectives (the gloo rehearsal)."""
+
+    def __new__(cls, *a, transport: str | None = None, **kw):
+        if cls is ShardedBinner:
+            group = kw.get("group")
+            if transport is None:
+                transport = "c" if dist.get_backend(group) == "nccl" else "torch"
+            if transport == "c":
+                return super().__new__(GroupBinner)
+        return super().__new__(cls)
 
     def __init__(self, K: int, M: int, cutoff: int, max_read_len: int, device: int = 0,
-                 group=None, flags: int = 0):
+                 group=None, flags: int = 0, transport: str | None = None):
         self.engine = Engine(K, M, cutoff=cutoff, max_read_len=max_read_len, device=device,
                              flags=flags)
         self.group = group
@@ -309,3 +329,65 @@ class ShardedBinner:
         self.last_times = {"plan_ms": unit["times"][0] * 1e3, "pack_ms": 0.0,
                            "exchange_ms": unit["times"][1] * 1e3 + (t1 - t0) * 1e3,
                            "receive_ms": (t2 - t1) * 1e3}
+
+
+class GroupBinner(ShardedBinner):
+    """ShardedBinner over the C-ABI multi-GPU group: kb_group_create_rank on
+    this rank's device (torch.distributed broadcasts the 128-byte RCCL unique
+    id, nothing else), then per unit kb_group_send (route, counts all-gather,
+    records by grouped ncclSend/ncclRecv -- left in flight) and
+    kb_group_receive (bin on the receiver).  Same interface: step, send /
+    receive / wait, engine (the receiver context), last_times, last_counts."""
+
+    def __init__(self, K: int, M: int, cutoff: int, max_read_len: int, device: int = 0,
+                 group=None, flags: int = 0, transport: str | None = None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = torch.device("cuda", device)
+        box = [group_unique_id() if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                   group=group)
+        self.grp = Group(K, M, cutoff=cutoff, max_read_len=max_read_len, rank=self.rank, n_ranks=self.world,
+                         unique_id=box[0], device=device, flags=flags)
+        self.engine = self.grp.ctx(0)
+        self.last_counts = None
+        self.last_times = {}
+        self._prune = True
+        self._units = []  # units in flight, oldest first
+
+    def _load(self, words, lens, n_reads, words_per_read, first_id, part, n_parts):
+        self.grp.reset()
+        self.grp.submit_packed_device(0, words.data_ptr(), lens.data_ptr(), n_reads, words_per_read, first_id)
+        if n_parts > 1:
+            self.grp.set_partition(part, n_parts)
+
+    def step(self, words: torch.Tensor, lens: torch.Tensor, n_reads: int, words_per_read: int,
+             first_id: int, prune: bool = True, part: int = 0, n_parts: int = 1) -> None:
+        unit = self.send(words, lens, n_reads, words_per_read, first_id, part, n_parts)
+        self.receive(unit, prune)
+
+    def send(self, words: torch.Tensor, lens: torch.Tensor, n_reads: int, words_per_read: int,
+             first_id: int, part: int = 0, n_parts: int = 1):
+        t0 = time.perf_counter()
+        self._load(words, lens, n_reads, words_per_read, first_id, part, n_parts)
+        counts = self.grp.send()
+        unit = {"counts": counts, "part": part, "n_parts": n_parts, "times": (time.perf_counter() - t0, 0.0)}
+        self._units.append(unit)
+        return unit
+
+    def wait(self, unit) -> None:
+        """drop a unit nobody receives (its records land, unbinned)"""
+        assert self._units and self._units[0] is unit, "units leave in the order they were sent"
+        self._units.pop(0)
+        self.grp.discard()
+
+    def receive(self, unit, prune: bool = True) -> None:
+        assert self._units and self._units[0] is unit, "units are received in the order they were sent"
+        t0 = time.perf_counter()
+        self.grp.receive(prune)
+        self._units.pop(0)
+        c = unit["counts"]
+        self.last_counts = (c[self.rank].tolist(), c[:, self.rank].tolist())
+        self.last_times = {"plan_ms": unit["times"][0] * 1e3, "pack_ms": 0.0, "exchange_ms": 0.0,
+                           "receive_ms": (time.perf_counter() - t0) * 1e3}

@@ -15,6 +15,11 @@
  *       (expand_read_id_list, find_kmer_extensions, print_kmers) runs
  *       unchanged.  Returns `hash_table` (the reference has no return,
  *       binning.c:1144).
+ *   void expand_read_id_list(struct ZHashTable *)
+ *       binning.c:857-888.  The same nodes the reference builds (an outer
+ *       create_node_item list of strlen(key) nodes per kmer entry: the
+ *       original id list, then duplicate_llist copies), every node its own
+ *       malloc block, built by worker threads over the level-2 tables.
  *
  * Error convention: like the reference (zhash.c:236/247 exit on OOM), any
  * engine failure prints kb_last_error() to stderr and calls exit(EXIT_FAILURE).
@@ -38,9 +43,21 @@ extern "C" {
 
 struct ZHashTable *process_read(struct ZHashTable *hash_table, char *read, int read_id);
 struct ZHashTable *prune_data(struct ZHashTable *hash_table);
+/* binning.c:857-888: every kmer's id list -> strlen(key) list nodes holding
+ * the original list and strlen(key) - 1 malloc'd copies (worker threads) */
+void expand_read_id_list(struct ZHashTable *hashtable);
 
 /* explicit configuration (else the compile-time defaults); device = HIP ordinal */
 int kbh_configure(int K, int M, int cutoff, int device);
+
+/* Several GPUs behind the same process_read / prune_data surface: the reads
+ * are kept on the host until prune_data, cut into n_gpus contiguous ranges and
+ * binned by one multi-GPU group (kb_group_create: mmer-sharded, records
+ * exchanged over RCCL); the tables materialised are identical to one GPU's.
+ * devices: NULL = 0 .. n_gpus-1 (a device may repeat: virtual shards).  The
+ * unchanged reference program gets the same from KBH_GPUS in the
+ * environment ("8", or "0,1,2,3"). */
+int kbh_configure_gpus(int n_gpus, const int *devices);
 
 /* like prune_data but without the prune (every key kept) */
 struct ZHashTable *kbh_finish_unpruned(struct ZHashTable *hash_table);
@@ -60,6 +77,8 @@ typedef struct {
     double group_ms;        /* materialise: level 1 */
     double fill_ms;         /* materialise: level-2 tables and lists (worker threads) */
     double release_ms;      /* kbh_release: the engine context's device and pinned memory */
+    double expand_ms;       /* the last expand_read_id_list */
+    uint64_t expand_nodes;  /* ll_nodes it allocated (outer nodes + list copies) */
 } kbh_times;
 int kbh_last_times(kbh_times *out);
 

@@ -279,6 +279,61 @@ int kb_set_partition(kb_ctx *ctx, uint32_t part, uint32_t n_parts);
  * to order their own work against the engine. */
 void *kb_stream(kb_ctx *ctx);
 
+/* ---- multi-GPU groups (SURVEY.md §8(b) kb_create(..., n_gpus, ...), §8(e))
+ * A group of G ranks bins one job sharded by canonical mmer: every rank's
+ * reads are scanned where they are, each super-k-mer record goes to rank
+ * owner(mmer) (kb_route_scatter), the records move in ONE exchange -- the
+ * per-destination counts (ncclAllGather), then grouped ncclSend/ncclRecv,
+ * over RCCL / xGMI, called from C -- and every rank bins what it received
+ * (kb_submit_superkmers_device + kb_finalize).  The ranks' results are
+ * disjoint; their union is the single-GPU result, entry for entry and list
+ * for list, provided read ids increase with the global call order (rank r's
+ * ids below rank r+1's) and are >= 0: they are the reverse-call-order key of
+ * the lists (binning.c:1061-1068).
+ *   kb_group_create: every rank in this process, one per device of
+ *     devices[0..n_gpus) (NULL: 0..n_gpus-1); RCCL communicators from
+ *     ncclCommInitAll.  Devices listed more than once (virtual shards, tests
+ *     on one GPU) -- or KB_GROUP_TRANSPORT=local -- move the records with
+ *     device copies instead, on the same code path.
+ *   kb_group_create_rank: one rank per process (params->device is this
+ *     rank's device); every process passes the same 128-byte unique id, made
+ *     once by kb_group_unique_id and distributed by the caller.
+ * Reads go to a LOCAL rank (0 .. n_local-1) with kb_group_submit_ids /
+ * kb_group_submit_packed_device and stay until kb_group_reset, so partitioned
+ * passes (kb_group_set_partition, then send/receive per pass) reuse them.
+ * kb_group_send routes and starts the exchange of the reads' records (the
+ * pass's partition only) and returns once it is in flight; kb_group_receive
+ * bins the oldest unit in flight on every local rank.  Two units may be in
+ * flight, so a caller can send unit i+1 before receiving unit i (the
+ * exchange overlaps the binning).  kb_group_discard waits for the oldest
+ * unit's records and drops them unbinned.  kb_group_finalize = send +
+ * receive.  kb_group_reset drops the submitted reads (units in flight keep
+ * their records).
+ * h_counts (optional, G*G): records from rank s to rank d at [s*G + d].
+ * Each local rank's result is its receiver context (kb_group_ctx): kb_export,
+ * kb_export_device, kb_digest and kb_get_timing apply.  Errors: status codes,
+ * message in kb_last_error(). */
+typedef struct kb_group kb_group;
+#define KB_TRANSPORT_RCCL 1
+#define KB_TRANSPORT_LOCAL 2
+int kb_group_unique_id(void *out, size_t len);
+int kb_group_create(const kb_params *params, int n_gpus, const int *devices, kb_group **out);
+int kb_group_create_rank(const kb_params *params, int rank, int n_ranks, const void *unique_id, size_t len,
+                         kb_group **out);
+void kb_group_destroy(kb_group *grp);
+int kb_group_info(kb_group *grp, int *n_ranks, int *n_local, int *rank0, int *transport);
+int kb_group_submit_ids(kb_group *grp, int local, const char *bases, const uint32_t *lens, uint64_t n_reads,
+                        const int32_t *ids);
+int kb_group_submit_packed_device(kb_group *grp, int local, const uint64_t *d_words, const uint32_t *d_lens,
+                                  uint64_t n_reads, uint32_t words_per_read, int32_t first_id);
+int kb_group_set_partition(kb_group *grp, uint32_t part, uint32_t n_parts);
+int kb_group_send(kb_group *grp, uint64_t *h_counts);
+int kb_group_receive(kb_group *grp, int prune);
+int kb_group_finalize(kb_group *grp, int prune);
+int kb_group_discard(kb_group *grp);
+int kb_group_reset(kb_group *grp);
+kb_ctx *kb_group_ctx(kb_group *grp, int local);
+
 /* Message for the last failing call on this thread. */
 const char *kb_last_error(void);
 

@@ -17,7 +17,8 @@
 #                                 shipped (its own main: bin, prune, expand,
 #                                 unitig extension, print_kmers)
 #   build_ref.sh dropin K M [C]   dropin_k<K>_m<M>_c<C>: the SAME reference
-#                                 program, but its process_read/prune_data are
+#                                 program, but its process_read/prune_data/
+#                                 expand_read_id_list are
 #                                 weakened and the GPU shim's strong definitions
 #                                 (genome-assembly_amd/host/binning_gpu.c over
 #                                 libkbin.so) win at link time -- the drop-in
@@ -87,7 +88,7 @@ case $MODE in
     else
       LIB="$REPO/genome-assembly_amd/lib"
       [ -f "$LIB/libkbin.so" ] || { echo "build libkbin.so first" >&2; exit 1; }
-      objcopy --weaken-symbol=process_read --weaken-symbol=prune_data "$TMP/binning.o"
+      objcopy --weaken-symbol=process_read --weaken-symbol=prune_data --weaken-symbol=expand_read_id_list "$TMP/binning.o"
       # the shim includes our kb_zhash.h (same layout as zhash.h/llist.h); its
       # container calls resolve to the reference's zhash.o / llist.o
       gcc -O2 -w -pthread $DEFS -c "$REPO/genome-assembly_amd/host/binning_gpu.c" -o "$TMP/shim.o"

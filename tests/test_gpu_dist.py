@@ -314,3 +314,150 @@ def test_ranks_rehearsal(tmp_path):
         union.update(part)
         assert z["sent"].sum() > 0 and z["recv"].sum() > 0
     assert union == want
+
+
+# ---- multi-GPU groups through the C-ABI (kb_group_*: routing, exchange over
+# RCCL or device copies, receivers -- all in C; kbin.h "multi-GPU groups")
+
+def _group_union(grp, G_local):
+    union = {}
+    for g in range(G_local):
+        part = _result_dict(grp.ctx(g).export())
+        assert all(kbin.dist.owner_of(mm, grp.n_ranks) == grp.rank0 + g for mm, _ in part)
+        assert not (set(part) & set(union))
+        union.update(part)
+    return union
+
+
+@pytest.mark.parametrize("K,M,G", [(31, 7, 2), (31, 7, 4), (31, 7, 8), (21, 5, 3), (63, 7, 4), (40, 6, 2)])
+def test_group_virtual_shards(K, M, G, engine):
+    """G ranks in this process on one device (virtual shards: the device-copy
+    transport on the same C routing code): each rank gets a contiguous slice
+    of the reads, and the union of the receivers equals the oracle, pruned
+    and not; every rank owns exactly its owner(mmer) share"""
+    reads = _reads()
+    bases, lens = kbin.pack_reads(reads)
+    ids = np.arange(len(reads), dtype=np.int32) * 2 + 5  # increasing with the call order
+    off = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    cuts = np.linspace(0, len(reads), G + 1).astype(int)
+    with kbin.Group(K, M, cutoff=1, max_read_len=300, devices=[0] * G) as grp:
+        assert grp.transport == kbin.KB_TRANSPORT_LOCAL and grp.n_ranks == G == grp.n_local
+        for prune in (True, False):
+            grp.reset()
+            for g in range(G):
+                a, b = cuts[g], cuts[g + 1]
+                grp.submit(g, bases=bases[off[a]:off[b]], lens=lens[a:b], ids=ids[a:b])
+            grp.finalize(prune)
+            want = skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, prune, ids=ids))
+            assert _group_union(grp, G) == want
+
+
+def _c2_prefix(n):
+    import bench
+    wl = bench.WORKLOADS["c2"]
+    L = wl["read_len"]
+    wpr = (L + 31) // 32
+    w = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    ln = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(w.data_ptr(), ln.data_ptr(), n, L, wl["genome"], wl["err_ppm"],
+                               bench.gen_seed(wl["seed"]))
+    torch.cuda.synchronize()
+    bases, lens = kbin.unpack_reads_to_host(w.data_ptr(), ln.data_ptr(), n, wpr, n * L)
+    return w, ln, wpr, L, bases, lens
+
+
+@pytest.mark.parametrize("api", ["create", "create_rank"])
+def test_group_rccl_c2_prefix(api, engine):
+    """G = 1 through RCCL itself (ncclCommInitAll / ncclCommInitRank with a
+    unique id; counts all-gathered, records by ncclSend/ncclRecv to self),
+    bit-exact against the oracle on the C2 generator's first 40 K reads"""
+    n = 40_000
+    w, ln, wpr, L, bases, lens = _c2_prefix(n)
+    kw = dict(cutoff=1, max_read_len=L)
+    if api == "create":
+        grp = kbin.Group(31, 7, devices=[0], **kw)
+    else:
+        grp = kbin.Group(31, 7, rank=0, n_ranks=1, unique_id=kbin.group_unique_id(), device=0, **kw)
+    with grp:
+        assert grp.transport == kbin.KB_TRANSPORT_RCCL
+        grp.submit_packed_device(0, w.data_ptr(), ln.data_ptr(), n, wpr, 0)
+        counts = grp.send()
+        assert counts.shape == (1, 1) and int(counts[0, 0]) > 0
+        grp.receive(True)
+        got = grp.ctx(0).export()
+    assert_same_as_oracle(got, oracle.bin_reads(bases, lens, 31, 7, 1, True))
+
+
+def assert_same_as_oracle(res, ora):
+    c = res.canonical()
+    assert c.n_entries == ora.n_entries
+    for f in ("mmer", "kmer_hi", "kmer_lo", "count", "offset", "ids"):
+        np.testing.assert_array_equal(getattr(c, f), getattr(ora, f))
+
+
+def test_group_pipelined_partitions(engine):
+    """two units in flight (send, send, receive, receive ...) over partitioned
+    passes of the same reads: the passes' union over 4 virtual ranks equals
+    the oracle; a third unit in flight is KB_ESTATE; a discarded unit is
+    dropped unbinned"""
+    n = 12_000
+    w, ln, wpr, L, bases, lens = _c2_prefix(n)
+    G, P = 4, 3
+    cuts = np.linspace(0, n, G + 1).astype(int)
+    union = {}
+    with kbin.Group(31, 7, cutoff=1, max_read_len=L, devices=[0] * G) as grp:
+        for g in range(G):
+            a = int(cuts[g])
+            grp.submit_packed_device(g, w[a * wpr:].data_ptr(), ln[a:].data_ptr(), int(cuts[g + 1]) - a, wpr, a)
+        grp.set_partition(0, P)
+        grp.send()
+        grp.set_partition(1, P)
+        grp.send()
+        with pytest.raises(kbin.KbError) as ei:
+            grp.send()
+        assert ei.value.code == kbin.KB_ESTATE
+        grp.discard()
+        grp.discard()
+        grp.set_partition(0, P)
+        grp.send()
+        for p in range(P):
+            if p + 1 < P:
+                grp.set_partition(p + 1, P)
+                grp.send()
+            grp.receive(True)
+            part = _group_union(grp, G)
+            assert not (set(part) & set(union))
+            union.update(part)
+    assert union == skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, 31, 7, 1, True))
+
+
+def test_group_track_first(engine):
+    """first occurrences through a group (the drop-in's multi-GPU mode): the
+    sender switches to plan/pack (read order), receivers keep (id << 16 |
+    position) of every key exactly as one engine over all reads does"""
+    reads = _reads(400)
+    bases, lens = kbin.pack_reads(reads)
+    ids = np.arange(len(reads), dtype=np.int32)
+    K, M, G = 31, 7, 3
+    with kbin.Engine(K, M, max_read_len=300, flags=kbin.KB_TRACK_FIRST) as whole:
+        whole.submit(bases=bases, lens=lens, ids=ids)
+        whole.finalize(prune=False)
+        ref = whole.export().canonical()
+    firsts = {(int(ref.mmer[e]), int(ref.kmer_lo[e])): int(ref.first[e]) for e in range(ref.n_entries)}
+    want = _result_dict(ref)
+    off = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    cuts = np.linspace(0, len(reads), G + 1).astype(int)
+    with kbin.Group(K, M, max_read_len=300, devices=[0] * G, flags=kbin.KB_TRACK_FIRST) as grp:
+        for g in range(G):
+            a, b = cuts[g], cuts[g + 1]
+            grp.submit(g, bases=bases[off[a]:off[b]], lens=lens[a:b], ids=ids[a:b])
+        grp.finalize(False)
+        seen = 0
+        union = {}
+        for g in range(G):
+            r = grp.ctx(g).export()
+            for e in range(r.n_entries):
+                assert firsts[(int(r.mmer[e]), int(r.kmer_lo[e]))] == int(r.first[e])
+                seen += 1
+            union.update(_result_dict(r))
+    assert seen == ref.n_entries and union == want

@@ -88,6 +88,53 @@ def test_random_vs_oracle(K, M):
         assert_same(res, ora)
 
 
+def test_result_invariant_fails_loudly(engine, monkeypatch):
+    """a result whose pre-prune counts do not add up to the
+    pass's k-mers (or entries > distinct > k-mers) is KB_EDEVICE, never KB_OK.
+    KB_DIAG_CORRUPT=1 makes block 0 add one to a table count; the same input
+    without it stays bit-exact."""
+    rng = np.random.default_rng(11)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=4000)
+    reads = [genome[s:s + 150].tobytes() for s in rng.integers(0, 3850, 2000)]
+    bases, lens = kbin.pack_reads(reads)
+    ora = oracle.bin_reads(bases, lens, 31, 7, 1, True)
+    assert_same(gpu_result(bases, lens, 31, 7), ora)
+    if engine != "binned":
+        pytest.skip("the corruption knob is the binned engine's")
+    monkeypatch.setenv("KB_DIAG_CORRUPT", "1")
+    with pytest.raises(kbin.KbError) as ei:
+        gpu_result(bases, lens, 31, 7)
+    assert ei.value.code == kbin.KB_EDEVICE and "invariant" in str(ei.value)
+
+
+@pytest.mark.parametrize("knob", ["KB_BIN_LDSBAR", "KB_BIN_STAGE6", "KB_BIN_TS_ADAPT", "KB_BIN_DEFER_TAIL"])
+@pytest.mark.parametrize("heavy", [False, True])
+def test_default_knobs_off(knob, heavy, engine, monkeypatch):
+    """the paths on by default (LDS-only barriers, the split 6-B
+    stage, per-bin table sizes, the deferred tail) in their OTHER state stay
+    bit-exact: a C2-like input, and one forced onto heavy bins (small tables,
+    flat lists, the pre-filter)"""
+    if engine != "binned":
+        pytest.skip("binned engine knobs")
+    rng = np.random.default_rng(5)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20000)
+    reads = []
+    for s in rng.integers(0, 19850, 6000):
+        r = genome[s:s + 150].copy()
+        m = rng.random(150) < 0.002
+        r[m] = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=int(m.sum()))
+        reads.append(r.tobytes())
+    bases, lens = kbin.pack_reads(reads)
+    monkeypatch.setenv(knob, "0")
+    if heavy:
+        monkeypatch.setenv("KB_BIN_TS_LOG2", "10")
+        monkeypatch.setenv("KB_BIN_FLAT_L", "1")
+        monkeypatch.setenv("KB_BIN_PF", "1")
+    for prune in (True, False):
+        ora = oracle.bin_reads(bases, lens, 31, 7, 1, prune)
+        assert_same(gpu_result(bases, lens, 31, 7, 1, prune, batches=2), ora)
+
+
 def test_binned_engine_selected(engine):
     """the engine the environment asks for is the one that runs (K <= 31)"""
     rng = np.random.default_rng(3)
@@ -658,6 +705,44 @@ def test_dropin_reference_program(golden_dir):
         out = subprocess.run([str(exe), str(golden_dir / row["input"])], check=True,
                              capture_output=True, timeout=300).stdout
         assert hashlib.sha256(out).hexdigest() == row["sha256"], row
+        ran += 1
+    if not ran:
+        pytest.skip("drop-in binaries not built (needs the reference at build time)")
+
+
+def test_host_cli_multi_gpu(digests, golden_dir):
+    """kbin_main --gpus: the reference surface over a multi-GPU group (reads
+    cut into contiguous per-rank ranges, mmer-sharded, records exchanged, the
+    ranks' results merged and materialised) gives the known-answer digests.
+    On one GPU the ranks are virtual shards ("0,0,0": the device-copy
+    transport of the same C routing code)."""
+    import subprocess
+    exe = kbin.LIB_DIR / "kbin_main"
+    for row in digests[:8]:
+        out = subprocess.run([str(exe), str(golden_dir / row["input"]), str(row["K"]), str(row["M"]),
+                              str(row["read_length"]), str(row["cutoff"]), "1" if row["prune"] else "0",
+                              "--gpus", "0,0,0"], check=True, capture_output=True, timeout=120).stdout
+        assert hashlib.sha256(out).hexdigest() == row["sha256"], row
+
+
+def test_dropin_reference_program_multi_gpu(golden_dir):
+    """the unchanged reference program on several GPUs (KBH_GPUS): its stdout
+    (unitig extension and print_kmers over the materialised tables) stays
+    byte-identical to the reference program's -- the merged multi-GPU result
+    reproduces the exact zhash layout, first occurrences included"""
+    import json
+    import os
+    import subprocess
+    rows = json.loads((golden_dir / "unitigs.json").read_text())
+    ran = 0
+    for row in rows:
+        exe = kbin.REPO_ROOT / "oracle" / "_ref" / f"dropin_k{row['K']}_m{row['M']}_c1"
+        if not exe.exists():
+            continue
+        for gpus in ("0,0", "0,0,0,0"):
+            out = subprocess.run([str(exe), str(golden_dir / row["input"])], check=True, capture_output=True,
+                                 timeout=300, env=dict(os.environ, KBH_GPUS=gpus)).stdout
+            assert hashlib.sha256(out).hexdigest() == row["sha256"], (row, gpus)
         ran += 1
     if not ran:
         pytest.skip("drop-in binaries not built (needs the reference at build time)")

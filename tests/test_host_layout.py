@@ -69,3 +69,92 @@ def test_direct_layout_equals_replay(n, K, M, heavy, prune):
     assert lib.kbh_materialise_csr(b, C.byref(csr), prune, 0) == 0
     assert lib.kbh_layout_digest(a) == lib.kbh_layout_digest(b)
     del keep
+
+
+class _Node(C.Structure):
+    pass
+
+
+_Node._fields_ = [("next", C.POINTER(_Node)), ("item", C.c_void_p)]
+
+
+class _Entry(C.Structure):
+    pass
+
+
+_Entry._fields_ = [("key", C.c_char_p), ("val", C.c_void_p), ("next", C.POINTER(_Entry))]
+
+
+class _Table(C.Structure):
+    _fields_ = [("size_index", C.c_size_t), ("entry_count", C.c_size_t), ("entries", C.POINTER(C.POINTER(_Entry)))]
+
+
+LADDER = [53, 101, 211, 503, 1553, 3407, 6803, 12503, 25013, 50261, 104729, 250007, 500009, 1000003]
+
+
+def _entries(tab_addr):
+    t = _Table.from_address(tab_addr)
+    for b in range(LADDER[t.size_index]):
+        e = t.entries[b]
+        while e:
+            yield e.contents
+            e = e.contents.next
+
+
+def _chain(head_addr):
+    """(node address, read id) of an ll_node list"""
+    out = []
+    p = head_addr
+    while p:
+        nd = _Node.from_address(p)
+        out.append((p, C.c_int.from_address(p + 8).value))
+        p = C.cast(nd.next, C.c_void_p).value
+    return out
+
+
+@pytest.mark.parametrize("threads", ["1", "5"])
+@pytest.mark.parametrize("n,K,M", [(0, 31, 7), (600, 31, 7), (900, 21, 3), (300, 63, 7)])
+def test_expand_read_id_list(n, K, M, threads, monkeypatch):
+    """expand_read_id_list (binning.c:857-888) on materialised tables: every
+    kmer entry's value becomes strlen(key) = K outer nodes (create_node_item,
+    llist.c:13-18); the first holds the ORIGINAL list (same nodes), the other
+    K - 1 hold fresh copies (duplicate_llist, llist.c:83-99): same ids in the
+    same order, every node a distinct block.  Tables and keys are untouched."""
+    monkeypatch.setenv("KBH_THREADS", threads)
+    lib = host_lib()
+    lib.expand_read_id_list.argtypes = [C.c_void_p]
+    rng = np.random.default_rng(n + K)
+    csr, keep = synthetic_csr(rng, n, K, M)
+    assert lib.kbh_configure(K, M, 1, 0) == 0
+    h = lib.zcreate_hash_table()
+    assert lib.kbh_materialise_csr(h, C.byref(csr), 1, 0) == 0
+    before = {}
+    for me in _entries(h):
+        for ke in _entries(me.val):
+            before[(me.key, ke.key)] = (ke.val, _chain(ke.val))
+    layout = lib.kbh_layout_digest(h)  # (walks the lists: taken before the expansion)
+    lib.expand_read_id_list(h)
+    seen = set()
+    n_after = 0
+    for me in _entries(h):
+        for ke in _entries(me.val):
+            head, ids = before[(me.key, ke.key)]
+            outer = _chain(ke.val)
+            assert len(outer) == len(ke.key) == K
+            items = [C.c_void_p.from_address(a + 8).value for a, _ in outer]
+            assert items[0] == head
+            assert _chain(items[0]) == ids  # the original list, untouched
+            for it in items[1:]:
+                cp = _chain(it)
+                assert [i for _, i in cp] == [i for _, i in ids]
+                for a, _ in cp:
+                    assert a not in seen
+                    seen.add(a)
+            for a, _ in outer:
+                assert a not in seen
+                seen.add(a)
+            n_after += 1
+    assert n_after == len(before)
+    for _, ids in before.values():
+        assert not any(a in seen for a, _ in ids)
+    del keep, layout
