@@ -2059,6 +2059,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             const bool pf_ok = prune && c->p.cutoff >= 1 && !(c->p.flags & KB_TRACK_FIRST) && flat_l;
             a.pf = pf_ok && (pf_env == 1 || (pf_env < 0 && c->rho >= 0.3f && c->rho_tab > 0.f)) ? 1u : 0u;
             a.rho_tab = c->rho_tab > 0.f ? c->rho_tab : a.rho;
+            a.pf_light = a.pf && KW == 2 && env_int("KB_BIN_PF_LIGHT", 1) != 0 ? 1u : 0u;
             a.tab_keys = reinterpret_cast<unsigned long long*>(c->totals.p + 11);
         }
         if (attempt) HIPCHK(hipMemsetAsync(c->pstat.p, 0, KB_PSTAT * sizeof(unsigned long long), c->s));
@@ -2239,6 +2240,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         c->tm.prefiltered = ps[5];
         c->tm.offset_partitions = ps[6];
         c->tm.flat_partitions = ps[7];
+        c->tm.light_prefilter_bins = (uint32_t)ps[8];
         c->tm.long_lists = c->h_misc[4];
         c->tm.clustered_lists = c->h_misc[5];
         const kb_ctx::BucketMap* bm = bucketed ? bmap_find(c, NB) : nullptr;  // (before this pass's learning)

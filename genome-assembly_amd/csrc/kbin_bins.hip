@@ -1008,6 +1008,17 @@ struct BinTable {
     }
 };
 
+// Light pre-filtered bins (two-word keys): a bin whose keys seen twice or more
+// fit under the flat depth stays light.  A 2-bit sketch of all its k-mers,
+// built once per bin in LDS of its own (past the rings: the two-word carve
+// leaves room), screens the sweeps: a k-mer whose cell was hit once is the
+// only occurrence of its key -- count 1 <= cutoff, counted as one distinct key,
+// never inserted or staged.  Exact, as for the flat bins' sketch.
+constexpr uint32_t PFL_WORDS = 8192;       // 32 KiB: 131072 cells
+constexpr double PFL_LOAD = 0.15;          // at most this many distinct keys per cell
+DEV uint32_t sk_cell(const TKey<1>& k, uint32_t cells);
+DEV uint32_t sk_cell(const TKey<2>& k, uint32_t cells);
+
 // Expand the k-mers of the bin's records that fall in partition (p, l) and
 // hand them to f.  Records are the bin's super-k-mers, streamed from the
 // bin-ordered SoA arrays, one record per lane, the next chunk's loads issued
@@ -1020,9 +1031,12 @@ struct BinTable {
 //   Offset range [olo, ohi) (offset partitions; [0, 64) = every offset): only
 // the k-mers j whose minimizer sits at offset so - j inside the k-mer, a
 // contiguous run [ja, jb) of each record.
+//   psk (light pre-filtered bins): k-mers whose sketch cell was hit once are
+// singles -- not handed to f, counted into *nsingle
 template <int KW, typename F>
 DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, uint32_t l, uint32_t olo,
-                       uint32_t ohi, uint64_t* qa, uint64_t* qb, uint32_t* qo, uint16_t* qp, uint32_t* ctr, F&& f) {
+                       uint32_t ohi, uint64_t* qa, uint64_t* qb, uint32_t* qo, uint16_t* qp, uint32_t* ctr, F&& f,
+                       const uint32_t* psk = nullptr, uint32_t* nsingle = nullptr) {
     constexpr uint32_t Q = bin_q<KW>(), FL = Q / 2;
     const int K = A.K;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1031,6 +1045,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
     const bool track = A.e_first != nullptr;  // k-mer positions only for KB_TRACK_FIRST
     const bool ringfree = A.ringfree != 0;
     uint32_t head = 0, fill = 0;  // wave-uniform ring state
+    uint32_t singles = 0;         // (psk) this lane's singles
     auto ring = [&](uint32_t i) {
         if constexpr (KW == 1) return TKey<1>{qa[i]};
         else return TKey<2>{qa[i], qb[i]};
@@ -1154,6 +1169,13 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
                 key[u] = sp.key(K, fl);
                 sp.step();
                 take[u] = (uint32_t)(j + u - ja) < (uint32_t)nl && (l == 0 || (key[u].part() & pmask) == p);
+                if (psk && take[u]) {
+                    const uint32_t q = sk_cell(key[u], PFL_WORDS * 16u);
+                    if (!((psk[q >> 4] >> (2u * (q & 15u) + 1u)) & 1u)) {
+                        take[u] = false;
+                        singles++;
+                    }
+                }
                 m[u] = __ballot(take[u]);
             }
             uint32_t f0 = fill;
@@ -1173,6 +1195,10 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
         }
     }
     if (fill) flush(fill);
+    if (psk) {
+        const uint32_t ws = wave_sum_u32(singles);
+        if (lane == 0 && ws) atomicAdd(nsingle, ws);
+    }
 #ifdef KB_BIN_ABL
     if (abl_acc == 0x123456789ull) qo[0] = 1u;  // (keeps the ablated work alive)
 #endif
@@ -1435,6 +1461,10 @@ DEV void bin_body(const BinArgs& A) {
     uint32_t* qo = reinterpret_cast<uint32_t*>(ring0 + KW * BIN_WAVES * Q) + wq;
     uint16_t* qp = reinterpret_cast<uint16_t*>(reinterpret_cast<uint32_t*>(ring0 + KW * BIN_WAVES * Q) +
                                                BIN_WAVES * Q) + wq;
+    // (two-word keys) the light pre-filter's sketch, past the rings
+    uint32_t* const pfl_sk = KW == 2 ? reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ring0) +
+                                                                   (size_t)BIN_WAVES * Q * (8u * KW + 6u))
+                                     : nullptr;
     const uint64_t nbins = min(A.totals[2], A.max_bins);
     const uint32_t tid = threadIdx.x;
 #ifdef KB_BIN_PROF
@@ -1540,6 +1570,21 @@ DEV void bin_body(const BinArgs& A) {
         // coverage) -- its build and its partitions then spread over the chip
         bool flat = PHASE == 1 ? !(S.l0 & SPLIT_BIT)
                                : (A.flat_l && (l0 >= A.flat_l || (A.big_occ && l0 >= 1 && occ_tot > A.big_occ)));
+        // a would-be flat bin of two-word keys whose keys seen twice or more
+        // (the learned table keys per occurrence) fit under the flat depth, and
+        // whose distinct keys load the sketch lightly, stays light: one sketch
+        // sweep, then its partitions' sweeps skip the singles
+        bool pfl = false;
+        if (PHASE == 0 && KW == 2 && A.pf_light && flat && !(A.big_occ && occ_tot > A.big_occ)) {
+            const double want_t = (double)occ_tot * A.rho_tab / ((double)A.fill * TS);
+            uint32_t l1 = 0;
+            while ((double)(1u << l1) < want_t && l1 < 16) l1++;
+            if (l1 < A.flat_l && (double)occ_tot * rho <= PFL_LOAD * (double)(PFL_WORDS * 16u)) {
+                flat = false;
+                pfl = true;
+                l0 = l1;
+            }
+        }
         // a big light bin (over a fair share of one block, or over the split
         // threshold) whose depth at the light load stays offset-partitioned is
         // split by offset range instead: phase 1 bins each range on any block,
@@ -1564,7 +1609,7 @@ DEV void bin_body(const BinArgs& A) {
         // bins the partitions on any block, each re-expanding the records with
         // the partition filter -- the light path, in parallel
         bool split = (PHASE == 1 && !flat) || osplit;
-        if (PHASE == 0 && !flat && !osplit && A.split_occ && occ_tot > A.split_occ) {
+        if (PHASE == 0 && !flat && !osplit && !pfl && A.split_occ && occ_tot > A.split_occ) {
             const uint32_t lmax = A.flat_l ? A.flat_l - 1u : 3u;
             while (l0 < lmax && (occ_tot >> l0) > A.split_occ) l0++;
             split = l0 >= 1;
@@ -1650,11 +1695,24 @@ DEV void bin_body(const BinArgs& A) {
         // table four times larger before it splits
         uint32_t tsb = TS;
         if (PHASE == 0 && A.ts_adapt && !flat && !split && l0 == 0) {
-            const double keys = (double)occ_tot * rho;
+            const double keys = (double)occ_tot * (pfl ? A.rho_tab : rho);
             tsb = (uint32_t)BIN_THREADS;
             while (tsb < TS && keys > (double)A.fill_light * tsb) tsb <<= 1;
         }
         const uint32_t p_lo = PHASE == 0 ? 0u : S.part0, p_hi = PHASE == 0 ? (1u << l0) : S.part0 + 1u;
+        if constexpr (KW == 2) {
+            if (pfl) {  // the bin's sketch: bit 2c seen, bit 2c+1 seen again
+                for (uint32_t i = tid; i < PFL_WORDS; i += BIN_THREADS) pfl_sk[i] = 0;
+                bar_lds(A);
+                expand_bin<KW>(A, lo, hi, [&](const TKey<KW>& k, uint32_t, uint32_t) {
+                    const uint32_t cl = sk_cell(k, PFL_WORDS * 16u);
+                    const uint32_t bit = 1u << (2u * (cl & 15u));
+                    if (atomicOr(&pfl_sk[cl >> 4], bit) & bit) atomicOr(&pfl_sk[cl >> 4], bit << 1);
+                });
+                bar_lds(A);
+                if (tid == 0 && A.pstat) atomicAdd(&A.pstat[8], 1ull);
+            }
+        }
         for (uint32_t p0 = p_lo; p0 < p_hi; p0++) {
         const uint32_t olo = omode ? A.ocut[l0][p0] : 0u, ohi = omode ? A.ocut[l0][p0 + 1] : 64u;
         if (tid == 0) {
@@ -1815,7 +1873,8 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_ABL
                 if (A.ablate != 5)  // 5: no sweep 1 at all (the per-bin overheads alone)
 #endif
-                for_each_kmer<KW>(A, lo, hi, P, Lv, olo, ohi, qa, qb, qo, qp, &S.n_stage, insert2);
+                for_each_kmer<KW>(A, lo, hi, P, Lv, olo, ohi, qa, qb, qo, qp, &S.n_stage, insert2,
+                                  pfl ? pfl_sk : nullptr, &S.n_single);
             } else if constexpr (PHASE == 1) {
                 // the partition's flat list, two entries per lane; a deeper split
                 // (Lv > l0) filters it, entries keep their index (sweep 2 filters too)
@@ -3917,7 +3976,8 @@ size_t bins_lds_bytes(uint32_t ts_log2, int KW) {
     const size_t TS = (size_t)1 << ts_log2;
     const size_t Q = KW == 1 ? bin_q<1>() : bin_q<2>();
     return sizeof(BinShared) + TS * (KW * sizeof(uint64_t) + sizeof(uint32_t)) +
-           (size_t)BIN_WAVES * Q * (KW * sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint16_t));
+           (size_t)BIN_WAVES * Q * (KW * sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint16_t)) +
+           (KW == 2 ? PFL_WORDS * sizeof(uint32_t) : 0);
 }
 
 // the bin kernel's blocks (every CU, as many as fit) and the per-launch split

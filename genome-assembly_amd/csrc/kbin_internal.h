@@ -298,6 +298,8 @@ struct BinArgs {
     // (with cutoff >= 1 they are pruned anyway: exact).  Partitions are then
     // sized by the keys that do enter the table (rho_tab) and by the sketch
     uint32_t pf;               // 1: pre-filter the flat bins (prune, cutoff >= 1, no first-occurrence tracking)
+    uint32_t pf_light;         // 1 (two-word keys, with pf): a bin the pre-filter brings under the flat
+                               // depth stays light, its singles screened by a per-bin LDS sketch
     uint32_t fs_lds;           // 1: heavy bins with 9..2048 partitions write their lists LDS-staged
     float rho_tab;             // expected table keys per occurrence under the pre-filter
     unsigned long long* tab_keys;  // (zeroed) keys that entered a table
@@ -312,7 +314,7 @@ struct BinArgs {
     uint32_t corrupt;          // diagnostic (KB_DIAG_CORRUPT=1): block 0 adds one to a count, so the
                                // finalize's invariant (sum of pre-prune counts == k-mers) must fail
 };
-constexpr int KB_PSTAT = 8;
+constexpr int KB_PSTAT = 9;  // (h_totals[16 .. 16 + KB_PSTAT) in the stats copy)
 
 struct ListArgs {
     const uint64_t* totals;    // totals[0] = entries

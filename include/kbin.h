@@ -130,6 +130,8 @@ typedef struct {
     uint32_t tail_reruns;   /* binned: 1 when this finalize left the tail kernels
                                out (the last one needed none) and then ran them
                                after all (a heavy bin published, lists queued) */
+    uint32_t light_prefilter_bins; /* two-word keys: bins kept light by the
+                               singleton pre-filter (an LDS sketch per bin) */
 } kb_timing;
 
 /* Create a context (kb_create replaces zcreate_hash_table for the level-1

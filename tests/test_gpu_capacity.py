@@ -87,10 +87,14 @@ def test_c3_coverage_regime(n, genome, P, p):
 
 
 @pytest.mark.timeout(900)
-def test_c5_singleton_prefilter_default_knobs():
+@pytest.mark.parametrize("light", ["1", "0"])
+def test_c5_singleton_prefilter_default_knobs(light, monkeypatch):
     """the C5 generator (L250, K63 M7, 1 % errors): pass 0 of 2 learns the
-    singleton ratio, pass 1 runs its heavy bins with the pre-filter (default
-    knobs); both passes bit-exact against the oracle on their partitions"""
+    singleton ratio, pass 1 runs with the pre-filter (default knobs): its
+    would-be heavy bins stay light behind a per-bin sketch (KB_BIN_PF_LIGHT=1,
+    the default) or take the pre-filtered flat lists (0); both passes
+    bit-exact against the oracle on their partitions"""
+    monkeypatch.setenv("KB_BIN_PF_LIGHT", light)
     wl = bench.WORKLOADS["c5"]
     n, L, K, M, P = 2_000_000, wl["read_len"], wl["K"], wl["M"], 2
     words, lens, wpr = _generate(n, L, wl["genome"], wl["err_ppm"], bench.gen_seed(wl["seed"]))
@@ -103,8 +107,12 @@ def test_c5_singleton_prefilter_default_knobs():
             eng.finalize(True)
             tim.append(eng.timing())
             out.append(eng.export())
-    assert tim[0]["heavy_bins"] > 0 and tim[1]["heavy_bins"] > 0, tim
+    assert tim[0]["heavy_bins"] > 0, tim
     assert tim[1]["prefiltered"] > 0, tim[1]
+    if light == "1":
+        assert tim[1]["light_prefilter_bins"] > 0, tim[1]
+    else:
+        assert tim[1]["heavy_bins"] > 0 and tim[1]["light_prefilter_bins"] == 0, tim[1]
     bases, hl = _unpack(words, lens, n, wpr, L)
     for p in range(P):
         ora = oracle.bin_reads(bases, hl, K, M, 1, True, mmer_mask=part_mask(M, p, P))

@@ -487,6 +487,54 @@ def test_singleton_prefilter(K, ts_log2, cutoff, parts, err, engine, monkeypatch
             assert nd == distinct
 
 
+@pytest.mark.parametrize("ts_log2,flat_l,cutoff,parts,err", [(10, 2, 1, 1, 30000), (11, 3, 2, 2, 30000),
+                                                             (12, 3, 1, 1, 20000), (10, 1, 1, 3, 50000)])
+@pytest.mark.parametrize("light", ["1", "0"])
+def test_light_prefilter_two_word(ts_log2, flat_l, cutoff, parts, err, light, engine, monkeypatch):
+    """two-word keys (K63) with 2-5 % errors: bins that would go flat stay
+    light when their keys seen twice fit under the flat depth -- a per-bin LDS
+    sketch screens the singles out of every partition's sweep (KB_BIN_PF_LIGHT,
+    on by default; 0 keeps the flat path).  Result and distinct count (before
+    the prune) equal the oracle's, with cutoffs 1 and 2 and partitioned
+    passes; the second run (learned densities) takes the light path"""
+    import torch
+    if engine != "binned":
+        pytest.skip("binned engine only")
+    monkeypatch.setenv("KB_BIN_TS_LOG2", str(ts_log2))
+    monkeypatch.setenv("KB_BIN_FLAT_L", str(flat_l))
+    monkeypatch.setenv("KB_BIN_PF", "1")
+    monkeypatch.setenv("KB_BIN_PF_LIGHT", light)
+    n, L, K = 30000, 150, 63
+    wpr = (L + 31) // 32
+    words = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, 60000, err, 23)
+    torch.cuda.synchronize()
+    bases, hl = kbin.unpack_reads_to_host(words.data_ptr(), lens.data_ptr(), n, wpr, n * L)
+    ora = oracle.bin_reads(bases, hl, K, 7, cutoff, True)
+    distinct = oracle.bin_reads(bases, hl, K, 7, cutoff, False).n_entries
+    with kbin.Engine(K, 7, cutoff=cutoff, max_read_len=L) as eng:
+        eng.set_timing(True)
+        for run in range(2):
+            eng.reset()
+            eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
+            got, nd, lpb, pre = [], 0, 0, 0
+            for p in range(parts):
+                if parts > 1:
+                    eng.set_partition(p, parts)
+                eng.finalize(True)
+                t = eng.timing()
+                lpb += t["light_prefilter_bins"]
+                pre += t["prefiltered"]
+                r = eng.export()
+                nd += r.n_distinct
+                got.append(r)
+            assert_same(kbin.Result.concat(got) if parts > 1 else got[0], ora)
+            assert nd == distinct
+            if run == 1:
+                assert (lpb > 0) == (light == "1") and pre > 0, (lpb, pre)
+
+
 @pytest.mark.parametrize("genome,flat_l,ts_log2,K", [(3000, 3, 13, 31), (3000, 2, 10, 31), (200000, 3, 13, 31),
                                                       (200000, 3, 11, 31), (3000, 3, 12, 63), (200000, 3, 11, 63)])
 def test_split_bins(genome, flat_l, ts_log2, K, engine, monkeypatch):

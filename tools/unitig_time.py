@@ -7,9 +7,10 @@ shape (READ_LENGTH 152, oracle/build_ref.sh KB_REF_READ_LENGTH).
 For each read count n: the C2 generator's first n reads go to a file, one per
 line; dropin_k31_m7_c1_rl152 (reference main, GPU process_read/prune_data)
 and, when asked, full_k31_m7_c1_rl152 (the reference as shipped) run on it.
-stdout is hashed as it streams.  The drop-in's KBH_TRACE line gives
-prune_data's own time, so the rest of the wall is the read loop, the
-extension and print_kmers.  Prints one JSON line per run."""
+stdout is hashed as it streams.  The drop-in's KBH_TRACE lines give
+prune_data's and expand_read_id_list's own times (the drop-in replaces both),
+so the rest of the wall is the read loop, the extension, print_kmers and the
+exit.  Prints one JSON line per run."""
 import argparse
 import hashlib
 import json
@@ -54,6 +55,11 @@ def run(exe, path, timeout, env=None):
     for ln in err.splitlines():
         if ln.startswith("{\"prune_data_ms\""):
             out["prune_data"] = json.loads(ln)
+        elif ln.startswith("{\"expand_ms\""):  # the shim's expand_read_id_list (binning.c:857-888)
+            out["expand"] = json.loads(ln)
+    if "prune_data" in out and "expand" in out:
+        pd = out["prune_data"]["prune_data_ms"] / 1e3
+        out["rest_s"] = round(wall - pd - out["expand"]["expand_ms"] / 1e3, 3)  # read loop, extension, print, exit
     return out
 
 
