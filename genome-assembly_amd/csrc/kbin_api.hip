@@ -261,6 +261,7 @@ struct kb_ctx {
     DevBuf<uint32_t> stage_ord;   // light bins: the stage as ordinals ...
     DevBuf<uint16_t> stage_slot;  // ... and LDS slots (6 B per occurrence)
     DevBuf<uint64_t> kstage;   // heavy bins: per-occurrence k-mer code + 1
+    DevBuf<uint32_t> rrank, rord;  // ranked bins: record -> rank, rank -> ordinal (BinArgs::rank_mode)
     DevBuf<uint32_t> long_q;   // entries with 257..4096 ids (lists_long_kernel)
     DevBuf<uint64_t> lq;       // list items for lists_kernel (BinArgs::lq_items); [0] the counter
     DevBuf<uint32_t> border;   // bin processing order
@@ -466,7 +467,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->map_done) (void)hipEventDestroy(c->map_done);
     if (c->h_alpha) (void)hipHostFree(c->h_alpha);
     c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->stage_ord.release(); c->stage_slot.release(); c->kstage.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->stage_ord.release(); c->stage_slot.release(); c->kstage.release(); c->rrank.release(); c->rord.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
     c->regions.release(); c->bfill.release(); c->bbase.release(); c->rbase.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release(); c->e_hi_zeroed = nullptr;
@@ -2067,6 +2068,19 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.ldsbar = (uint32_t)(env_int("KB_BIN_LDSBAR", 1) != 0);
         a.ts_adapt = (uint32_t)(env_int("KB_BIN_TS_ADAPT", 1) != 0);
         a.corrupt = (uint32_t)(env_int("KB_DIAG_CORRUPT", 0) != 0);
+        // ranked bins where lists are long (the last finalize's mean list
+        // length, C3: ~2200 ids): KB_BIN_RANK=0 off, 2 always
+        {
+            const int rk = env_int("KB_BIN_RANK", 1);
+            const bool long_lists = c->hint_entries && c->hint_ids >= 64 * c->hint_entries;
+            a.rank_mode = (rk == 2 || (rk == 1 && long_lists)) && stage6 && !a.e_first ? 1u : 0u;
+            if (a.rank_mode) {
+                HIPCHK(c->rrank.ensure(std::max<uint64_t>(R, 1)));
+                HIPCHK(c->rord.ensure(std::max<uint64_t>(R, 1)));
+                a.rrank = c->rrank.p;
+                a.rord = c->rord.p;
+            }
+        }
         // The tail kernels -- the heavy bins' list builds and partitions, the
         // list kernels -- have work only when bin_kernel publishes a heavy bin
         // or queues a list, and cost ~4.5 us per empty launch (8 of them: 2 %
@@ -2241,6 +2255,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         c->tm.offset_partitions = ps[6];
         c->tm.flat_partitions = ps[7];
         c->tm.light_prefilter_bins = (uint32_t)ps[8];
+        c->tm.ranked_bins = (uint32_t)ps[9];
+        c->tm.bitmap_partitions = (uint32_t)ps[10];
         c->tm.long_lists = c->h_misc[4];
         c->tm.clustered_lists = c->h_misc[5];
         const kb_ctx::BucketMap* bm = bucketed ? bmap_find(c, NB) : nullptr;  // (before this pass's learning)

@@ -760,6 +760,7 @@ struct alignas(16) BinShared {
     uint32_t n_single;  // pre-filter: keys seen once in this partition
     uint32_t maxc;      // the partition's longest kept list (the LDS id windows)
     uint32_t sumc;      // the partition's occurrences counted in its table (the finalize's invariant)
+    uint32_t rk_min, rk_max, dup;  // ranked bins: ordinal range; a bitmap bit set twice
     uint32_t ts;        // LDS table slots of the next partition (<= the carved TS)
     unsigned long long wkey;  // LDS id windows: cursor << 32 | entry << 16 | scan index of the next window's start
     unsigned long long e0, i0, stage_base;
@@ -1036,7 +1037,7 @@ DEV uint32_t sk_cell(const TKey<2>& k, uint32_t cells);
 template <int KW, typename F>
 DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, uint32_t l, uint32_t olo,
                        uint32_t ohi, uint64_t* qa, uint64_t* qb, uint32_t* qo, uint16_t* qp, uint32_t* ctr, F&& f,
-                       const uint32_t* psk = nullptr, uint32_t* nsingle = nullptr) {
+                       const uint32_t* psk = nullptr, uint32_t* nsingle = nullptr, const uint32_t* rk = nullptr) {
     constexpr uint32_t Q = bin_q<KW>(), FL = Q / 2;
     const int K = A.K;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1083,23 +1084,27 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
     };
     uint32_t base = lo + wid * 64;
     uint64_t nhd = 0;
+    uint32_t nrk = 0;  // (rk) the record's rank in its bin, staged instead of its ordinal
 #ifdef KB_BIN_ABL
     uint64_t abl_acc = 0;
 #endif
     Span<KW> nsp{};
     if (base + lane < hi) {
         nsp.load_rec(A, base + lane, nhd);
+        if (rk) nrk = rk[base + lane];
     }
     for (; base < hi; base += BIN_THREADS) {
         const uint64_t hd = nhd;
+        const uint32_t crk = nrk;
         Span<KW> sp = nsp;
         const uint32_t nxt = base + BIN_THREADS + lane;
         nhd = 0;
         if (nxt < hi) {  // prefetch the next chunk
             nsp.load_rec(A, nxt, nhd);
+            if (rk) nrk = rk[nxt];
         }
         const int n = (int)((hd >> 32) & 63u);
-        const uint32_t ord = (uint32_t)hd;
+        const uint32_t ord = rk ? crk : (uint32_t)hd;
         const uint32_t rlo = (uint32_t)((hd >> 45) & 0xFFFFu);  // the record's first k-mer in its read
         const uint64_t fl = 0ull - ((hd >> 44) & 1ull);        // complement wins: flip every bit
         // records of a bin are sorted longest first: lane 0 holds the chunk's max
@@ -1311,10 +1316,12 @@ DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane);
 
 // (so, ss: the split stage of a light bin -- ordinals and slots -- or null:
 // the 8-B stage entries)
+// (rord_bin: a ranked bin's stage holds ranks; its ordinal is rord_bin[rank])
 template <int KW>
 DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, uint32_t* win, uint32_t win_cap,
                    uint32_t ns, unsigned long long e0, unsigned long long i0, uint32_t n_ent, uint32_t n_ids,
-                   const uint64_t* stage, const uint32_t* so, const uint16_t* ss, uint32_t e_mine PROF_PARAMS) {
+                   const uint64_t* stage, const uint32_t* so, const uint16_t* ss, uint32_t e_mine,
+                   const uint32_t* rord_bin PROF_PARAMS) {
     const uint32_t tid = threadIdx.x;
     const int lane = (int)(tid & 63u);
     const uint32_t per = TS / BIN_THREADS;
@@ -1373,6 +1380,11 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
                     vo[u] = (uint32_t)x;
                     vs[u] = (uint32_t)(x >> 48);
                 }
+            }
+            if (rord_bin) {
+#pragma unroll
+                for (int u = 0; u < WL; u++)
+                    if (vs[u]) vo[u] = rord_bin[vo[u]];
             }
 #pragma unroll
             for (int u = 0; u < WL; u++) {
@@ -1436,6 +1448,157 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
         elo = ehi;
         slo = shi;
     }
+}
+
+// ---- ranked bins (long lists): records ranked by call ordinal, lists
+// emitted from per-key bitmaps over the ranks (BinArgs::rank_mode)
+constexpr uint32_t RANK_MIN = 512;    // fewer records: lists short, nothing to gain
+constexpr uint32_t RANK_NBK = 1024;   // ordinal buckets of the ranking
+constexpr uint32_t RANK_TILE = 2048;  // ranks whose ordinals are staged in LDS at once (emission)
+constexpr uint32_t RANK_GROUPS = 8;   // most passes over the stage (entries whose bitmaps fit at once)
+
+// rank of every record of the bin [lo, hi) by descending call ordinal (ties
+// by record index): bucket the ordinals (LDS histogram over their range,
+// largest first), scatter (ordinal, index) pairs by bucket, and count each
+// record's predecessors inside its bucket.  rrank[r] = rank of record r,
+// rord[lo + k] = ordinal of rank k.  lds: RANK_NBK + 2 (hi - lo) words,
+// everything past BinShared (the table and rings are not live yet)
+DEV void bin_ranks(const BinArgs& A, BinShared& S, uint32_t lo, uint32_t hi, uint32_t* lds) {
+    const uint32_t tid = threadIdx.x, R = hi - lo;
+    uint32_t* hist = lds;
+    uint64_t* pr = reinterpret_cast<uint64_t*>(lds + RANK_NBK);
+    if (tid == 0) {
+        S.rk_min = 0xFFFFFFFFu;
+        S.rk_max = 0;
+    }
+    for (uint32_t i = tid; i < RANK_NBK; i += BIN_THREADS) hist[i] = 0;
+    __syncthreads();
+    uint32_t mn = 0xFFFFFFFFu, mx = 0;
+    for (uint32_t i = tid; i < R; i += BIN_THREADS) {
+        const uint32_t o = (uint32_t)rec_hdr(A, lo + i);
+        mn = min(mn, o);
+        mx = max(mx, o);
+    }
+    mn = ~wave_max_u32(~mn);
+    mx = wave_max_u32(mx);
+    if ((tid & 63u) == 0) {
+        atomicMin(&S.rk_min, mn);
+        atomicMax(&S.rk_max, mx);
+    }
+    __syncthreads();
+    const uint32_t omax = S.rk_max;
+    const uint64_t span = (uint64_t)(omax - S.rk_min) + 1ull;
+    auto bucket = [&](uint32_t o) { return (uint32_t)(((uint64_t)(omax - o) * RANK_NBK) / span); };
+    for (uint32_t i = tid; i < R; i += BIN_THREADS) atomicAdd(&hist[bucket((uint32_t)rec_hdr(A, lo + i))], 1u);
+    __syncthreads();
+    uint64_t tot;
+    const uint32_t h = tid < RANK_NBK ? hist[tid] : 0u;
+    const uint32_t start = (uint32_t)block_excl_scan_u64(h, S.red, tot);
+    if (tid < RANK_NBK) hist[tid] = start;  // cursor (then the bucket's end)
+    __syncthreads();
+    for (uint32_t i = tid; i < R; i += BIN_THREADS) {
+        const uint32_t o = (uint32_t)rec_hdr(A, lo + i);
+        pr[atomicAdd(&hist[bucket(o)], 1u)] = ((uint64_t)o << 32) | i;
+    }
+    __syncthreads();
+    for (uint32_t p = tid; p < R; p += BIN_THREADS) {
+        const uint64_t x = pr[p];
+        const uint32_t o = (uint32_t)(x >> 32), idx = (uint32_t)x, b = bucket(o);
+        const uint32_t b0 = b ? hist[b - 1] : 0u, b1 = hist[b];
+        uint32_t rank = b0;
+        for (uint32_t q = b0; q < b1; q++) {
+            const uint64_t y = pr[q];
+            const uint32_t yo = (uint32_t)(y >> 32);
+            rank += (yo > o || (yo == o && (uint32_t)y < idx)) ? 1u : 0u;
+        }
+        A.rrank[lo + idx] = rank;
+        A.rord[lo + rank] = o;
+    }
+    __syncthreads();  // (the ranks go out to HBM before sweep 1 reads them; the LDS is the table's next)
+}
+
+// A ranked partition's lists from bitmaps: every kept key gets a bitmap over
+// the bin's R ranks; each staged occurrence (slot, rank) sets its bit (a bit
+// already set -- the same record holding the key twice -- aborts: false, cnt
+// restored, the caller takes the cursor path); then each list is emitted in
+// rank order (descending ordinal = reverse call order) by one wave, 64 ranks
+// per step, the ordinals of a rank tile staged in LDS.  Entries are handled
+// in groups whose bitmaps fit the window area, one stage pass per group.
+template <int KW>
+DEV bool bitmap_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t ts, uint32_t* win, uint32_t win_cap,
+                      uint32_t ns, unsigned long long e0, unsigned long long i0, uint32_t n_ent, uint32_t e_mine,
+                      const uint32_t* so, const uint16_t* ss, uint32_t R, const uint32_t* rord_bin) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t per = ts / BIN_THREADS, W = (R + 31u) / 32u;
+    uint32_t* offs = win;                  // [n_ent] next position of each list (relative to i0)
+    uint32_t* tile = offs + ((n_ent + 3u) & ~3u);  // [RANK_TILE] ordinals of the current ranks
+    uint32_t* bm = tile + RANK_TILE;       // [G * W] the group's bitmaps
+    const uint32_t G = (win_cap - (uint32_t)(bm - win)) / W;
+    // kept slot -> entry index (the prune's scan order), its list start
+    {
+        uint32_t e = e_mine;
+        for (uint32_t k = 0; k < per; k++) {
+            const uint32_t i = tid + k * BIN_THREADS, c = cnt[i];
+            if (c < PRUNED) {
+                offs[e] = c;
+                cnt[i] = e++;
+            }
+        }
+    }
+    for (uint32_t g0 = 0; g0 < n_ent; g0 += G) {
+        const uint32_t g1 = min(n_ent, g0 + G);
+        for (uint32_t i = tid; i < (g1 - g0) * W; i += BIN_THREADS) bm[i] = 0;
+        if (tid == 0) S.dup = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
+            const uint32_t sl = ss[i];
+            if (!sl) continue;
+            const uint32_t e = cnt[sl - 1u];
+            if (e < g0 || e >= g1) continue;  // (pruned slots hold PRUNED)
+            const uint32_t r = so[i], bit = 1u << (r & 31u);
+            if (atomicOr(&bm[(e - g0) * W + (r >> 5)], bit) & bit) S.dup = 1;
+        }
+        __syncthreads();
+        if (S.dup) {  // uniform: back to the cursors (every list restarts; ids are rewritten)
+            uint32_t e = e_mine;
+            for (uint32_t k = 0; k < per; k++) {
+                const uint32_t i = tid + k * BIN_THREADS;
+                if (cnt[i] < PRUNED) cnt[i] = (uint32_t)(A.e_off[e0 + e++] - i0);
+            }
+            __syncthreads();
+            return false;
+        }
+        for (uint32_t t0 = 0; t0 < R; t0 += RANK_TILE) {
+            const uint32_t tn = min(RANK_TILE, R - t0);
+            for (uint32_t i = tid; i < tn; i += BIN_THREADS) tile[i] = rord_bin[t0 + i];
+            __syncthreads();
+            for (uint32_t e = g0 + wid; e < g1; e += BIN_WAVES) {
+                const uint32_t* b = bm + (e - g0) * W;
+                uint32_t run = offs[e];
+                // four 64-rank steps per trip: their bitmap reads in flight together
+                for (uint32_t c0 = 0; c0 < tn; c0 += 256u) {
+                    uint32_t x[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t r = t0 + c0 + 64u * u + lane;
+                        x[u] = c0 + 64u * u + lane < tn ? b[r >> 5] : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t r = t0 + c0 + 64u * u + lane;
+                        const bool on = (x[u] >> (r & 31u)) & 1u;
+                        const uint64_t m = __ballot(on);
+                        if (on)
+                            A.ids_out[i0 + run + lanes_below(m)] = id_of(tile[c0 + 64u * u + lane], A.read_ids, A.id_off);
+                        run += (uint32_t)__popcll(m);
+                    }
+                }
+                if (lane == 0) offs[e] = run;
+            }
+            __syncthreads();
+        }
+    }
+    return true;
 }
 
 template <int KW, int PHASE>
@@ -1713,6 +1876,19 @@ DEV void bin_body(const BinArgs& A) {
                 if (tid == 0 && A.pstat) atomicAdd(&A.pstat[8], 1ull);
             }
         }
+        // ranked bin (long lists expected): records ranked by call ordinal,
+        // the stage holds ranks (see bitmap_lists)
+        bool rmode = false;
+        if (PHASE == 0 && A.rank_mode && !flat && !split) {
+            const uint32_t words = TS + 2u * KW * TS + (uint32_t)BIN_WAVES * Q * (8u * KW + 6u) / 4u;
+            const uint32_t R = hi - lo;
+            rmode = R >= RANK_MIN && RANK_NBK + 2u * R <= words;
+            if (rmode) {
+                bar_lds(A);
+                bin_ranks(A, S, lo, hi, cnt);
+                if (tid == 0 && A.pstat) atomicAdd(&A.pstat[9], 1ull);
+            }
+        }
         for (uint32_t p0 = p_lo; p0 < p_hi; p0++) {
         const uint32_t olo = omode ? A.ocut[l0][p0] : 0u, ohi = omode ? A.ocut[l0][p0 + 1] : 64u;
         if (tid == 0) {
@@ -1874,7 +2050,7 @@ DEV void bin_body(const BinArgs& A) {
                 if (A.ablate != 5)  // 5: no sweep 1 at all (the per-bin overheads alone)
 #endif
                 for_each_kmer<KW>(A, lo, hi, P, Lv, olo, ohi, qa, qb, qo, qp, &S.n_stage, insert2,
-                                  pfl ? pfl_sk : nullptr, &S.n_single);
+                                  pfl ? pfl_sk : nullptr, &S.n_single, rmode ? A.rrank : nullptr);
             } else if constexpr (PHASE == 1) {
                 // the partition's flat list, two entries per lane; a deeper split
                 // (Lv > l0) filters it, entries keep their index (sweep 2 filters too)
@@ -2065,6 +2241,19 @@ DEV void bin_body(const BinArgs& A) {
             PROF_MARK(3);
             if (!room) continue;
             const uint32_t n_ent = (uint32_t)tot, n_ids = (uint32_t)(tot >> 32);
+            // a ranked partition with long lists: emitted from bitmaps over the
+            // ranks when they fit the window area in at most RANK_GROUPS groups
+            if (rmode && n_ent && n_ids >= 32u * n_ent) {
+                const uint32_t R = hi - lo, W = (R + 31u) / 32u;
+                const uint32_t fixed = ((n_ent + 3u) & ~3u) + RANK_TILE;
+                const uint32_t G = fixed + W <= win_cap ? (win_cap - fixed) / W : 0u;
+                if (G && (n_ent + G - 1u) / G <= RANK_GROUPS &&
+                    bitmap_lists<KW>(A, S, cnt, ts, win, win_cap, S.n_stage, e0, i0, n_ent, (uint32_t)ex, sp_ord,
+                                     sp_slot, R, A.rord + lo)) {
+                    if (tid == 0 && A.pstat) atomicAdd(&A.pstat[10], 1ull);
+                    continue;
+                }
+            }
             // LDS id windows for short lists (mean <= 64 ids): light bins, and
             // the heavy bins' unfiltered partitions with one-word keys (C4
             // share 588 -> 502 ms per step); long lists (C3: 357 -> 479 ms)
@@ -2072,7 +2261,7 @@ DEV void bin_body(const BinArgs& A) {
             const bool win_phase = PHASE == 0 || (KW == 1 && A.win_heavy && !(flat && Lv > l0));
             if (win_phase && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
                 lds_lists<KW>(A, S, cnt, ts, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage, sp_ord, sp_slot,
-                              (uint32_t)ex PROF_ARGS);
+                              (uint32_t)ex, rmode ? A.rord + lo : nullptr PROF_ARGS);
                 PROF_MARK(4);
                 continue;
             }
@@ -2094,7 +2283,7 @@ DEV void bin_body(const BinArgs& A) {
                     // takes at most cutoff adds, so it never reaches a real position
                     const uint32_t pos = atomicAdd(&cnt[ls], 1u);
                     if (pos < PRUNED) {
-                        A.ids_ord[i0 + pos] = (uint32_t)v;
+                        A.ids_ord[i0 + pos] = rmode ? A.rord[lo + (uint32_t)v] : (uint32_t)v;
                         // (ordinal << 16 | position): binning.c inserts a key at its first
                         // occurrence (1045-1057); KB_TRACK_FIRST keeps it for the zhash layout
                         if (A.e_first)

@@ -308,13 +308,24 @@ struct BinArgs {
     // [2] partitions swept to their prune [3] partitions redone split (overflow)
     // [4] deepest partition depth (max) [5] keys kept out by the pre-filter
     // [6] offset-range partitions [7] partitions swept from flat lists
+    // [8] light pre-filtered bins [9] ranked bins [10] partitions emitted from rank bitmaps
     unsigned long long* pstat;
     uint32_t ts_adapt;         // 1: one-table light bins take the smallest table for their keys (KB_BIN_TS_ADAPT)
     uint32_t ldsbar;           // 1: barriers that order LDS only skip the global-store drain (KB_BIN_LDSBAR)
     uint32_t corrupt;          // diagnostic (KB_DIAG_CORRUPT=1): block 0 adds one to a count, so the
                                // finalize's invariant (sum of pre-prune counts == k-mers) must fail
+    // Ranked bins (long lists, C3's coverage): a light bin first ranks its
+    // records by call ordinal (descending, ties by record index) -- rrank[r] is
+    // record r's rank inside its bin, rord[lo + k] the ordinal of rank k -- and
+    // its stage holds ranks instead of ordinals.  A partition whose lists are
+    // long then places every kept occurrence as one bit of its key's bitmap
+    // over the bin's ranks and emits each list by walking the bitmap: reverse
+    // call order (binning.c:1061-1068) with no sort and no list kernels
+    uint32_t rank_mode;        // 1: rank bins of 512 .. rank_max records (KB_BIN_RANK)
+    uint32_t* rrank;           // [R] record -> rank in its bin
+    uint32_t* rord;            // [R] (bin start + rank) -> ordinal
 };
-constexpr int KB_PSTAT = 9;  // (h_totals[16 .. 16 + KB_PSTAT) in the stats copy)
+constexpr int KB_PSTAT = 11;  // (h_totals[16 .. 16 + KB_PSTAT) in the stats copy)
 
 struct ListArgs {
     const uint64_t* totals;    // totals[0] = entries

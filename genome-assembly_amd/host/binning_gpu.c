@@ -14,6 +14,7 @@
 #endif
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -269,6 +270,28 @@ static void heap_pad_end(void)
 {
 #if defined(__GLIBC__) && defined(M_TOP_PAD)
     if (!getenv("KBH_NO_TOP_PAD")) mallopt(M_TOP_PAD, 128 << 10);
+#endif
+}
+
+/* Transparent huge pages for the arenas the worker threads fill: a glibc
+ * thread arena is a 64 MiB-aligned 64 MiB mapping (HEAP_MAX_SIZE), so the
+ * first block a thread gets in a new one names it; madvise(MADV_HUGEPAGE)
+ * on it is a paging hint only (512x fewer page faults while ~10^9 small
+ * blocks are written, and a faster unmap at exit).  KBH_NO_THP=1: off. */
+#define ARENA_SPAN ((uintptr_t)64 << 20)
+static void thp_hint(const void *p, uintptr_t *last)
+{
+#if defined(__linux__) && defined(MADV_HUGEPAGE)
+    const uintptr_t base = (uintptr_t)p & ~(ARENA_SPAN - 1);
+    if (base != *last) {
+        *last = base;
+        static int off = -1;
+        if (off < 0) off = getenv("KBH_NO_THP") != NULL;
+        if (!off) (void)madvise((void *)base, ARENA_SPAN, MADV_HUGEPAGE);
+    }
+#else
+    (void)p;
+    (void)last;
 #endif
 }
 
@@ -601,6 +624,7 @@ static void *direct_tables(void *arg)
     const int nc = (g_K + CHUNK_CHARS - 1) / CHUNK_CHARS;
     replay_buf b = {0};
     uint64_t nodes = 0, kept = 0;
+    uintptr_t arena = 0;
     char ks[129];
     for (;;) {
         const uint64_t w = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
@@ -636,6 +660,7 @@ static void *direct_tables(void *arg)
                 ll_node *head = NULL, **lt = &head;
                 for (uint64_t k = o0; k < o1; k++) {
                     ll_node *nd = xmalloc(sizeof *nd); /* create_node_num, llist.c:6-11 */
+                    thp_hint(nd, &arena);
                     nd->next = NULL;
                     nd->read_id = r->ids[k];
                     *lt = nd;
@@ -1094,6 +1119,9 @@ static void *expand_tables(void *arg)
 {
     expand_job *j = arg;
     uint64_t nodes = 0;
+    int *ids = NULL;
+    size_t cap = 0;
+    uintptr_t arena = 0;
     for (;;) {
         const uint64_t w = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
         if (w >= j->n) break;
@@ -1103,21 +1131,31 @@ static void *expand_tables(void *arg)
             for (struct ZHashEntry *ke = level2->entries[b2]; ke; ke = ke->next) {
                 ll_node *const list = ke->val;
                 const size_t klen = strlen(ke->key);
+                /* the list's ids once, then every copy from them */
+                size_t n = 0;
+                for (const ll_node *s = list; s; s = s->next) {
+                    if (n == cap) {
+                        cap = cap ? 2 * cap : 1024;
+                        ids = realloc(ids, cap * sizeof(int));
+                        if (!ids) exit(EXIT_FAILURE);
+                    }
+                    ids[n++] = s->read_id;
+                }
                 ll_node *outer = NULL, **ot = &outer;
                 for (size_t i = 0; i < klen; i++) {
                     ll_node *copy = list;
                     if (i) { /* duplicate_llist */
                         ll_node **ct = &copy;
-                        for (const ll_node *s = list; s; s = s->next) {
+                        for (size_t q = 0; q < n; q++) {
                             ll_node *nd = xmalloc(sizeof *nd);
+                            thp_hint(nd, &arena);
                             nd->next = NULL;
-                            nd->read_id = s->read_id;
+                            nd->read_id = ids[q];
                             *ct = nd;
                             ct = &nd->next;
-                            nodes++;
                         }
+                        nodes += n;
                         *ct = NULL;
-                        if (!list) copy = NULL;
                     }
                     ll_node *o = xmalloc(sizeof *o); /* create_node_item */
                     o->next = NULL;
@@ -1130,6 +1168,7 @@ static void *expand_tables(void *arg)
             }
         }
     }
+    free(ids);
     __atomic_fetch_add(&j->nodes, nodes, __ATOMIC_RELAXED);
     return NULL;
 }
@@ -1158,9 +1197,9 @@ void expand_read_id_list(struct ZHashTable *hashtable)
     free(j.tabs);
     g_times.expand_ms = now_ms() - t;
     g_times.expand_nodes = j.nodes;
-    if (getenv("KBH_TRACE"))
-        fprintf(stderr, "{\"expand_ms\": %.3f, \"expand_nodes\": %llu}\n", g_times.expand_ms,
-                (unsigned long long)j.nodes);
+    if (getenv("KBH_TRACE")) /* (t_end_s: CLOCK_MONOTONIC, so a parent can time what follows) */
+        fprintf(stderr, "{\"expand_ms\": %.3f, \"expand_nodes\": %llu, \"t_end_s\": %.6f}\n", g_times.expand_ms,
+                (unsigned long long)j.nodes, now_ms() * 1e-3);
 }
 
 struct ZHashTable *kbh_finish_unpruned(struct ZHashTable *hash_table) { return finish(hash_table, 0); }

@@ -82,7 +82,8 @@ class kb_timing(C.Structure):
                 ("max_depth", C.c_uint32), ("overflow_redos", C.c_uint32), ("prefiltered", C.c_uint64),
                 ("long_lists", C.c_uint32), ("clustered_lists", C.c_uint32),
                 ("split_mmers", C.c_uint32), ("tail_reruns", C.c_uint32),
-                ("light_prefilter_bins", C.c_uint32)]
+                ("light_prefilter_bins", C.c_uint32), ("ranked_bins", C.c_uint32),
+                ("bitmap_partitions", C.c_uint32)]
 
 
 _lib = None

@@ -132,6 +132,10 @@ typedef struct {
                                after all (a heavy bin published, lists queued) */
     uint32_t light_prefilter_bins; /* two-word keys: bins kept light by the
                                singleton pre-filter (an LDS sketch per bin) */
+    uint32_t ranked_bins;   /* bins whose records were ranked by call ordinal
+                               (long lists: the last finalize's mean >= 64) */
+    uint32_t bitmap_partitions; /* partitions whose lists were emitted from
+                               per-key bitmaps over the ranks (no sort) */
 } kb_timing;
 
 /* Create a context (kb_create replaces zcreate_hash_table for the level-1

@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r4g3; mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_parity.py \
-  tests/test_gpu_capacity.py -k "light_prefilter or singleton_prefilter or c5_singleton" -m gpu > $O/tests.txt 2>&1 || exit 1
+  tests/test_gpu_capacity.py -k "light_prefilter or c5_singleton" -m gpu > $O/tests.txt 2>&1 || exit 1
 NOX="--cpu-sample 0 --no-capacity --no-host-input"
 timeout -k 10 400 python -u bench.py $NOX --workload c5 --steps 2 --warmup 1 --digest > $O/c5_light.json 2> $O/c5_light.err || exit 1
 KB_BIN_PF_LIGHT=0 timeout -k 10 400 python -u bench.py $NOX --workload c5 --steps 2 --warmup 1 --digest > $O/c5_flat.json 2> $O/c5_flat.err || exit 1
