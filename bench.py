@@ -499,6 +499,8 @@ def main():
                     help="fresh: every step bins new reads of the same genome (all sets generated before "
                          "timing); replay: the same reads every step; auto: fresh when the sets fit in "
                          "5%% of the HBM")
+    ap.add_argument("--host-input", dest="host_input", action="store_true", default=True,
+                    help=argparse.SUPPRESS)  # (the host leg is on by default; kept for older command lines)
     ap.add_argument("--no-host-input", dest="host_input", action="store_false",
                     help="N=1: skip the host-ingest leg (kb_submit of host ASCII, finalize, kb_export, "
                          "H2D and D2H reported separately; on by default)")

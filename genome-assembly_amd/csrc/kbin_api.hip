@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <ctime>
 #include <cstdarg>
@@ -49,7 +50,9 @@ static int fail(int code, const char* fmt, ...) {
                         #expr, hipGetErrorString(_e), __FILE__, __LINE__);                \
     } while (0)
 
-static double g_alloc_ms = 0;  // (KB_DEBUG) host time in DevBuf allocations since the last report
+// (KB_DEBUG) host time in DevBuf allocations since the last report; per host
+// thread (a multi-GPU group drives its contexts from one thread each)
+static thread_local double g_alloc_ms = 0;
 static double alloc_now_ms() {
     timespec t;
     clock_gettime(CLOCK_MONOTONIC, &t);
@@ -412,15 +415,15 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
         // size on first use (milliseconds, once per process and device): a
         // map-sized warm-up copy here keeps it out of the first finalize; so
         // does resolving the kernels (load_bin_kernels)
-        static bool warm[64] = {};
-        if (p.device >= 0 && p.device < 64 && !warm[p.device]) {
+        static std::atomic<bool> warm[64] = {};  // (contexts of several devices may be created concurrently)
+        if (p.device >= 0 && p.device < 64 && !warm[p.device].load(std::memory_order_acquire)) {
             DevBuf<uint8_t> t;
             const uint64_t nb = half * sizeof(uint32_t);
             if (t.ensure_exact(nb) == hipSuccess &&
                 hipMemcpyAsync(t.p, c->map_stage.p, nb, hipMemcpyHostToDevice, c->s) == hipSuccess &&
                 hipStreamSynchronize(c->s) == hipSuccess &&
                 (getenv("KB_PRELOAD") && atoi(getenv("KB_PRELOAD")) == 0 ? true : load_bin_kernels() == hipSuccess))
-                warm[p.device] = true;
+                warm[p.device].store(true, std::memory_order_release);
             t.release();
         }
     }
@@ -1900,8 +1903,13 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         h.K = c->p.K;
         h.M = M;
         // large passes estimate from the bins of 1/8 of the mmers (whole bins:
-        // the ratio of a sample of bins, 1/8 of the expansion work)
-        const uint32_t sample = R >= (1u << 20) && max_bins >= 256 ? (uint32_t)std::max(1, env_int("KB_BIN_HLL_SAMPLE", 8)) : 1u;
+        // the ratio of a sample of bins, 1/8 of the expansion work) -- when the
+        // pass holds enough mmers for the sample to be a fair one: at least 64
+        // sampled of the canonical mmers a partition expects; received records
+        // (one rank's share of the mmers, unknown here) are never sampled
+        const uint32_t sample_div = (uint32_t)std::max(1, env_int("KB_BIN_HLL_SAMPLE", 8));
+        const uint64_t mm_expect = (1ull << (2 * M - 1)) / std::max<uint32_t>(1u, c->part_n);
+        const uint32_t sample = R >= (1u << 20) && !received && mm_expect / sample_div >= 64 ? sample_div : 1u;
         // (registers, the u64 occurrence count, then the estimate: read by the
         // bin kernel from device memory -- the host never waits for it; the
         // finalize's own distinct count replaces it afterwards)
