@@ -403,7 +403,7 @@ def path_counters(passes):
     """which bin-phase paths the passes took (kb_timing path counters, summed)"""
     keys = ("n_bins", "split_mmers", "heavy_bins", "split_bins", "partitions", "offset_partitions",
             "flat_partitions", "overflow_redos", "prefiltered", "long_lists", "clustered_lists",
-            "tail_reruns")
+            "tail_reruns", "light_prefilter_bins", "ranked_bins", "bitmap_partitions")
     out = {k: int(sum(int(t.get(k, 0)) for _, t in passes)) for k in keys}
     out["max_depth"] = int(max(int(t.get("max_depth", 0)) for _, t in passes))
     return out

@@ -284,6 +284,7 @@ struct kb_ctx {
     uint8_t ocut[5][17] = {};  // offset partitions' ranges (offset_cuts)
     float rho = 0.f;           // learned distinct / occurrences
     float rho_tab = 0.f;       // learned table keys / occurrences under the singleton pre-filter
+    bool pfl_regime = false;   // (sticky) a finalize ran light pre-filtered bins: sub-bins sized for the sketch
     DevBuf<uint32_t> hll;      // cold pass: HyperLogLog registers (launch_hll)
     bool bucket_failed = false;  // a bucket overflowed its mmer map: radix path from now on
     bool prior_off = false;      // a prior map overflowed a bucket: hash routing for first passes
@@ -1230,7 +1231,11 @@ static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
     int bmax = std::min<int>((int)SUB_MAX_B, std::max(0, env_int("KB_BIN_SUB", (int)SUB_MAX_B)));
     if (!sub_room(c->p.K, c->p.M, 2 * c->KW)) bmax = 0;  // (no spare span bits for the stamp)
     const double ts = c->KW == 1 ? 8192.0 : 4096.0;
-    const double cap = ts * std::min(4.0, std::max(0.2, env_int("KB_BIN_SUB_FILL_PCT", 80) / 100.0));
+    double cap = ts * std::min(4.0, std::max(0.2, env_int("KB_BIN_SUB_FILL_PCT", 80) / 100.0));
+    // light pre-filtered bins (two-word keys, singleton-heavy): a sub-bin's
+    // distinct keys only have to load the bin's sketch lightly (PFL_LOAD of
+    // its PFL_CELLS); the table holds the keys seen twice
+    if (c->KW == 2 && c->pfl_regime) cap = std::max(cap, PFL_LOAD * (double)PFL_CELLS);
     uint32_t b = 0;
     while ((int)b < bmax && (keys / (double)(1u << (2 * b)) > cap || w / (double)(1u << (2 * b)) > 1.5 * mean)) b++;
     return b;
@@ -1240,7 +1245,10 @@ static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
 // sub-bins of the split ones (bmap_build keeps within it)
 static uint64_t bin_budget(const kb_ctx* c, uint32_t NB) {
     const uint64_t half = 1ull << (2 * c->p.M - 1);
-    const uint64_t per_bucket = (uint64_t)std::min(120, std::max(0, env_int("KB_BIN_SUB_EXTRA", 48)));
+    // (at most 240: a bucket orders up to BK_SLOTS = 256 bins, one per mmer plus its extra sub-bins)
+    // (the light pre-filtered regime splits every heavy mmer ~64 ways: a larger budget)
+    const uint64_t per_bucket =
+        (uint64_t)std::min(240, std::max(0, env_int("KB_BIN_SUB_EXTRA", c->pfl_regime ? 160 : 48)));
     return half + (sub_room(c->p.K, c->p.M, 2 * c->KW) ? per_bucket * NB : 0ull);
 }
 
@@ -1316,7 +1324,7 @@ static int bmap_build(kb_ctx* c, uint32_t NB, double rho, bool prior = false) {
     if (!prior || env_int("KB_BIN_PRIOR_LPT", 0))
         std::sort(items.begin(), items.end(), [](const Item& a, const Item& b) { return a.w > b.w; });
     const double tb2 = now_ms();
-    // longest processing time first onto the least loaded bucket; at most 128
+    // longest processing time first onto the least loaded bucket; at most 248
     // bins per bucket (bucket_kernel maps 256).  A binary min-heap of packed
     // (load in 1/16 records << 11 | bucket) words: one compare per level, the
     // top replaced in place (no pop + push)
@@ -1340,7 +1348,7 @@ static int bmap_build(kb_ctx* c, uint32_t NB, double rho, bool prior = false) {
     for (size_t k = 0; serp && k < items.size(); k++) {
         const Item& it = items[k];
         const uint32_t r = (uint32_t)(k / NB), q = (uint32_t)(k % NB);
-        const uint32_t b = (r & 1u) ? NB - 1u - q : q;  // (at most ceil(items / NB) <= 128 per bucket)
+        const uint32_t b = (r & 1u) ? NB - 1u - q : q;  // (at most ceil(items / NB) <= 248 per bucket)
         if (it.sub == ~0u) h[it.mm - half] = b;
         else subs[(h[it.mm - half] & 0x0FFFFFFFu) + it.sub] = (uint16_t)b;
         nm[b]++;
@@ -1348,7 +1356,7 @@ static int bmap_build(kb_ctx* c, uint32_t NB, double rho, bool prior = false) {
     }
     for (const Item& it : items) {
         if (serp) break;
-        while (hn > 1 && nm[heap[0] & 2047u] >= 128) {  // full: retire it
+        while (hn > 1 && nm[heap[0] & 2047u] >= 248) {  // full: retire it
             std::swap(heap[0], heap[--hn]);  // (kept past the heap: its load still counts)
             sift(0);
         }
@@ -2069,6 +2077,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             a.pf = pf_ok && (pf_env == 1 || (pf_env < 0 && c->rho >= 0.3f && c->rho_tab > 0.f)) ? 1u : 0u;
             a.rho_tab = c->rho_tab > 0.f ? c->rho_tab : a.rho;
             a.pf_light = a.pf && KW == 2 && env_int("KB_BIN_PF_LIGHT", 1) != 0 ? 1u : 0u;
+            if (a.pf_light) c->pfl_regime = true;  // (the next maps split for the sketch)
             a.tab_keys = reinterpret_cast<unsigned long long*>(c->totals.p + 11);
         }
         if (attempt) HIPCHK(hipMemsetAsync(c->pstat.p, 0, KB_PSTAT * sizeof(unsigned long long), c->s));

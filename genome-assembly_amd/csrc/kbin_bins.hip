@@ -1015,8 +1015,8 @@ struct BinTable {
 // leaves room), screens the sweeps: a k-mer whose cell was hit once is the
 // only occurrence of its key -- count 1 <= cutoff, counted as one distinct key,
 // never inserted or staged.  Exact, as for the flat bins' sketch.
-constexpr uint32_t PFL_WORDS = 8192;       // 32 KiB: 131072 cells
-constexpr double PFL_LOAD = 0.15;          // at most this many distinct keys per cell
+constexpr uint32_t PFL_WORDS = PFL_CELLS / 16u;  // 32 KiB: 131072 two-bit cells
+// (PFL_LOAD, kbin_internal.h: at most this many distinct keys per cell)
 DEV uint32_t sk_cell(const TKey<1>& k, uint32_t cells);
 DEV uint32_t sk_cell(const TKey<2>& k, uint32_t cells);
 
@@ -1174,7 +1174,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
                 key[u] = sp.key(K, fl);
                 sp.step();
                 take[u] = (uint32_t)(j + u - ja) < (uint32_t)nl && (l == 0 || (key[u].part() & pmask) == p);
-                if (psk && take[u]) {
+                if (KW == 2 && psk && take[u]) {
                     const uint32_t q = sk_cell(key[u], PFL_WORDS * 16u);
                     if (!((psk[q >> 4] >> (2u * (q & 15u) + 1u)) & 1u)) {
                         take[u] = false;
@@ -1200,7 +1200,7 @@ DEV void for_each_kmer(const BinArgs& A, uint32_t lo, uint32_t hi, uint32_t p, u
         }
     }
     if (fill) flush(fill);
-    if (psk) {
+    if (KW == 2 && psk) {
         const uint32_t ws = wave_sum_u32(singles);
         if (lane == 0 && ws) atomicAdd(nsingle, ws);
     }
@@ -1456,31 +1456,47 @@ constexpr uint32_t RANK_MIN = 512;    // fewer records: lists short, nothing to 
 constexpr uint32_t RANK_NBK = 1024;   // ordinal buckets of the ranking
 constexpr uint32_t RANK_TILE = 2048;  // ranks whose ordinals are staged in LDS at once (emission)
 constexpr uint32_t RANK_GROUPS = 8;   // most passes over the stage (entries whose bitmaps fit at once)
+constexpr uint32_t RANK_LONG = 256;   // ranked bins: lists longer than this take the bitmaps
+constexpr uint32_t LONGB = 0x40000000u;  // cnt of a ranked bin's kept long list: LONGB | cursor (< PRUNED)
 
 // rank of every record of the bin [lo, hi) by descending call ordinal (ties
 // by record index): bucket the ordinals (LDS histogram over their range,
-// largest first), scatter (ordinal, index) pairs by bucket, and count each
+// largest first), scatter the record indices by bucket, and count each
 // record's predecessors inside its bucket.  rrank[r] = rank of record r,
-// rord[lo + k] = ordinal of rank k.  lds: RANK_NBK + 2 (hi - lo) words,
-// everything past BinShared (the table and rings are not live yet)
-DEV void bin_ranks(const BinArgs& A, BinShared& S, uint32_t lo, uint32_t hi, uint32_t* lds) {
+// rord[lo + k] = ordinal of rank k.  lds: RANK_NBK + R ordinals + R 16-bit
+// indices (6 R + 4 KiB bytes), everything past BinShared (the table and
+// rings are not live yet)
+DEV void bin_ranks(const uint64_t* __restrict__ hdr, uint32_t* __restrict__ rrank, uint32_t* __restrict__ rord,
+                   BinShared& S, uint32_t lo, uint32_t hi, uint32_t* lds) {
     const uint32_t tid = threadIdx.x, R = hi - lo;
-    uint32_t* hist = lds;
-    uint64_t* pr = reinterpret_cast<uint64_t*>(lds + RANK_NBK);
+    uint32_t* hist = lds;              // [RANK_NBK] counts, then bucket ends
+    uint32_t* ordv = lds + RANK_NBK;   // [R] ordinal of record index i
+    uint16_t* pidx = reinterpret_cast<uint16_t*>(ordv + R);  // [R] record indices by bucket
     if (tid == 0) {
         S.rk_min = 0xFFFFFFFFu;
         S.rk_max = 0;
     }
     for (uint32_t i = tid; i < RANK_NBK; i += BIN_THREADS) hist[i] = 0;
-    __syncthreads();
     uint32_t mn = 0xFFFFFFFFu, mx = 0;
-    for (uint32_t i = tid; i < R; i += BIN_THREADS) {
-        const uint32_t o = (uint32_t)rec_hdr(A, lo + i);
-        mn = min(mn, o);
-        mx = max(mx, o);
+    for (uint32_t i0 = tid; i0 < R; i0 += 4u * BIN_THREADS) {  // (four header loads in flight)
+        uint32_t o[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + (uint32_t)u * BIN_THREADS;
+            o[u] = i < R ? (uint32_t)hdr[2 * (uint64_t)(lo + i)] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + (uint32_t)u * BIN_THREADS;
+            if (i >= R) continue;
+            ordv[i] = o[u];
+            mn = min(mn, o[u]);
+            mx = max(mx, o[u]);
+        }
     }
     mn = ~wave_max_u32(~mn);
     mx = wave_max_u32(mx);
+    __syncthreads();
     if ((tid & 63u) == 0) {
         atomicMin(&S.rk_min, mn);
         atomicMax(&S.rk_max, mx);
@@ -1489,81 +1505,106 @@ DEV void bin_ranks(const BinArgs& A, BinShared& S, uint32_t lo, uint32_t hi, uin
     const uint32_t omax = S.rk_max;
     const uint64_t span = (uint64_t)(omax - S.rk_min) + 1ull;
     auto bucket = [&](uint32_t o) { return (uint32_t)(((uint64_t)(omax - o) * RANK_NBK) / span); };
-    for (uint32_t i = tid; i < R; i += BIN_THREADS) atomicAdd(&hist[bucket((uint32_t)rec_hdr(A, lo + i))], 1u);
+    for (uint32_t i = tid; i < R; i += BIN_THREADS) atomicAdd(&hist[bucket(ordv[i])], 1u);
     __syncthreads();
     uint64_t tot;
     const uint32_t h = tid < RANK_NBK ? hist[tid] : 0u;
     const uint32_t start = (uint32_t)block_excl_scan_u64(h, S.red, tot);
     if (tid < RANK_NBK) hist[tid] = start;  // cursor (then the bucket's end)
     __syncthreads();
-    for (uint32_t i = tid; i < R; i += BIN_THREADS) {
-        const uint32_t o = (uint32_t)rec_hdr(A, lo + i);
-        pr[atomicAdd(&hist[bucket(o)], 1u)] = ((uint64_t)o << 32) | i;
-    }
+    for (uint32_t i = tid; i < R; i += BIN_THREADS) pidx[atomicAdd(&hist[bucket(ordv[i])], 1u)] = (uint16_t)i;
     __syncthreads();
-    for (uint32_t p = tid; p < R; p += BIN_THREADS) {
-        const uint64_t x = pr[p];
-        const uint32_t o = (uint32_t)(x >> 32), idx = (uint32_t)x, b = bucket(o);
+    for (uint32_t i = tid; i < R; i += BIN_THREADS) {
+        const uint32_t o = ordv[i], b = bucket(o);
         const uint32_t b0 = b ? hist[b - 1] : 0u, b1 = hist[b];
         uint32_t rank = b0;
         for (uint32_t q = b0; q < b1; q++) {
-            const uint64_t y = pr[q];
-            const uint32_t yo = (uint32_t)(y >> 32);
-            rank += (yo > o || (yo == o && (uint32_t)y < idx)) ? 1u : 0u;
+            const uint32_t j = pidx[q], oj = ordv[j];
+            rank += (oj > o || (oj == o && j < i)) ? 1u : 0u;
         }
-        A.rrank[lo + idx] = rank;
-        A.rord[lo + rank] = o;
+        rrank[lo + i] = rank;
+        rord[lo + rank] = o;
     }
     __syncthreads();  // (the ranks go out to HBM before sweep 1 reads them; the LDS is the table's next)
 }
 
-// A ranked partition's lists from bitmaps: every kept key gets a bitmap over
-// the bin's R ranks; each staged occurrence (slot, rank) sets its bit (a bit
-// already set -- the same record holding the key twice -- aborts: false, cnt
-// restored, the caller takes the cursor path); then each list is emitted in
-// rank order (descending ordinal = reverse call order) by one wave, 64 ranks
-// per step, the ordinals of a rank tile staged in LDS.  Entries are handled
-// in groups whose bitmaps fit the window area, one stage pass per group.
+// A ranked partition's LONG lists (> RANK_LONG ids; their slots hold LONGB |
+// cursor, their entries follow the short ones) from bitmaps: every long key
+// gets a bitmap over the bin's R ranks; each staged occurrence (slot, rank)
+// sets its bit (a bit already set -- the same record holding the key twice --
+// aborts: false, the slots' cursors restored, the caller takes the cursor
+// path); then each list is emitted in rank order (descending ordinal =
+// reverse call order, binning.c:1061-1068) by one wave, 64 ranks per step
+// (ballot + mbcnt give the positions), the ordinals of a rank tile staged in
+// LDS.  Keys are handled in groups whose bitmaps fit the window area, one
+// stage pass per group.
 template <int KW>
-DEV bool bitmap_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t ts, uint32_t* win, uint32_t win_cap,
-                      uint32_t ns, unsigned long long e0, unsigned long long i0, uint32_t n_ent, uint32_t e_mine,
-                      const uint32_t* so, const uint16_t* ss, uint32_t R, const uint32_t* rord_bin) {
+DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __restrict__ e_cnt, int32_t* __restrict__ ids_out,
+                                          const int32_t* __restrict__ read_ids, uint32_t id_off, BinShared& S,
+                                          uint32_t* cnt, uint32_t ts, uint32_t* win, uint32_t win_cap, uint32_t ns,
+                                          unsigned long long e0, unsigned long long i0, uint32_t n_long, uint32_t e_base,
+                                          uint32_t e_mine, const uint32_t* so, const uint16_t* ss, uint32_t R,
+                                          const uint32_t* rord_bin) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t per = ts / BIN_THREADS, W = (R + 31u) / 32u;
-    uint32_t* offs = win;                  // [n_ent] next position of each list (relative to i0)
-    uint32_t* tile = offs + ((n_ent + 3u) & ~3u);  // [RANK_TILE] ordinals of the current ranks
+    uint32_t* offs = win;                  // [n_long] next position of each list (relative to i0)
+    uint32_t* tile = offs + ((n_long + 3u) & ~3u);  // [RANK_TILE] ordinals of the current ranks
     uint32_t* bm = tile + RANK_TILE;       // [G * W] the group's bitmaps
     const uint32_t G = (win_cap - (uint32_t)(bm - win)) / W;
-    // kept slot -> entry index (the prune's scan order), its list start
+    auto is_long = [](uint32_t c) { return (c & (LONGB | PRUNED)) == LONGB; };
+    // long slot -> LONGB | long-entry index (the prune's scan order), its list start
     {
         uint32_t e = e_mine;
         for (uint32_t k = 0; k < per; k++) {
             const uint32_t i = tid + k * BIN_THREADS, c = cnt[i];
-            if (c < PRUNED) {
-                offs[e] = c;
-                cnt[i] = e++;
+            if (is_long(c)) {
+                offs[e] = c & ~LONGB;
+                cnt[i] = LONGB | e++;
             }
         }
     }
-    for (uint32_t g0 = 0; g0 < n_ent; g0 += G) {
-        const uint32_t g1 = min(n_ent, g0 + G);
+    for (uint32_t g0 = 0; g0 < n_long; g0 += G) {
+        const uint32_t g1 = min(n_long, g0 + G);
         for (uint32_t i = tid; i < (g1 - g0) * W; i += BIN_THREADS) bm[i] = 0;
         if (tid == 0) S.dup = 0;
         __syncthreads();
-        for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
-            const uint32_t sl = ss[i];
-            if (!sl) continue;
-            const uint32_t e = cnt[sl - 1u];
-            if (e < g0 || e >= g1) continue;  // (pruned slots hold PRUNED)
-            const uint32_t r = so[i], bit = 1u << (r & 31u);
-            if (atomicOr(&bm[(e - g0) * W + (r >> 5)], bit) & bit) S.dup = 1;
+        // (BL occurrences' stage loads in flight per thread; the bits go in
+        // with non-returning atomics -- a bit set twice shows as a bitmap
+        // holding fewer bits than its key's count, checked below)
+        constexpr int BL = 4;
+        for (uint32_t j0 = tid; j0 < ns; j0 += (uint32_t)BL * BIN_THREADS) {
+            uint32_t vs[BL], vr[BL];
+#pragma unroll
+            for (int u = 0; u < BL; u++) {
+                const uint32_t i = j0 + (uint32_t)u * BIN_THREADS;
+                vs[u] = i < ns ? (uint32_t)ss[i] : 0u;
+                vr[u] = i < ns ? so[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < BL; u++) {
+                if (!vs[u]) continue;
+                const uint32_t c = cnt[vs[u] - 1u];
+                if (!is_long(c)) continue;
+                const uint32_t e = c & ~LONGB;
+                if (e < g0 || e >= g1) continue;
+                __hip_atomic_fetch_or(&bm[(e - g0) * W + (vr[u] >> 5)], 1u << (vr[u] & 31u), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
         __syncthreads();
-        if (S.dup) {  // uniform: back to the cursors (every list restarts; ids are rewritten)
+        // every bitmap holds exactly its key's count of bits (one per occurrence)
+        for (uint32_t e = g0 + wid; e < g1; e += BIN_WAVES) {
+            uint32_t pc = 0;
+            for (uint32_t w = lane; w < W; w += 64u) pc += (uint32_t)__popc(bm[(e - g0) * W + w]);
+            pc = wave_sum_u32(pc);
+            if (lane == 0 && pc != e_cnt[e0 + e_base + e]) S.dup = 1;
+        }
+        __syncthreads();
+        if (S.dup) {  // uniform: back to the cursors (every long list restarts; its ids are rewritten)
             uint32_t e = e_mine;
             for (uint32_t k = 0; k < per; k++) {
                 const uint32_t i = tid + k * BIN_THREADS;
-                if (cnt[i] < PRUNED) cnt[i] = (uint32_t)(A.e_off[e0 + e++] - i0);
+                if (is_long(cnt[i])) cnt[i] = LONGB | (uint32_t)(e_off[e0 + e_base + e++] - i0);
             }
             __syncthreads();
             return false;
@@ -1589,7 +1630,7 @@ DEV bool bitmap_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t ts
                         const bool on = (x[u] >> (r & 31u)) & 1u;
                         const uint64_t m = __ballot(on);
                         if (on)
-                            A.ids_out[i0 + run + lanes_below(m)] = id_of(tile[c0 + 64u * u + lane], A.read_ids, A.id_off);
+                            ids_out[i0 + run + lanes_below(m)] = id_of(tile[c0 + 64u * u + lane], read_ids, id_off);
                         run += (uint32_t)__popcll(m);
                     }
                 }
@@ -1601,7 +1642,10 @@ DEV bool bitmap_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t ts
     return true;
 }
 
-template <int KW, int PHASE>
+// RANKED: the variant of bin_kernel that ranks bins (BinArgs::rank_mode); the
+// plain one compiles none of that code, so the sweeps' register allocation
+// is not taxed by it
+template <int KW, int PHASE, bool RANKED = false>
 DEV void bin_body(const BinArgs& A) {
     constexpr uint32_t Q = bin_q<KW>();
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -1879,13 +1923,13 @@ DEV void bin_body(const BinArgs& A) {
         // ranked bin (long lists expected): records ranked by call ordinal,
         // the stage holds ranks (see bitmap_lists)
         bool rmode = false;
-        if (PHASE == 0 && A.rank_mode && !flat && !split) {
+        if (RANKED && PHASE == 0 && A.rank_mode && !flat && !split) {
             const uint32_t words = TS + 2u * KW * TS + (uint32_t)BIN_WAVES * Q * (8u * KW + 6u) / 4u;
             const uint32_t R = hi - lo;
-            rmode = R >= RANK_MIN && RANK_NBK + 2u * R <= words;
+            rmode = R >= RANK_MIN && R <= 65536u && RANK_NBK + R + (R + 1u) / 2u <= words;
             if (rmode) {
                 bar_lds(A);
-                bin_ranks(A, S, lo, hi, cnt);
+                bin_ranks(A.hdr, A.rrank, A.rord, S, lo, hi, cnt);
                 if (tid == 0 && A.pstat) atomicAdd(&A.pstat[9], 1ull);
             }
         }
@@ -2164,7 +2208,9 @@ DEV void bin_body(const BinArgs& A) {
             // ---- prune (binning.c:1094-1102) + CSR allocation.  Thread t owns
             // slots t, t + 1024, ...: a wave's reads of the table are consecutive
             // words (owning 8 adjacent slots put 16 lanes on one LDS bank)
-            uint64_t mine = 0;  // (ids << 32) | entries over this thread's slots
+            // (a ranked bin's lists longer than RANK_LONG get entries and ids
+            // of their own after the short ones: bitmap_lists emits them)
+            uint64_t mine = 0, mine_l = 0;  // (ids << 32) | entries over this thread's slots: short, long
             uint32_t allc = 0;  // every key's count, kept or not
             const uint32_t per = ts / BIN_THREADS;  // ts >= BIN_THREADS
             for (uint32_t k = 0; k < per; k++) {
@@ -2172,13 +2218,18 @@ DEV void bin_body(const BinArgs& A) {
                 const uint32_t c = cnt[i];
                 if (T.ca[i]) {
                     allc += c;
-                    if (c > A.keep_gt) mine += ((uint64_t)c << 32) + 1ull;
+                    if (c > A.keep_gt) {
+                        if (rmode && c > RANK_LONG) mine_l += ((uint64_t)c << 32) + 1ull;
+                        else mine += ((uint64_t)c << 32) + 1ull;
+                    }
                 }
             }
             allc = wave_sum_u32(allc);
             if ((tid & 63u) == 0 && allc) atomicAdd(&S.sumc, allc);
-            uint64_t tot;
-            uint64_t ex = block_excl_scan_u64(mine, S.red, tot, A.ldsbar != 0);
+            uint64_t tot_s, tot_l = 0, ex_l = 0;
+            uint64_t ex = block_excl_scan_u64(mine, S.red, tot_s, A.ldsbar != 0);
+            if (rmode) ex_l = block_excl_scan_u64(mine_l, S.red, tot_l, A.ldsbar != 0);  // (uniform)
+            const uint64_t tot = tot_s + tot_l;  // (both fields < 2^32)
             if (tid == 0) {
                 const uint32_t ne = (uint32_t)tot, ni = (uint32_t)(tot >> 32);
                 atomicAdd(&A.gcount[2], (unsigned long long)(S.n_keys + S.n_single));  // distinct before prune
@@ -2205,16 +2256,19 @@ DEV void bin_body(const BinArgs& A) {
             bar_lds(A);
             const unsigned long long e0 = S.e0, i0 = S.i0;
             const bool room = !(e0 + (uint32_t)tot > A.max_entries || i0 + (uint32_t)(tot >> 32) > A.max_ids);
-            uint32_t mc = 0;  // (the longest kept list: the LDS windows hold whole lists)
+            uint32_t mc = 0;  // (the longest kept short list: the LDS windows hold whole lists)
             {
                 uint32_t e = (uint32_t)ex, off = (uint32_t)(ex >> 32);
+                uint32_t el = (uint32_t)tot_s + (uint32_t)ex_l, offl = (uint32_t)(tot_s >> 32) + (uint32_t)(ex_l >> 32);
                 for (uint32_t k = 0; k < per; k++) {
                     const uint32_t i = tid + k * BIN_THREADS;
                     const uint32_t c = cnt[i];
                     if (T.ca[i] && c > A.keep_gt) {
-                        mc = max(mc, c);
+                        const bool lg = rmode && c > RANK_LONG;
+                        if (!lg) mc = max(mc, c);
+                        const uint32_t ee = lg ? el : e, oo = lg ? offl : off;
                         if (room) {
-                            const uint64_t ge = e0 + e;
+                            const uint64_t ge = e0 + ee;
                             TKey<KW> key;
                             key.a = T.ca[i];
                             if constexpr (KW == 2) key.b = T.cb[i];
@@ -2224,12 +2278,18 @@ DEV void bin_body(const BinArgs& A) {
                             if constexpr (KW == 2) A.e_hi[ge] = khi;  // (one-word keys: kept zero, finalize_binned)
                             A.e_lo[ge] = klo;
                             A.e_cnt[ge] = c;
-                            A.e_off[ge] = i0 + off;
+                            A.e_off[ge] = i0 + oo;
                         }
                         if (A.e_first) T.ca[i] = ~0ull;  // first occurrence (min) from sweep 2 on
-                        cnt[i] = off;  // cursor (relative to i0)
-                        e++;
-                        off += c;
+                        if (lg) {
+                            cnt[i] = LONGB | offl;  // cursor (relative to i0) of a long list
+                            el++;
+                            offl += c;
+                        } else {
+                            cnt[i] = off;  // cursor (relative to i0)
+                            e++;
+                            off += c;
+                        }
                     } else {
                         cnt[i] = PRUNED;
                     }
@@ -2240,19 +2300,55 @@ DEV void bin_body(const BinArgs& A) {
             __syncthreads();
             PROF_MARK(3);
             if (!room) continue;
-            const uint32_t n_ent = (uint32_t)tot, n_ids = (uint32_t)(tot >> 32);
-            // a ranked partition with long lists: emitted from bitmaps over the
-            // ranks when they fit the window area in at most RANK_GROUPS groups
-            if (rmode && n_ent && n_ids >= 32u * n_ent) {
+            const uint32_t n_ent_all = (uint32_t)tot;
+            const uint32_t n_ent = (uint32_t)tot_s, n_ids = (uint32_t)(tot_s >> 32);  // the short lists
+            // a ranked partition's long lists: from bitmaps over the ranks when
+            // they fit the window area in at most RANK_GROUPS groups, else (or on
+            // a key seen twice in one record) ordinals at their cursors and the
+            // list kernels; then their slots leave the short lists' way
+            if (n_ent_all > n_ent) {
+                const uint32_t n_long = n_ent_all - n_ent;
                 const uint32_t R = hi - lo, W = (R + 31u) / 32u;
-                const uint32_t fixed = ((n_ent + 3u) & ~3u) + RANK_TILE;
+                const uint32_t fixed = ((n_long + 3u) & ~3u) + RANK_TILE;
                 const uint32_t G = fixed + W <= win_cap ? (win_cap - fixed) / W : 0u;
-                if (G && (n_ent + G - 1u) / G <= RANK_GROUPS &&
-                    bitmap_lists<KW>(A, S, cnt, ts, win, win_cap, S.n_stage, e0, i0, n_ent, (uint32_t)ex, sp_ord,
-                                     sp_slot, R, A.rord + lo)) {
+                const bool bm_ok = G && (n_long + G - 1u) / G <= RANK_GROUPS &&
+                                   bitmap_lists<KW>(A.e_off, A.e_cnt, A.ids_out, A.read_ids, A.id_off, S, cnt, ts, win, win_cap,
+                                                    S.n_stage, e0, i0, n_long, n_ent, (uint32_t)ex_l, sp_ord, sp_slot,
+                                                    R, A.rord + lo);
+                if (bm_ok) {
                     if (tid == 0 && A.pstat) atomicAdd(&A.pstat[10], 1ull);
-                    continue;
+                } else {
+                    // ranks at their cursors, then the long lists' id range mapped
+                    // to ordinals in one coalesced pass (no gather inside the
+                    // atomics' dependent chain)
+                    const uint32_t ns = S.n_stage;
+                    for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
+                        const uint32_t sl = sp_slot[i];
+                        if (!sl || (cnt[sl - 1u] & (LONGB | PRUNED)) != LONGB) continue;
+                        const uint32_t pos = atomicAdd(&cnt[sl - 1u], 1u) & ~LONGB;
+                        A.ids_ord[i0 + pos] = sp_ord[i];
+                    }
+                    __syncthreads();
+                    const uint32_t l0i = (uint32_t)(tot_s >> 32), l1i = (uint32_t)(tot >> 32);
+                    for (uint32_t k = l0i + tid; k < l1i; k += BIN_THREADS)
+                        A.ids_ord[i0 + k] = A.rord[lo + A.ids_ord[i0 + k]];
+                    if (A.lq_items && tid == 0) {
+                        const uint32_t nit = (n_long + 255u) / 256u;
+                        const unsigned long long q = atomicAdd(A.lq_n, (unsigned long long)nit);
+                        for (uint32_t k = 0; k < nit; k++)
+                            if (q + k < A.lq_cap)
+                                A.lq_items[q + k] =
+                                    ((e0 + n_ent + 256ull * k) << 16) | (uint64_t)min(256u, n_long - 256u * k);
+                    }
                 }
+                __syncthreads();
+                for (uint32_t k = 0; k < per; k++) {
+                    const uint32_t i = tid + k * BIN_THREADS;
+                    if ((cnt[i] & (LONGB | PRUNED)) == LONGB) cnt[i] = PRUNED;
+                }
+                __threadfence_block();
+                __syncthreads();
+                if (!n_ent) continue;
             }
             // LDS id windows for short lists (mean <= 64 ids): light bins, and
             // the heavy bins' unfiltered partitions with one-word keys (C4
@@ -2342,7 +2438,13 @@ DEV void bin_body(const BinArgs& A) {
 // phase 0: every light bin, and each heavy bin's flat lists
 template <int KW>
 __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
-    bin_body<KW, 0>(A);
+    bin_body<KW, 0, false>(A);
+}
+
+// phase 0 with ranked bins (the long-list regime)
+template <int KW>
+__global__ __launch_bounds__(BIN_THREADS) void bin_kernel_ranked(BinArgs A) {
+    bin_body<KW, 0, true>(A);
 }
 
 // phase 1: the heavy bins' partitions, any block any partition
@@ -4227,7 +4329,8 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     if (e != hipSuccess) return e;
     // timing: the kernel's own start and stop (hipExtLaunchKernelGGL) -- an
     // event recorded on the stream before and after it idled the GPU ~6 us each
-    hipExtLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS),
+    hipExtLaunchKernelGGL(a.rank_mode ? bin_kernel_ranked<KW> : bin_kernel<KW>,
+                          dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS),
                           (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr, ev_bin ? ev_bin[1] : nullptr, 0u, a2);
     e = hipGetLastError();
     if (e != hipSuccess || !heavy) return e;
@@ -4339,6 +4442,7 @@ hipError_t load_bin_kernels() {
         (const void*)bucket_bases_kernel, (const void*)bucket_stats_kernel, (const void*)bins_order_kernel,
         (const void*)bins_desc_kernel, (const void*)bins_plan_kernel, (const void*)hll_kernel<1>, (const void*)hll_kernel<2>,
         (const void*)hll_finish_kernel, (const void*)bin_kernel<1>, (const void*)bin_kernel<2>,
+        (const void*)bin_kernel_ranked<1>, (const void*)bin_kernel_ranked<2>,
         (const void*)flat_count_kernel<1>, (const void*)flat_count_kernel<2>, (const void*)flat_scan_kernel,
         (const void*)flat_scatter_kernel<1>, (const void*)flat_scatter_kernel<2>,
         (const void*)flat_scatter_lds_kernel<1>, (const void*)flat_scatter_lds_kernel<2>,

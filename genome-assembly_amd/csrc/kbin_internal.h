@@ -325,7 +325,11 @@ struct BinArgs {
     uint32_t* rrank;           // [R] record -> rank in its bin
     uint32_t* rord;            // [R] (bin start + rank) -> ordinal
 };
-constexpr int KB_PSTAT = 11;  // (h_totals[16 .. 16 + KB_PSTAT) in the stats copy)
+constexpr int KB_PSTAT = 11;
+// light pre-filtered bins (kbin_bins.hip): the per-bin sketch's cells and the
+// distinct-key load it takes (the host sizes sub-bins by them)
+constexpr uint32_t PFL_CELLS = 8192u * 16u;
+constexpr double PFL_LOAD = 0.15;  // (h_totals[16 .. 16 + KB_PSTAT) in the stats copy)
 
 struct ListArgs {
     const uint64_t* totals;    // totals[0] = entries

@@ -1179,8 +1179,14 @@ static int cmp_table_size(const void *a, const void *b)
     return x > y ? -1 : x < y;
 }
 
+/* KBH_TRACE: when exit() starts (after the caller's main has returned), so a
+ * parent can split the drop-in's tail into printing and process teardown */
+static void trace_exit(void) { fprintf(stderr, "{\"t_exit_s\": %.6f}\n", now_ms() * 1e-3); }
+
 void expand_read_id_list(struct ZHashTable *hashtable)
 {
+    static int traced = 0;
+    if (getenv("KBH_TRACE") && !traced) traced = atexit(trace_exit) == 0;
     double t = now_ms();
     const size_t m1 = LADDER[hashtable->size_index];
     uint64_t nt2 = 0;

@@ -48,6 +48,7 @@ def run(exe, path, timeout, env=None):
         if time.perf_counter() > deadline:
             p.kill()
             return {"timeout_s": timeout}
+    t_eof = time.monotonic()  # (CLOCK_MONOTONIC, as the shim's trace stamps)
     err = p.stderr.read().decode(errors="replace")
     rc = p.wait()
     wall = time.perf_counter() - t0
@@ -57,6 +58,12 @@ def run(exe, path, timeout, env=None):
             out["prune_data"] = json.loads(ln)
         elif ln.startswith("{\"expand_ms\""):  # the shim's expand_read_id_list (binning.c:857-888)
             out["expand"] = json.loads(ln)
+        elif ln.startswith("{\"t_exit_s\""):  # exit() started: the reference's main has returned
+            out["t_exit_s"] = json.loads(ln)["t_exit_s"]
+    if "expand" in out and "t_exit_s" in out:
+        # after the expansion: find_kmer_extensions x2 + print_kmers; after exit(): teardown
+        out["after_expand_to_exit_s"] = round(out["t_exit_s"] - out["expand"]["t_end_s"], 3)
+        out["exit_to_eof_s"] = round(t_eof - out.pop("t_exit_s"), 3)
     if "prune_data" in out and "expand" in out:
         pd = out["prune_data"]["prune_data_ms"] / 1e3
         out["rest_s"] = round(wall - pd - out["expand"]["expand_ms"] / 1e3, 3)  # read loop, extension, print, exit
