@@ -1973,6 +1973,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.order = c->border.p;
         a.bdesc = use_desc ? c->bdesc.p : nullptr;
         a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
+        a.sched_static = (uint32_t)(env_int("KB_BIN_SCHED", 0) == 1);
         a.stage = c->stage.p;
         a.stage_ord = stage6 ? c->stage_ord.p : nullptr;
         a.stage_slot = stage6 ? c->stage_slot.p : nullptr;
@@ -2229,6 +2230,14 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         if (learn) {
             const uint64_t nb = std::min<uint64_t>(c->h_totals[2], max_bins);
             const uint32_t* hb = c->h_bins.p;
+            if (const char* dp = getenv("KB_DIAG_BINS")) {  // (diagnostic: this pass's bins, appended)
+                if (FILE* f = fopen(dp, "a")) {
+                    for (uint64_t i = 0; i < nb; i++)
+                        fprintf(f, "%u %u %u %u %u\n", c->part, hb[i] & 0xFFFFu, hb[i] >> 16, hb[max_bins + i],
+                                hb[2 * max_bins + i]);
+                    fclose(f);
+                }
+            }
             kb_ctx::BucketMap* bm0 = bmap_find(c, NB);
             if (bm0) {  // rebuilt when this key is next binned
                 bm0->p_mm.assign(hb, hb + nb);

@@ -720,7 +720,7 @@ hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint6
 // ---------------------------------------------------------------------------
 #ifdef KB_BIN_PROF
 // per-phase cycle accounting (tid 0, between barriers): a diagnostic build only
-__device__ unsigned long long g_bin_prof[16];
+__device__ unsigned long long g_bin_prof[22];
 #define PROF_MARK(ph)                                              \
     do {                                                           \
         if (tid == 0) {                                            \
@@ -1502,9 +1502,13 @@ DEV void bin_ranks(const uint64_t* __restrict__ hdr, uint32_t* __restrict__ rran
         atomicMax(&S.rk_max, mx);
     }
     __syncthreads();
-    const uint32_t omax = S.rk_max;
-    const uint64_t span = (uint64_t)(omax - S.rk_min) + 1ull;
-    auto bucket = [&](uint32_t o) { return (uint32_t)(((uint64_t)(omax - o) * RANK_NBK) / span); };
+    // (buckets by a shift of the distance from the largest ordinal: at least
+    // half of the RANK_NBK buckets in use, no division per record)
+    const uint32_t omax = S.rk_max, d = omax - S.rk_min;
+    const int lg = d ? 32 - __clz((int)d) : 0;  // bits of the largest distance
+    const uint32_t sh = lg > 10 ? (uint32_t)(lg - 10) : 0u;
+    static_assert(RANK_NBK == 1024u, "the shift assumes 1024 buckets");
+    auto bucket = [&](uint32_t o) { return (omax - o) >> sh; };
     for (uint32_t i = tid; i < R; i += BIN_THREADS) atomicAdd(&hist[bucket(ordv[i])], 1u);
     __syncthreads();
     uint64_t tot;
@@ -1544,7 +1548,7 @@ DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __rest
                                           uint32_t* cnt, uint32_t ts, uint32_t* win, uint32_t win_cap, uint32_t ns,
                                           unsigned long long e0, unsigned long long i0, uint32_t n_long, uint32_t e_base,
                                           uint32_t e_mine, const uint32_t* so, const uint16_t* ss, uint32_t R,
-                                          const uint32_t* rord_bin) {
+                                          const uint32_t* rord_bin PROF_PARAMS) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t per = ts / BIN_THREADS, W = (R + 31u) / 32u;
     uint32_t* offs = win;                  // [n_long] next position of each list (relative to i0)
@@ -1592,6 +1596,7 @@ DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __rest
             }
         }
         __syncthreads();
+        PROF_MARK(18);
         // every bitmap holds exactly its key's count of bits (one per occurrence)
         for (uint32_t e = g0 + wid; e < g1; e += BIN_WAVES) {
             uint32_t pc = 0;
@@ -1609,35 +1614,50 @@ DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __rest
             __syncthreads();
             return false;
         }
+        // the tiles' ordinals: the next tile's loads in flight during this
+        // tile's emission (the tile holds read ids: the emission is LDS reads,
+        // a wave scan and stores, no dependent global load)
+        constexpr uint32_t TPT = RANK_TILE / BIN_THREADS;
+        uint32_t nx[TPT];
+        auto fetch = [&](uint32_t t) {
+#pragma unroll
+            for (uint32_t u = 0; u < TPT; u++) {
+                const uint32_t i = t + tid + u * BIN_THREADS;
+                nx[u] = i < R ? rord_bin[i] : 0u;
+            }
+        };
+        fetch(0);
         for (uint32_t t0 = 0; t0 < R; t0 += RANK_TILE) {
             const uint32_t tn = min(RANK_TILE, R - t0);
-            for (uint32_t i = tid; i < tn; i += BIN_THREADS) tile[i] = rord_bin[t0 + i];
-            __syncthreads();
+#pragma unroll
+            for (uint32_t u = 0; u < TPT; u++) {
+                const uint32_t i = tid + u * BIN_THREADS;
+                if (i < tn) tile[i] = (uint32_t)id_of(nx[u], read_ids, id_off);
+            }
+            lds_barrier();
+            if (t0 + RANK_TILE < R) fetch(t0 + RANK_TILE);
+            static_assert(RANK_TILE == 64u * 32u, "one bitmap word per lane covers a tile");
             for (uint32_t e = g0 + wid; e < g1; e += BIN_WAVES) {
                 const uint32_t* b = bm + (e - g0) * W;
                 uint32_t run = offs[e];
-                // four 64-rank steps per trip: their bitmap reads in flight together
-                for (uint32_t c0 = 0; c0 < tn; c0 += 256u) {
-                    uint32_t x[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t r = t0 + c0 + 64u * u + lane;
-                        x[u] = c0 + 64u * u + lane < tn ? b[r >> 5] : 0u;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t r = t0 + c0 + 64u * u + lane;
-                        const bool on = (x[u] >> (r & 31u)) & 1u;
-                        const uint64_t m = __ballot(on);
-                        if (on)
-                            ids_out[i0 + run + lanes_below(m)] = id_of(tile[c0 + 64u * u + lane], read_ids, id_off);
-                        run += (uint32_t)__popcll(m);
-                    }
+                // one bitmap word (32 ranks) per lane: a wave scan of the
+                // words' bit counts gives each lane its first position, then
+                // each lane writes its set bits' ids in rank order
+                uint32_t x = lane * 32u < tn ? b[(t0 >> 5) + lane] : 0u;
+                const uint32_t pc = (uint32_t)__popc(x);
+                const uint32_t inc = wave_incl_scan(pc, (int)lane);
+                uint32_t pos = run + inc - pc;
+                while (x) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(x);
+                    x &= x - 1u;
+                    ids_out[i0 + pos++] = (int32_t)tile[lane * 32u + bit];
                 }
+                run += (uint32_t)__shfl((int)inc, 63, 64);
                 if (lane == 0) offs[e] = run;
             }
-            __syncthreads();
+            lds_barrier();  // (the tile is the next tile's)
         }
+        PROF_MARK(19);
     }
     return true;
 }
@@ -1675,14 +1695,15 @@ DEV void bin_body(const BinArgs& A) {
     const uint64_t nbins = min(A.totals[2], A.max_bins);
     const uint32_t tid = threadIdx.x;
 #ifdef KB_BIN_PROF
-    unsigned long long pacc[16] = {};
+    unsigned long long pacc[22] = {};
     unsigned long long pt = clock64();
 #endif
     if (tid < 64) S.dummy[tid] = 0;  // (the first loop barrier publishes it)
     // phase 0: block thread 0 claims the next bin one bin ahead, so the
     // claim's round trip overlaps this bin's work instead of opening the next
     unsigned long long next_item = 0;
-    if (PHASE == 0 && tid == 0) next_item = atomicAdd(A.work, 1ull);
+    if (PHASE == 0 && tid == 0 && !A.sched_static) next_item = atomicAdd(A.work, 1ull);
+    uint32_t round = 0;  // (static schedule: serpentine over the largest-first order)
 
     while (true) {
         // phase 0: persistent blocks take bins from a shared counter, largest
@@ -1691,7 +1712,11 @@ DEV void bin_body(const BinArgs& A) {
         // workgroup's serial loop)
         bar_lds(A);
         if (tid == 0) {
-            if (PHASE == 0) {
+            if (PHASE == 0 && A.sched_static) {
+                const uint32_t G = gridDim.x;
+                S.item = round * G + ((round & 1u) ? G - 1u - blockIdx.x : blockIdx.x);
+                round++;
+            } else if (PHASE == 0) {
                 S.item = (uint32_t)min(next_item, 0xFFFFFFFFull);
                 if (next_item < nbins) next_item = atomicAdd(A.work, 1ull);
             } else {
@@ -1711,6 +1736,7 @@ DEV void bin_body(const BinArgs& A) {
             }
         }
         bar_lds(A);
+        PROF_MARK(20);
         if (PHASE == 0 ? S.item >= nbins : S.item == 0xFFFFFFFFu) break;  // uniform
         if (PHASE == 1) {  // one flat partition of bin S.item
             const uint32_t b = S.item;
@@ -1758,6 +1784,7 @@ DEV void bin_body(const BinArgs& A) {
             bar_lds(A);
         }
         uint64_t* stage = A.stage + S.stage_base;  // (flat: moved to each partition's list)
+        PROF_MARK(21);
         PROF_CNT(11, PHASE == 0);
         PROF_CNT(0, PHASE == 0 ? (hi - lo) : 0u);  // records once per bin
         PROF_CNT(14, occ_tot);
@@ -1929,7 +1956,9 @@ DEV void bin_body(const BinArgs& A) {
             rmode = R >= RANK_MIN && R <= 65536u && RANK_NBK + R + (R + 1u) / 2u <= words;
             if (rmode) {
                 bar_lds(A);
+                PROF_MARK(7);
                 bin_ranks(A.hdr, A.rrank, A.rord, S, lo, hi, cnt);
+                PROF_MARK(16);
                 if (tid == 0 && A.pstat) atomicAdd(&A.pstat[9], 1ull);
             }
         }
@@ -1953,14 +1982,15 @@ DEV void bin_body(const BinArgs& A) {
         const bool sp_ord_w = !(PHASE == 1 && flat);
         while (true) {
             const uint32_t ts = S.ts, bmask = ts / 4 - 1, limit = ts - ts / 4;  // (uniform)
+            // (the stack is stable here: every write to it is followed by a
+            // barrier before the loop comes round; the pop is published after
+            // the zeroing barrier, so no wave reads S.sp while tid 0 writes it,
+            // and the empty stack leaves without zeroing a table no one uses)
+            const uint32_t sp0 = S.sp;
+            if (sp0 == 0) break;  // uniform
             if (tid == 0) {
-                if (S.sp == 0) {
-                    S.cur_l = 0xFFFFFFFFu;
-                } else {
-                    S.sp--;
-                    S.cur_p = S.stack_p[S.sp];
-                    S.cur_l = S.stack_l[S.sp];
-                }
+                S.cur_p = S.stack_p[sp0 - 1u];
+                S.cur_l = S.stack_l[sp0 - 1u];
                 S.n_keys = 0;
                 S.overflow = 0;
                 S.n_stage = 0;
@@ -1977,9 +2007,9 @@ DEV void bin_body(const BinArgs& A) {
             if (PHASE == 1 && pfb)
                 for (uint32_t i = tid; i < sk_words; i += BIN_THREADS) sk[i] = 0;
             bar_lds(A);
+            if (tid == 0) S.sp = sp0 - 1u;
             PROF_MARK(1);
             const uint32_t P = S.cur_p, Lv = S.cur_l;
-            if (Lv == 0xFFFFFFFFu) break;  // uniform
             PROF_CNT(8, 1);
             PROF_CNT(15, (PHASE == 0 || !flat) ? (hi - lo) : 0u);  // records expanded (all partitions)
             // ---- sweep 1: insert + count (binning.c:1042-1069 semantics per key)
@@ -2307,6 +2337,7 @@ DEV void bin_body(const BinArgs& A) {
             // a key seen twice in one record) ordinals at their cursors and the
             // list kernels; then their slots leave the short lists' way
             if (n_ent_all > n_ent) {
+                PROF_MARK(3);
                 const uint32_t n_long = n_ent_all - n_ent;
                 const uint32_t R = hi - lo, W = (R + 31u) / 32u;
                 const uint32_t fixed = ((n_long + 3u) & ~3u) + RANK_TILE;
@@ -2314,7 +2345,7 @@ DEV void bin_body(const BinArgs& A) {
                 const bool bm_ok = G && (n_long + G - 1u) / G <= RANK_GROUPS &&
                                    bitmap_lists<KW>(A.e_off, A.e_cnt, A.ids_out, A.read_ids, A.id_off, S, cnt, ts, win, win_cap,
                                                     S.n_stage, e0, i0, n_long, n_ent, (uint32_t)ex_l, sp_ord, sp_slot,
-                                                    R, A.rord + lo);
+                                                    R, A.rord + lo PROF_ARGS);
                 if (bm_ok) {
                     if (tid == 0 && A.pstat) atomicAdd(&A.pstat[10], 1ull);
                 } else {
@@ -2348,6 +2379,7 @@ DEV void bin_body(const BinArgs& A) {
                 }
                 __threadfence_block();
                 __syncthreads();
+                PROF_MARK(17);
                 if (!n_ent) continue;
             }
             // LDS id windows for short lists (mean <= 64 ids): light bins, and
@@ -2424,7 +2456,7 @@ DEV void bin_body(const BinArgs& A) {
     }
 #ifdef KB_BIN_PROF
     if (tid == 0)
-        for (int i = 0; i < 16; i++) {
+        for (int i = 0; i < 22; i++) {
             if (i == 12) continue;
             if (i == 13) {  // max over blocks (and that bin's occurrences)
                 if (atomicMax(&g_bin_prof[13], pacc[13]) < pacc[13]) g_bin_prof[12] = pacc[12];
@@ -2838,7 +2870,7 @@ __global__ __launch_bounds__(FSL_THREADS) void flat_scatter_lds_kernel(BinArgs A
 
 #ifdef KB_BIN_PROF
 void bins_prof_report(hipStream_t s) {
-    unsigned long long h[16];
+    unsigned long long h[22];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bin_prof), sizeof(h));
     {
@@ -2848,14 +2880,14 @@ void bins_prof_report(hipStream_t s) {
         unsigned long long z8[8] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sk_prof), z8, sizeof(z8));
     }
-    static const char* nm[16] = {"bin records", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
+    static const char* nm[22] = {"bin records", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
                                  "partitions", "overflows", "omode-ovf(1e6*n+1e3*width+Lv)", "bins", "slowest-bin-occ", "slowest-bin-cycles",
-                                 "occ", "records expanded"};
+                                 "occ", "records expanded", "rank", "long bitmaps", "bitmap set", "bitmap emit", "bin claim", "bin desc"};
     fprintf(stderr, "[bin_prof]");
-    for (int i = 0; i < 16; i++)
+    for (int i = 0; i < 22; i++)
         if (h[i]) fprintf(stderr, " %s=%llu", nm[i], h[i]);
     fprintf(stderr, "\n");
-    unsigned long long z[16] = {};
+    unsigned long long z[22] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bin_prof), z, sizeof(z));
 }
 #endif
