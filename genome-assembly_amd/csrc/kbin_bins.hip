@@ -720,7 +720,7 @@ hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint6
 // ---------------------------------------------------------------------------
 #ifdef KB_BIN_PROF
 // per-phase cycle accounting (tid 0, between barriers): a diagnostic build only
-__device__ unsigned long long g_bin_prof[22];
+__device__ unsigned long long g_bin_prof[26];
 #define PROF_MARK(ph)                                              \
     do {                                                           \
         if (tid == 0) {                                            \
@@ -1453,30 +1453,30 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
 // ---- ranked bins (long lists): records ranked by call ordinal, lists
 // emitted from per-key bitmaps over the ranks (BinArgs::rank_mode)
 constexpr uint32_t RANK_MIN = 512;    // fewer records: lists short, nothing to gain
-constexpr uint32_t RANK_NBK = 1024;   // ordinal buckets of the ranking
 constexpr uint32_t RANK_TILE = 2048;  // ranks whose ordinals are staged in LDS at once (emission)
 constexpr uint32_t RANK_GROUPS = 8;   // most passes over the stage (entries whose bitmaps fit at once)
 constexpr uint32_t RANK_LONG = 256;   // ranked bins: lists longer than this take the bitmaps
 constexpr uint32_t LONGB = 0x40000000u;  // cnt of a ranked bin's kept long list: LONGB | cursor (< PRUNED)
 
 // rank of every record of the bin [lo, hi) by descending call ordinal (ties
-// by record index): bucket the ordinals (LDS histogram over their range,
-// largest first), scatter the record indices by bucket, and count each
-// record's predecessors inside its bucket.  rrank[r] = rank of record r,
-// rord[lo + k] = ordinal of rank k.  lds: RANK_NBK + R ordinals + R 16-bit
-// indices (6 R + 4 KiB bytes), everything past BinShared (the table and
+// by record index): bucket the ordinals by a shift of their distance from the
+// largest (nbk buckets, a power of two near R / 4: a few records each, the
+// read ordinals being spread evenly), scatter the record indices by bucket,
+// and count each record's predecessors inside its bucket (a few compares).
+// rrank[r] = rank of record r, rord[lo + k] = ordinal of rank k.  lds: nbk +
+// R ordinals + R 16-bit indices, everything past BinShared (the table and
 // rings are not live yet)
 DEV void bin_ranks(const uint64_t* __restrict__ hdr, uint32_t* __restrict__ rrank, uint32_t* __restrict__ rord,
-                   BinShared& S, uint32_t lo, uint32_t hi, uint32_t* lds) {
-    const uint32_t tid = threadIdx.x, R = hi - lo;
-    uint32_t* hist = lds;              // [RANK_NBK] counts, then bucket ends
-    uint32_t* ordv = lds + RANK_NBK;   // [R] ordinal of record index i
+                   BinShared& S, uint32_t lo, uint32_t hi, uint32_t nbk_log2, uint32_t* lds PROF_PARAMS) {
+    const uint32_t tid = threadIdx.x, R = hi - lo, nbk = 1u << nbk_log2;
+    uint32_t* hist = lds;         // [nbk] counts, then bucket ends
+    uint32_t* ordv = lds + nbk;   // [R] ordinal of record index i
     uint16_t* pidx = reinterpret_cast<uint16_t*>(ordv + R);  // [R] record indices by bucket
     if (tid == 0) {
         S.rk_min = 0xFFFFFFFFu;
         S.rk_max = 0;
     }
-    for (uint32_t i = tid; i < RANK_NBK; i += BIN_THREADS) hist[i] = 0;
+    for (uint32_t i = tid; i < nbk; i += BIN_THREADS) hist[i] = 0;
     uint32_t mn = 0xFFFFFFFFu, mx = 0;
     for (uint32_t i0 = tid; i0 < R; i0 += 4u * BIN_THREADS) {  // (four header loads in flight)
         uint32_t o[4];
@@ -1502,22 +1502,33 @@ DEV void bin_ranks(const uint64_t* __restrict__ hdr, uint32_t* __restrict__ rran
         atomicMax(&S.rk_max, mx);
     }
     __syncthreads();
-    // (buckets by a shift of the distance from the largest ordinal: at least
-    // half of the RANK_NBK buckets in use, no division per record)
+    PROF_MARK(22);
+    // (the shift leaves at least half of the buckets in use; no division)
     const uint32_t omax = S.rk_max, d = omax - S.rk_min;
-    const int lg = d ? 32 - __clz((int)d) : 0;  // bits of the largest distance
-    const uint32_t sh = lg > 10 ? (uint32_t)(lg - 10) : 0u;
-    static_assert(RANK_NBK == 1024u, "the shift assumes 1024 buckets");
+    const uint32_t lg = d ? 32u - (uint32_t)__clz((int)d) : 0u;  // bits of the largest distance
+    const uint32_t sh = lg > nbk_log2 ? lg - nbk_log2 : 0u;
     auto bucket = [&](uint32_t o) { return (omax - o) >> sh; };
     for (uint32_t i = tid; i < R; i += BIN_THREADS) atomicAdd(&hist[bucket(ordv[i])], 1u);
     __syncthreads();
-    uint64_t tot;
-    const uint32_t h = tid < RANK_NBK ? hist[tid] : 0u;
-    const uint32_t start = (uint32_t)block_excl_scan_u64(h, S.red, tot);
-    if (tid < RANK_NBK) hist[tid] = start;  // cursor (then the bucket's end)
+    PROF_MARK(23);
+    // exclusive scan: each thread its run of nbk / BIN_THREADS counters
+    // (nbk >= BIN_THREADS), then one block scan of the runs
+    {
+        const uint32_t run = nbk / BIN_THREADS, c0 = tid * run;
+        uint32_t sum = 0;
+        for (uint32_t k = 0; k < run; k++) sum += hist[c0 + k];
+        uint64_t tot;
+        uint32_t at = (uint32_t)block_excl_scan_u64(sum, S.red, tot);
+        for (uint32_t k = 0; k < run; k++) {
+            const uint32_t h = hist[c0 + k];
+            hist[c0 + k] = at;  // cursor (then the bucket's end)
+            at += h;
+        }
+    }
     __syncthreads();
     for (uint32_t i = tid; i < R; i += BIN_THREADS) pidx[atomicAdd(&hist[bucket(ordv[i])], 1u)] = (uint16_t)i;
     __syncthreads();
+    PROF_MARK(24);
     for (uint32_t i = tid; i < R; i += BIN_THREADS) {
         const uint32_t o = ordv[i], b = bucket(o);
         const uint32_t b0 = b ? hist[b - 1] : 0u, b1 = hist[b];
@@ -1529,7 +1540,12 @@ DEV void bin_ranks(const uint64_t* __restrict__ hdr, uint32_t* __restrict__ rran
         rrank[lo + i] = rank;
         rord[lo + rank] = o;
     }
+#ifdef KB_BIN_PROF
+    lds_barrier();
+    PROF_MARK(16);
+#endif
     __syncthreads();  // (the ranks go out to HBM before sweep 1 reads them; the LDS is the table's next)
+    PROF_MARK(25);
 }
 
 // A ranked partition's LONG lists (> RANK_LONG ids; their slots hold LONGB |
@@ -1695,7 +1711,7 @@ DEV void bin_body(const BinArgs& A) {
     const uint64_t nbins = min(A.totals[2], A.max_bins);
     const uint32_t tid = threadIdx.x;
 #ifdef KB_BIN_PROF
-    unsigned long long pacc[22] = {};
+    unsigned long long pacc[26] = {};
     unsigned long long pt = clock64();
 #endif
     if (tid < 64) S.dummy[tid] = 0;  // (the first loop barrier publishes it)
@@ -1953,12 +1969,16 @@ DEV void bin_body(const BinArgs& A) {
         if (RANKED && PHASE == 0 && A.rank_mode && !flat && !split) {
             const uint32_t words = TS + 2u * KW * TS + (uint32_t)BIN_WAVES * Q * (8u * KW + 6u) / 4u;
             const uint32_t R = hi - lo;
-            rmode = R >= RANK_MIN && R <= 65536u && RANK_NBK + R + (R + 1u) / 2u <= words;
+            // buckets: a power of two near R / 4 (at least one per thread), as
+            // many as the LDS leaves room for
+            uint32_t nl = 10;
+            while (nl < 13 && (2u << nl) <= R / 4u) nl++;
+            while (nl > 10 && (1u << nl) + R + (R + 1u) / 2u > words) nl--;
+            rmode = R >= RANK_MIN && R <= 65536u && (1u << nl) + R + (R + 1u) / 2u <= words;
             if (rmode) {
                 bar_lds(A);
                 PROF_MARK(7);
-                bin_ranks(A.hdr, A.rrank, A.rord, S, lo, hi, cnt);
-                PROF_MARK(16);
+                bin_ranks(A.hdr, A.rrank, A.rord, S, lo, hi, nl, cnt PROF_ARGS);
                 if (tid == 0 && A.pstat) atomicAdd(&A.pstat[9], 1ull);
             }
         }
@@ -2456,7 +2476,7 @@ DEV void bin_body(const BinArgs& A) {
     }
 #ifdef KB_BIN_PROF
     if (tid == 0)
-        for (int i = 0; i < 22; i++) {
+        for (int i = 0; i < 26; i++) {
             if (i == 12) continue;
             if (i == 13) {  // max over blocks (and that bin's occurrences)
                 if (atomicMax(&g_bin_prof[13], pacc[13]) < pacc[13]) g_bin_prof[12] = pacc[12];
@@ -2870,7 +2890,7 @@ __global__ __launch_bounds__(FSL_THREADS) void flat_scatter_lds_kernel(BinArgs A
 
 #ifdef KB_BIN_PROF
 void bins_prof_report(hipStream_t s) {
-    unsigned long long h[22];
+    unsigned long long h[26];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bin_prof), sizeof(h));
     {
@@ -2880,14 +2900,14 @@ void bins_prof_report(hipStream_t s) {
         unsigned long long z8[8] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sk_prof), z8, sizeof(z8));
     }
-    static const char* nm[22] = {"bin records", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
+    static const char* nm[26] = {"bin records", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
                                  "partitions", "overflows", "omode-ovf(1e6*n+1e3*width+Lv)", "bins", "slowest-bin-occ", "slowest-bin-cycles",
-                                 "occ", "records expanded", "rank", "long bitmaps", "bitmap set", "bitmap emit", "bin claim", "bin desc"};
+                                 "occ", "records expanded", "rank", "long bitmaps", "bitmap set", "bitmap emit", "bin claim", "bin desc", "rank loads", "rank hist", "rank scatter", "rank stores"};
     fprintf(stderr, "[bin_prof]");
-    for (int i = 0; i < 22; i++)
+    for (int i = 0; i < 26; i++)
         if (h[i]) fprintf(stderr, " %s=%llu", nm[i], h[i]);
     fprintf(stderr, "\n");
-    unsigned long long z[22] = {};
+    unsigned long long z[26] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bin_prof), z, sizeof(z));
 }
 #endif
