@@ -2092,6 +2092,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             const int rk = env_int("KB_BIN_RANK", 1);
             const bool long_lists = c->hint_entries && c->hint_ids >= 64 * c->hint_entries;
             a.rank_mode = (rk == 2 || (rk == 1 && long_lists)) && stage6 && !a.e_first ? 1u : 0u;
+            a.rank_merge = (uint32_t)(env_int("KB_BIN_RANK_MERGE", 1) != 0);
             if (a.rank_mode) {
                 HIPCHK(c->rrank.ensure(std::max<uint64_t>(R, 1)));
                 HIPCHK(c->rord.ensure(std::max<uint64_t>(R, 1)));

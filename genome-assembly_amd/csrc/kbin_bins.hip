@@ -1300,6 +1300,14 @@ DEV void bar_lds(const BinArgs& A) {
     else __syncthreads();
 }
 
+// ---- ranked bins (see bin_ranks, bitmap_lists)
+constexpr uint32_t RANK_MIN = 512;    // fewer records: lists short, nothing to gain
+constexpr uint32_t RANK_TILE = 2048;  // ranks whose ordinals are staged in LDS at once (emission)
+constexpr uint32_t RANK_GROUPS = 8;   // most passes over the stage (entries whose bitmaps fit at once)
+constexpr uint32_t RANK_LONG = 256;   // ranked bins: lists longer than this take the bitmaps
+constexpr uint32_t LONGB = 0x40000000u;  // cnt of a ranked bin's kept long list: LONGB | cursor (< PRUNED)
+DEV bool is_long_slot(uint32_t c) { return (c & (LONGB | PRUNED)) == LONGB; }
+
 // LDS path of one partition, after its prune: the kept occurrences' ordinals
 // go to an LDS window at their list positions (cursor atomics on cnt), each
 // list is put in reverse call order there (binning.c:1065-1068 prepends:
@@ -1316,12 +1324,15 @@ DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane);
 
 // (so, ss: the split stage of a light bin -- ordinals and slots -- or null:
 // the 8-B stage entries)
-// (rord_bin: a ranked bin's stage holds ranks; its ordinal is rord_bin[rank])
-template <int KW>
+// (RK, rord_bin: a ranked bin's stage holds ranks; its ordinal is
+// rord_bin[rank]; only the kept short lists' occurrences are mapped.  bmw:
+// the long lists' bitmaps (bmW words each, past win_cap) -- their slots hold
+// LONGB | long entry, and the first window's stage pass sets their bits)
+template <int KW, bool RK = false>
 DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, uint32_t* win, uint32_t win_cap,
                    uint32_t ns, unsigned long long e0, unsigned long long i0, uint32_t n_ent, uint32_t n_ids,
                    const uint64_t* stage, const uint32_t* so, const uint16_t* ss, uint32_t e_mine,
-                   const uint32_t* rord_bin PROF_PARAMS) {
+                   const uint32_t* rord_bin, uint32_t* bmw, uint32_t bmW PROF_PARAMS) {
     const uint32_t tid = threadIdx.x;
     const int lane = (int)(tid & 63u);
     const uint32_t per = TS / BIN_THREADS;
@@ -1353,7 +1364,7 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
             uint32_t e = e_mine;
             for (uint32_t k = 0; k < per; k++) {
                 const uint32_t i = tid + k * BIN_THREADS, c = cnt[i];
-                if (c >= PRUNED) continue;
+                if (c >= PRUNED || (RK && bmw && (c & LONGB))) continue;  // (pruned, or a bitmap list)
                 if (c <= X) best = ((unsigned long long)c << 32) | ((unsigned long long)e << 16) | (tid * per + k);
                 e++;
             }
@@ -1381,10 +1392,28 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
                     vs[u] = (uint32_t)(x >> 48);
                 }
             }
-            if (rord_bin) {
+            if constexpr (RK) {
+                if (rord_bin) {
+                    // only kept short lists of this window gather their ordinal;
+                    // a bitmap list's occurrence sets its rank's bit (first window)
 #pragma unroll
-                for (int u = 0; u < WL; u++)
-                    if (vs[u]) vo[u] = rord_bin[vo[u]];
+                    for (int u = 0; u < WL; u++) {
+                        if (!vs[u]) continue;
+                        const uint32_t ls = vs[u] - 1u, c = cnt[ls];
+                        const uint32_t o = (ls & (BIN_THREADS - 1u)) * per + ls / BIN_THREADS;
+                        if (bmw && is_long_slot(c)) {
+                            if (wlo == 0)
+                                __hip_atomic_fetch_or(&bmw[(c & ~LONGB) * bmW + (vo[u] >> 5)], 1u << (vo[u] & 31u),
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            vs[u] = 0;
+                        } else if (c >= PRUNED || o - slo >= shi - slo) {
+                            vs[u] = 0;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < WL; u++)
+                        if (vs[u]) vo[u] = rord_bin[vo[u]];
+                }
             }
 #pragma unroll
             for (int u = 0; u < WL; u++) {
@@ -1452,11 +1481,6 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
 
 // ---- ranked bins (long lists): records ranked by call ordinal, lists
 // emitted from per-key bitmaps over the ranks (BinArgs::rank_mode)
-constexpr uint32_t RANK_MIN = 512;    // fewer records: lists short, nothing to gain
-constexpr uint32_t RANK_TILE = 2048;  // ranks whose ordinals are staged in LDS at once (emission)
-constexpr uint32_t RANK_GROUPS = 8;   // most passes over the stage (entries whose bitmaps fit at once)
-constexpr uint32_t RANK_LONG = 256;   // ranked bins: lists longer than this take the bitmaps
-constexpr uint32_t LONGB = 0x40000000u;  // cnt of a ranked bin's kept long list: LONGB | cursor (< PRUNED)
 
 // rank of every record of the bin [lo, hi) by descending call ordinal (ties
 // by record index): bucket the ordinals by a shift of their distance from the
@@ -1548,41 +1572,110 @@ DEV void bin_ranks(const uint64_t* __restrict__ hdr, uint32_t* __restrict__ rran
     PROF_MARK(25);
 }
 
+// long slot -> LONGB | long-entry index (the prune's scan order); offs[e] =
+// its list start (relative to i0)
+DEV void bm_remap(uint32_t* cnt, uint32_t per, uint32_t e_mine, uint32_t* offs) {
+    uint32_t e = e_mine;
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t i = threadIdx.x + k * BIN_THREADS, c = cnt[i];
+        if (is_long_slot(c)) {
+            offs[e] = c & ~LONGB;
+            cnt[i] = LONGB | e++;
+        }
+    }
+}
+
+// every bitmap of the group [g0, g1) holds exactly its key's count of bits
+// (one per occurrence); else (a bit set twice: the same record holding the
+// key twice) the long slots get their cursors back and the result is false
+DEV bool bm_check(const uint64_t* __restrict__ e_off, const uint32_t* __restrict__ e_cnt, BinShared& S,
+                  uint32_t* cnt, uint32_t per, unsigned long long e0, unsigned long long i0, uint32_t e_base,
+                  uint32_t e_mine, uint32_t g0, uint32_t g1, const uint32_t* bm, uint32_t W) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    for (uint32_t e = g0 + wid; e < g1; e += BIN_WAVES) {
+        uint32_t pc = 0;
+        for (uint32_t w = lane; w < W; w += 64u) pc += (uint32_t)__popc(bm[(e - g0) * W + w]);
+        pc = wave_sum_u32(pc);
+        if (lane == 0 && pc != e_cnt[e0 + e_base + e]) S.dup = 1;
+    }
+    __syncthreads();
+    if (!S.dup) return true;  // (uniform)
+    uint32_t e = e_mine;  // back to the cursors (every long list restarts; its ids are rewritten)
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t i = tid + k * BIN_THREADS;
+        if (is_long_slot(cnt[i])) cnt[i] = LONGB | (uint32_t)(e_off[e0 + e_base + e++] - i0);
+    }
+    __syncthreads();
+    return false;
+}
+
+// the group's lists in rank order (descending ordinal = reverse call order,
+// binning.c:1061-1068): one wave per list and 2048-rank tile, one bitmap word
+// (32 ranks) per lane -- a wave scan of the words' bit counts gives each lane
+// its first position, then each lane writes its set bits' read ids from the
+// tile (the next tile's ordinals loaded during this tile's emission)
+DEV void bm_emit(int32_t* __restrict__ ids_out, const int32_t* __restrict__ read_ids, uint32_t id_off,
+                 unsigned long long i0, uint32_t g0, uint32_t g1, const uint32_t* bm, uint32_t W, uint32_t* offs,
+                 uint32_t* tile, uint32_t R, const uint32_t* rord_bin) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    constexpr uint32_t TPT = RANK_TILE / BIN_THREADS;
+    uint32_t nx[TPT];
+    auto fetch = [&](uint32_t t) {
+#pragma unroll
+        for (uint32_t u = 0; u < TPT; u++) {
+            const uint32_t i = t + tid + u * BIN_THREADS;
+            nx[u] = i < R ? rord_bin[i] : 0u;
+        }
+    };
+    fetch(0);
+    for (uint32_t t0 = 0; t0 < R; t0 += RANK_TILE) {
+        const uint32_t tn = min(RANK_TILE, R - t0);
+#pragma unroll
+        for (uint32_t u = 0; u < TPT; u++) {
+            const uint32_t i = tid + u * BIN_THREADS;
+            if (i < tn) tile[i] = (uint32_t)id_of(nx[u], read_ids, id_off);
+        }
+        lds_barrier();
+        if (t0 + RANK_TILE < R) fetch(t0 + RANK_TILE);
+        static_assert(RANK_TILE == 64u * 32u, "one bitmap word per lane covers a tile");
+        for (uint32_t e = g0 + wid; e < g1; e += BIN_WAVES) {
+            const uint32_t* b = bm + (e - g0) * W;
+            uint32_t run = offs[e];
+            uint32_t x = lane * 32u < tn ? b[(t0 >> 5) + lane] : 0u;
+            const uint32_t pc = (uint32_t)__popc(x);
+            const uint32_t inc = wave_incl_scan(pc, (int)lane);
+            uint32_t pos = run + inc - pc;
+            while (x) {
+                const uint32_t bit = (uint32_t)__builtin_ctz(x);
+                x &= x - 1u;
+                ids_out[i0 + pos++] = (int32_t)tile[lane * 32u + bit];
+            }
+            run += (uint32_t)__shfl((int)inc, 63, 64);
+            if (lane == 0) offs[e] = run;
+        }
+        lds_barrier();  // (the tile is the next tile's)
+    }
+}
+
 // A ranked partition's LONG lists (> RANK_LONG ids; their slots hold LONGB |
 // cursor, their entries follow the short ones) from bitmaps: every long key
 // gets a bitmap over the bin's R ranks; each staged occurrence (slot, rank)
-// sets its bit (a bit already set -- the same record holding the key twice --
-// aborts: false, the slots' cursors restored, the caller takes the cursor
-// path); then each list is emitted in rank order (descending ordinal =
-// reverse call order, binning.c:1061-1068) by one wave, 64 ranks per step
-// (ballot + mbcnt give the positions), the ordinals of a rank tile staged in
-// LDS.  Keys are handled in groups whose bitmaps fit the window area, one
-// stage pass per group.
+// sets its bit, then bm_check and bm_emit.  Keys are handled in groups whose
+// bitmaps fit the window area, one stage pass per group.  False: a bit set
+// twice, the slots' cursors restored, the caller takes the cursor path.
 template <int KW>
 DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __restrict__ e_cnt, int32_t* __restrict__ ids_out,
-                                          const int32_t* __restrict__ read_ids, uint32_t id_off, BinShared& S,
-                                          uint32_t* cnt, uint32_t ts, uint32_t* win, uint32_t win_cap, uint32_t ns,
-                                          unsigned long long e0, unsigned long long i0, uint32_t n_long, uint32_t e_base,
-                                          uint32_t e_mine, const uint32_t* so, const uint16_t* ss, uint32_t R,
-                                          const uint32_t* rord_bin PROF_PARAMS) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+                      const int32_t* __restrict__ read_ids, uint32_t id_off, BinShared& S, uint32_t* cnt, uint32_t ts,
+                      uint32_t* win, uint32_t win_cap, uint32_t ns, unsigned long long e0, unsigned long long i0,
+                      uint32_t n_long, uint32_t e_base, uint32_t e_mine, const uint32_t* so, const uint16_t* ss,
+                      uint32_t R, const uint32_t* rord_bin PROF_PARAMS) {
+    const uint32_t tid = threadIdx.x;
     const uint32_t per = ts / BIN_THREADS, W = (R + 31u) / 32u;
     uint32_t* offs = win;                  // [n_long] next position of each list (relative to i0)
-    uint32_t* tile = offs + ((n_long + 3u) & ~3u);  // [RANK_TILE] ordinals of the current ranks
+    uint32_t* tile = offs + ((n_long + 3u) & ~3u);  // [RANK_TILE] read ids of the current ranks
     uint32_t* bm = tile + RANK_TILE;       // [G * W] the group's bitmaps
     const uint32_t G = (win_cap - (uint32_t)(bm - win)) / W;
-    auto is_long = [](uint32_t c) { return (c & (LONGB | PRUNED)) == LONGB; };
-    // long slot -> LONGB | long-entry index (the prune's scan order), its list start
-    {
-        uint32_t e = e_mine;
-        for (uint32_t k = 0; k < per; k++) {
-            const uint32_t i = tid + k * BIN_THREADS, c = cnt[i];
-            if (is_long(c)) {
-                offs[e] = c & ~LONGB;
-                cnt[i] = LONGB | e++;
-            }
-        }
-    }
+    bm_remap(cnt, per, e_mine, offs);
     for (uint32_t g0 = 0; g0 < n_long; g0 += G) {
         const uint32_t g1 = min(n_long, g0 + G);
         for (uint32_t i = tid; i < (g1 - g0) * W; i += BIN_THREADS) bm[i] = 0;
@@ -1590,7 +1683,7 @@ DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __rest
         __syncthreads();
         // (BL occurrences' stage loads in flight per thread; the bits go in
         // with non-returning atomics -- a bit set twice shows as a bitmap
-        // holding fewer bits than its key's count, checked below)
+        // holding fewer bits than its key's count, bm_check)
         constexpr int BL = 4;
         for (uint32_t j0 = tid; j0 < ns; j0 += (uint32_t)BL * BIN_THREADS) {
             uint32_t vs[BL], vr[BL];
@@ -1604,7 +1697,7 @@ DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __rest
             for (int u = 0; u < BL; u++) {
                 if (!vs[u]) continue;
                 const uint32_t c = cnt[vs[u] - 1u];
-                if (!is_long(c)) continue;
+                if (!is_long_slot(c)) continue;
                 const uint32_t e = c & ~LONGB;
                 if (e < g0 || e >= g1) continue;
                 __hip_atomic_fetch_or(&bm[(e - g0) * W + (vr[u] >> 5)], 1u << (vr[u] & 31u), __ATOMIC_RELAXED,
@@ -1613,66 +1706,8 @@ DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __rest
         }
         __syncthreads();
         PROF_MARK(18);
-        // every bitmap holds exactly its key's count of bits (one per occurrence)
-        for (uint32_t e = g0 + wid; e < g1; e += BIN_WAVES) {
-            uint32_t pc = 0;
-            for (uint32_t w = lane; w < W; w += 64u) pc += (uint32_t)__popc(bm[(e - g0) * W + w]);
-            pc = wave_sum_u32(pc);
-            if (lane == 0 && pc != e_cnt[e0 + e_base + e]) S.dup = 1;
-        }
-        __syncthreads();
-        if (S.dup) {  // uniform: back to the cursors (every long list restarts; its ids are rewritten)
-            uint32_t e = e_mine;
-            for (uint32_t k = 0; k < per; k++) {
-                const uint32_t i = tid + k * BIN_THREADS;
-                if (is_long(cnt[i])) cnt[i] = LONGB | (uint32_t)(e_off[e0 + e_base + e++] - i0);
-            }
-            __syncthreads();
-            return false;
-        }
-        // the tiles' ordinals: the next tile's loads in flight during this
-        // tile's emission (the tile holds read ids: the emission is LDS reads,
-        // a wave scan and stores, no dependent global load)
-        constexpr uint32_t TPT = RANK_TILE / BIN_THREADS;
-        uint32_t nx[TPT];
-        auto fetch = [&](uint32_t t) {
-#pragma unroll
-            for (uint32_t u = 0; u < TPT; u++) {
-                const uint32_t i = t + tid + u * BIN_THREADS;
-                nx[u] = i < R ? rord_bin[i] : 0u;
-            }
-        };
-        fetch(0);
-        for (uint32_t t0 = 0; t0 < R; t0 += RANK_TILE) {
-            const uint32_t tn = min(RANK_TILE, R - t0);
-#pragma unroll
-            for (uint32_t u = 0; u < TPT; u++) {
-                const uint32_t i = tid + u * BIN_THREADS;
-                if (i < tn) tile[i] = (uint32_t)id_of(nx[u], read_ids, id_off);
-            }
-            lds_barrier();
-            if (t0 + RANK_TILE < R) fetch(t0 + RANK_TILE);
-            static_assert(RANK_TILE == 64u * 32u, "one bitmap word per lane covers a tile");
-            for (uint32_t e = g0 + wid; e < g1; e += BIN_WAVES) {
-                const uint32_t* b = bm + (e - g0) * W;
-                uint32_t run = offs[e];
-                // one bitmap word (32 ranks) per lane: a wave scan of the
-                // words' bit counts gives each lane its first position, then
-                // each lane writes its set bits' ids in rank order
-                uint32_t x = lane * 32u < tn ? b[(t0 >> 5) + lane] : 0u;
-                const uint32_t pc = (uint32_t)__popc(x);
-                const uint32_t inc = wave_incl_scan(pc, (int)lane);
-                uint32_t pos = run + inc - pc;
-                while (x) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(x);
-                    x &= x - 1u;
-                    ids_out[i0 + pos++] = (int32_t)tile[lane * 32u + bit];
-                }
-                run += (uint32_t)__shfl((int)inc, 63, 64);
-                if (lane == 0) offs[e] = run;
-            }
-            lds_barrier();  // (the tile is the next tile's)
-        }
+        if (!bm_check(e_off, e_cnt, S, cnt, per, e0, i0, e_base, e_mine, g0, g1, bm, W)) return false;
+        bm_emit(ids_out, read_ids, id_off, i0, g0, g1, bm, W, offs, tile, R, rord_bin);
         PROF_MARK(19);
     }
     return true;
@@ -2356,18 +2391,44 @@ DEV void bin_body(const BinArgs& A) {
             // they fit the window area in at most RANK_GROUPS groups, else (or on
             // a key seen twice in one record) ordinals at their cursors and the
             // list kernels; then their slots leave the short lists' way
-            if (n_ent_all > n_ent) {
+            const bool win_phase = PHASE == 0 || (KW == 1 && A.win_heavy && !(flat && Lv > l0));
+            if (RANKED && n_ent_all > n_ent) {
                 PROF_MARK(3);
                 const uint32_t n_long = n_ent_all - n_ent;
                 const uint32_t R = hi - lo, W = (R + 31u) / 32u;
                 const uint32_t fixed = ((n_long + 3u) & ~3u) + RANK_TILE;
-                const uint32_t G = fixed + W <= win_cap ? (win_cap - fixed) / W : 0u;
-                const bool bm_ok = G && (n_long + G - 1u) / G <= RANK_GROUPS &&
-                                   bitmap_lists<KW>(A.e_off, A.e_cnt, A.ids_out, A.read_ids, A.id_off, S, cnt, ts, win, win_cap,
-                                                    S.n_stage, e0, i0, n_long, n_ent, (uint32_t)ex_l, sp_ord, sp_slot,
-                                                    R, A.rord + lo PROF_ARGS);
-                if (bm_ok) {
+                // merged: the short lists take the LDS windows and every long
+                // list's bitmap sits past them, so the windows' first stage pass
+                // also sets the bits (one stage pass less)
+                const uint32_t tail = fixed + n_long * W;
+                const bool merged = n_ent && win_phase && lds_ok && tail + S.maxc + 3u + 256u <= win_cap &&
+                                    n_ids <= 64u * n_ent && A.rank_merge;
+                bool bm_ok;
+                if (merged) {
+                    uint32_t* offs = win + (win_cap - tail);
+                    uint32_t* tile = offs + ((n_long + 3u) & ~3u);
+                    uint32_t* bm = tile + RANK_TILE;
+                    bm_remap(cnt, per, (uint32_t)ex_l, offs);
+                    for (uint32_t i = tid; i < n_long * W; i += BIN_THREADS) bm[i] = 0;
+                    if (tid == 0) S.dup = 0;
+                    __syncthreads();
+                    lds_lists<KW, RANKED>(A, S, cnt, ts, win, win_cap - tail, S.n_stage, e0, i0, n_ent, n_ids, stage,
+                                          sp_ord, sp_slot, (uint32_t)ex, A.rord + lo, bm, W PROF_ARGS);
+                    __syncthreads();
+                    PROF_MARK(18);
+                    bm_ok = bm_check(A.e_off, A.e_cnt, S, cnt, per, e0, i0, n_ent, (uint32_t)ex_l, 0u, n_long, bm, W);
+                    if (bm_ok) bm_emit(A.ids_out, A.read_ids, A.id_off, i0, 0u, n_long, bm, W, offs, tile, R, A.rord + lo);
+                    PROF_MARK(19);
                     if (tid == 0 && A.pstat) atomicAdd(&A.pstat[10], 1ull);
+                } else {
+                    const uint32_t G = fixed + W <= win_cap ? (win_cap - fixed) / W : 0u;
+                    bm_ok = G && (n_long + G - 1u) / G <= RANK_GROUPS &&
+                            bitmap_lists<KW>(A.e_off, A.e_cnt, A.ids_out, A.read_ids, A.id_off, S, cnt, ts, win, win_cap,
+                                             S.n_stage, e0, i0, n_long, n_ent, (uint32_t)ex_l, sp_ord, sp_slot,
+                                             R, A.rord + lo PROF_ARGS);
+                }
+                if (bm_ok) {
+                    if (!merged && tid == 0 && A.pstat) atomicAdd(&A.pstat[10], 1ull);
                 } else {
                     // ranks at their cursors, then the long lists' id range mapped
                     // to ordinals in one coalesced pass (no gather inside the
@@ -2400,16 +2461,15 @@ DEV void bin_body(const BinArgs& A) {
                 __threadfence_block();
                 __syncthreads();
                 PROF_MARK(17);
-                if (!n_ent) continue;
+                if (!n_ent || merged) continue;  // (merged: the short lists are out too)
             }
             // LDS id windows for short lists (mean <= 64 ids): light bins, and
             // the heavy bins' unfiltered partitions with one-word keys (C4
             // share 588 -> 502 ms per step); long lists (C3: 357 -> 479 ms)
             // and two-word keys (C5: 624 -> 641 ms) keep the global path
-            const bool win_phase = PHASE == 0 || (KW == 1 && A.win_heavy && !(flat && Lv > l0));
             if (win_phase && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
-                lds_lists<KW>(A, S, cnt, ts, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage, sp_ord, sp_slot,
-                              (uint32_t)ex, rmode ? A.rord + lo : nullptr PROF_ARGS);
+                lds_lists<KW, RANKED>(A, S, cnt, ts, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage, sp_ord,
+                                      sp_slot, (uint32_t)ex, rmode ? A.rord + lo : nullptr, nullptr, 0u PROF_ARGS);
                 PROF_MARK(4);
                 continue;
             }

@@ -323,6 +323,7 @@ struct BinArgs {
     // over the bin's ranks and emits each list by walking the bitmap: reverse
     // call order (binning.c:1061-1068) with no sort and no list kernels
     uint32_t rank_mode;        // 1: rank bins of 512 .. rank_max records (KB_BIN_RANK)
+    uint32_t rank_merge;       // ranked bins: long lists' bitmaps set in the id windows' stage pass (KB_BIN_RANK_MERGE)
     uint32_t* rrank;           // [R] record -> rank in its bin
     uint32_t* rord;            // [R] (bin start + rank) -> ordinal
 };
