@@ -7,6 +7,10 @@
  * materialises the surviving (mmer, kmer) entries into the caller's level-1
  * table as reference-layout ZHashTable / ll_node structures.
  */
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE /* RTLD_DEFAULT */
+#endif
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdio.h>
 #if defined(__GLIBC__)
@@ -293,6 +297,81 @@ static void thp_hint(const void *p, uintptr_t *last)
     (void)p;
     (void)last;
 #endif
+}
+
+/* List-node arena.  The drop-in's ~10^9-10^10 list nodes (the prune's
+ * materialised lists, create_node_num; expand_read_id_list's copies,
+ * duplicate_llist) are 16-B blocks that glibc rounds up to 32-B chunks, one
+ * locked-arena malloc each.  When this file's free() is the process's free
+ * (the drop-in executable links it: a strong definition in the executable
+ * interposes libc's for every library), nodes are instead bumped out of
+ * per-thread 64 MiB chunks of one reserved mapping (huge-page hinted, 16 B
+ * per node), and free() of a pointer inside it is a no-op -- the reference's
+ * own frees of nodes (free_llist, merge_lists: llist.c:101-108,
+ * binning.c:174-181) stay valid, the memory returns at exit.  Every other
+ * pointer goes to glibc's __libc_free.  Loaded any other way (a ctypes
+ * library, RTLD_LOCAL) the process's free is libc's, the arena stays off and
+ * nodes are malloc'd.  KBH_NODE_ARENA=0: off. */
+#define NODE_ARENA_RESERVE ((uint64_t)512 << 30)
+#define NODE_ARENA_CHUNK ((uint64_t)64 << 20)
+static char *volatile g_node_base; /* set once, before any node exists */
+static uint64_t g_node_next;
+static pthread_once_t g_node_once = PTHREAD_ONCE_INIT;
+extern void __libc_free(void *);
+
+static void node_free(void *p)
+{
+    char *const b = g_node_base;
+    if (b && (char *)p >= b && (char *)p < b + NODE_ARENA_RESERVE) return;
+    __libc_free(p);
+}
+void free(void *p) __attribute__((alias("node_free")));
+
+static void node_arena_init(void)
+{
+#if defined(__linux__)
+    const char *e = getenv("KBH_NODE_ARENA");
+    if (e && *e == '0') return;
+    void *(*const d)(void *, const char *) = dlsym;
+    if ((void *)d(RTLD_DEFAULT, "free") != (void *)node_free) return; /* not the process's free */
+    void *m = mmap(NULL, NODE_ARENA_RESERVE, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE,
+                   -1, 0);
+    if (m == MAP_FAILED) return;
+#if defined(MADV_HUGEPAGE)
+    if (!getenv("KBH_NO_THP")) (void)madvise(m, NODE_ARENA_RESERVE, MADV_HUGEPAGE);
+#endif
+    g_node_base = m;
+#endif
+}
+
+int kbh_node_arena_active(void)
+{
+    pthread_once(&g_node_once, node_arena_init);
+    return g_node_base != NULL;
+}
+
+typedef struct {
+    char *cur, *end;
+    uintptr_t thp; /* (the malloc path's huge-page hint) */
+} node_alloc_t;
+
+static inline ll_node *node_new(node_alloc_t *a)
+{
+    if (a->cur == a->end) {
+        pthread_once(&g_node_once, node_arena_init);
+        const uint64_t off = g_node_base ? __atomic_fetch_add(&g_node_next, NODE_ARENA_CHUNK, __ATOMIC_RELAXED)
+                                         : NODE_ARENA_RESERVE;
+        if (off + NODE_ARENA_CHUNK > NODE_ARENA_RESERVE) { /* no arena (or it is spent): malloc */
+            ll_node *nd = xmalloc(sizeof *nd);
+            thp_hint(nd, &a->thp);
+            return nd;
+        }
+        a->cur = g_node_base + off;
+        a->end = a->cur + NODE_ARENA_CHUNK;
+    }
+    ll_node *nd = (ll_node *)a->cur;
+    a->cur += sizeof(ll_node);
+    return nd;
 }
 
 /* run fn(arg) on up to 16 threads (the caller is one of them) */
@@ -624,7 +703,7 @@ static void *direct_tables(void *arg)
     const int nc = (g_K + CHUNK_CHARS - 1) / CHUNK_CHARS;
     replay_buf b = {0};
     uint64_t nodes = 0, kept = 0;
-    uintptr_t arena = 0;
+    node_alloc_t na = {0, 0, 0};
     char ks[129];
     for (;;) {
         const uint64_t w = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
@@ -659,8 +738,7 @@ static void *direct_tables(void *arg)
                 const uint64_t o0 = kr->o0 & ~REC_ALIVE, o1 = o0 + kr->len;
                 ll_node *head = NULL, **lt = &head;
                 for (uint64_t k = o0; k < o1; k++) {
-                    ll_node *nd = xmalloc(sizeof *nd); /* create_node_num, llist.c:6-11 */
-                    thp_hint(nd, &arena);
+                    ll_node *nd = node_new(&na); /* create_node_num, llist.c:6-11 */
                     nd->next = NULL;
                     nd->read_id = r->ids[k];
                     *lt = nd;
@@ -1121,7 +1199,7 @@ static void *expand_tables(void *arg)
     uint64_t nodes = 0;
     int *ids = NULL;
     size_t cap = 0;
-    uintptr_t arena = 0;
+    node_alloc_t na = {0, 0, 0};
     for (;;) {
         const uint64_t w = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
         if (w >= j->n) break;
@@ -1147,8 +1225,7 @@ static void *expand_tables(void *arg)
                     if (i) { /* duplicate_llist */
                         ll_node **ct = &copy;
                         for (size_t q = 0; q < n; q++) {
-                            ll_node *nd = xmalloc(sizeof *nd);
-                            thp_hint(nd, &arena);
+                            ll_node *nd = node_new(&na);
                             nd->next = NULL;
                             nd->read_id = ids[q];
                             *ct = nd;
@@ -1157,7 +1234,7 @@ static void *expand_tables(void *arg)
                         nodes += n;
                         *ct = NULL;
                     }
-                    ll_node *o = xmalloc(sizeof *o); /* create_node_item */
+                    ll_node *o = node_new(&na); /* create_node_item */
                     o->next = NULL;
                     o->item = copy;
                     *ot = o;

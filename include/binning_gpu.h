@@ -88,6 +88,9 @@ int kbh_last_times(kbh_times *out);
  * slow, obviously-reference path) instead of the direct layout -- the two
  * must give identical tables (kbh_layout_digest). */
 int kbh_materialise_csr(struct ZHashTable *hash_table, const kb_csr *r, int prune, int replay_only);
+/* 1 when list nodes come from the node arena (binning_gpu.c: this library's
+ * free() is the process's, KBH_NODE_ARENA not 0), else 0 (malloc'd nodes) */
+int kbh_node_arena_active(void);
 /* digest of a two-level table's exact layout: size steps, counts, bucket
  * index and chain order of every entry, keys, list contents and order */
 uint64_t kbh_layout_digest(struct ZHashTable *hash_table);

@@ -5,6 +5,8 @@ unlinks, zhash.c:53-76/184-214, binning.c:1085-1144) on synthetic CSRs:
 identical size steps, bucket chains, chain order, keys and lists
 (kbh_layout_digest).  No GPU: the CSR is host memory built here."""
 import ctypes as C
+import os
+import pathlib
 
 import numpy as np
 import pytest
@@ -158,3 +160,29 @@ def test_expand_read_id_list(n, K, M, threads, monkeypatch):
     for _, ids in before.values():
         assert not any(a in seen for a, _ in ids)
     del keep, layout
+
+
+@pytest.mark.parametrize("threads", ["1", "8"])
+def test_node_arena(tmp_path, threads):
+    """The drop-in's list-node arena (binning_gpu.c node_new): a program
+    linked like the drop-in (its free() is the library's) gets arena nodes,
+    KBH_NODE_ARENA=0 malloc'd ones; the expanded lists are identical and
+    every node can be freed one by one as free_llist does (llist.c:101-108).
+    Loaded through ctypes (this process) the arena stays off."""
+    import subprocess
+    repo = pathlib.Path(__file__).resolve().parents[1]
+    lib = repo / "genome-assembly_amd" / "lib"
+    exe = tmp_path / "node_arena_check"
+    subprocess.run(["gcc", "-O2", "-pthread", str(repo / "tests" / "helpers" / "node_arena_check.c"),
+                    f"-L{lib}", "-lkbin_host", "-lkbin", f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
+    out = {}
+    for arena in ("1", "0"):
+        env = dict(os.environ, KBH_NODE_ARENA=arena, KBH_THREADS=threads)
+        r = subprocess.run([str(exe), "30000"], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        f = r.stdout.split()
+        out[arena] = (f[1], f[3], f[5], f[7])
+    assert out["1"][:3] == out["0"][:3]
+    assert int(out["1"][1]) > 0 and int(out["1"][2]) > 0
+    assert out["1"][3] == "1" and out["0"][3] == "0"
+    assert host_lib().kbh_node_arena_active() == 0
