@@ -4224,8 +4224,12 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
                                                                  uint64_t* __restrict__ regions, uint64_t cap,
                                                                  const uint64_t* __restrict__ rbase,
                                                                  unsigned long long* bfill, uint32_t* status,
-                                                                 unsigned long long* n_kmers) {
+                                                                 unsigned long long* n_kmers, int diag_group) {
     constexpr int PERT = 8;
+    // (diagnostic, KB_DIAG_CONVERT_GROUP: only the blocks of one XCD group
+    // b % 8 == 0 convert their records -- the rest are dropped, results wrong
+    // by design -- so a WRITE_SIZE pass can price cross-XCD line sharing)
+    if (diag_group && (blockIdx.x & 7u)) return;
     __shared__ uint32_t cnt[SK_MAX_DEST];
     __shared__ unsigned long long base[SK_MAX_DEST];
     const uint32_t maskM = (1u << (2 * M)) - 1u, halfM = 1u << (2 * M - 1);
@@ -4366,12 +4370,13 @@ hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int r
     if (!n_rec) return hipSuccess;
     if (NB < 1 || NB > SK_MAX_DEST || (spw != 2 && spw != 4)) return hipErrorInvalidValue;
     const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
+    static const int diag = getenv("KB_DIAG_CONVERT_GROUP") ? atoi(getenv("KB_DIAG_CONVERT_GROUP")) : 0;
     if (spw == 2)
         hipLaunchKernelGGL(sk_convert_buckets_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, K, bucket_map, sub_map, sub_stamp, regions, cap, rbase, bfill, status, n_kmers);
+                           NB, K, bucket_map, sub_map, sub_stamp, regions, cap, rbase, bfill, status, n_kmers, diag);
     else
         hipLaunchKernelGGL(sk_convert_buckets_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
-                           NB, K, bucket_map, sub_map, sub_stamp, regions, cap, rbase, bfill, status, n_kmers);
+                           NB, K, bucket_map, sub_map, sub_stamp, regions, cap, rbase, bfill, status, n_kmers, diag);
     return hipGetLastError();
 }
 
