@@ -4212,6 +4212,111 @@ hipError_t launch_bucket_sort(const BucketArgs& a, uint32_t NB, hipStream_t s) {
     return hipGetLastError();
 }
 
+// The receiver's plan for PERT records of a block trip (record k0 + j * 256 +
+// tid): the destination of its (last) piece, and of its edge piece when it is
+// cut (ne > 0 k-mers), its pay-layout header and span words.  In phases, so
+// that the record loads, then the map lookups, then the sub-bin lookups of all
+// PERT records are in flight together (one record's chain of dependent global
+// loads at a time left the kernel latency-bound).
+template <int SPW, int PERT>
+DEV void convert_plan(const uint64_t* __restrict__ recs, uint64_t n_rec, int rw, int M, uint32_t NB, int K,
+                      const uint32_t* __restrict__ bucket_map, const uint16_t* __restrict__ sub_map, uint64_t k0,
+                      uint32_t (&dst)[PERT], uint32_t (&dst2)[PERT], uint32_t (&ne)[PERT], uint32_t (&sub1)[PERT],
+                      uint64_t (&pay0)[PERT], uint64_t (&ps)[PERT][SPW], bool& neg, uint64_t& kmers) {
+    const uint32_t maskM = (1u << (2 * M)) - 1u, halfM = 1u << (2 * M - 1);
+    uint32_t canon[PERT], me[PERT];
+#pragma unroll
+    for (int j = 0; j < PERT; j++) {
+        const uint64_t k = k0 + (uint64_t)j * 256 + threadIdx.x;
+        dst[j] = 0xFFFFFFFFu;
+        ne[j] = 0;
+        sub1[j] = 0;
+        me[j] = 0;
+        if (k >= n_rec) continue;
+        const uint64_t* r = recs + k * (uint64_t)rw;
+        pay0[j] = r[0];
+#pragma unroll
+        for (int w = 0; w < SPW; w++) ps[j][w] = w + 1 < rw ? r[w + 1] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < PERT; j++) {
+        if (k0 + (uint64_t)j * 256 + threadIdx.x >= n_rec) continue;
+        const uint64_t h = pay0[j];
+        const uint32_t id = (uint32_t)h;
+        const uint64_t lo = (h >> 32) & 0xFFFFu, n = (h >> 48) & 63u, so = (h >> 54) & 63u;
+        // the signature (so <= 56) ends inside the first two span words
+        const uint32_t sm = (uint32_t)(span_window(ps[j][0], ps[j][1], 0ull, 0ull, (int)so) >> (64 - 2 * M));
+        const bool rev = sm < halfM;  // complement wins (binning.c:1029-1040)
+        canon[j] = rev ? maskM - sm : sm;
+        neg |= (int32_t)id < 0;
+        kmers += n;
+        pay0[j] = (uint64_t)id | (n << 32) | (so << 38) | ((uint64_t)rev << 44) | (lo << 45);
+        dst[j] = 0;
+    }
+    if (bucket_map) {
+#pragma unroll
+        for (int j = 0; j < PERT; j++)
+            if (dst[j] != 0xFFFFFFFFu) me[j] = bucket_map[canon[j] - halfM];
+#pragma unroll
+        for (int j = 0; j < PERT; j++) {
+            if (dst[j] == 0xFFFFFFFFu) continue;
+            const uint32_t b = bm_depth(me[j]);
+            if (!b) {
+                dst[j] = me[j] & 1023u;
+                continue;
+            }
+            const uint64_t h = pay0[j];
+            const int n = (int)((h >> 32) & 63u), so = (int)((h >> 38) & 63u);
+            const bool rev = ((h >> 44) & 1u) != 0;
+            const int e = sub_edge(so, n, K, M, b);
+            // the context at so + M: past the first two span words
+            // when a long (K > 31) record's first k-mers are its edge
+            const uint64_t wc = span_window(ps[j][0], ps[j][1], SPW > 2 ? ps[j][SPW > 2 ? 2 : 0] : 0ull,
+                                            SPW > 3 ? ps[j][SPW > 3 ? 3 : 0] : 0ull, so + M);
+            if (e > 0 && e < n) ne[j] = (uint32_t)e;
+            sub1[j] = sub_ctx(so - (int)ne[j], K, M, b, wc, rev);
+        }
+#pragma unroll
+        for (int j = 0; j < PERT; j++) {
+            if (dst[j] == 0xFFFFFFFFu || !(me[j] & BM_SPLIT)) continue;
+            const uint32_t off = me[j] & 0x0FFFFFFFu;
+            dst[j] = sub_map[off + sub1[j]];
+            if (ne[j]) dst2[j] = sub_map[off];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < PERT; j++)
+            if (dst[j] != 0xFFFFFFFFu) dst[j] = dest_of(canon[j], NB, BUCKET_SALT);
+    }
+}
+
+// the 1 + SPW words of one piece of a planned record: the edge piece (its
+// first ne k-mers, same span start, sub-bin 0) or the (last) piece (k-mers
+// ne.., span from base ne, signature ne closer, its sub-bin stamped)
+template <int SPW>
+DEV void convert_piece(uint64_t h, const uint64_t (&ps)[SPW], uint32_t ne, uint32_t sub1, uint64_t stamp, bool edge,
+                       uint64_t (&o)[1 + SPW]) {
+    if (edge) {
+        o[0] = (h & ~(63ull << 32)) | ((uint64_t)ne << 32);
+#pragma unroll
+        for (int w = 0; w < SPW; w++) o[1 + w] = w + 1 == SPW ? ps[w] & ~stamp : ps[w];
+    } else if (ne) {
+        const uint64_t c = ne;
+        const uint64_t n = (h >> 32) & 63u, so = (h >> 38) & 63u, lo = (h >> 45) & 0xFFFFu;
+        o[0] = (h & 0xFFFFFFFFull) | ((n - c) << 32) | ((so - c) << 38) | (h & (1ull << 44)) | ((lo + c) << 45);
+        const uint64_t sw[4] = {ps[0], ps[1], SPW > 2 ? ps[SPW > 2 ? 2 : 0] : 0ull, SPW > 3 ? ps[SPW > 3 ? 3 : 0] : 0ull};
+#pragma unroll
+        for (int w = 0; w < SPW; w++) {
+            const uint64_t x = span_window(sw[0], sw[1], sw[2], sw[3], (int)c + 32 * w);
+            o[1 + w] = w + 1 == SPW ? (x & ~stamp) | (sub1 & stamp) : x;
+        }
+    } else {
+        o[0] = h;
+#pragma unroll
+        for (int w = 0; w < SPW; w++) o[1 + w] = w + 1 == SPW ? (ps[w] & ~stamp) | (sub1 & stamp) : ps[w];
+    }
+}
+
 // received routed records -> local bucket regions (pay layout, ordinal = id,
 // 1 + spw words); a block reserves one range per bucket for its 256 x 8
 // records.  A split mmer's record goes to its context sub-bin's bucket, cut in
@@ -4232,83 +4337,16 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
     if (diag_group && (blockIdx.x & 7u)) return;
     __shared__ uint32_t cnt[SK_MAX_DEST];
     __shared__ unsigned long long base[SK_MAX_DEST];
-    const uint32_t maskM = (1u << (2 * M)) - 1u, halfM = 1u << (2 * M - 1);
     bool neg = false;
     uint64_t kmers = 0;
+    const uint64_t stamp = sub_stamp ? SUB_MASK : 0ull;  // (a bucket record's last span word carries its sub-bin)
     for (uint64_t k0 = (uint64_t)blockIdx.x * 256 * PERT; k0 < n_rec; k0 += (uint64_t)gridDim.x * 256 * PERT) {
         for (uint32_t d = threadIdx.x; d < NB; d += 256) cnt[d] = 0;
         __syncthreads();
-        // per record: the destination of its (last) piece, and of its edge
-        // piece when it is cut (ne > 0 k-mers).  In phases, so that the
-        // record loads, then the map lookups, then the sub-bin lookups of all
-        // PERT records are in flight together (one record's chain of
-        // dependent global loads at a time left the kernel latency-bound)
-        uint32_t dst[PERT], dst2[PERT], ne[PERT], sub1[PERT];  // sub1: the (last) piece's sub-bin
-        uint32_t canon[PERT], me[PERT];
+        uint32_t dst[PERT], dst2[PERT], ne[PERT], sub1[PERT];
         uint64_t pay0[PERT], ps[PERT][SPW];
-#pragma unroll
-        for (int j = 0; j < PERT; j++) {
-            const uint64_t k = k0 + (uint64_t)j * 256 + threadIdx.x;
-            dst[j] = 0xFFFFFFFFu;
-            ne[j] = 0;
-            sub1[j] = 0;
-            me[j] = 0;
-            if (k >= n_rec) continue;
-            const uint64_t* r = recs + k * (uint64_t)rw;
-            pay0[j] = r[0];
-#pragma unroll
-            for (int w = 0; w < SPW; w++) ps[j][w] = w + 1 < rw ? r[w + 1] : 0ull;
-        }
-#pragma unroll
-        for (int j = 0; j < PERT; j++) {
-            if (k0 + (uint64_t)j * 256 + threadIdx.x >= n_rec) continue;
-            const uint64_t h = pay0[j];
-            const uint32_t id = (uint32_t)h;
-            const uint64_t lo = (h >> 32) & 0xFFFFu, n = (h >> 48) & 63u, so = (h >> 54) & 63u;
-            // the signature (so <= 56) ends inside the first two span words
-            const uint32_t sm = (uint32_t)(span_window(ps[j][0], ps[j][1], 0ull, 0ull, (int)so) >> (64 - 2 * M));
-            const bool rev = sm < halfM;  // complement wins (binning.c:1029-1040)
-            canon[j] = rev ? maskM - sm : sm;
-            neg |= (int32_t)id < 0;
-            kmers += n;
-            pay0[j] = (uint64_t)id | (n << 32) | (so << 38) | ((uint64_t)rev << 44) | (lo << 45);
-            dst[j] = 0;
-        }
-        if (bucket_map) {
-#pragma unroll
-            for (int j = 0; j < PERT; j++)
-                if (dst[j] != 0xFFFFFFFFu) me[j] = bucket_map[canon[j] - halfM];
-#pragma unroll
-            for (int j = 0; j < PERT; j++) {
-                if (dst[j] == 0xFFFFFFFFu) continue;
-                const uint32_t b = bm_depth(me[j]);
-                if (!b) {
-                    dst[j] = me[j] & 1023u;
-                    continue;
-                }
-                const uint64_t h = pay0[j];
-                const int n = (int)((h >> 32) & 63u), so = (int)((h >> 38) & 63u);
-                const bool rev = ((h >> 44) & 1u) != 0;
-                const int e = sub_edge(so, n, K, M, b);
-                // the context at so + M: past the first two span words
-                // when a long (K > 31) record's first k-mers are its edge
-                const uint64_t wc = span_window(ps[j][0], ps[j][1], SPW > 2 ? ps[j][SPW > 2 ? 2 : 0] : 0ull,
-                                                SPW > 3 ? ps[j][SPW > 3 ? 3 : 0] : 0ull, so + M);
-                if (e > 0 && e < n) ne[j] = (uint32_t)e;
-                sub1[j] = sub_ctx(so - (int)ne[j], K, M, b, wc, rev);
-            }
-#pragma unroll
-            for (int j = 0; j < PERT; j++) {
-                if (dst[j] == 0xFFFFFFFFu || !(me[j] & BM_SPLIT)) continue;
-                const uint32_t off = me[j] & 0x0FFFFFFFu;
-                dst[j] = sub_map[off + sub1[j]];
-                if (ne[j]) dst2[j] = sub_map[off];
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < PERT; j++)
-                if (dst[j] != 0xFFFFFFFFu) dst[j] = dest_of(canon[j], NB, BUCKET_SALT);
-        }
+        convert_plan<SPW, PERT>(recs, n_rec, rw, M, NB, K, bucket_map, sub_map, k0, dst, dst2, ne, sub1, pay0, ps,
+                                neg, kmers);
 #pragma unroll
         for (int j = 0; j < PERT; j++) {
             if (dst[j] == 0xFFFFFFFFu) continue;
@@ -4324,36 +4362,22 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
 #pragma unroll
         for (int j = 0; j < PERT; j++) {
             if (dst[j] == 0xFFFFFFFFu) continue;
-            const uint64_t h = pay0[j];
-            // (a bucket record's last span word carries its sub-bin, sub_room)
-            const uint64_t stamp = sub_stamp ? SUB_MASK : 0ull;
-            if (ne[j]) {  // the edge piece (sub-bin 0): the record's first ne k-mers, same span start
+            uint64_t o[1 + SPW];
+            if (ne[j]) {  // the edge piece first
                 const uint64_t slot = base[dst2[j]] + atomicAdd(&cnt[dst2[j]], 1u);
                 if (slot < region_room(rbase, cap, dst2[j])) {
-                    uint64_t* o = regions + (region_off(rbase, cap, dst2[j]) + slot) * (1 + SPW);
-                    o[0] = (h & ~(63ull << 32)) | ((uint64_t)ne[j] << 32);
+                    convert_piece<SPW>(pay0[j], ps[j], ne[j], sub1[j], stamp, true, o);
+                    uint64_t* op = regions + (region_off(rbase, cap, dst2[j]) + slot) * (1 + SPW);
 #pragma unroll
-                    for (int w = 0; w < SPW; w++) o[1 + w] = w + 1 == SPW ? ps[j][w] & ~stamp : ps[j][w];
+                    for (int w = 0; w <= SPW; w++) op[w] = o[w];
                 }
             }
             const uint64_t slot = base[dst[j]] + atomicAdd(&cnt[dst[j]], 1u);
             if (slot >= region_room(rbase, cap, dst[j])) continue;  // counted: the caller retries bigger
-            uint64_t* o = regions + (region_off(rbase, cap, dst[j]) + slot) * (1 + SPW);
-            if (ne[j]) {  // the rest: k-mers ne.., span from base ne, signature ne closer
-                const uint64_t c = ne[j];
-                const uint64_t n = (h >> 32) & 63u, so = (h >> 38) & 63u, lo = (h >> 45) & 0xFFFFu;
-                o[0] = (h & 0xFFFFFFFFull) | ((n - c) << 32) | ((so - c) << 38) | (h & (1ull << 44)) | ((lo + c) << 45);
-                uint64_t sw[4] = {ps[j][0], ps[j][1], SPW > 2 ? ps[j][SPW > 2 ? 2 : 0] : 0ull, SPW > 3 ? ps[j][SPW > 3 ? 3 : 0] : 0ull};
+            convert_piece<SPW>(pay0[j], ps[j], ne[j], sub1[j], stamp, false, o);
+            uint64_t* op = regions + (region_off(rbase, cap, dst[j]) + slot) * (1 + SPW);
 #pragma unroll
-                for (int w = 0; w < SPW; w++) {
-                    const uint64_t x = span_window(sw[0], sw[1], sw[2], sw[3], (int)c + 32 * w);
-                    o[1 + w] = w + 1 == SPW ? (x & ~stamp) | (sub1[j] & stamp) : x;
-                }
-            } else {
-                o[0] = h;
-#pragma unroll
-                for (int w = 0; w < SPW; w++) o[1 + w] = w + 1 == SPW ? (ps[j][w] & ~stamp) | (sub1[j] & stamp) : ps[j][w];
-            }
+            for (int w = 0; w <= SPW; w++) op[w] = o[w];
         }
         __syncthreads();
     }
@@ -4369,8 +4393,8 @@ hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int r
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s) {
     if (!n_rec) return hipSuccess;
     if (NB < 1 || NB > SK_MAX_DEST || (spw != 2 && spw != 4)) return hipErrorInvalidValue;
-    const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
     static const int diag = getenv("KB_DIAG_CONVERT_GROUP") ? atoi(getenv("KB_DIAG_CONVERT_GROUP")) : 0;
+    const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
     if (spw == 2)
         hipLaunchKernelGGL(sk_convert_buckets_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
                            NB, K, bucket_map, sub_map, sub_stamp, regions, cap, rbase, bfill, status, n_kmers, diag);
