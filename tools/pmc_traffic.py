@@ -66,13 +66,18 @@ def main():
                                                         "bin_parts_kernel",
                                                         "bins_final_kernel"))]
     if phase:
-        # (a member dispatched once ran in the cold pass only -- the plain
-        # bin_kernel before ranked bins are enabled: no steady bytes)
-        steady_m = [k for k in phase if table[k]["dispatches"] > 1]
+        # (of the bin kernel's variants only the most dispatched counts: the
+        # plain bin_kernel runs the passes before ranked bins are enabled --
+        # the cold one -- and bin_kernel_ranked every later one)
+        bk = [k for k in phase if "bin_kernel" in k]
+        main_bk = max(bk, key=lambda k: table[k]["dispatches"]) if bk else None
+        steady_m = [k for k in phase if "bin_kernel" not in k or k == main_bk]
+        first_bk = min(bk, key=lambda k: table[k]["dispatches"]) if bk else None  # (ran the cold pass)
+        cold_m = [k for k in phase if "bin_kernel" not in k or k == first_bk]
         table["bin phase"] = {"dispatches": min(table[k]["dispatches"] for k in steady_m or phase),
                               "members": sorted(phase),
                               "steady": {"bytes": sum(table[k]["steady"]["bytes"] for k in steady_m)},
-                              "cold": {"bytes": sum(table[k]["cold"]["bytes"] for k in phase)}}
+                              "cold": {"bytes": sum(table[k]["cold"]["bytes"] for k in cold_m)}}
     p = pathlib.Path(out)
     doc = json.loads(p.read_text()) if p.exists() else {}
     doc[tag] = {"hbm_bytes_per_launch": table[roof[0]]["steady"]["bytes"] if roof else None,
