@@ -1,10 +1,12 @@
-# r04 final evidence 5: C3 / C4 share / C5 share benches (digests), routed
+# r04 final evidence 5: the default bench line (reads the regenerated
+# traffic.json), C3 / C4 share / C5 share benches (digests), routed
 # C2, C3 kernel trace, the drop-in's C2 wall time
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r4f7; mkdir -p $O
 NOX="--cpu-sample 0 --no-capacity --no-host-input"
+timeout -k 10 600 python -u bench.py > $O/c2_bench.json 2> $O/c2_bench.err || exit 1
 timeout -k 10 400 python -u bench.py --cpu-sample 0 --workload c3 --steps 2 --warmup 1 --digest > $O/c3.json 2> $O/c3.err || exit 1
 timeout -k 10 400 python -u bench.py --cpu-sample 0 --workload c4 --steps 2 --warmup 1 --digest > $O/c4_share.json 2> $O/c4_share.err || exit 1
 timeout -k 10 500 python -u bench.py --cpu-sample 0 --workload c5 --steps 2 --warmup 2 --digest > $O/c5_share.json 2> $O/c5_share.err || exit 1
