@@ -1973,7 +1973,6 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.order = c->border.p;
         a.bdesc = use_desc ? c->bdesc.p : nullptr;
         a.work = reinterpret_cast<unsigned long long*>(c->totals.p + 7);
-        a.sched_static = (uint32_t)(env_int("KB_BIN_SCHED", 0) == 1);
         a.stage = c->stage.p;
         a.stage_ord = stage6 ? c->stage_ord.p : nullptr;
         a.stage_slot = stage6 ? c->stage_slot.p : nullptr;

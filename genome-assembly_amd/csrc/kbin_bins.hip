@@ -1753,8 +1753,7 @@ DEV void bin_body(const BinArgs& A) {
     // phase 0: block thread 0 claims the next bin one bin ahead, so the
     // claim's round trip overlaps this bin's work instead of opening the next
     unsigned long long next_item = 0;
-    if (PHASE == 0 && tid == 0 && !A.sched_static) next_item = atomicAdd(A.work, 1ull);
-    uint32_t round = 0;  // (static schedule: serpentine over the largest-first order)
+    if (PHASE == 0 && tid == 0) next_item = atomicAdd(A.work, 1ull);
 
     while (true) {
         // phase 0: persistent blocks take bins from a shared counter, largest
@@ -1763,11 +1762,7 @@ DEV void bin_body(const BinArgs& A) {
         // workgroup's serial loop)
         bar_lds(A);
         if (tid == 0) {
-            if (PHASE == 0 && A.sched_static) {
-                const uint32_t G = gridDim.x;
-                S.item = round * G + ((round & 1u) ? G - 1u - blockIdx.x : blockIdx.x);
-                round++;
-            } else if (PHASE == 0) {
+            if (PHASE == 0) {
                 S.item = (uint32_t)min(next_item, 0xFFFFFFFFull);
                 if (next_item < nbins) next_item = atomicAdd(A.work, 1ull);
             } else {

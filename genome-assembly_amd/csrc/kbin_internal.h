@@ -221,7 +221,6 @@ struct BinArgs {
     const uint4* bdesc;        // [2 nbins] or null: per processing slot {bin, start, count, mmer},
                                // {occurrences, stage base lo, hi, 0} (bins_desc_kernel)
     unsigned long long* work;  // work counter (zeroed)
-    uint32_t sched_static;     // phase 0: bins handed out serpentine by block (KB_BIN_SCHED=1), no claims
     uint64_t* stage;           // [N] (LDS slot << 48 | position << 32 | ordinal) per occurrence
     // light bins of the first phase without first-occurrence tracking: the
     // stage as two arrays, 6 B per occurrence (null: the 8-B stage everywhere)
