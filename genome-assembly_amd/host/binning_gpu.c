@@ -309,7 +309,8 @@ static void thp_hint(const void *p, uintptr_t *last)
  * per node), and free() of a pointer inside it is a no-op -- the reference's
  * own frees of nodes (free_llist, merge_lists: llist.c:101-108,
  * binning.c:174-181) stay valid, the memory returns at exit.  Every other
- * pointer goes to glibc's __libc_free.  Loaded any other way (a ctypes
+ * pointer goes to the free() this one shadows (RTLD_NEXT: a preloaded
+ * allocator's, else glibc's).  Loaded any other way (a ctypes
  * library, RTLD_LOCAL) the process's free is libc's, the arena stays off and
  * nodes are malloc'd.  KBH_NODE_ARENA=0: off. */
 #define NODE_ARENA_RESERVE ((uint64_t)512 << 30)
@@ -319,11 +320,28 @@ static uint64_t g_node_next;
 static pthread_once_t g_node_once = PTHREAD_ONCE_INIT;
 extern void __libc_free(void *);
 
+/* the free() this one shadows: the next definition in lookup order (an
+ * LD_PRELOADed allocator's, else glibc's), resolved once; until then, and if
+ * the lookup fails, glibc's own */
+static void (*volatile g_next_free)(void *);
+static int g_next_state; /* 0 unresolved, 1 resolving, 2 done */
+
 static void node_free(void *p)
 {
     char *const b = g_node_base;
     if (b && (char *)p >= b && (char *)p < b + NODE_ARENA_RESERVE) return;
-    __libc_free(p);
+    void (*f)(void *) = g_next_free;
+    if (!f) {
+        int expect = 0;
+        if (__atomic_compare_exchange_n(&g_next_state, &expect, 1, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+            void *(*const d)(void *, const char *) = dlsym; /* (may free: those go to glibc meanwhile) */
+            void (*nf)(void *) = (void (*)(void *))d(RTLD_NEXT, "free");
+            g_next_free = nf ? nf : __libc_free;
+            __atomic_store_n(&g_next_state, 2, __ATOMIC_RELEASE);
+        }
+        f = g_next_free ? g_next_free : __libc_free;
+    }
+    f(p);
 }
 void free(void *p) __attribute__((alias("node_free")));
 
