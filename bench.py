@@ -279,7 +279,11 @@ def load_traffic(tag: str, kernel: str):
         if not d:
             return None
         k = "bin phase" if kernel.startswith("bin phase") else kernel.split("<")[0]
-        row = next((v for name, v in d.get("per_kernel", {}).items() if k in name), None)
+        pk = d.get("per_kernel", {})
+        # (the tag's roofline kernel is its most-dispatched variant: ranked bins
+        # run bin_kernel_ranked, the cold pass the plain bin_kernel)
+        row = pk.get(d.get("kernel")) if k != "bin phase" and k in (d.get("kernel") or "") else None
+        row = row or next((v for name, v in pk.items() if k in name), None)
         if not row or "steady" not in row:
             return None
         return {"hbm_bytes_per_launch": row["steady"]["bytes"], "cold_bytes": row["cold"]["bytes"],
