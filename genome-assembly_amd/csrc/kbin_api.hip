@@ -285,6 +285,7 @@ struct kb_ctx {
     float rho = 0.f;           // learned distinct / occurrences
     float rho_tab = 0.f;       // learned table keys / occurrences under the singleton pre-filter
     bool pfl_regime = false;   // (sticky) a finalize ran light pre-filtered bins: sub-bins sized for the sketch
+    bool rank_regime = false;  // (sticky) a finalize ranked bins (long lists): smaller sub-bins, so more get ranked
     DevBuf<uint32_t> hll;      // cold pass: HyperLogLog registers (launch_hll)
     bool bucket_failed = false;  // a bucket overflowed its mmer map: radix path from now on
     bool prior_off = false;      // a prior map overflowed a bucket: hash routing for first passes
@@ -1231,7 +1232,10 @@ static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
     int bmax = std::min<int>((int)SUB_MAX_B, std::max(0, env_int("KB_BIN_SUB", (int)SUB_MAX_B)));
     if (!sub_room(c->p.K, c->p.M, 2 * c->KW)) bmax = 0;  // (no spare span bits for the stamp)
     const double ts = c->KW == 1 ? 8192.0 : 4096.0;
-    double cap = ts * std::min(4.0, std::max(0.2, env_int("KB_BIN_SUB_FILL_PCT", 80) / 100.0));
+    // (the long-list regime: sub-bins at 40 % of a table, so that they stay under
+    // the ranking's LDS limit and their long lists take the bitmaps -- C3 261 ->
+    // 247 ms per step, the list kernels 26 -> 4.5 ms)
+    double cap = ts * std::min(4.0, std::max(0.2, env_int("KB_BIN_SUB_FILL_PCT", c->rank_regime ? 40 : 80) / 100.0));
     // light pre-filtered bins (two-word keys, singleton-heavy): a sub-bin's
     // distinct keys only have to load the bin's sketch lightly (PFL_LOAD of
     // its PFL_CELLS); the table holds the keys seen twice
@@ -1248,7 +1252,7 @@ static uint64_t bin_budget(const kb_ctx* c, uint32_t NB) {
     // (at most 240: a bucket orders up to BK_SLOTS = 256 bins, one per mmer plus its extra sub-bins)
     // (the light pre-filtered regime splits every heavy mmer ~64 ways: a larger budget)
     const uint64_t per_bucket =
-        (uint64_t)std::min(240, std::max(0, env_int("KB_BIN_SUB_EXTRA", c->pfl_regime ? 160 : 48)));
+        (uint64_t)std::min(240, std::max(0, env_int("KB_BIN_SUB_EXTRA", c->rank_regime ? 240 : c->pfl_regime ? 160 : 48)));
     return half + (sub_room(c->p.K, c->p.M, 2 * c->KW) ? per_bucket * NB : 0ull);
 }
 
@@ -2092,6 +2096,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             const bool long_lists = c->hint_entries && c->hint_ids >= 64 * c->hint_entries;
             a.rank_mode = (rk == 2 || (rk == 1 && long_lists)) && stage6 && !a.e_first ? 1u : 0u;
             a.rank_merge = (uint32_t)(env_int("KB_BIN_RANK_MERGE", 1) != 0);
+            if (a.rank_mode) c->rank_regime = true;  // (the next maps split finer)
             if (a.rank_mode) {
                 HIPCHK(c->rrank.ensure(std::max<uint64_t>(R, 1)));
                 HIPCHK(c->rord.ensure(std::max<uint64_t>(R, 1)));

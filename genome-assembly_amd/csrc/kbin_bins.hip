@@ -1303,6 +1303,7 @@ DEV void bar_lds(const BinArgs& A) {
 // ---- ranked bins (see bin_ranks, bitmap_lists)
 constexpr uint32_t RANK_MIN = 512;    // fewer records: lists short, nothing to gain
 constexpr uint32_t RANK_TILE = 2048;  // ranks whose ordinals are staged in LDS at once (emission)
+constexpr uint32_t RANK_TILE_WORDS = 64u * 33u;  // the tile in LDS: lane l's 32 ranks at 33 l (no bank conflicts)
 constexpr uint32_t RANK_GROUPS = 8;   // most passes over the stage (entries whose bitmaps fit at once)
 constexpr uint32_t RANK_LONG = 256;   // ranked bins: lists longer than this take the bitmaps
 constexpr uint32_t LONGB = 0x40000000u;  // cnt of a ranked bin's kept long list: LONGB | cursor (< PRUNED)
@@ -1633,7 +1634,7 @@ DEV void bm_emit(int32_t* __restrict__ ids_out, const int32_t* __restrict__ read
 #pragma unroll
         for (uint32_t u = 0; u < TPT; u++) {
             const uint32_t i = tid + u * BIN_THREADS;
-            if (i < tn) tile[i] = (uint32_t)id_of(nx[u], read_ids, id_off);
+            if (i < tn) tile[(i >> 5) * 33u + (i & 31u)] = (uint32_t)id_of(nx[u], read_ids, id_off);
         }
         lds_barrier();
         if (t0 + RANK_TILE < R) fetch(t0 + RANK_TILE);
@@ -1648,7 +1649,7 @@ DEV void bm_emit(int32_t* __restrict__ ids_out, const int32_t* __restrict__ read
             while (x) {
                 const uint32_t bit = (uint32_t)__builtin_ctz(x);
                 x &= x - 1u;
-                ids_out[i0 + pos++] = (int32_t)tile[lane * 32u + bit];
+                ids_out[i0 + pos++] = (int32_t)tile[lane * 33u + bit];
             }
             run += (uint32_t)__shfl((int)inc, 63, 64);
             if (lane == 0) offs[e] = run;
@@ -1672,8 +1673,8 @@ DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __rest
     const uint32_t tid = threadIdx.x;
     const uint32_t per = ts / BIN_THREADS, W = (R + 31u) / 32u;
     uint32_t* offs = win;                  // [n_long] next position of each list (relative to i0)
-    uint32_t* tile = offs + ((n_long + 3u) & ~3u);  // [RANK_TILE] read ids of the current ranks
-    uint32_t* bm = tile + RANK_TILE;       // [G * W] the group's bitmaps
+    uint32_t* tile = offs + ((n_long + 3u) & ~3u);  // [RANK_TILE_WORDS] read ids of the current ranks
+    uint32_t* bm = tile + RANK_TILE_WORDS;  // [G * W] the group's bitmaps
     const uint32_t G = (win_cap - (uint32_t)(bm - win)) / W;
     bm_remap(cnt, per, e_mine, offs);
     for (uint32_t g0 = 0; g0 < n_long; g0 += G) {
@@ -2391,7 +2392,7 @@ DEV void bin_body(const BinArgs& A) {
                 PROF_MARK(3);
                 const uint32_t n_long = n_ent_all - n_ent;
                 const uint32_t R = hi - lo, W = (R + 31u) / 32u;
-                const uint32_t fixed = ((n_long + 3u) & ~3u) + RANK_TILE;
+                const uint32_t fixed = ((n_long + 3u) & ~3u) + RANK_TILE_WORDS;
                 // merged: the short lists take the LDS windows and every long
                 // list's bitmap sits past them, so the windows' first stage pass
                 // also sets the bits (one stage pass less)
@@ -2402,7 +2403,7 @@ DEV void bin_body(const BinArgs& A) {
                 if (merged) {
                     uint32_t* offs = win + (win_cap - tail);
                     uint32_t* tile = offs + ((n_long + 3u) & ~3u);
-                    uint32_t* bm = tile + RANK_TILE;
+                    uint32_t* bm = tile + RANK_TILE_WORDS;
                     bm_remap(cnt, per, (uint32_t)ex_l, offs);
                     for (uint32_t i = tid; i < n_long * W; i += BIN_THREADS) bm[i] = 0;
                     if (tid == 0) S.dup = 0;
