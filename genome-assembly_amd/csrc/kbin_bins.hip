@@ -1642,17 +1642,6 @@ DEV void bm_emit(int32_t* __restrict__ ids_out, const int32_t* __restrict__ read
         for (uint32_t e = g0 + wid; e < g1; e += BIN_WAVES) {
             const uint32_t* b = bm + (e - g0) * W;
             uint32_t run = offs[e];
-#ifdef KB_EMIT_BALLOT
-            // (A/B build) 64 ranks per step, consecutive lanes on consecutive
-            // ranks: the set ones' ids go out in one coalesced store per step
-            for (uint32_t c0 = 0; c0 < tn; c0 += 64u) {
-                const uint32_t r = c0 + lane;
-                const bool on = r < tn && ((b[(t0 + r) >> 5] >> (r & 31u)) & 1u);
-                const uint64_t m = __ballot(on);
-                if (on) ids_out[i0 + run + lanes_below(m)] = (int32_t)tile[(r >> 5) * 33u + (r & 31u)];
-                run += (uint32_t)__popcll(m);
-            }
-#else
             uint32_t x = lane * 32u < tn ? b[(t0 >> 5) + lane] : 0u;
             const uint32_t pc = (uint32_t)__popc(x);
             const uint32_t inc = wave_incl_scan(pc, (int)lane);
@@ -1663,7 +1652,6 @@ DEV void bm_emit(int32_t* __restrict__ ids_out, const int32_t* __restrict__ read
                 ids_out[i0 + pos++] = (int32_t)tile[lane * 33u + bit];
             }
             run += (uint32_t)__shfl((int)inc, 63, 64);
-#endif
             if (lane == 0) offs[e] = run;
         }
         lds_barrier();  // (the tile is the next tile's)
