@@ -1,6 +1,5 @@
 # r04 final evidence 10: the committed final tree -- GPU suite, smoke, default
-# via RTLD_NEXT, traffic lookup fixed): GPU suite, smoke, default bench line,
-# C3 leg with digest
+# bench line, C3 leg with digest
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
