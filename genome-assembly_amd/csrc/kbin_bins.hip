@@ -1306,7 +1306,7 @@ constexpr uint32_t RANK_TILE = 2048;  // ranks whose ordinals are staged in LDS 
 constexpr uint32_t RANK_TILE_WORDS = 64u * 33u;  // the tile in LDS: lane l's 32 ranks at 33 l (no bank conflicts)
 constexpr uint32_t RANK_GROUPS = 8;   // most passes over the stage (entries whose bitmaps fit at once)
 #ifndef KB_RANK_LONG
-#define KB_RANK_LONG 256
+#define KB_RANK_LONG 64
 #endif
 constexpr uint32_t RANK_LONG = KB_RANK_LONG;  // ranked bins: lists longer than this take the bitmaps (A/B builds: -DKB_RANK_LONG)
 constexpr uint32_t LONGB = 0x40000000u;  // cnt of a ranked bin's kept long list: LONGB | cursor (< PRUNED)
