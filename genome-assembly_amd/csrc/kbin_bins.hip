@@ -1301,7 +1301,10 @@ DEV void bar_lds(const BinArgs& A) {
 }
 
 // ---- ranked bins (see bin_ranks, bitmap_lists)
-constexpr uint32_t RANK_MIN = 512;    // fewer records: lists short, nothing to gain
+#ifndef KB_RANK_MIN
+#define KB_RANK_MIN 512
+#endif
+constexpr uint32_t RANK_MIN = KB_RANK_MIN;  // fewer records: lists short, nothing to gain (A/B builds: -DKB_RANK_MIN)
 constexpr uint32_t RANK_TILE = 2048;  // ranks whose ordinals are staged in LDS at once (emission)
 constexpr uint32_t RANK_TILE_WORDS = 64u * 33u;  // the tile in LDS: lane l's 32 ranks at 33 l (no bank conflicts)
 constexpr uint32_t RANK_GROUPS = 8;   // most passes over the stage (entries whose bitmaps fit at once)
