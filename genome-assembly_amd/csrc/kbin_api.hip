@@ -347,7 +347,7 @@ static int set_device(kb_ctx* c) {
     return KB_OK;
 }
 
-extern "C" int kb_abi_version(void) { return 2; }  // 2: kb_timing path counters
+extern "C" int kb_abi_version(void) { return 3; }  // 2: kb_timing path counters; 3: ranked-bin counters, kb_group_*
 
 extern "C" const char* kb_last_error(void) { return g_err.c_str(); }
 // (kbin_group.hip: a group call's failure is this thread's last error too)
@@ -2089,12 +2089,16 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.ldsbar = (uint32_t)(env_int("KB_BIN_LDSBAR", 1) != 0);
         a.ts_adapt = (uint32_t)(env_int("KB_BIN_TS_ADAPT", 1) != 0);
         a.corrupt = (uint32_t)(env_int("KB_DIAG_CORRUPT", 0) != 0);
+        a.skew = (uint32_t)std::max(0, env_int("KB_DIAG_SKEW", 0));
         // ranked bins where lists are long (the last finalize's mean list
         // length, C3: ~2200 ids): KB_BIN_RANK=0 off, 2 always
         {
             const int rk = env_int("KB_BIN_RANK", 1);
             const bool long_lists = c->hint_entries && c->hint_ids >= 64 * c->hint_entries;
-            a.rank_mode = (rk == 2 || (rk == 1 && long_lists)) && stage6 && !a.e_first ? 1u : 0u;
+            // (the bitmaps emit the long lists outside the list kernels, which
+            // then must take only the queued items: no ranking without the
+            // list queue, KB_BIN_LDS_LISTS=0)
+            a.rank_mode = (rk == 2 || (rk == 1 && long_lists)) && stage6 && !a.e_first && a.lq_items ? 1u : 0u;
             a.rank_merge = (uint32_t)(env_int("KB_BIN_RANK_MERGE", 1) != 0);
             if (a.rank_mode) c->rank_regime = true;  // (the next maps split finer)
             if (a.rank_mode) {

@@ -756,7 +756,12 @@ DEV uint64_t lds_load_u64(const uint64_t* p) {
 }
 
 struct alignas(16) BinShared {
-    uint32_t n_keys, overflow, sp, cur_p, cur_l, item, n_stage, part0;
+    uint32_t n_keys, overflow, cur_p, cur_l, item, n_stage, part0;
+    // the partition stack's depth, one word per partition parity: a partition
+    // (re)starts its stack without a barrier after the waves read the last
+    // one's empty stack, so it must not write the word a lagging wave is
+    // about to read (bin_body; round 4's KB_EDEVICE at r4f6)
+    uint32_t spq[2];
     uint32_t n_single;  // pre-filter: keys seen once in this partition
     uint32_t maxc;      // the partition's longest kept list (the LDS id windows)
     uint32_t sumc;      // the partition's occurrences counted in its table (the finalize's invariant)
@@ -2021,8 +2026,17 @@ DEV void bin_body(const BinArgs& A) {
         }
         for (uint32_t p0 = p_lo; p0 < p_hi; p0++) {
         const uint32_t olo = omode ? A.ocut[l0][p0] : 0u, ohi = omode ? A.ocut[l0][p0 + 1] : 64u;
+        // (this partition's stack depth lives in spq[p0 & 1]: a wave released
+        // from the last barrier of partition p0 - 1 may still be about to read
+        // that partition's empty word, spq[(p0 - 1) & 1], while tid 0 is
+        // already here -- writing it would send that wave into a partition
+        // loop the others have left, one barrier out of step with them for the
+        // rest of the bin: lost counts and keys claimed twice.  Partition
+        // p0 + 1 rewrites spq[(p0 + 1) & 1] only after p0's first zeroing
+        // barrier, which every wave passes after reading the old word)
+        const uint32_t pq = p0 & 1u;
         if (tid == 0) {
-            S.sp = 1;
+            S.spq[pq] = 1;
             S.stack_p[0] = omode ? 0u : p0;
             S.stack_l[0] = omode ? 0u : l0;
             S.ts = tsb;
@@ -2041,9 +2055,18 @@ DEV void bin_body(const BinArgs& A) {
             const uint32_t ts = S.ts, bmask = ts / 4 - 1, limit = ts - ts / 4;  // (uniform)
             // (the stack is stable here: every write to it is followed by a
             // barrier before the loop comes round; the pop is published after
-            // the zeroing barrier, so no wave reads S.sp while tid 0 writes it,
-            // and the empty stack leaves without zeroing a table no one uses)
-            const uint32_t sp0 = S.sp;
+            // the zeroing barrier, so no wave reads the depth while tid 0
+            // writes it, and the empty stack leaves without zeroing a table no
+            // one uses.  The next partition's start writes the other parity's
+            // word: see spq)
+#ifdef KB_BIN_ABL
+            // (diagnostic builds: one wave arrives late at every loop top --
+            // KB_DIAG_SKEW=w + 1 -- so a write-after-read across the last
+            // barrier shows deterministically; the test suite runs it)
+            if (A.skew && (tid >> 6) == A.skew - 1u)
+                for (int z = 0; z < 8; z++) __builtin_amdgcn_s_sleep(127);
+#endif
+            const uint32_t sp0 = S.spq[pq];
             if (sp0 == 0) break;  // uniform
             if (tid == 0) {
                 S.cur_p = S.stack_p[sp0 - 1u];
@@ -2064,7 +2087,7 @@ DEV void bin_body(const BinArgs& A) {
             if (PHASE == 1 && pfb)
                 for (uint32_t i = tid; i < sk_words; i += BIN_THREADS) sk[i] = 0;
             bar_lds(A);
-            if (tid == 0) S.sp = sp0 - 1u;
+            if (tid == 0) S.spq[pq] = sp0 - 1u;
             PROF_MARK(1);
             const uint32_t P = S.cur_p, Lv = S.cur_l;
             PROF_CNT(8, 1);
@@ -2274,19 +2297,20 @@ DEV void bin_body(const BinArgs& A) {
                 PROF_CNT(10, omode ? 1000000u + (ohi - olo) * 1000u + Lv : 0u);  // (diagnostic: offset-range overflows)
                 if (tid == 0) {
                     if (A.pstat) atomicAdd(&A.pstat[3], 1ull);
+                    uint32_t& sp = S.spq[pq];
                     if (ts < TS) {  // a larger table first
                         S.ts = min(TS, ts << 2);
-                        S.stack_p[S.sp] = P;
-                        S.stack_l[S.sp] = Lv;
-                        S.sp++;
-                    } else if (Lv >= 20 || S.sp + 2 > BIN_STACK) {
+                        S.stack_p[sp] = P;
+                        S.stack_l[sp] = Lv;
+                        sp++;
+                    } else if (Lv >= 20 || sp + 2 > BIN_STACK) {
                         atomicOr(A.status, ST_PROBE_LIMIT);
                     } else {
-                        S.stack_p[S.sp] = P;
-                        S.stack_l[S.sp] = Lv + 1;
-                        S.stack_p[S.sp + 1] = P + (1u << Lv);
-                        S.stack_l[S.sp + 1] = Lv + 1;
-                        S.sp += 2;
+                        S.stack_p[sp] = P;
+                        S.stack_l[sp] = Lv + 1;
+                        S.stack_p[sp + 1] = P + (1u << Lv);
+                        S.stack_l[sp + 1] = Lv + 1;
+                        sp += 2;
                     }
                 }
                 __syncthreads();
@@ -2387,6 +2411,10 @@ DEV void bin_body(const BinArgs& A) {
             __syncthreads();
             PROF_MARK(3);
             if (!room) continue;
+            // (read once here: a path that ends without another barrier --
+            // no kept ids -- must not read them after tid 0 reset them for the
+            // next partition)
+            const uint32_t n_stage = S.n_stage, maxc = S.maxc;
             const uint32_t n_ent_all = (uint32_t)tot;
             const uint32_t n_ent = (uint32_t)tot_s, n_ids = (uint32_t)(tot_s >> 32);  // the short lists
             // a ranked partition's long lists: from bitmaps over the ranks when
@@ -2403,7 +2431,7 @@ DEV void bin_body(const BinArgs& A) {
                 // list's bitmap sits past them, so the windows' first stage pass
                 // also sets the bits (one stage pass less)
                 const uint32_t tail = fixed + n_long * W;
-                const bool merged = n_ent && win_phase && lds_ok && tail + S.maxc + 3u + 256u <= win_cap &&
+                const bool merged = n_ent && win_phase && lds_ok && tail + maxc + 3u + 256u <= win_cap &&
                                     n_ids <= 64u * n_ent && A.rank_merge;
                 bool bm_ok;
                 if (merged) {
@@ -2414,7 +2442,7 @@ DEV void bin_body(const BinArgs& A) {
                     for (uint32_t i = tid; i < n_long * W; i += BIN_THREADS) bm[i] = 0;
                     if (tid == 0) S.dup = 0;
                     __syncthreads();
-                    lds_lists<KW, RANKED>(A, S, cnt, ts, win, win_cap - tail, S.n_stage, e0, i0, n_ent, n_ids, stage,
+                    lds_lists<KW, RANKED>(A, S, cnt, ts, win, win_cap - tail, n_stage, e0, i0, n_ent, n_ids, stage,
                                           sp_ord, sp_slot, (uint32_t)ex, A.rord + lo, bm, W PROF_ARGS);
                     __syncthreads();
                     PROF_MARK(18);
@@ -2426,7 +2454,7 @@ DEV void bin_body(const BinArgs& A) {
                     const uint32_t G = fixed + W <= win_cap ? (win_cap - fixed) / W : 0u;
                     bm_ok = G && (n_long + G - 1u) / G <= RANK_GROUPS &&
                             bitmap_lists<KW>(A.e_off, A.e_cnt, A.ids_out, A.read_ids, A.id_off, S, cnt, ts, win, win_cap,
-                                             S.n_stage, e0, i0, n_long, n_ent, (uint32_t)ex_l, sp_ord, sp_slot,
+                                             n_stage, e0, i0, n_long, n_ent, (uint32_t)ex_l, sp_ord, sp_slot,
                                              R, A.rord + lo PROF_ARGS);
                 }
                 if (bm_ok) {
@@ -2435,7 +2463,7 @@ DEV void bin_body(const BinArgs& A) {
                     // ranks at their cursors, then the long lists' id range mapped
                     // to ordinals in one coalesced pass (no gather inside the
                     // atomics' dependent chain)
-                    const uint32_t ns = S.n_stage;
+                    const uint32_t ns = n_stage;
                     for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
                         const uint32_t sl = sp_slot[i];
                         if (!sl || (cnt[sl - 1u] & (LONGB | PRUNED)) != LONGB) continue;
@@ -2469,8 +2497,8 @@ DEV void bin_body(const BinArgs& A) {
             // the heavy bins' unfiltered partitions with one-word keys (C4
             // share 588 -> 502 ms per step); long lists (C3: 357 -> 479 ms)
             // and two-word keys (C5: 624 -> 641 ms) keep the global path
-            if (win_phase && lds_ok && S.maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
-                lds_lists<KW, RANKED>(A, S, cnt, ts, win, win_cap, S.n_stage, e0, i0, n_ent, n_ids, stage, sp_ord,
+            if (win_phase && lds_ok && maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
+                lds_lists<KW, RANKED>(A, S, cnt, ts, win, win_cap, n_stage, e0, i0, n_ent, n_ids, stage, sp_ord,
                                       sp_slot, (uint32_t)ex, rmode ? A.rord + lo : nullptr, nullptr, 0u PROF_ARGS);
                 PROF_MARK(4);
                 continue;
@@ -2478,9 +2506,9 @@ DEV void bin_body(const BinArgs& A) {
             // ---- sweep 2: drop every surviving occurrence's call ordinal in place
             {
 #ifdef KB_BIN_ABL
-                const uint32_t ns = A.ablate ? 0u : S.n_stage;
+                const uint32_t ns = A.ablate ? 0u : n_stage;
 #else
-                const uint32_t ns = S.n_stage;
+                const uint32_t ns = n_stage;
 #endif
                 const bool filt = PHASE == 1 && flat && Lv > l0;
                 const uint32_t pmask = (1u << Lv) - 1u;

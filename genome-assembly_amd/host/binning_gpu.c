@@ -1014,6 +1014,50 @@ static void prune_materialised(struct ZHashTable *level1, int cutoff)
     }
 }
 
+/* ---- the rest of the reference's calling surface (north_star: the host keeps
+ * the getbp/getval 2-bit encoding and the prune API), for a host that links
+ * only libkbin_host + libkbin.  Weak: in the drop-in the reference's own
+ * binning.o defines the same symbols, and its strong ones win. */
+
+/* binning.c:69-88: 0..3 -> T, G, C, A; anything else -> 'A' */
+__attribute__((weak)) char getbp(int bp) { return bp >= 0 && bp < 4 ? BP[bp] : 'A'; }
+
+/* binning.c:91-111: T, G, C, A -> 0..3; any other byte -> 3 (as 'A') */
+__attribute__((weak)) int getval(char c)
+{
+    switch (c) {
+    case 'T': return 0;
+    case 'G': return 1;
+    case 'C': return 2;
+    default: return 3;
+    }
+}
+
+/* binning.c:114-124: the base-4 value, first character most significant
+ * (int arithmetic; long strings wrap as the reference's -O2 build does) */
+__attribute__((weak)) int getscore(char *string)
+{
+    unsigned score = 0;
+    for (; *string != '\0'; string++) score = score * 4u + (unsigned)getval(*string);
+    return (int)score;
+}
+
+/* binning.c:1085-1123 on one level-2 (kmer) table: every entry whose id list
+ * holds <= ABUNDANCE_CUTOFF (kbh_configure's cutoff) nodes is unlinked and
+ * freed, the table is never resized (the reference's iterator deletes in
+ * place), and an emptied table is freed and NULL returned.  (The reference
+ * frees only a pruned list's head node, :1106; the whole list is freed here.) */
+__attribute__((weak)) struct ZHashTable *prune_kmers(struct ZHashTable *hash_table)
+{
+    prune_level2(hash_table, g_cutoff);
+    if (hash_table->entry_count == 0) {
+        free(hash_table->entries);
+        free(hash_table);
+        return NULL;
+    }
+    return hash_table;
+}
+
 /* Multi-GPU: the reads of the whole loop, cut into G contiguous ranges (rank
  * g's reads all precede rank g+1's, so arrival order at every receiver is the
  * call order), each submitted with its call ORDINALS as ids -- lists then come

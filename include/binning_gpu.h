@@ -47,6 +47,19 @@ struct ZHashTable *prune_data(struct ZHashTable *hash_table);
  * the original list and strlen(key) - 1 malloc'd copies (worker threads) */
 void expand_read_id_list(struct ZHashTable *hashtable);
 
+/* The rest of binning.c's calling surface, same semantics, exported weak (a
+ * drop-in that links the reference's binning.o keeps the reference's own):
+ *   getbp     binning.c:69-88    0..3 -> 'T','G','C','A' (else 'A')
+ *   getval    binning.c:91-111   'T','G','C','A' -> 0..3 (else 3)
+ *   getscore  binning.c:114-124  base-4 value of a string, first char high
+ *   prune_kmers binning.c:1085-1123  one level-2 table: entries with <=
+ *             cutoff ids removed in place (no resize); NULL (table freed)
+ *             when it empties -- prune_data runs it over every mmer */
+char getbp(int bp);
+int getval(char c);
+int getscore(char *string);
+struct ZHashTable *prune_kmers(struct ZHashTable *hash_table);
+
 /* explicit configuration (else the compile-time defaults); device = HIP ordinal */
 int kbh_configure(int K, int M, int cutoff, int device);
 

@@ -343,7 +343,8 @@ kb_ctx *kb_group_ctx(kb_group *grp, int local);
 /* Message for the last failing call on this thread. */
 const char *kb_last_error(void);
 
-/* ABI version (bumped on incompatible change) */
+/* ABI version (bumped on incompatible change): 3 = kb_timing with the ranked-bin
+ * counters (ranked_bins, bitmap_partitions, ...) and the kb_group_* calls */
 int kb_abi_version(void);
 
 #ifdef __cplusplus

@@ -1,0 +1,66 @@
+"""Subprocess body of tests/test_gpu_race.py (the library build a process loads
+is fixed at its first load: KB_LIB_PATH picks the diagnostic build).
+
+Bins one seeded input three times in one context (cold pass, learned maps,
+KB_TIMING_KERNEL like bench.py's timed steps) and compares every finalize with
+the oracle.  Prints one JSON line: {"ok": bool, "finalizes": [...], "paths": {...}}.
+"""
+import json
+import pathlib
+import sys
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "genome-assembly_amd"))
+sys.path.insert(0, str(REPO / "oracle"))
+
+import numpy as np  # noqa: E402
+
+import kbin  # noqa: E402
+import oracle  # noqa: E402
+
+
+def same(res, ora):
+    c = res.canonical()
+    if c.n_entries != ora.n_entries:
+        return f"entries {c.n_entries} != {ora.n_entries}"
+    for f in ("mmer", "kmer_hi", "kmer_lo", "count", "offset", "ids"):
+        if not np.array_equal(getattr(c, f), getattr(ora, f)):
+            return f"field {f} differs"
+    return ""
+
+
+def main():
+    n_reads, glen, seed = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    rng = np.random.default_rng(seed)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=glen)
+    starts = rng.integers(0, glen - 150, n_reads)
+    reads = [genome[s:s + 150].tobytes() for s in starts]
+    bases, lens = kbin.pack_reads(reads)
+    ora = oracle.bin_reads(bases, lens, 31, 7, 1, True)
+    out = {"ok": True, "finalizes": [], "paths": {}}
+    with kbin.Engine(31, 7, cutoff=1, max_read_len=150) as eng:
+        for mode in (False, False, "kernel"):
+            eng.reset()
+            eng.set_timing(mode)
+            eng.submit(bases=bases, lens=lens, first_id=0)
+            try:
+                eng.finalize(prune=True)
+                err = same(eng.export(), ora)
+            except kbin.KbError as e:
+                err = str(e)
+            out["finalizes"].append(err or "ok")
+            if err:
+                out["ok"] = False
+        eng.set_timing(True)
+        eng.reset()
+        eng.submit(bases=bases, lens=lens, first_id=0)
+        try:
+            eng.finalize(prune=True)
+            out["paths"] = {k: v for k, v in eng.timing().items() if isinstance(v, (int, float))}
+        except kbin.KbError as e:
+            out["paths"] = {"error": str(e)}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

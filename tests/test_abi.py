@@ -51,7 +51,7 @@ def test_host_exports_reference_surface():
 
 
 def test_abi_version():
-    assert kbin.load_library().kb_abi_version() == 2
+    assert kbin.load_library().kb_abi_version() == 3
 
 
 def test_struct_layouts_match_header(tmp_path):

@@ -115,3 +115,35 @@ def test_result_digest_properties():
     assert np.any(ids != r.ids)
     swapped = kbin.Result(r.mmer, r.kmer_hi, r.kmer_lo, r.count, r.offset, ids, 0, 0)
     assert kbin.result_digest(swapped)[3] != d[3]
+
+
+def test_reference_surface_standalone(tmp_path):
+    """a C host linking only libkbin_host + libkbin finds
+    getbp / getval / getscore (binning.c:69-124) and prune_kmers
+    (binning.c:1085-1123) with the reference's semantics
+    (tests/helpers/host_surface_check.c; no GPU call)"""
+    import os
+    import pathlib
+    import subprocess
+    repo = pathlib.Path(__file__).resolve().parents[1]
+    lib = repo / "genome-assembly_amd" / "lib"
+    exe = tmp_path / "host_surface_check"
+    subprocess.run(["gcc", "-O2", "-pthread", str(repo / "tests" / "helpers" / "host_surface_check.c"),
+                    f"-L{lib}", "-lkbin_host", "-lkbin", f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=dict(os.environ))
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[-1] == "ok"
+    val = {"T": 0, "G": 1, "C": 2, "A": 3}
+    for ln in lines:
+        if not ln.startswith("score "):
+            continue
+        _, s, got = ln.split()
+        s = "" if s == "-" else s
+        want = 0
+        for ch in s:
+            want = (want * 4 + val[ch]) & 0xFFFFFFFF
+        want = want - (1 << 32) if want >= 1 << 31 else want
+        assert int(got) == want, (s, got, want)
+    assert any("all pruned -> NULL" in ln for ln in lines)
+    assert sum("kept" in ln for ln in lines) == 3
