@@ -265,6 +265,7 @@ struct kb_ctx {
     DevBuf<uint16_t> stage_slot;  // ... and LDS slots (6 B per occurrence)
     DevBuf<uint64_t> kstage;   // heavy bins: per-occurrence k-mer code + 1
     DevBuf<uint32_t> rrank, rord;  // ranked bins: record -> rank, rank -> ordinal (BinArgs::rank_mode)
+    DevBuf<BinArgs> bargs;         // the bin kernels' arguments (launch_bins)
     DevBuf<uint32_t> long_q;   // entries with 257..4096 ids (lists_long_kernel)
     DevBuf<uint64_t> lq;       // list items for lists_kernel (BinArgs::lq_items); [0] the counter
     DevBuf<uint32_t> border;   // bin processing order
@@ -472,7 +473,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     if (c->map_done) (void)hipEventDestroy(c->map_done);
     if (c->h_alpha) (void)hipHostFree(c->h_alpha);
     c->table.release(); c->occ_a.release();
-    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->stage_ord.release(); c->stage_slot.release(); c->kstage.release(); c->rrank.release(); c->rord.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
+    c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->stage_ord.release(); c->stage_slot.release(); c->kstage.release(); c->rrank.release(); c->rord.release(); c->bargs.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
     c->regions.release(); c->bfill.release(); c->bbase.release(); c->rbase.release(); c->kpart.release(); c->rcount.release();
     c->occ_b.release(); c->os_flags.release(); c->os_aux.release(); c->read_ids.release(); c->starts.release();
     c->e_mmer.release(); c->e_cnt.release(); c->e_hi.release(); c->e_hi_zeroed = nullptr;
@@ -2116,7 +2117,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         // totals say bin_kernel published or queued something
         const bool defer = attempt == 0 && c->hint_heavy == 0 && c->hint_lq == 0 && a.lq_items &&
                            env_int("KB_BIN_DEFER_TAIL", 1) != 0;
-        HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr, !defer));
+        HIPCHK(c->bargs.ensure_exact(1));
+        HIPCHK(launch_bins(a, max_bins, KW, c->s, c->timing ? &c->ev[6] : nullptr, !defer, c->bargs.p));
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
 #endif
@@ -2167,7 +2169,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             // full grids, then the totals again
             c->tm.tail_reruns++;
             a.heavy_hint = ~0ull;
-            HIPCHK(launch_bins_heavy(a, KW, c->s));
+            HIPCHK(launch_bins_heavy(a, KW, c->s, c->bargs.p));
             HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries,
                                      flat_l ? c->flat_n.p : nullptr, a.lq_n, c->s));
             la.lq_hint = ~0ull;

@@ -1331,6 +1331,9 @@ DEV bool is_long_slot(uint32_t c) { return (c & (LONGB | PRUNED)) == LONGB; }
 // from e_cnt / e_off (this block wrote them: L2).  Not inlined: its sorting
 // registers stay out of the sweeps' allocation.
 DEV void sort_lists_lane(uint32_t* p, uint32_t n);
+// words past a list window that sort_lists_lane may read (never write): the
+// end of bin_kernel's LDS carve and lists_kernel's window are padded by it
+constexpr uint32_t LIST_READ_PAD = 32;
 template <int R>
 DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane);
 
@@ -2577,22 +2580,34 @@ DEV void bin_body(const BinArgs& A) {
 #endif
 }
 
+// The bin kernels read their arguments from device memory (bin_args_kernel
+// puts them there, stream-ordered, right before): a by-value BinArgs is
+// loaded into SGPRs at entry and stays live through the whole persistent loop
+// (297 SGPRs and 25 VGPRs spilled, 104 B of scratch per lane in bin_kernel<1>);
+// through a pointer the fields are loaded nearer their uses
+__global__ __launch_bounds__(64) void bin_args_kernel(BinArgs a, BinArgs* __restrict__ dst) {
+    static_assert(sizeof(BinArgs) % 8 == 0, "copied in 8-B words");
+    constexpr uint32_t NW = sizeof(BinArgs) / 8;
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&a);
+    for (uint32_t i = threadIdx.x; i < NW; i += 64) reinterpret_cast<uint64_t*>(dst)[i] = src[i];
+}
+
 // phase 0: every light bin, and each heavy bin's flat lists
 template <int KW>
-__global__ __launch_bounds__(BIN_THREADS) void bin_kernel(BinArgs A) {
-    bin_body<KW, 0, false>(A);
+__global__ __launch_bounds__(BIN_THREADS) void bin_kernel(const BinArgs* __restrict__ A) {
+    bin_body<KW, 0, false>(*A);
 }
 
 // phase 0 with ranked bins (the long-list regime)
 template <int KW>
-__global__ __launch_bounds__(BIN_THREADS) void bin_kernel_ranked(BinArgs A) {
-    bin_body<KW, 0, true>(A);
+__global__ __launch_bounds__(BIN_THREADS) void bin_kernel_ranked(const BinArgs* __restrict__ A) {
+    bin_body<KW, 0, true>(*A);
 }
 
 // phase 1: the heavy bins' partitions, any block any partition
 template <int KW>
-__global__ __launch_bounds__(BIN_THREADS) void bin_parts_kernel(BinArgs A) {
-    bin_body<KW, 1>(A);
+__global__ __launch_bounds__(BIN_THREADS) void bin_parts_kernel(const BinArgs* __restrict__ A) {
+    bin_body<KW, 1>(*A);
 }
 
 // ---- the parallel build of published (heavy / split) bins.  Work items are
@@ -3184,11 +3199,21 @@ DEV void wave_sort_list(const uint32_t* __restrict__ src, int32_t* __restrict__ 
 // index is < N: a list of n <= N ids padded with zeros (below every id + 1)
 // keeps its pads in place, so the pruned network sorts it.  NP = 32: 191
 // comparators (the bitonic network: 240); N = 24: 132; 16: 63; 8: 19
+// (2 <= n <= N.  The loads and stores are branch-free -- a branch per
+// position saved the exec mask in an SGPR pair, and in bin_kernel those were
+// spilled to VGPR lanes: all N words are read (p[0 .. N) must lie inside the
+// LDS allocation: both callers leave LIST_READ_PAD words after their windows)
+// and the pads masked; position j >= n writes p[n - 1] instead, the stores
+// going out from the last position down, so p[n - 1] ends with its own value)
 template <int N, int NP>
 DEV void sort_net_desc(uint32_t* p, uint32_t n) {
     uint32_t v[N];
+    const uint32_t last = n - 1u;
 #pragma unroll
-    for (int j = 0; j < N; j++) v[j] = (uint32_t)j < n ? p[j] : 0u;
+    for (int j = 0; j < N; j++) {
+        const uint32_t x = p[j];
+        v[j] = (uint32_t)j < n ? x : 0u;
+    }
 #pragma unroll
     for (int q = 1; q < NP; q <<= 1)
 #pragma unroll
@@ -3205,8 +3230,7 @@ DEV void sort_net_desc(uint32_t* p, uint32_t n) {
                     }
                 }
 #pragma unroll
-    for (int j = 0; j < N; j++)
-        if ((uint32_t)j < n) p[j] = v[j];
+    for (int j = N - 1; j >= 0; j--) p[min((uint32_t)j, last)] = v[j];
 }
 
 // every lane's list of 2..32 ids (n outside that: nothing) in descending
@@ -3247,7 +3271,7 @@ __global__ __launch_bounds__(LIST_THREADS) __attribute__((amdgpu_waves_per_eu(5,
 #endif
     // staged chunks: ibuf = the chunk's ids (ordinal + 1); other chunks: buf =
     // block sort space (LIST_CAP), wave windows inside
-    __shared__ uint32_t lds[LIST_SPAN];
+    __shared__ uint32_t lds[LIST_SPAN + LIST_READ_PAD];  // (the pad: sort_lists_lane's reads)
     static_assert(LIST_CAP <= LIST_SPAN, "block sort space aliases the staging area");
     uint32_t* const ibuf = lds;
     uint32_t* const buf = lds;
@@ -4361,10 +4385,15 @@ __global__ __launch_bounds__(256) void sk_convert_buckets_kernel(const uint64_t*
                                                                  unsigned long long* bfill, uint32_t* status,
                                                                  unsigned long long* n_kmers, int diag_group) {
     constexpr int PERT = 8;
-    // (diagnostic, KB_DIAG_CONVERT_GROUP: only the blocks of one XCD group
-    // b % 8 == 0 convert their records -- the rest are dropped, results wrong
-    // by design -- so a WRITE_SIZE pass can price cross-XCD line sharing)
+#ifdef KB_BIN_ABL
+    // (diagnostic builds only, KB_DIAG_CONVERT_GROUP: only the blocks of one
+    // XCD group b % 8 == 0 convert their records -- the rest are dropped,
+    // results wrong by design -- so a WRITE_SIZE pass can price cross-XCD
+    // line sharing; ADVICE r04: never in the product library)
     if (diag_group && (blockIdx.x & 7u)) return;
+#else
+    (void)diag_group;
+#endif
     __shared__ uint32_t cnt[SK_MAX_DEST];
     __shared__ unsigned long long base[SK_MAX_DEST];
     bool neg = false;
@@ -4423,7 +4452,11 @@ hipError_t launch_sk_convert_buckets(const uint64_t* recs, uint64_t n_rec, int r
                                      uint32_t* status, unsigned long long* n_kmers, hipStream_t s) {
     if (!n_rec) return hipSuccess;
     if (NB < 1 || NB > SK_MAX_DEST || (spw != 2 && spw != 4)) return hipErrorInvalidValue;
+#ifdef KB_BIN_ABL
     static const int diag = getenv("KB_DIAG_CONVERT_GROUP") ? atoi(getenv("KB_DIAG_CONVERT_GROUP")) : 0;
+#else
+    const int diag = 0;
+#endif
     const uint64_t blocks = std::min<uint64_t>((n_rec + 2047) / 2048, 4096);
     if (spw == 2)
         hipLaunchKernelGGL(sk_convert_buckets_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, M,
@@ -4439,7 +4472,7 @@ size_t bins_lds_bytes(uint32_t ts_log2, int KW) {
     const size_t Q = KW == 1 ? bin_q<1>() : bin_q<2>();
     return sizeof(BinShared) + TS * (KW * sizeof(uint64_t) + sizeof(uint32_t)) +
            (size_t)BIN_WAVES * Q * (KW * sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint16_t)) +
-           (KW == 2 ? PFL_WORDS * sizeof(uint32_t) : 0);
+           (KW == 2 ? PFL_WORDS * sizeof(uint32_t) : 0) + LIST_READ_PAD * sizeof(uint32_t);
 }
 
 // the bin kernel's blocks (every CU, as many as fit) and the per-launch split
@@ -4468,8 +4501,10 @@ static hipError_t bins_grid(const BinArgs& a, uint64_t& blocks, int& cus, size_t
 // small when the last finalize published no such bin -- an empty launch then
 // costs its dispatch only; every kernel strides over its work, so a surprise
 // heavy bin is still binned, more slowly, once)
+// (d_args: this finalize's bin arguments, put there by launch_bins_kw's
+// bin_args_kernel -- bin_parts_kernel reads the same ones)
 template <int KW>
-static hipError_t launch_heavy_kw(const BinArgs& a, hipStream_t s) {
+static hipError_t launch_heavy_kw(const BinArgs& a, hipStream_t s, const BinArgs* d_args) {
     if (!a.flat_l) return hipSuccess;
     uint64_t blocks = 0;
     int cus = 0;
@@ -4486,35 +4521,40 @@ static hipError_t launch_heavy_kw(const BinArgs& a, hipStream_t s) {
     if (a2.fs_lds)
         hipLaunchKernelGGL(flat_scatter_lds_kernel<KW>, dim3(few ? 32u : (unsigned)std::max(1, cus)),
                            dim3(FSL_THREADS), fsl_lds_bytes<KW>(), s, a2);
-    hipLaunchKernelGGL(bin_parts_kernel<KW>, dim3(few ? 32u : (unsigned)blocks), dim3(BIN_THREADS), lds, s, a2);
+    hipLaunchKernelGGL(bin_parts_kernel<KW>, dim3(few ? 32u : (unsigned)blocks), dim3(BIN_THREADS), lds, s, d_args);
     return hipGetLastError();
 }
 
 template <int KW>
-static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_t s, hipEvent_t* ev_bin, bool heavy) {
+static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_t s, hipEvent_t* ev_bin, bool heavy,
+                                 BinArgs* d_args) {
     uint64_t blocks = 0;
     int cus = 0;
     size_t lds = 0;
     BinArgs a2;
     hipError_t e = bins_grid<KW>(a, blocks, cus, lds, a2);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(bin_args_kernel, dim3(1), dim3(64), 0, s, a2, d_args);
     // timing: the kernel's own start and stop (hipExtLaunchKernelGGL) -- an
     // event recorded on the stream before and after it idled the GPU ~6 us each
     hipExtLaunchKernelGGL(a.rank_mode ? bin_kernel_ranked<KW> : bin_kernel<KW>,
                           dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS),
-                          (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr, ev_bin ? ev_bin[1] : nullptr, 0u, a2);
+                          (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr, ev_bin ? ev_bin[1] : nullptr, 0u,
+                          (const BinArgs*)d_args);
     e = hipGetLastError();
     if (e != hipSuccess || !heavy) return e;
-    return launch_heavy_kw<KW>(a, s);
+    return launch_heavy_kw<KW>(a, s, d_args);
 }
 
-hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin, bool heavy) {
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin, bool heavy,
+                       BinArgs* d_args) {
     if (!max_bins) return hipSuccess;
-    return KW == 1 ? launch_bins_kw<1>(a, max_bins, s, ev_bin, heavy) : launch_bins_kw<2>(a, max_bins, s, ev_bin, heavy);
+    return KW == 1 ? launch_bins_kw<1>(a, max_bins, s, ev_bin, heavy, d_args)
+                   : launch_bins_kw<2>(a, max_bins, s, ev_bin, heavy, d_args);
 }
 
-hipError_t launch_bins_heavy(const BinArgs& a, int KW, hipStream_t s) {
-    return KW == 1 ? launch_heavy_kw<1>(a, s) : launch_heavy_kw<2>(a, s);
+hipError_t launch_bins_heavy(const BinArgs& a, int KW, hipStream_t s, const BinArgs* d_args) {
+    return KW == 1 ? launch_heavy_kw<1>(a, s, d_args) : launch_heavy_kw<2>(a, s, d_args);
 }
 
 __global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
@@ -4617,7 +4657,7 @@ hipError_t load_bin_kernels() {
         (const void*)flat_count_kernel<1>, (const void*)flat_count_kernel<2>, (const void*)flat_scan_kernel,
         (const void*)flat_scatter_kernel<1>, (const void*)flat_scatter_kernel<2>,
         (const void*)flat_scatter_lds_kernel<1>, (const void*)flat_scatter_lds_kernel<2>,
-        (const void*)bin_parts_kernel<1>, (const void*)bin_parts_kernel<2>, (const void*)bins_final_kernel,
+        (const void*)bin_parts_kernel<1>, (const void*)bin_parts_kernel<2>, (const void*)bins_final_kernel, (const void*)bin_args_kernel,
         (const void*)lists_kernel, (const void*)lists_bucket_kernel, (const void*)lists_long_kernel,
         (const void*)clear_kernel};
     for (const void* f : k) {

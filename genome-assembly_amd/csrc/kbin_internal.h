@@ -375,10 +375,12 @@ hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t 
                             hipStream_t s);
 // ev_bin[2]: recorded right before and right after bin_kernel (timing), or null
 // heavy: also the published bins' kernels (flat lists, partitions); without,
-// launch_bins_heavy runs them later (a finalize that expected none)
-hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin = nullptr,
-                       bool heavy = true);
-hipError_t launch_bins_heavy(const BinArgs& a, int KW, hipStream_t s);
+// launch_bins_heavy runs them later (a finalize that expected none).
+// d_args: one BinArgs of device memory; the bin kernels read their arguments
+// there (launch_bins writes them, stream-ordered; launch_bins_heavy reuses them)
+hipError_t launch_bins(const BinArgs& a, uint64_t max_bins, int KW, hipStream_t s, hipEvent_t* ev_bin, bool heavy,
+                       BinArgs* d_args);
+hipError_t launch_bins_heavy(const BinArgs& a, int KW, hipStream_t s, const BinArgs* d_args);
 // launch_bins_order + launch_bins_desc in one launch (bucketed path)
 hipError_t launch_bins_plan(const uint32_t* bstart, const uint32_t* bcount, const uint32_t* bmmer,
                             const uint32_t* bocc, const uint64_t* totals, uint64_t max_bins, uint32_t* order,

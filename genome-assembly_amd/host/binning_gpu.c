@@ -345,6 +345,20 @@ static void node_free(void *p)
 }
 void free(void *p) __attribute__((alias("node_free")));
 
+/* resolve the shadowed free at load time, before the program can start threads
+ * (a free() racing the lazy lookup went to glibc even when an
+ * LD_PRELOADed allocator owns the pointer); frees inside dlsym itself, during
+ * this single-threaded load, still take the fallback */
+__attribute__((constructor)) static void node_free_resolve(void)
+{
+    int expect = 0;
+    if (!__atomic_compare_exchange_n(&g_next_state, &expect, 1, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) return;
+    void *(*const d)(void *, const char *) = dlsym;
+    void (*nf)(void *) = (void (*)(void *))d(RTLD_NEXT, "free");
+    g_next_free = nf ? nf : __libc_free;
+    __atomic_store_n(&g_next_state, 2, __ATOMIC_RELEASE);
+}
+
 static void node_arena_init(void)
 {
 #if defined(__linux__)

@@ -101,9 +101,16 @@ static void pack_code(const char *s, int n, uint64_t *hi, uint64_t *lo)
     *lo = l;
 }
 
+/* where scan_read's records go: the record vector (kbo_bin), or a caller's
+ * function (the streaming digest below) */
+typedef struct sink {
+    recvec_t *vec;
+    int (*put)(struct sink *, const rec_t *);
+} sink_t;
+
 /* process_read restated (binning.c:902-1076).  Emits one record per k-mer. */
 static int scan_read(const char *read, int read_len, int K, int M, uint32_t ord,
-                     const uint8_t *mmer_mask, recvec_t *out, uint64_t *n_kmers, int *alphabet_ok)
+                     const uint8_t *mmer_mask, sink_t *out, uint64_t *n_kmers, int *alphabet_ok)
 {
     const char *kmer = read;
     const char *signature = NULL; /* binning.c:906 */
@@ -167,15 +174,13 @@ static int scan_read(const char *read, int read_len, int K, int M, uint32_t ord,
             }
         }
 
-        /* binning.c:1023-1040: copy, then complement in place (no reversal) */
+        /* binning.c:1023-1040: copy, then complement in place (no reversal);
+         * (the test-side mmer filter looks at the signature before the k-mer
+         * key is built: a filtered-out key's string is never needed) */
         memcpy(signature_cpy, signature, (size_t)M);
-        memcpy(kmer_key, kmer, (size_t)K);
         signature_cpy[M] = '\0';
-        kmer_key[K] = '\0';
-        if (is_rev) {
+        if (is_rev)
             for (j = 0; j < M; j++) signature_cpy[j] = o_getbp(3 - o_getval(signature_cpy[j]));
-            for (j = 0; j < K; j++) kmer_key[j] = o_getbp(3 - o_getval(kmer_key[j]));
-        }
 
         rec_t r;
         uint64_t mh, ml;
@@ -183,9 +188,13 @@ static int scan_read(const char *read, int read_len, int K, int M, uint32_t ord,
         r.mmer = (uint32_t)ml;
         (*n_kmers)++;
         if (!mmer_mask || mmer_mask[r.mmer]) { /* test-side partition filter */
+            memcpy(kmer_key, kmer, (size_t)K);
+            kmer_key[K] = '\0';
+            if (is_rev)
+                for (j = 0; j < K; j++) kmer_key[j] = o_getbp(3 - o_getval(kmer_key[j]));
             pack_code(kmer_key, K, &r.hi, &r.lo);
             r.ord = ord;
-            if (push(out, r)) return -1;
+            if (out->put ? out->put(out, &r) : push(out->vec, r)) return -1;
         }
         kmer++;                                                /* binning.c:1072 */
     }
@@ -218,11 +227,12 @@ int kbo_bin_masked(const char *bases, const uint64_t *read_off, uint64_t n_reads
     memset(out, 0, sizeof(*out));
     if (K < 1 || K > 64 || M < 1 || M > 8 || M > K) return KBO_EINVAL;
     recvec_t v = {0};
+    sink_t sk = {&v, NULL};
     int alphabet_ok = 1;
     uint64_t n_kmers = 0;
     for (uint64_t r = 0; r < n_reads; r++) {
         int len = (int)(read_off[r + 1] - read_off[r]);
-        if (scan_read(bases + read_off[r], len, K, M, (uint32_t)r, mmer_mask, &v, &n_kmers, &alphabet_ok)) {
+        if (scan_read(bases + read_off[r], len, K, M, (uint32_t)r, mmer_mask, &sk, &n_kmers, &alphabet_ok)) {
             free(v.r);
             return KBO_ENOMEM;
         }
@@ -351,6 +361,283 @@ void kbo_free_reads(char *bases, uint64_t *off)
 {
     free(bases);
     free(off);
+}
+
+/* ------------------------------------------------------------------------
+ * The bench's synthetic reads on the CPU, and the kb_digest of a result too
+ * large to hold (C3: 100 M reads, 12 G k-mer occurrences, 2 G ids), computed
+ * by this oracle's own scan_read -- so the full-size digests bench.py asserts
+ * come from the oracle, not from the GPU's history.
+ * ------------------------------------------------------------------------ */
+
+/* splitmix64 finaliser: the generator's and the digest's mixer (the product's
+ * kbin_device.h mix64, restated) */
+static uint64_t o_mix64(uint64_t x)
+{
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+static uint64_t o_rng(uint64_t stream, uint64_t ctr)
+{
+    return o_mix64(stream * 0x9E3779B97F4A7C15ull + ctr + 0x632BE59BD9B4E019ull);
+}
+
+/* CPU twin of the device generator (kb_generate_reads_device_at; its kernel
+ * mirrors generate_reads.py:93-112: an iid uniform genome of genome_len
+ * bases, a uniform start per read, the forward strand, substitutions at
+ * err_ppm per million bases, each to one of the three other bases) -- reads
+ * read_base .. read_base + n_reads - 1 of the stream `seed` defines, as ASCII
+ * (getbp: 0 T, 1 G, 2 C, 3 A), read_len bytes each.  A GPU test pins it
+ * against the device on prefixes. */
+void kbo_gen_reads(uint64_t n_reads, uint32_t L, uint64_t genome_len, uint32_t err_ppm, uint64_t seed,
+                   uint64_t read_base, char *out)
+{
+    const uint64_t s_genome = o_mix64(seed ^ 0x1111111111111111ull);
+    const uint64_t s_start = o_mix64(seed ^ 0x2222222222222222ull);
+    const uint64_t s_err = o_mix64(seed ^ 0x3333333333333333ull);
+    for (uint64_t r = 0; r < n_reads; r++) {
+        const uint64_t rg = read_base + r;
+        const uint64_t start = o_rng(s_start, rg) % (genome_len - L + 1);
+        char *o = out + r * L;
+        for (uint32_t b = 0; b < L; b++) {
+            const uint64_t pos = start + b;
+            uint32_t v = (uint32_t)(o_rng(s_genome, pos >> 5) >> (2 * (pos & 31))) & 3u;
+            if (err_ppm) {
+                const uint64_t u = o_rng(s_err, rg * (uint64_t)L + b);
+                if ((uint32_t)(u % 1000000ull) < err_ppm) v = (v + 1u + (uint32_t)((u >> 32) % 3ull)) & 3u;
+            }
+            o[b] = o_getbp((int)v);
+        }
+    }
+}
+
+/* kb_digest's terms (kbin_digest.hip, kbin.result_digest): per kept key
+ * mix64(key ^ count << 1); per list position j (1-based, the list in reverse
+ * call order) mix64(key ^ (j << 32 | (uint32) id)); key = mix64(mix64(mix64(
+ * mmer) ^ hi) ^ lo); sums mod 2^64 */
+static uint64_t o_dkey(uint32_t mmer, uint64_t hi, uint64_t lo)
+{
+    return o_mix64(o_mix64(o_mix64((uint64_t)mmer) ^ hi) ^ lo);
+}
+
+/* one worker's keys: an open-addressed table of (mmer, hi, lo) -> count, then
+ * (second pass) the list position left to hand out */
+typedef struct {
+    uint64_t *hi, *lo;
+    uint32_t *mm;   /* mmer + 1 (0: empty slot) */
+    uint32_t *cnt;
+    uint64_t mask, n;
+} dtab_t;
+
+typedef struct {
+    sink_t sk;      /* (first: scan_read's sink) */
+    dtab_t t;
+    int pass;       /* 1: count, 2: list terms */
+    uint32_t cur_id;
+    int cutoff, prune;
+    uint64_t dl, ids, err;
+} dwork_t;
+
+static uint64_t *dslot(dtab_t *t, const rec_t *r, int insert, int *fresh)
+{
+    uint64_t h = o_dkey(r->mmer, r->hi, r->lo) & t->mask;
+    for (;;) {
+        if (t->mm[h] == 0) {
+            if (!insert) return NULL;
+            t->mm[h] = r->mmer + 1u;
+            t->hi[h] = r->hi;
+            t->lo[h] = r->lo;
+            t->cnt[h] = 0;
+            t->n++;
+            *fresh = 1;
+            return &t->hi[h];
+        }
+        if ((t->mm[h] & 0x7FFFFFFFu) == r->mmer + 1u && t->lo[h] == r->lo && t->hi[h] == r->hi) return &t->hi[h];
+        h = (h + 1) & t->mask;
+    }
+}
+
+static int dput(sink_t *s, const rec_t *r)
+{
+    dwork_t *w = (dwork_t *)s;
+    int fresh = 0;
+    uint64_t *p = dslot(&w->t, r, w->pass == 1, &fresh);
+    if (!p) { w->err = 1; return -1; }
+    const uint64_t h = (uint64_t)(p - w->t.hi);
+    if (w->pass == 1) {
+        if (w->t.n * 10 > (w->t.mask + 1) * 8) { w->err = 2; return -1; }  /* > 80 % full */
+        w->t.cnt[h]++;
+        return 0;
+    }
+    /* second pass: the occurrence's list position, counted down from the key's
+     * count (call order t = 0 .. c - 1 sits at position c - t: prepend,
+     * binning.c:1065-1068) */
+    const uint32_t j = w->t.cnt[h]--;
+    if (!w->prune || (w->t.mm[h] >> 31) == 0) {  /* (bit 31 of mm: a pruned key, set after pass 1) */
+        w->dl += o_mix64(o_dkey(r->mmer, r->hi, r->lo) ^ (((uint64_t)j << 32) | w->cur_id));
+        w->ids++;
+    }
+    return 0;
+}
+
+typedef struct {
+    const char *reads;      /* n_reads x L ASCII, or NULL: */
+    const uint64_t *packed; /* n_reads x ceil(L / 32) words, 2-bit codes first base high (the device layout) */
+    uint64_t n_reads;
+    uint32_t L;
+    int K, M, cutoff, prune;
+    int32_t id0;
+    int nw, w;              /* worker w of nw: the mmers with owner(m) == w */
+    uint64_t cap_log2;
+    uint64_t out[5];        /* entries, ids, key sum, list sum, k-mers */
+    int rc;
+} djob_t;
+
+static int owner_of(uint32_t m, int nw) { return (int)(o_mix64((uint64_t)m + 0x5bd1e995ull) % (uint64_t)nw); }
+
+#include <pthread.h>
+static void *dworker(void *arg)
+{
+    djob_t *jb = arg;
+    const uint32_t nm = 1u << (2 * jb->M);
+    uint8_t *mask = calloc(nm, 1);
+    char *buf = malloc((size_t)jb->L + 1);
+    dwork_t w;
+    memset(&w, 0, sizeof w);
+    w.sk.put = dput;
+    w.cutoff = jb->cutoff;
+    w.prune = jb->prune;
+    const uint64_t cap = 1ull << jb->cap_log2;
+    w.t.mask = cap - 1;
+    w.t.hi = malloc(cap * 8);
+    w.t.lo = malloc(cap * 8);
+    w.t.mm = calloc(cap, 4);
+    w.t.cnt = malloc(cap * 4);
+    if (!mask || !buf || !w.t.hi || !w.t.lo || !w.t.mm || !w.t.cnt) { jb->rc = KBO_ENOMEM; goto done; }
+    for (uint32_t m = 0; m < nm; m++) mask[m] = owner_of(m, jb->nw) == jb->w;
+    for (w.pass = 1; w.pass <= 2; w.pass++) {
+        uint64_t nk = 0;
+        int aok = 1;
+        const uint32_t RW = (jb->L + 31u) / 32u;
+        for (uint64_t r = 0; r < jb->n_reads; r++) {
+            w.cur_id = (uint32_t)(jb->id0 + (int32_t)r);
+            const char *rd = jb->reads ? jb->reads + r * jb->L : buf;
+            if (!jb->reads)
+                for (uint32_t b = 0; b < jb->L; b++)
+                    buf[b] = o_getbp((int)((jb->packed[r * RW + b / 32u] >> (62u - 2u * (b % 32u))) & 3u));
+            if (scan_read(rd, (int)jb->L, jb->K, jb->M, (uint32_t)r, mask, &w.sk, &nk, &aok)) {
+                jb->rc = w.err == 2 ? KBO_ENOMEM : KBO_EINVAL;
+                goto done;
+            }
+        }
+        jb->out[4] = nk;
+        if (w.pass == 1) {  /* the kept keys' terms; pruned keys marked */
+            uint64_t dk = 0, ent = 0;
+            for (uint64_t h = 0; h < cap; h++) {
+                if (!w.t.mm[h]) continue;
+                const uint32_t c = w.t.cnt[h];
+                if (jb->prune && c <= (uint32_t)jb->cutoff) { w.t.mm[h] |= 0x80000000u; continue; }
+                dk += o_mix64(o_dkey(w.t.mm[h] - 1u, w.t.hi[h], w.t.lo[h]) ^ ((uint64_t)c << 1));
+                ent++;
+            }
+            jb->out[0] = ent;
+            jb->out[2] = dk;
+        }
+    }
+    jb->out[1] = w.ids;
+    jb->out[3] = w.dl;
+done:
+    free(mask);
+    free(buf);
+    free(w.t.hi); free(w.t.lo); free(w.t.mm); free(w.t.cnt);
+    return NULL;
+}
+
+/* kb_digest of binning n_reads ASCII reads of length L (ids id0, id0 + 1, ...)
+ * in one pass: entries, ids, key sum, list sum, and the k-mers scanned.
+ * n_workers threads each own the mmers of one hash class (and scan every
+ * read); a worker's table holds 2^cap_log2 keys at most 80 % full. */
+static int stream_digest(const char *reads, const uint64_t *packed, uint64_t n_reads, uint32_t L, int K, int M,
+                         int cutoff, int prune, int32_t id0, int n_workers, int cap_log2, uint64_t out[5])
+{
+    if (K < 1 || K > 64 || M < 1 || M > 8 || M > K || n_workers < 1 || n_workers > 256) return KBO_EINVAL;
+    djob_t *jobs = calloc((size_t)n_workers, sizeof(djob_t));
+    pthread_t *th = calloc((size_t)n_workers, sizeof(pthread_t));
+    if (!jobs || !th) { free(jobs); free(th); return KBO_ENOMEM; }
+    for (int i = 0; i < n_workers; i++) {
+        jobs[i] = (djob_t){reads, packed, n_reads, L, K, M, cutoff, prune, id0, n_workers, i, (uint64_t)cap_log2,
+                           {0}, 0};
+        pthread_create(&th[i], NULL, dworker, &jobs[i]);
+    }
+    int rc = KBO_OK;
+    memset(out, 0, 5 * sizeof(uint64_t));
+    for (int i = 0; i < n_workers; i++) {
+        pthread_join(th[i], NULL);
+        if (jobs[i].rc) rc = jobs[i].rc;
+        for (int k = 0; k < 4; k++) out[k] += jobs[i].out[k];
+        out[4] = jobs[i].out[4];
+    }
+    free(jobs);
+    free(th);
+    return rc;
+}
+
+int kbo_stream_digest(const char *reads, uint64_t n_reads, uint32_t L, int K, int M, int cutoff, int prune,
+                      int32_t id0, int n_workers, int cap_log2, uint64_t out[5])
+{
+    return stream_digest(reads, NULL, n_reads, L, K, M, cutoff, prune, id0, n_workers, cap_log2, out);
+}
+
+/* the generator's reads packed 2-bit (first base high, the device layout) */
+typedef struct {
+    uint64_t *w;
+    uint64_t r0, r1, read_base, genome_len, seed;
+    uint32_t L, err_ppm;
+} gjob_t;
+
+static void *gworker(void *arg)
+{
+    gjob_t *g = arg;
+    const uint32_t RW = (g->L + 31u) / 32u;
+    char *buf = malloc(g->L);
+    for (uint64_t r = g->r0; r < g->r1; r++) {
+        kbo_gen_reads(1, g->L, g->genome_len, g->err_ppm, g->seed, g->read_base + r, buf);
+        for (uint32_t k = 0; k < RW; k++) g->w[r * RW + k] = 0;
+        for (uint32_t b = 0; b < g->L; b++)
+            g->w[r * RW + b / 32u] |= (uint64_t)o_getval(buf[b]) << (62u - 2u * (b % 32u));
+    }
+    free(buf);
+    return NULL;
+}
+
+/* kbo_stream_digest of the generator's reads read_base .. + n_reads - 1
+ * (kbo_gen_reads), ids id0 + read index: the full-size C3 digest from the
+ * oracle (tools/oracle_digest.py) */
+int kbo_gen_stream_digest(uint64_t n_reads, uint32_t L, uint64_t genome_len, uint32_t err_ppm, uint64_t seed,
+                          uint64_t read_base, int K, int M, int cutoff, int prune, int32_t id0, int n_workers,
+                          int cap_log2, uint64_t out[5])
+{
+    const uint32_t RW = (L + 31u) / 32u;
+    uint64_t *w = malloc(n_reads * RW * sizeof(uint64_t) + 8);
+    gjob_t *g = calloc((size_t)n_workers, sizeof(gjob_t));
+    pthread_t *th = calloc((size_t)n_workers, sizeof(pthread_t));
+    if (!w || !g || !th) { free(w); free(g); free(th); return KBO_ENOMEM; }
+    for (int i = 0; i < n_workers; i++) {
+        g[i] = (gjob_t){w, n_reads * (uint64_t)i / (uint64_t)n_workers, n_reads * (uint64_t)(i + 1) / (uint64_t)n_workers,
+                        read_base, genome_len, seed, L, err_ppm};
+        pthread_create(&th[i], NULL, gworker, &g[i]);
+    }
+    for (int i = 0; i < n_workers; i++) pthread_join(th[i], NULL);
+    free(g);
+    free(th);
+    const int rc = stream_digest(NULL, w, n_reads, L, K, M, cutoff, prune, id0, n_workers, cap_log2, out);
+    free(w);
+    return rc;
 }
 
 #ifdef KBO_MAIN

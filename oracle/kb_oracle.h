@@ -35,4 +35,20 @@ int kbo_read_fgets(const char *path, int read_length, char **bases_out,
                    uint64_t **off_out, uint64_t *n_out);
 void kbo_free_reads(char *bases, uint64_t *off);
 
+/* the device generator's reads (kb_generate_reads_device_at) on the CPU:
+ * n_reads x L ASCII bytes, reads read_base .. of the stream `seed` defines */
+void kbo_gen_reads(uint64_t n_reads, uint32_t L, uint64_t genome_len, uint32_t err_ppm, uint64_t seed,
+                   uint64_t read_base, char *out);
+/* kb_digest (kbin.h) of binning reads too many to hold as a result, from this
+ * oracle's scan: out = {entries, ids, key sum, list sum, k-mers}.  Reads are
+ * n_reads x L ASCII with ids id0 + index; n_workers threads own the mmers of
+ * one hash class each, each table 2^cap_log2 keys (<= 80 % full, else
+ * KBO_ENOMEM). */
+int kbo_stream_digest(const char *reads, uint64_t n_reads, uint32_t L, int K, int M, int cutoff, int prune,
+                      int32_t id0, int n_workers, int cap_log2, uint64_t out[5]);
+/* the same over kbo_gen_reads' reads, generated and held 2-bit packed */
+int kbo_gen_stream_digest(uint64_t n_reads, uint32_t L, uint64_t genome_len, uint32_t err_ppm, uint64_t seed,
+                          uint64_t read_base, int K, int M, int cutoff, int prune, int32_t id0, int n_workers,
+                          int cap_log2, uint64_t out[5]);
+
 #endif

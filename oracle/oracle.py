@@ -50,6 +50,16 @@ def lib() -> C.CDLL:
         l.kbo_read_fgets.restype = C.c_int
         l.kbo_free_reads.argtypes = [C.c_void_p, C.c_void_p]
         l.kbo_free_reads.restype = None
+        l.kbo_gen_reads.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64,
+                                    C.c_char_p]
+        l.kbo_gen_reads.restype = None
+        l.kbo_stream_digest.argtypes = [C.c_char_p, C.c_uint64, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.c_int32, C.c_int, C.c_int, C.POINTER(C.c_uint64)]
+        l.kbo_stream_digest.restype = C.c_int
+        l.kbo_gen_stream_digest.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64,
+                                            C.c_int, C.c_int, C.c_int, C.c_int, C.c_int32, C.c_int, C.c_int,
+                                            C.POINTER(C.c_uint64)]
+        l.kbo_gen_stream_digest.restype = C.c_int
         _lib = l
     return _lib
 
@@ -130,3 +140,38 @@ def ref_binary(K: int, M: int, cutoff: int = 1) -> pathlib.Path | None:
         subprocess.run(["bash", str(HERE / "build_ref.sh"), str(K), str(M), str(cutoff)],
                        check=False, capture_output=True)
     return p if p.exists() else None
+
+
+def gen_reads(n_reads: int, read_len: int, genome_len: int, err_ppm: int, seed: int, read_base: int = 0) -> bytes:
+    """the device generator's reads (kb_generate_reads_device_at) on the CPU:
+    n_reads x read_len ASCII bytes (oracle/kb_oracle.c kbo_gen_reads)"""
+    buf = C.create_string_buffer(max(1, n_reads * read_len))
+    lib().kbo_gen_reads(n_reads, read_len, genome_len, err_ppm, seed, read_base, buf)
+    return buf.raw[:n_reads * read_len]
+
+
+def _digest_out(rc, out):
+    if rc:
+        raise RuntimeError(f"kbo stream digest failed: {rc}")
+    return tuple(int(x) for x in out[:4]), int(out[4])
+
+
+def stream_digest(bases: bytes, n_reads: int, read_len: int, K: int, M: int, cutoff: int = 1, prune: bool = True,
+                  id0: int = 0, workers: int = 4, cap_log2: int = 20):
+    """kb_digest (entries, ids, key sum, list sum) of binning fixed-length
+    reads, computed by the oracle's scan without holding the result; and the
+    k-mers scanned"""
+    out = (C.c_uint64 * 5)()
+    rc = lib().kbo_stream_digest(bases, n_reads, read_len, K, M, cutoff, 1 if prune else 0, id0, workers, cap_log2,
+                                 out)
+    return _digest_out(rc, out)
+
+
+def gen_stream_digest(n_reads: int, read_len: int, genome_len: int, err_ppm: int, seed: int, K: int, M: int,
+                      cutoff: int = 1, prune: bool = True, read_base: int = 0, id0: int = 0, workers: int = 8,
+                      cap_log2: int = 24):
+    """stream_digest over gen_reads' reads (generated inside, 2-bit packed)"""
+    out = (C.c_uint64 * 5)()
+    rc = lib().kbo_gen_stream_digest(n_reads, read_len, genome_len, err_ppm, seed, read_base, K, M, cutoff,
+                                     1 if prune else 0, id0, workers, cap_log2, out)
+    return _digest_out(rc, out)

@@ -31,10 +31,18 @@ def same(res, ora):
 
 def main():
     n_reads, glen, seed = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    err = float(sys.argv[4]) if len(sys.argv) > 4 else 0.0
     rng = np.random.default_rng(seed)
-    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=glen)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    genome = rng.choice(acgt, size=glen)
     starts = rng.integers(0, glen - 150, n_reads)
-    reads = [genome[s:s + 150].tobytes() for s in starts]
+    reads = []
+    for s in starts:
+        r = genome[s:s + 150].copy()
+        if err:
+            m = rng.random(150) < err
+            r[m] = rng.choice(acgt, size=int(m.sum()))
+        reads.append(r.tobytes())
     bases, lens = kbin.pack_reads(reads)
     ora = oracle.bin_reads(bases, lens, 31, 7, 1, True)
     out = {"ok": True, "finalizes": [], "paths": {}}

@@ -86,6 +86,39 @@ def test_c3_coverage_regime(n, genome, P, p):
     assert_same(got, ora)
 
 
+@pytest.mark.timeout(1200)
+def test_c3_repeated_finalizes_default_knobs():
+    """the path C3 really runs -- ranking switched on by
+    the LAST finalize's mean list length (>= 64 ids), the sticky long-list
+    regime's finer sub-bins from the maps learned on it, bitmap emission with
+    KB_BIN_RANK_MERGE -- at default knobs over repeated finalizes of one
+    context: partition 3 of 8 of the C3 generator at ~3000x coverage (4 M reads
+    over 200 Kbp), finalized three times (cold; then ranked, on learned maps),
+    each bit-exact against the oracle on the same mmers, the later two
+    asserted ranked and bitmap-emitted"""
+    wl = bench.WORKLOADS["c3"]
+    n, genome, P, p = 4_000_000, 200_000, 8, 3
+    L, K, M = wl["read_len"], wl["K"], wl["M"]
+    words, lens, wpr = _generate(n, L, genome, wl["err_ppm"], bench.gen_seed(wl["seed"]))
+    mask = part_mask(M, p, P)
+    bases, hl = _unpack(words, lens, n, wpr, L)
+    ora = oracle.bin_reads(bases, hl, K, M, 1, True, mmer_mask=mask)
+    del bases
+    tim = []
+    with kbin.Engine(K, M, cutoff=1, max_read_len=L) as eng:
+        eng.set_timing(True)
+        for f in range(3):
+            eng.reset()
+            eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
+            eng.set_partition(p, P)
+            eng.finalize(True)
+            tim.append(eng.timing())
+            assert_same(eng.export(), ora)
+    assert tim[0]["ranked_bins"] == 0, tim[0]  # (no last finalize to learn from)
+    for t in tim[1:]:
+        assert t["ranked_bins"] > 100 and t["bitmap_partitions"] > 100, t
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("light", ["1", "0"])
 def test_c5_singleton_prefilter_default_knobs(light, monkeypatch):

@@ -31,10 +31,11 @@ ABL = REPO / "genome-assembly_amd" / "lib" / "abl" / "libkbin.so"
 pytestmark = pytest.mark.gpu
 
 
-def run_worker(lib: pathlib.Path, skew: int, n_reads=12000, glen=60000, seed=7, extra=None):
+def run_worker(lib: pathlib.Path, skew: int, n_reads=60000, glen=2_000_000, seed=7, err=0.0, extra=None):
     env = dict(os.environ, KB_LIB_PATH=str(lib), KB_DIAG_SKEW=str(skew), KB_BIN_TS_LOG2="10", KB_ENGINE="binned")
     env.update(extra or {})
-    p = subprocess.run([sys.executable, str(REPO / "tests" / "race_worker.py"), str(n_reads), str(glen), str(seed)],
+    p = subprocess.run([sys.executable, str(REPO / "tests" / "race_worker.py"), str(n_reads), str(glen), str(seed),
+                        str(err)],
                        env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads(p.stdout.strip().splitlines()[-1])
@@ -55,7 +56,8 @@ def test_partition_loop_skew(skew):
 @pytest.mark.skipif(not ABL.exists(), reason="diagnostic build lib/abl not built")
 def test_partition_loop_skew_ranked():
     """the same late wave in the ranked kernel (long lists: bitmaps, ranks)"""
-    out = run_worker(ABL, 6, n_reads=20000, glen=8000, seed=9, extra={"KB_BIN_RANK": "2"})
+    out = run_worker(ABL, 6, n_reads=40000, glen=3000, seed=9, err=0.005,
+                     extra={"KB_BIN_RANK": "2", "KB_BIN_TS_LOG2": "13"})
     assert out["ok"], out
     assert out["paths"].get("ranked_bins", 0) > 0, out["paths"]
 

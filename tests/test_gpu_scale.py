@@ -242,3 +242,38 @@ def test_c2_prefix_vs_reference_binary():
     for line in kbin.dump_lines(res, 31, 7):
         h.update(line.encode())
     assert h.hexdigest() == want
+
+
+@pytest.mark.parametrize("wl_name,read_base", [("c2", 0), ("c3", 0), ("c3", 99_950_000), ("c4", 875_000_000),
+                                               ("c5", 62_450_000)])
+def test_generator_twin(wl_name, read_base):
+    """the oracle's CPU twin of the device generator
+    (oracle.gen_reads, kb_oracle.c kbo_gen_reads) gives the same reads as
+    kb_generate_reads_device_at -- at the start of each workload's stream and
+    at its far end (C3's last reads, C4 rank 7's range, C5's last share reads)
+    -- so the oracle-computed full-size digests (tests/golden/
+    oracle_digests.json) are of the bench's own reads"""
+    wl = bench.WORKLOADS[wl_name]
+    n, L = 20_000, wl["read_len"]
+    seed = bench.gen_seed(wl["seed"])
+    words, lens, wpr = _generate(n, L, wl["genome"], wl["err_ppm"], seed, read_base=read_base)
+    bases, _ = _unpack(words, lens, n, wpr, L)
+    assert oracle.gen_reads(n, L, wl["genome"], wl["err_ppm"], seed, read_base) == bases
+
+
+@pytest.mark.timeout(600)
+def test_c2_full_oracle_digest():
+    """C2 in full against the oracle-computed digest fixture (tools/
+    oracle_digest.py c2): the same check bench.py's C3 leg makes, on a size
+    the fixture script computes in 30 s"""
+    import json
+    fx = json.loads((bench.REPO / "tests" / "golden" / "oracle_digests.json").read_text())["c2"]
+    wl = bench.WORKLOADS["c2"]
+    n, L = wl["reads"], wl["read_len"]
+    assert fx["reads"] == n and fx["seed"] == bench.gen_seed(wl["seed"])
+    words, lens, wpr = _generate(n, L, wl["genome"], wl["err_ppm"], fx["seed"])
+    with kbin.Engine(wl["K"], wl["M"], cutoff=1, max_read_len=L) as eng:
+        eng.submit_packed_device(words.data_ptr(), lens.data_ptr(), n, wpr, 0)
+        eng.finalize(True)
+        dig = [hex(x) for x in eng.digest()]
+    assert dig == fx["digest"]
