@@ -633,7 +633,7 @@ def main():
             # no unit crosses into the timed region: the timed steps send their
             # own first unit (and one last prefetch goes unused -- counted in)
             while pending:
-                runner.wait(pending.pop())
+                runner.discard(pending.pop())
     else:
         eng, step = single_gpu_runner(K, M, L, args.cutoff, n, wpr, P, local, reads, pass_log,
                                       scan_once=not args.no_scan_once)

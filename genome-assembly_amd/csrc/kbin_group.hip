@@ -29,10 +29,12 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -145,6 +147,11 @@ struct Unit {  // one send in flight (a slot)
     bool busy = false;
     uint32_t part = 0, n_parts = 1;
     std::vector<uint64_t> C;  // [G * G] counts: C[s * G + d] records from rank s to rank d
+    // the send stage (route, counts, records) runs on the group's sender
+    // thread: done once it has returned, rc / err its outcome
+    bool done = true;
+    int rc = KB_OK;
+    std::string err;
 };
 
 struct Rank {
@@ -155,9 +162,11 @@ struct Rank {
     ncclComm_t comm = nullptr;
     hipStream_t xs = nullptr;  // exchange stream
     hipEvent_t landed[SLOTS] = {};  // the slot's records received (and its sends done)
+    hipEvent_t routed = nullptr;    // the sender stream's routing of the unit being sent
     GBuf regions[SLOTS], rbuf[SLOTS];
-    GBuf cdev;                  // [G] this rank's counts, then [G * G] all counts (all-gather)
-    uint64_t* h_counts = nullptr;  // pinned [G * G]
+    GBuf cdev;                  // [G + 1] this rank's row, then [G * (G + 1)] every rank's (all-gather)
+    uint64_t* h_counts = nullptr;  // pinned [G * (G + 1)]: row s = rank s's G counts + its routing status
+    int route_rc = KB_OK;       // this unit's routing outcome (travels with the counts)
     uint64_t cap = 0;           // region capacity (records per destination), learned
     bool ordered = false;       // plan/pack sender (destination-major, read order)
     std::vector<uint64_t> soff[SLOTS];  // the slot's first record per destination
@@ -176,6 +185,17 @@ struct kb_group {
     uint32_t part = 0, n_parts = 1;
     int head = 0, tail = 0, inflight = 0;  // slots: next to send, next to receive
     Unit u[SLOTS];
+    std::vector<uint64_t> last_C;  // counts of the last unit received or discarded
+    // the sender thread: units' send stages in send order (RCCL calls on a
+    // communicator stay in one order on every rank), so kb_group_send_async
+    // returns at once and the caller's receive of the previous unit bins
+    // while this one routes and exchanges
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<int> jobs;  // slots queued
+    int running = 0;       // a job taken, not finished
+    bool stop = false;
 };
 
 namespace {
@@ -212,8 +232,9 @@ int rank_init(kb_group* g, Rank& rk) {
     GKB(kb_create(&p, &rk.send));
     GHIP(hipStreamCreateWithFlags(&rk.xs, hipStreamNonBlocking));
     for (auto& e : rk.landed) GHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    GHIP(hipHostMalloc((void**)&rk.h_counts, (size_t)g->G * g->G * sizeof(uint64_t), hipHostMallocDefault));
-    GHIP(rk.cdev.ensure((uint64_t)g->G * (g->G + 1)));
+    GHIP(hipEventCreateWithFlags(&rk.routed, hipEventDisableTiming));
+    GHIP(hipHostMalloc((void**)&rk.h_counts, (size_t)g->G * (g->G + 1) * sizeof(uint64_t), hipHostMallocDefault));
+    GHIP(rk.cdev.ensure((uint64_t)(g->G + 1) * (g->G + 1)));
     return KB_OK;
 }
 
@@ -238,6 +259,7 @@ void rank_free(Rank& rk) {
     if (rk.h_counts) (void)hipHostFree(rk.h_counts);
     for (auto& e : rk.landed)
         if (e) (void)hipEventDestroy(e);
+    if (rk.routed) (void)hipEventDestroy(rk.routed);
     if (rk.xs) (void)hipStreamDestroy(rk.xs);
 }
 
@@ -246,14 +268,21 @@ void rank_free(Rank& rk) {
 // particular order -- the binned receivers order lists by read id), or, for
 // receivers that number occurrences by arrival (first-occurrence tracking,
 // the table engine), plan/pack: destination-major, read order.
+int rank_route_body(kb_group* g, int i, int s);
 int rank_route(kb_group* g, int i, int s) {
+    Rank& rk = g->r[i];
+    rk.route_rc = rank_route_body(g, i, s);
+    rk.err = rk.route_rc ? kb_last_error() : "";
+    return rk.route_rc;
+}
+int rank_route_body(kb_group* g, int i, int s) {
     Rank& rk = g->r[i];
     GHIP(hipSetDevice(rk.dev));
     // (the slot's last sends must be out before its regions are rewritten)
     GHIP(hipStreamWaitEvent((hipStream_t)kb_stream(rk.send), rk.landed[s], 0));
     const int G = g->G;
     const uint64_t W = g->W;
-    uint64_t* cnt = rk.h_counts + (uint64_t)rk.grank * G;  // (this rank's row of C)
+    uint64_t* cnt = rk.h_counts + (uint64_t)rk.grank * (G + 1);  // (this rank's row of C)
     std::vector<uint64_t>& off = rk.soff[s];
     off.assign((size_t)G, 0);
     if (!rk.ordered) {
@@ -287,38 +316,56 @@ int rank_route(kb_group* g, int i, int s) {
 }
 
 // the counts matrix on every rank: RCCL all-gather of each rank's row, or
-// (local transport) the rows are already in this process
+// (local transport) the rows are already in this process.  A row carries its
+// rank's routing status after its G counts, so a rank whose routing failed
+// still takes part in the all-gather and every rank returns the failure
+// (an early return left the peers blocked in ncclAllGather)
 int exchange_counts(kb_group* g, Unit& un) {
-    const int G = g->G;
+    const int G = g->G, RS = G + 1;
     un.C.assign((size_t)G * G, 0);
+    for (auto& rk : g->r) rk.h_counts[(size_t)rk.grank * RS + G] = (uint64_t)(uint32_t)rk.route_rc;
+    std::vector<uint64_t> rows((size_t)G * RS);
     if (g->local) {
         for (auto& rk : g->r)
-            memcpy(&un.C[(size_t)rk.grank * G], rk.h_counts + (size_t)rk.grank * G, G * sizeof(uint64_t));
-        return KB_OK;
+            memcpy(&rows[(size_t)rk.grank * RS], rk.h_counts + (size_t)rk.grank * RS, RS * sizeof(uint64_t));
+    } else {
+        Rccl& R = rccl();
+        for (auto& rk : g->r) {
+            GHIP(hipSetDevice(rk.dev));
+            GHIP(hipMemcpyAsync(rk.cdev.p, rk.h_counts + (size_t)rk.grank * RS, RS * sizeof(uint64_t),
+                                hipMemcpyHostToDevice, rk.xs));
+        }
+        GNCCL(R.GroupStart());
+        for (auto& rk : g->r)
+            GNCCL(R.AllGather(rk.cdev.p, rk.cdev.p + RS, (size_t)RS, ncclUint64, rk.comm, rk.xs));
+        GNCCL(R.GroupEnd());
+        for (auto& rk : g->r) {
+            GHIP(hipSetDevice(rk.dev));
+            GHIP(hipMemcpyAsync(rk.h_counts, rk.cdev.p + RS, (size_t)G * RS * sizeof(uint64_t),
+                                hipMemcpyDeviceToHost, rk.xs));
+        }
+        // (the sizes of the record sends are the host's to know: this is the
+        // exchange's one host wait, on the group's sender thread)
+        for (auto& rk : g->r) {
+            GHIP(hipSetDevice(rk.dev));
+            GHIP(hipStreamSynchronize(rk.xs));
+        }
+        memcpy(rows.data(), g->r[0].h_counts, rows.size() * sizeof(uint64_t));
+        for (size_t k = 1; k < g->r.size(); k++)
+            if (memcmp(rows.data(), g->r[k].h_counts, rows.size() * sizeof(uint64_t)))
+                return gfail(KB_EDEVICE, "internal: ranks disagree on the record counts");
     }
-    Rccl& R = rccl();
-    for (auto& rk : g->r) {
-        GHIP(hipSetDevice(rk.dev));
-        GHIP(hipMemcpyAsync(rk.cdev.p, rk.h_counts + (size_t)rk.grank * G, G * sizeof(uint64_t),
-                            hipMemcpyHostToDevice, rk.xs));
+    for (int src = 0; src < G; src++) {
+        const uint64_t st = rows[(size_t)src * RS + G];
+        if (st) {
+            const Rank* mine = nullptr;
+            for (auto& rk : g->r)
+                if (rk.grank == src) mine = &rk;
+            return gfail((int)st, "rank %d failed to route its records%s%s", src, mine ? ": " : " (peer)",
+                         mine ? mine->err.c_str() : "");
+        }
+        memcpy(&un.C[(size_t)src * G], &rows[(size_t)src * RS], G * sizeof(uint64_t));
     }
-    GNCCL(R.GroupStart());
-    for (auto& rk : g->r)
-        GNCCL(R.AllGather(rk.cdev.p, rk.cdev.p + G, (size_t)G, ncclUint64, rk.comm, rk.xs));
-    GNCCL(R.GroupEnd());
-    for (auto& rk : g->r) {
-        GHIP(hipSetDevice(rk.dev));
-        GHIP(hipMemcpyAsync(rk.h_counts, rk.cdev.p + G, (size_t)G * G * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                            rk.xs));
-    }
-    for (auto& rk : g->r) {
-        GHIP(hipSetDevice(rk.dev));
-        GHIP(hipStreamSynchronize(rk.xs));
-    }
-    memcpy(un.C.data(), g->r[0].h_counts, (size_t)G * G * sizeof(uint64_t));
-    for (size_t k = 1; k < g->r.size(); k++)
-        if (memcmp(un.C.data(), g->r[k].h_counts, (size_t)G * G * sizeof(uint64_t)))
-            return gfail(KB_EDEVICE, "internal: ranks disagree on the record counts");
     return KB_OK;
 }
 
@@ -334,8 +381,16 @@ int exchange_records(kb_group* g, Unit& un, int s) {
         // (the receive slot of the unit received two sends ago: its finalize
         // has returned, nothing references it now)
         GHIP(rk.rbuf[s].ensure(std::max<uint64_t>(tot, 1) * W));
-        // (the regions were written on the sender's stream)
-        GHIP(hipStreamSynchronize((hipStream_t)kb_stream(rk.send)));
+        // (the regions were written on the sender's stream: the exchange
+        // streams wait for them there, no host wait)
+        GHIP(hipEventRecord(rk.routed, (hipStream_t)kb_stream(rk.send)));
+    }
+    for (auto& rk : g->r) {
+        GHIP(hipSetDevice(rk.dev));
+        if (g->local)  // (device copies read every local sender's regions)
+            for (auto& src : g->r) GHIP(hipStreamWaitEvent(rk.xs, src.routed, 0));
+        else
+            GHIP(hipStreamWaitEvent(rk.xs, rk.routed, 0));
     }
     if (g->local) {
         for (auto& dst : g->r) {
@@ -374,6 +429,58 @@ int exchange_records(kb_group* g, Unit& un, int s) {
 }
 
 bool valid_local(kb_group* g, int i) { return g && i >= 0 && i < (int)g->r.size(); }
+
+// one unit's send stage (the sender thread): every local rank routes, the
+// counts (with each rank's routing status) go round, the records are sent
+int send_stage(kb_group* g, int s) {
+    Unit& un = g->u[s];
+    (void)for_ranks(g, [&](int i) { return rank_route(g, i, s); });  // (failures travel with the counts)
+    int rc = exchange_counts(g, un);
+    if (!rc) rc = exchange_records(g, un, s);
+    return rc;
+}
+
+void sender_loop(kb_group* g) {
+    std::unique_lock<std::mutex> lk(g->mu);
+    for (;;) {
+        g->cv.wait(lk, [&] { return g->stop || !g->jobs.empty(); });
+        if (g->jobs.empty()) return;  // (stop, nothing queued)
+        const int s = g->jobs.front();
+        g->jobs.pop_front();
+        g->running++;
+        lk.unlock();
+        const int rc = send_stage(g, s);
+        const std::string err = rc ? kb_last_error() : "";
+        lk.lock();
+        g->u[s].rc = rc;
+        g->u[s].err = err;
+        g->u[s].done = true;
+        g->running--;
+        g->cv.notify_all();
+    }
+}
+
+// the sender thread idle: no unit routing (the senders' reads may change)
+void wait_idle(kb_group* g) {
+    std::unique_lock<std::mutex> lk(g->mu);
+    g->cv.wait(lk, [&] { return g->jobs.empty() && g->running == 0; });
+}
+
+// the oldest unit's send stage finished; its outcome
+int wait_unit(kb_group* g, int s) {
+    std::unique_lock<std::mutex> lk(g->mu);
+    g->cv.wait(lk, [&] { return g->u[s].done; });
+    return g->u[s].rc;
+}
+
+int retire(kb_group* g, int s) {  // the oldest unit leaves (received or discarded)
+    Unit& un = g->u[s];
+    un.busy = false;
+    g->last_C = un.C;
+    g->tail = (s + 1) % SLOTS;
+    g->inflight--;
+    return KB_OK;
+}
 
 }  // namespace
 
@@ -462,6 +569,12 @@ extern "C" int kb_group_create_rank(const kb_params* p, int rank, int n_ranks, c
 
 extern "C" void kb_group_destroy(kb_group* g) {
     if (!g) return;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->stop = true;
+    }
+    g->cv.notify_all();
+    if (g->th.joinable()) g->th.join();  // (after the queued units' send stages)
     for (auto& rk : g->r) rank_free(rk);
     delete g;
 }
@@ -479,6 +592,7 @@ extern "C" kb_ctx* kb_group_ctx(kb_group* g, int local) { return valid_local(g, 
 
 extern "C" int kb_group_reset(kb_group* g) {
     if (!g) return gfail(KB_EINVAL, "null group");
+    wait_idle(g);  // (a unit still routing reads the senders' batches)
     // (units in flight keep their records: the regions and receive slots are
     // the group's, only the senders' read batches are dropped)
     for (auto& rk : g->r) {
@@ -493,6 +607,7 @@ extern "C" int kb_group_reset(kb_group* g) {
 extern "C" int kb_group_submit_ids(kb_group* g, int local, const char* bases, const uint32_t* lens, uint64_t n_reads,
                                    const int32_t* ids) {
     if (!valid_local(g, local)) return gfail(KB_EINVAL, "bad local rank %d", local);
+    wait_idle(g);
     GKB(kb_submit_ids(g->r[local].send, bases, lens, n_reads, ids));
     g->r[local].n_reads += n_reads;
     return KB_OK;
@@ -501,6 +616,7 @@ extern "C" int kb_group_submit_ids(kb_group* g, int local, const char* bases, co
 extern "C" int kb_group_submit_packed_device(kb_group* g, int local, const uint64_t* d_words, const uint32_t* d_lens,
                                              uint64_t n_reads, uint32_t words_per_read, int32_t first_id) {
     if (!valid_local(g, local)) return gfail(KB_EINVAL, "bad local rank %d", local);
+    wait_idle(g);
     GKB(kb_submit_packed_device(g->r[local].send, d_words, d_lens, n_reads, words_per_read, first_id));
     g->r[local].n_reads += n_reads;
     return KB_OK;
@@ -508,27 +624,58 @@ extern "C" int kb_group_submit_packed_device(kb_group* g, int local, const uint6
 
 extern "C" int kb_group_set_partition(kb_group* g, uint32_t part, uint32_t n_parts) {
     if (!g) return gfail(KB_EINVAL, "null group");
+    wait_idle(g);
     for (auto& rk : g->r) GKB(kb_set_partition(rk.send, part, n_parts));
     g->part = part;
     g->n_parts = n_parts;
     return KB_OK;
 }
 
-extern "C" int kb_group_send(kb_group* g, uint64_t* h_counts) {
+extern "C" int kb_group_send_async(kb_group* g) {
     if (!g) return gfail(KB_EINVAL, "null group");
     if (g->inflight == SLOTS) return gfail(KB_ESTATE, "kb_group_send: %d units in flight already", SLOTS);
+    wait_idle(g);  // (the last unit's routing read the senders: done before this one's starts)
     const int s = g->head;
     Unit& un = g->u[s];
-    int rc = for_ranks(g, [&](int i) { return rank_route(g, i, s); });
-    if (rc) return rc;
-    if ((rc = exchange_counts(g, un))) return rc;
-    if ((rc = exchange_records(g, un, s))) return rc;
     un.busy = true;
     un.part = g->part;
     un.n_parts = g->n_parts;
+    un.C.assign((size_t)g->G * g->G, 0);
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        un.done = false;
+        un.rc = KB_OK;
+        un.err.clear();
+        g->jobs.push_back(s);
+        if (!g->th.joinable()) g->th = std::thread(sender_loop, g);
+    }
+    g->cv.notify_all();
     g->head = (s + 1) % SLOTS;
     g->inflight++;
-    if (h_counts) memcpy(h_counts, un.C.data(), un.C.size() * sizeof(uint64_t));
+    return KB_OK;
+}
+
+extern "C" int kb_group_send(kb_group* g, uint64_t* h_counts) {
+    int rc = kb_group_send_async(g);
+    if (rc) return rc;
+    const int s = (g->head + SLOTS - 1) % SLOTS;
+    if ((rc = wait_unit(g, s))) {
+        // (a failed unit leaves at once: nothing of it is in flight)
+        const std::string e = g->u[s].err;
+        g->head = s;
+        g->u[s].busy = false;
+        g->u[s].done = true;
+        g->inflight--;
+        return gfail(rc, "%s", e.c_str());
+    }
+    if (h_counts) memcpy(h_counts, g->u[s].C.data(), g->u[s].C.size() * sizeof(uint64_t));
+    return KB_OK;
+}
+
+extern "C" int kb_group_unit_counts(kb_group* g, uint64_t* h_counts) {
+    if (!g || !h_counts) return gfail(KB_EINVAL, "kb_group_unit_counts: bad arguments");
+    if (g->last_C.empty()) return gfail(KB_ESTATE, "kb_group_unit_counts: no unit received yet");
+    memcpy(h_counts, g->last_C.data(), g->last_C.size() * sizeof(uint64_t));
     return KB_OK;
 }
 
@@ -538,6 +685,11 @@ extern "C" int kb_group_receive(kb_group* g, int prune) {
     const int s = g->tail;
     Unit& un = g->u[s];
     const int G = g->G;
+    if (const int src = wait_unit(g, s)) {
+        const std::string e = un.err;
+        retire(g, s);
+        return gfail(src, "%s", e.c_str());
+    }
     const int rc = for_ranks(g, [&](int i) -> int {
         Rank& rk = g->r[i];
         GHIP(hipSetDevice(rk.dev));
@@ -550,9 +702,7 @@ extern "C" int kb_group_receive(kb_group* g, int prune) {
         GKB(kb_finalize(rk.recv, prune));
         return KB_OK;
     });
-    un.busy = false;
-    g->tail = (s + 1) % SLOTS;
-    g->inflight--;
+    retire(g, s);
     return rc;
 }
 
@@ -560,13 +710,13 @@ extern "C" int kb_group_discard(kb_group* g) {
     if (!g) return gfail(KB_EINVAL, "null group");
     if (!g->inflight) return gfail(KB_ESTATE, "kb_group_discard: nothing sent");
     const int s = g->tail;
-    for (auto& rk : g->r) {
-        GHIP(hipSetDevice(rk.dev));
-        GHIP(hipEventSynchronize(rk.landed[s]));
-    }
-    g->u[s].busy = false;
-    g->tail = (s + 1) % SLOTS;
-    g->inflight--;
+    const int src = wait_unit(g, s);
+    if (!src)
+        for (auto& rk : g->r) {
+            GHIP(hipSetDevice(rk.dev));
+            GHIP(hipEventSynchronize(rk.landed[s]));
+        }
+    retire(g, s);
     return KB_OK;
 }
 

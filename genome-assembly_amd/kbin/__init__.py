@@ -39,6 +39,7 @@ EXPORTED = [
     "kb_group_unique_id", "kb_group_create", "kb_group_create_rank", "kb_group_destroy", "kb_group_info",
     "kb_group_submit_ids", "kb_group_submit_packed_device", "kb_group_set_partition", "kb_group_send",
     "kb_group_receive", "kb_group_finalize", "kb_group_discard", "kb_group_reset", "kb_group_ctx",
+    "kb_group_send_async", "kb_group_unit_counts",
 ]
 KB_TRANSPORT_RCCL, KB_TRANSPORT_LOCAL = 1, 2
 
@@ -145,6 +146,10 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_group_submit_packed_device.argtypes = [vp, C.c_int, vp, vp, u64, u32, i32]
     lib.kb_group_set_partition.argtypes = [vp, u32, u32]
     lib.kb_group_send.argtypes = [vp, C.POINTER(u64)]
+    # (A/B builds of an earlier tree -- KB_LIB_PATH -- may lack the newest calls)
+    for name, at in (("kb_group_send_async", [vp]), ("kb_group_unit_counts", [vp, C.POINTER(u64)])):
+        if hasattr(lib, name):
+            getattr(lib, name).argtypes = at
     lib.kb_group_receive.argtypes = [vp, C.c_int]
     lib.kb_group_finalize.argtypes = [vp, C.c_int]
     lib.kb_group_reset.argtypes = [vp]
@@ -152,7 +157,8 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_group_ctx.argtypes = [vp, C.c_int]
     lib.kb_group_ctx.restype = vp
     for name in EXPORTED:
-        if name not in ("kb_destroy", "kb_stream", "kb_last_error", "kb_group_destroy", "kb_group_ctx"):
+        if name not in ("kb_destroy", "kb_stream", "kb_last_error", "kb_group_destroy", "kb_group_ctx") and \
+                hasattr(lib, name):  # (test_abi checks that every one is exported)
             getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
@@ -519,6 +525,17 @@ class Group:
         """route + start the exchange; returns the G x G record counts"""
         c = np.zeros(self.n_ranks * self.n_ranks, dtype=np.uint64)
         _check(self.lib, self.lib.kb_group_send(self._h, c.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return c.reshape(self.n_ranks, self.n_ranks)
+
+    def send_async(self) -> None:
+        """queue the unit on the group's sender thread (kb_group_send_async):
+        returns at once; receive() / discard() report its failure"""
+        _check(self.lib, self.lib.kb_group_send_async(self._h))
+
+    def unit_counts(self) -> np.ndarray:
+        """G x G record counts of the last unit received or discarded"""
+        c = np.zeros(self.n_ranks * self.n_ranks, dtype=np.uint64)
+        _check(self.lib, self.lib.kb_group_unit_counts(self._h, c.ctypes.data_as(C.POINTER(C.c_uint64))))
         return c.reshape(self.n_ranks, self.n_ranks)
 
     def receive(self, prune: bool = True) -> None:

@@ -305,11 +305,15 @@ class ShardedBinner:
                 "counts": counts.tolist(), "times": (t1 - t0, t2 - t1)}
 
     def wait(self, unit) -> None:
-        """the unit's records have landed (also drops a unit nobody receives)"""
+        """the unit's records have landed (receive may follow)"""
         if unit["work"] is not None:
             unit["work"].wait()
             unit["work"] = None
         torch.cuda.current_stream(self.device).synchronize()
+
+    def discard(self, unit) -> None:
+        """drop a unit nobody receives (its records land, unbinned)"""
+        self.wait(unit)
 
     def receive(self, unit, prune: bool = True) -> None:
         eng = self.engine
@@ -369,25 +373,35 @@ class GroupBinner(ShardedBinner):
 
     def send(self, words: torch.Tensor, lens: torch.Tensor, n_reads: int, words_per_read: int,
              first_id: int, part: int = 0, n_parts: int = 1):
+        """queue the unit (kb_group_send_async): its routing and exchange run
+        on the group's sender thread while the caller receives the last one"""
         t0 = time.perf_counter()
         self._load(words, lens, n_reads, words_per_read, first_id, part, n_parts)
-        counts = self.grp.send()
-        unit = {"counts": counts, "part": part, "n_parts": n_parts, "times": (time.perf_counter() - t0, 0.0)}
+        self.grp.send_async()
+        unit = {"counts": None, "part": part, "n_parts": n_parts, "times": (time.perf_counter() - t0, 0.0)}
         self._units.append(unit)
         return unit
 
     def wait(self, unit) -> None:
-        """drop a unit nobody receives (its records land, unbinned)"""
+        """ShardedBinner.wait's contract (the unit may still be received):
+        kb_group_receive waits for the unit's send stage and records itself,
+        so nothing is to be done here"""
+        assert unit in self._units, "a unit in flight"
+
+    def discard(self, unit) -> None:
+        """drop a unit nobody receives (its records land, unbinned); the
+        unit's counts are then known (unit["counts"])"""
         assert self._units and self._units[0] is unit, "units leave in the order they were sent"
         self._units.pop(0)
         self.grp.discard()
+        unit["counts"] = self.grp.unit_counts()
 
     def receive(self, unit, prune: bool = True) -> None:
         assert self._units and self._units[0] is unit, "units are received in the order they were sent"
         t0 = time.perf_counter()
-        self.grp.receive(prune)
         self._units.pop(0)
-        c = unit["counts"]
+        self.grp.receive(prune)
+        c = unit["counts"] = self.grp.unit_counts()
         self.last_counts = (c[self.rank].tolist(), c[:, self.rank].tolist())
         self.last_times = {"plan_ms": unit["times"][0] * 1e3, "pack_ms": 0.0, "exchange_ms": 0.0,
                            "receive_ms": (time.perf_counter() - t0) * 1e3}

@@ -311,11 +311,20 @@ void *kb_stream(kb_ctx *ctx);
  * pass's partition only) and returns once it is in flight; kb_group_receive
  * bins the oldest unit in flight on every local rank.  Two units may be in
  * flight, so a caller can send unit i+1 before receiving unit i (the
- * exchange overlaps the binning).  kb_group_discard waits for the oldest
- * unit's records and drops them unbinned.  kb_group_finalize = send +
- * receive.  kb_group_reset drops the submitted reads (units in flight keep
- * their records).
- * h_counts (optional, G*G): records from rank s to rank d at [s*G + d].
+ * exchange overlaps the binning).  kb_group_send_async returns at once: the
+ * unit's routing, count exchange and record sends run on the group's own
+ * sender thread, in send order, so the caller's kb_group_receive of unit i
+ * bins while unit i+1 routes (kb_group_receive / _discard wait for their
+ * unit's send stage and return its failure; kb_group_reset, _submit_* and
+ * _set_partition wait until no unit is routing).  kb_group_discard waits
+ * for the oldest unit's records and drops them unbinned.  kb_group_finalize
+ * = send + receive.  kb_group_reset drops the submitted reads (units in
+ * flight keep their records).  A rank whose routing fails still takes part
+ * in the counts all-gather, with its status: every rank then fails that unit
+ * (no peer is left waiting in a collective).
+ * h_counts (optional, G*G): records from rank s to rank d at [s*G + d];
+ * kb_group_unit_counts gives the same for the last unit received or
+ * discarded (the async sender's counts).
  * Each local rank's result is its receiver context (kb_group_ctx): kb_export,
  * kb_export_device, kb_digest and kb_get_timing apply.  Errors: status codes,
  * message in kb_last_error(). */
@@ -334,6 +343,8 @@ int kb_group_submit_packed_device(kb_group *grp, int local, const uint64_t *d_wo
                                   uint64_t n_reads, uint32_t words_per_read, int32_t first_id);
 int kb_group_set_partition(kb_group *grp, uint32_t part, uint32_t n_parts);
 int kb_group_send(kb_group *grp, uint64_t *h_counts);
+int kb_group_send_async(kb_group *grp);
+int kb_group_unit_counts(kb_group *grp, uint64_t *h_counts);
 int kb_group_receive(kb_group *grp, int prune);
 int kb_group_finalize(kb_group *grp, int prune);
 int kb_group_discard(kb_group *grp);

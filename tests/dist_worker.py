@@ -45,7 +45,7 @@ def main():
         nxt = sb.send(words, lens, n, wpr, first_id=rank * n)
         sb.receive(unit)
         unit = nxt
-    sb.wait(unit)
+    sb.discard(unit)
     r = sb.engine.export()
     np.savez(out_dir / f"rank{rank}_pipe.npz", mmer=r.mmer, hi=r.kmer_hi, lo=r.kmer_lo, count=r.count,
              offset=r.offset, ids=r.ids)
