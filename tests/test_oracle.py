@@ -4,6 +4,7 @@ where the reference is buildable (this container), to the reference binary on
 fresh seeded inputs -- including K < 2M, where the reference's incremental
 branch (binning.c:992-1021) is live."""
 import hashlib
+import pathlib
 import subprocess
 
 import numpy as np
@@ -123,3 +124,50 @@ def test_masked_oracle_is_a_partition(K, M, prune):
         np.testing.assert_array_equal(getattr(part, f), getattr(full, f)[keep])
     lists = [full.ids[full.offset[e]:full.offset[e + 1]] for e in np.flatnonzero(keep)]
     np.testing.assert_array_equal(part.ids, np.concatenate(lists))
+
+
+@pytest.mark.parametrize("K,M,err", [(31, 7, 1000), (63, 7, 10000), (21, 5, 0), (6, 3, 2000)])
+def test_stream_digest_matches_result(K, M, err):
+    """oracle.stream_digest (the full-size digests' path, kb_oracle.c
+    kbo_stream_digest: scan_read into per-worker count tables, then the list
+    positions counted down in a second scan) equals kbin.result_digest of the
+    oracle's own result, pruned and not, over several workers"""
+    import kbin
+    n, L = 2500, 150
+    bases = oracle.gen_reads(n, L, 30000, err, 4242)
+    lens = np.full(n, L, np.uint32)
+    for prune in (True, False):
+        ora = oracle.bin_reads(bases, lens, K, M, 1, prune)
+        want = tuple(int(x) for x in kbin.result_digest(ora))
+        got, nk = oracle.stream_digest(bases, n, L, K, M, 1, prune, workers=3, cap_log2=19)
+        assert got == want and nk == ora.n_kmers
+
+
+def test_gen_reads_stream():
+    """kbo_gen_reads: reads read_base .. of one stream (any slice of it agrees
+    with the whole), ACGT only, substitutions at the asked rate"""
+    a = oracle.gen_reads(400, 150, 100000, 10000, 77)
+    b = oracle.gen_reads(100, 150, 100000, 10000, 77, read_base=250)
+    assert a[250 * 150:350 * 150] == b
+    assert set(a) <= set(b"ACGT")
+    clean = oracle.gen_reads(400, 150, 100000, 0, 77)
+    diff = sum(x != y for x, y in zip(a, clean)) / len(a)
+    assert 0.006 < diff < 0.014  # 1 % substitutions
+
+
+def test_full_size_digest_fixtures():
+    """tests/golden/oracle_digests.json (tools/oracle_digest.py) holds the
+    bench workloads' own parameters; its C2 entry recomputes in seconds"""
+    import json
+    import bench
+    fx = json.loads((pathlib.Path(__file__).parent / "golden" / "oracle_digests.json").read_text())
+    for name in ("c2", "c3"):
+        wl, f = bench.WORKLOADS[name], fx[name]
+        assert (f["reads"], f["read_len"], f["genome"], f["err_ppm"], f["K"], f["M"]) == \
+            (wl["reads"], wl["read_len"], wl["genome"], wl["err_ppm"], wl["K"], wl["M"])
+        assert f["seed"] == bench.gen_seed(wl["seed"]) and f["kmers"] == wl["reads"] * (wl["read_len"] - wl["K"] + 1)
+    assert tuple(fx["c3"]["digest"]) == bench.C3_DIGEST
+    f = fx["c2"]
+    dig, nk = oracle.gen_stream_digest(f["reads"], f["read_len"], f["genome"], f["err_ppm"], f["seed"], f["K"], f["M"],
+                                       workers=8, cap_log2=23)
+    assert [hex(x) for x in dig] == f["digest"] and nk == f["kmers"]
