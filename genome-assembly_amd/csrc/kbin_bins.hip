@@ -2066,8 +2066,10 @@ DEV void bin_body(const BinArgs& A) {
             // (diagnostic builds: one wave arrives late at every loop top --
             // KB_DIAG_SKEW=w + 1 -- so a write-after-read across the last
             // barrier shows deterministically; the test suite runs it)
-            if (A.skew && (tid >> 6) == A.skew - 1u)
+            if (A.skew && (tid >> 6) == A.skew - 1u) {
                 for (int z = 0; z < 8; z++) __builtin_amdgcn_s_sleep(127);
+                asm volatile("" ::: "memory");  // (the depth is read after the sleep, not hoisted above it)
+            }
 #endif
             const uint32_t sp0 = S.spq[pq];
             if (sp0 == 0) break;  // uniform

@@ -180,6 +180,13 @@ struct kb_group {
     kb_params p{};
     int G = 1;            // ranks in the group
     bool local = false;   // device-copy transport (every rank in this process)
+    // host transport (kb_group_create_rank_host): the caller's collectives
+    // over host memory move the counts and the records (a gloo process group
+    // rehearsing several ranks on one GPU, where RCCL refuses shared devices);
+    // the routing, counts, offsets and receivers are this file's
+    bool host = false;
+    kb_group_host_transport ht{};
+    std::vector<uint64_t> hsend, hrecv;  // staging, 8-B words
     std::vector<Rank> r;  // the ranks of this process
     uint32_t W = 0;       // record words
     uint32_t part = 0, n_parts = 1;
@@ -328,6 +335,10 @@ int exchange_counts(kb_group* g, Unit& un) {
     if (g->local) {
         for (auto& rk : g->r)
             memcpy(&rows[(size_t)rk.grank * RS], rk.h_counts + (size_t)rk.grank * RS, RS * sizeof(uint64_t));
+    } else if (g->host) {
+        const Rank& rk = g->r[0];
+        if (g->ht.allgather(g->ht.user, rk.h_counts + (size_t)rk.grank * RS, (uint64_t)RS, rows.data()))
+            return gfail(KB_EDEVICE, "host transport: counts all-gather failed");
     } else {
         Rccl& R = rccl();
         for (auto& rk : g->r) {
@@ -405,6 +416,34 @@ int exchange_records(kb_group* g, Unit& un, int s) {
                 off += n;
             }
         }
+    } else if (g->host) {
+        // the rank's region slices to the host (packed by destination), the
+        // caller's all-to-all, the received records back to the receive slot
+        Rank& rk = g->r[0];
+        std::vector<uint64_t> sb(G), rb(G);
+        uint64_t ns = 0, nr = 0;
+        for (int peer = 0; peer < G; peer++) {
+            sb[peer] = un.C[(size_t)rk.grank * G + peer] * W * sizeof(uint64_t);
+            rb[peer] = un.C[(size_t)peer * G + rk.grank] * W * sizeof(uint64_t);
+            ns += sb[peer] / 8;
+            nr += rb[peer] / 8;
+        }
+        g->hsend.resize(std::max<uint64_t>(ns, 1));
+        g->hrecv.resize(std::max<uint64_t>(nr, 1));
+        GHIP(hipSetDevice(rk.dev));
+        uint64_t o = 0;
+        for (int peer = 0; peer < G; peer++) {
+            if (sb[peer])
+                GHIP(hipMemcpyAsync(g->hsend.data() + o, rk.regions[s].p + rk.soff[s][peer] * W, sb[peer],
+                                    hipMemcpyDeviceToHost, rk.xs));
+            o += sb[peer] / 8;
+        }
+        GHIP(hipStreamSynchronize(rk.xs));
+        if (g->ht.alltoallv(g->ht.user, g->hsend.data(), sb.data(), g->hrecv.data(), rb.data()))
+            return gfail(KB_EDEVICE, "host transport: record all-to-all failed");
+        if (nr) GHIP(hipMemcpyAsync(rk.rbuf[s].p, g->hrecv.data(), nr * 8, hipMemcpyHostToDevice, rk.xs));
+        // (the staging is reused by the next unit: the copy completes first)
+        GHIP(hipStreamSynchronize(rk.xs));
     } else {
         Rccl& R = rccl();
         GNCCL(R.GroupStart());
@@ -567,6 +606,29 @@ extern "C" int kb_group_create_rank(const kb_params* p, int rank, int n_ranks, c
     return KB_OK;
 }
 
+extern "C" int kb_group_create_rank_host(const kb_params* p, int rank, int n_ranks, const kb_group_host_transport* t,
+                                         kb_group** out) {
+    if (!p || !out || !t || !t->allgather || !t->alltoallv || n_ranks < 1 || rank < 0 || rank >= n_ranks)
+        return gfail(KB_EINVAL, "kb_group_create_rank_host: bad arguments");
+    *out = nullptr;
+    kb_group* g = new kb_group();
+    g->p = *p;
+    g->G = n_ranks;
+    g->host = true;
+    g->ht = *t;
+    g->r.resize(1);
+    g->r[0].dev = p->device;
+    g->r[0].grank = rank;
+    const int rc = group_init(g);
+    if (rc) {
+        const std::string e = kb_last_error();
+        kb_group_destroy(g);
+        return gfail(rc, "%s", e.c_str());
+    }
+    *out = g;
+    return KB_OK;
+}
+
 extern "C" void kb_group_destroy(kb_group* g) {
     if (!g) return;
     {
@@ -584,7 +646,7 @@ extern "C" int kb_group_info(kb_group* g, int* n_ranks, int* n_local, int* rank0
     if (n_ranks) *n_ranks = g->G;
     if (n_local) *n_local = (int)g->r.size();
     if (rank0) *rank0 = g->r[0].grank;
-    if (transport) *transport = g->local ? KB_TRANSPORT_LOCAL : KB_TRANSPORT_RCCL;
+    if (transport) *transport = g->local ? KB_TRANSPORT_LOCAL : g->host ? KB_TRANSPORT_HOST : KB_TRANSPORT_RCCL;
     return KB_OK;
 }
 

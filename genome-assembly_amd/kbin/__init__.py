@@ -39,7 +39,7 @@ EXPORTED = [
     "kb_group_unique_id", "kb_group_create", "kb_group_create_rank", "kb_group_destroy", "kb_group_info",
     "kb_group_submit_ids", "kb_group_submit_packed_device", "kb_group_set_partition", "kb_group_send",
     "kb_group_receive", "kb_group_finalize", "kb_group_discard", "kb_group_reset", "kb_group_ctx",
-    "kb_group_send_async", "kb_group_unit_counts",
+    "kb_group_send_async", "kb_group_unit_counts", "kb_group_create_rank_host",
 ]
 KB_TRANSPORT_RCCL, KB_TRANSPORT_LOCAL = 1, 2
 
@@ -147,7 +147,9 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_group_set_partition.argtypes = [vp, u32, u32]
     lib.kb_group_send.argtypes = [vp, C.POINTER(u64)]
     # (A/B builds of an earlier tree -- KB_LIB_PATH -- may lack the newest calls)
-    for name, at in (("kb_group_send_async", [vp]), ("kb_group_unit_counts", [vp, C.POINTER(u64)])):
+    for name, at in (("kb_group_send_async", [vp]), ("kb_group_unit_counts", [vp, C.POINTER(u64)]),
+                     ("kb_group_create_rank_host", [C.POINTER(kb_params), C.c_int, C.c_int,
+                                                    C.POINTER(kb_group_host_transport), C.POINTER(vp)])):
         if hasattr(lib, name):
             getattr(lib, name).argtypes = at
     lib.kb_group_receive.argtypes = [vp, C.c_int]
@@ -455,16 +457,29 @@ def group_unique_id() -> bytes:
     return buf.raw
 
 
+KB_TRANSPORT_HOST = 3
+HOST_ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_uint64, C.POINTER(C.c_uint64))
+HOST_ALLTOALLV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p,
+                             C.POINTER(C.c_uint64))
+
+
+class kb_group_host_transport(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("allgather", HOST_ALLGATHER), ("alltoallv", HOST_ALLTOALLV)]
+
+
 class Group:
     """A multi-GPU binning group (kbin.h "multi-GPU groups"): G ranks sharded
     by canonical mmer; records exchanged over RCCL from C (or device copies
     for virtual shards on one device).  devices: every rank in this process
     (kb_group_create); rank/n_ranks/unique_id: this process is one rank
-    (kb_group_create_rank on `device`)."""
+    (kb_group_create_rank on `device`); rank/n_ranks/host=(allgather,
+    alltoallv): one rank whose counts and records move through the caller's
+    host-memory collectives (kb_group_create_rank_host; kbin.dist builds them
+    on a gloo process group)."""
 
     def __init__(self, K: int, M: int, cutoff: int = 1, max_read_len: int = 1024, *, devices=None,
                  rank: int | None = None, n_ranks: int | None = None, unique_id: bytes | None = None,
-                 device: int = 0, flags: int = 0, lib_path=None):
+                 device: int = 0, flags: int = 0, lib_path=None, host=None):
         self.lib = load_library(lib_path)
         self.K, self.M, self.cutoff = K, M, cutoff
         p = kb_params(K=K, M=M, cutoff=cutoff, max_read_len=max_read_len, device=device, flags=flags,
@@ -474,6 +489,11 @@ class Group:
             devs = list(devices) if devices is not None else [device]
             arr = (C.c_int * len(devs))(*devs)
             _check(self.lib, self.lib.kb_group_create(C.byref(p), len(devs), arr, C.byref(h)))
+        elif host is not None:
+            # (the callbacks live as long as the group: the sender thread calls them)
+            self._ht = kb_group_host_transport(None, HOST_ALLGATHER(host[0]), HOST_ALLTOALLV(host[1]))
+            _check(self.lib, self.lib.kb_group_create_rank_host(C.byref(p), int(rank), int(n_ranks),
+                                                                C.byref(self._ht), C.byref(h)))
         else:
             _check(self.lib, self.lib.kb_group_create_rank(C.byref(p), int(rank), int(n_ranks), unique_id,
                                                            len(unique_id), C.byref(h)))

@@ -36,7 +36,10 @@ r+1's): they are the reverse-call-order key of every id list.
 """
 from __future__ import annotations
 
+import ctypes as C
 import time
+
+import numpy as np
 
 import torch
 import torch.distributed as dist
@@ -335,6 +338,46 @@ class ShardedBinner:
                            "receive_ms": (t2 - t1) * 1e3}
 
 
+class HostCollectives:
+    """The host transport of a C group (kb_group_create_rank_host) over a
+    torch.distributed gloo process group of its own (the group's sender thread
+    calls these while the caller's thread may run collectives of its own on
+    the default group): the counts all-gather and the records' all-to-all, on
+    CPU tensors.  Exceptions become a failed unit (non-zero return)."""
+
+    def __init__(self, group=None):
+        ranks = list(range(dist.get_world_size(group))) if group is None else dist.get_process_group_ranks(group)
+        self.pg = dist.new_group(ranks=ranks, backend="gloo")
+        self.world = len(ranks)
+        self.errors = []
+
+    def allgather(self, user, mine, n, out) -> int:
+        try:
+            t = torch.from_numpy(np.ctypeslib.as_array(mine, shape=(n,)).view(np.int64).copy())
+            got = [torch.empty(n, dtype=torch.int64) for _ in range(self.world)]
+            dist.all_gather(got, t, group=self.pg)
+            np.ctypeslib.as_array(out, shape=(n * self.world,)).view(np.int64)[:] = torch.cat(got).numpy()
+            return 0
+        except Exception as e:  # (reported by the unit's receive)
+            self.errors.append(repr(e))
+            return 1
+
+    def alltoallv(self, user, send, send_bytes, recv, recv_bytes) -> int:
+        try:
+            sb = [int(x) for x in np.ctypeslib.as_array(send_bytes, shape=(self.world,))]
+            rb = [int(x) for x in np.ctypeslib.as_array(recv_bytes, shape=(self.world,))]
+            inp = torch.from_numpy(np.ctypeslib.as_array(C.cast(send, C.POINTER(C.c_uint8)), shape=(max(1, sum(sb)),))
+                                   [:sum(sb)].copy())
+            out = torch.empty(sum(rb), dtype=torch.uint8)
+            dist.all_to_all_single(out, inp, output_split_sizes=rb, input_split_sizes=sb, group=self.pg)
+            if sum(rb):
+                C.memmove(recv, out.data_ptr(), sum(rb))
+            return 0
+        except Exception as e:
+            self.errors.append(repr(e))
+            return 1
+
+
 class GroupBinner(ShardedBinner):
     """ShardedBinner over the C-ABI multi-GPU group: kb_group_create_rank on
     this rank's device (torch.distributed broadcasts the 128-byte RCCL unique
@@ -349,11 +392,16 @@ class GroupBinner(ShardedBinner):
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = torch.device("cuda", device)
-        box = [group_unique_id() if self.rank == 0 else None]
-        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
-                                   group=group)
-        self.grp = Group(K, M, cutoff=cutoff, max_read_len=max_read_len, rank=self.rank, n_ranks=self.world,
-                         unique_id=box[0], device=device, flags=flags)
+        if dist.get_backend(group) == "nccl":
+            box = [group_unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
+            self.grp = Group(K, M, cutoff=cutoff, max_read_len=max_read_len, rank=self.rank, n_ranks=self.world,
+                             unique_id=box[0], device=device, flags=flags)
+        else:  # (gloo: the C group over host collectives -- the rehearsal of the RCCL path's bookkeeping)
+            self._host = HostCollectives(group)
+            self.grp = Group(K, M, cutoff=cutoff, max_read_len=max_read_len, rank=self.rank, n_ranks=self.world,
+                             device=device, flags=flags, host=(self._host.allgather, self._host.alltoallv))
         self.engine = self.grp.ctx(0)
         self.last_counts = None
         self.last_times = {}

@@ -331,10 +331,28 @@ void *kb_stream(kb_ctx *ctx);
 typedef struct kb_group kb_group;
 #define KB_TRANSPORT_RCCL 1
 #define KB_TRANSPORT_LOCAL 2
+#define KB_TRANSPORT_HOST 3
+/* kb_group_create_rank_host: one rank per process whose counts and records
+ * move through the caller's collectives over host memory (e.g. a gloo process
+ * group rehearsing several ranks on one GPU, where RCCL refuses a shared
+ * device); routing, count bookkeeping, offsets and receivers are the group's
+ * own.  Called from the group's sender thread, in send order, on every rank:
+ *   allgather: every rank's n words, concatenated by rank, into all;
+ *   alltoallv: send holds send_bytes[d] bytes for rank d, packed by d; recv
+ *              gets recv_bytes[s] bytes from rank s, packed by s.
+ * Each returns 0 on success. */
+typedef struct {
+    void *user;
+    int (*allgather)(void *user, const uint64_t *mine, uint64_t n, uint64_t *all);
+    int (*alltoallv)(void *user, const void *send, const uint64_t *send_bytes, void *recv,
+                     const uint64_t *recv_bytes);
+} kb_group_host_transport;
 int kb_group_unique_id(void *out, size_t len);
 int kb_group_create(const kb_params *params, int n_gpus, const int *devices, kb_group **out);
 int kb_group_create_rank(const kb_params *params, int rank, int n_ranks, const void *unique_id, size_t len,
                          kb_group **out);
+int kb_group_create_rank_host(const kb_params *params, int rank, int n_ranks, const kb_group_host_transport *t,
+                              kb_group **out);
 void kb_group_destroy(kb_group *grp);
 int kb_group_info(kb_group *grp, int *n_ranks, int *n_local, int *rank0, int *transport);
 int kb_group_submit_ids(kb_group *grp, int local, const char *bases, const uint32_t *lens, uint64_t n_reads,

@@ -31,7 +31,9 @@ def main():
     kbin.generate_reads_device(words.data_ptr(), lens.data_ptr(), n, L, 300000, 2000, 77,
                                device=dev, read_base=rank * n)
     torch.cuda.synchronize()
-    sb = ShardedBinner(K, M, 1, L, device=dev)
+    # (KB_DIST_TRANSPORT=c under gloo: the C group -- its routing, counts and
+    # offsets -- over host collectives; default: the torch exchange)
+    sb = ShardedBinner(K, M, 1, L, device=dev, transport=os.environ.get("KB_DIST_TRANSPORT") or None)
     for _ in range(2):  # twice: buffers and contexts are reused across steps
         sb.step(words, lens, n, wpr, first_id=rank * n)
     r = sb.engine.export()

@@ -105,3 +105,50 @@ def test_encoder_roundtrip_single_rank():
     got = skmer_ref.bin_occurrences(skmer_ref.decode(recs, K, M))
     want = skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, True))
     assert got == want
+
+
+def _host_worker(rank, world, port, q):
+    import ctypes as C
+    from kbin.dist import HostCollectives
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hc = HostCollectives()
+        # counts rows (G counts + a status word, as kbin_group.hip sends them)
+        row = (C.c_uint64 * (world + 1))(*([10 * rank + d for d in range(world)] + [0]))
+        out = (C.c_uint64 * ((world + 1) * world))()
+        assert hc.allgather(None, row, world + 1, out) == 0, hc.errors
+        # records: rank r sends (r + 1)(d + 1) 8-B words to rank d, each word r << 8 | d
+        sw = [(rank + 1) * (d + 1) for d in range(world)]
+        rw_ = [(s + 1) * (rank + 1) for s in range(world)]
+        send = np.concatenate([np.full(n, (rank << 8) | d, np.uint64) for d, n in enumerate(sw)])
+        recv = np.zeros(sum(rw_), np.uint64)
+        sb = (C.c_uint64 * world)(*[8 * n for n in sw])
+        rb = (C.c_uint64 * world)(*[8 * n for n in rw_])
+        assert hc.alltoallv(None, send.ctypes.data, sb, recv.ctypes.data, rb) == 0, hc.errors
+        if rank == 1:
+            q.put((list(out), recv.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_group_host_collectives():
+    """kbin.dist.HostCollectives -- the host transport the C group
+    (kb_group_create_rank_host) calls for its counts all-gather and record
+    all-to-all under a gloo process group -- at world size 2 on CPU"""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rows, recv = got
+    assert rows == [0, 1, 0, 10, 11, 0]
+    # rank 1 receives 2 words from rank 0 (0 << 8 | 1), then 4 from itself (1 << 8 | 1)
+    assert recv == [1, 1] + [257] * 4
