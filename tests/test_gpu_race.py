@@ -13,8 +13,11 @@ partition parity.
 The diagnostic build (lib/abl, KB_BIN_ABL) lets one wave arrive ~60 K cycles
 late at every partition-loop top (KB_DIAG_SKEW = wave + 1): with the old
 single word that wave reads the next partition's depth every time a bin has a
-second partition, so the result breaks deterministically; every build must
-stay bit-exact under it.  Inputs use 1024-slot tables (KB_BIN_TS_LOG2=10) so
+second partition.  Evidence (gpurun_out/r5g3, profiles/r05/race/): round 4's
+single word (tools/race_ab.sh) under this stress ended its first finalize in
+an illegal memory access -- the out-of-step wave runs on stale cursors -- so
+that mutation check is NOT part of the suite (a faulting kernel risks the
+box); the fixed build stays bit-exact under it in every case below.  Inputs use 1024-slot tables (KB_BIN_TS_LOG2=10) so
 that most bins take several offset / hash partitions and overflow redos.
 """
 import json
@@ -61,14 +64,3 @@ def test_partition_loop_skew_ranked():
     assert out["ok"], out
     assert out["paths"].get("ranked_bins", 0) > 0, out["paths"]
 
-
-OLD = REPO / "genome-assembly_amd" / "lib" / "race_old" / "libkbin.so"
-
-
-@pytest.mark.skipif(not OLD.exists(), reason="evidence build lib/race_old not built (tools/race_ab.sh)")
-def test_skew_reproduces_round4_race():
-    """mutation check of the stress itself: round 4's single stack word
-    (tools/race_ab.sh) breaks under the late wave, so the stress does reach
-    the write-after-read the fix removes"""
-    out = run_worker(OLD, 6)
-    assert not out["ok"], out
