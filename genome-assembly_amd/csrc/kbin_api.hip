@@ -1230,10 +1230,7 @@ static kb_ctx::BucketMap* bmap_find(kb_ctx* c, uint32_t NB) {
 // bucket -- a light bin of its own in bin_kernel: no flat lists, no
 // re-expansion per partition, finer longest-first scheduling.
 static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
-    // (depth 5 only in the light pre-filtered regime, C5's giant mmers: the
-    // other regimes' bins are light at depth 4 already)
-    const int bdef = c->KW == 2 && c->pfl_regime ? (int)SUB_MAX_B : 4;
-    int bmax = std::min<int>((int)SUB_MAX_B, std::max(0, env_int("KB_BIN_SUB", bdef)));
+    int bmax = std::min<int>((int)SUB_MAX_B, std::max(0, env_int("KB_BIN_SUB", (int)SUB_MAX_B)));
     if (!sub_room(c->p.K, c->p.M, 2 * c->KW)) bmax = 0;  // (no spare span bits for the stamp)
     const double ts = c->KW == 1 ? 8192.0 : 4096.0;
     // (the long-list regime: sub-bins at 40 % of a table, so that they stay under
@@ -1256,7 +1253,7 @@ static uint64_t bin_budget(const kb_ctx* c, uint32_t NB) {
     // (at most 240: a bucket orders up to BK_SLOTS = 256 bins, one per mmer plus its extra sub-bins)
     // (the light pre-filtered regime splits every heavy mmer ~64 ways: a larger budget)
     const uint64_t per_bucket =
-        (uint64_t)std::min(240, std::max(0, env_int("KB_BIN_SUB_EXTRA", c->rank_regime || c->pfl_regime ? 240 : 48)));
+        (uint64_t)std::min(240, std::max(0, env_int("KB_BIN_SUB_EXTRA", c->rank_regime ? 240 : c->pfl_regime ? 160 : 48)));
     return half + (sub_room(c->p.K, c->p.M, 2 * c->KW) ? per_bucket * NB : 0ull);
 }
 

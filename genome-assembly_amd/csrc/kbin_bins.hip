@@ -2601,9 +2601,12 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(const BinArgs* __restr
 }
 
 // phase 0 with ranked bins (the long-list regime)
+// (the ranked variant keeps its arguments by value: through the pointer its
+// deep loops -- the windows' stage pass, the bitmap emission -- spilled more
+// VGPRs to scratch, C3 39.0 -> 44.9 ms per pass, gpurun_out r5g3)
 template <int KW>
-__global__ __launch_bounds__(BIN_THREADS) void bin_kernel_ranked(const BinArgs* __restrict__ A) {
-    bin_body<KW, 0, true>(*A);
+__global__ __launch_bounds__(BIN_THREADS) void bin_kernel_ranked(BinArgs A) {
+    bin_body<KW, 0, true>(A);
 }
 
 // phase 1: the heavy bins' partitions, any block any partition
@@ -4539,10 +4542,14 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     hipLaunchKernelGGL(bin_args_kernel, dim3(1), dim3(64), 0, s, a2, d_args);
     // timing: the kernel's own start and stop (hipExtLaunchKernelGGL) -- an
     // event recorded on the stream before and after it idled the GPU ~6 us each
-    hipExtLaunchKernelGGL(a.rank_mode ? bin_kernel_ranked<KW> : bin_kernel<KW>,
-                          dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS),
-                          (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr, ev_bin ? ev_bin[1] : nullptr, 0u,
-                          (const BinArgs*)d_args);
+    if (a.rank_mode)
+        hipExtLaunchKernelGGL(bin_kernel_ranked<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)),
+                              dim3(BIN_THREADS), (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr,
+                              ev_bin ? ev_bin[1] : nullptr, 0u, a2);
+    else
+        hipExtLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)),
+                              dim3(BIN_THREADS), (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr,
+                              ev_bin ? ev_bin[1] : nullptr, 0u, (const BinArgs*)d_args);
     e = hipGetLastError();
     if (e != hipSuccess || !heavy) return e;
     return launch_heavy_kw<KW>(a, s, d_args);

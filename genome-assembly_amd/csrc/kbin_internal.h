@@ -170,11 +170,12 @@ __device__ __forceinline__ uint64_t region_room(const uint64_t* base, uint64_t c
 // first so - (K - M - b) k-mers into the edge.  (Measured on uniform reads at
 // K31 M7: b = 2 leaves 1.2 % of the occurrences in the edge and cuts 9.5 % of
 // the records; the 16 context sub-bins hold 0.76..1.10 x their mean.)
-// (depth 5, 1025 sub-bins: C5's heaviest mmers -- up to 41 M occurrences
-// per pass -- split finely enough that their sub-bins stay light behind the
-// pre-filter's sketch; round 4 stopped at depth 4, 257)
-constexpr uint32_t SUB_MAX_B = 5;                      // 1025 sub-bins at most
-constexpr uint32_t SUB_BITS = 11;                      // sub-bin index bits (2 SUB_MAX_B + 1)
+// (round 5 tried depth 5, 1025 sub-bins, for C5's giant mmers with an 11-bit
+// stamp -- K63 M7 leaves 9 spare bases, so the record has room: 2.9 x the
+// bins, 6 x the light pre-filtered ones, but 35 % more heavy ones and the C5
+// share 490 -> 637 ms per step (gpurun_out r5g5); depth 4 stays)
+constexpr uint32_t SUB_MAX_B = 4;                      // 257 sub-bins at most
+constexpr uint32_t SUB_BITS = 9;                       // sub-bin index bits (2 SUB_MAX_B + 1)
 __host__ __device__ inline uint32_t sub_count(uint32_t b) { return b ? (1u << (2 * b)) + 1u : 1u; }
 
 // Bucket map entry (u32 per canonical mmer - 2^(2M-1)):
@@ -193,9 +194,7 @@ __device__ __forceinline__ uint32_t bm_bucket(uint32_t e, const uint16_t* sub_ma
 // read.  Splitting needs that room (and the bucket ordering then groups the
 // records by (mmer, sub-bin) without the map).  K31 M7 and K63 M7 leave 9
 // spare bases, the reference's K31 M4 six.
-__host__ __device__ inline bool sub_room(int K, int M, int spw) {
-    return 2 * (32 * spw - (2 * K - M)) >= (int)SUB_BITS;
-}
+__host__ __device__ inline bool sub_room(int K, int M, int spw) { return 32 * spw - (2 * K - M) >= 5; }
 static_assert(2 * SUB_MAX_B + 1 <= SUB_BITS, "the stamp holds every sub-bin index");
 constexpr uint64_t SUB_MASK = (1ull << SUB_BITS) - 1ull;
 
