@@ -2091,6 +2091,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         a.ts_adapt = (uint32_t)(env_int("KB_BIN_TS_ADAPT", 1) != 0);
         a.corrupt = (uint32_t)(env_int("KB_DIAG_CORRUPT", 0) != 0);
         a.skew = (uint32_t)std::max(0, env_int("KB_DIAG_SKEW", 0));
+        a.diag_alloc = (uint32_t)(env_int("KB_DIAG_ALLOC", 0) != 0);
         // ranked bins where lists are long (the last finalize's mean list
         // length, C3: ~2200 ids): KB_BIN_RANK=0 off, 2 always
         {

@@ -2363,10 +2363,25 @@ DEV void bin_body(const BinArgs& A) {
                 // entries and ids from ONE packed counter (entries << 32 | ids; both
                 // totals < 2^32): consecutive entries own consecutive id ranges,
                 // so offset[e + 1] ends entry e's list (the CSR contract)
+#ifdef KB_BIN_ABL
+                if (A.diag_alloc) {
+                    // (diagnostic: the price of this returning device-scope
+                    // atomic on the partition's critical path -- a second one
+                    // in series before it, results unchanged)
+                    const unsigned long long d = atomicAdd(&A.gcount[2], 0ull);
+                    const unsigned long long got = tot ? atomicAdd(&A.gcount[0] + (d == ~0ull ? 1 : 0),
+                                                                   ((unsigned long long)ne << 32) | ni)
+                                                       : 0ull;
+                    S.e0 = got >> 32;
+                    S.i0 = got & 0xFFFFFFFFull;
+                } else
+#endif
+                {
                 const unsigned long long got =
                     tot ? atomicAdd(&A.gcount[0], ((unsigned long long)ne << 32) | ni) : 0ull;
                 S.e0 = got >> 32;
                 S.i0 = got & 0xFFFFFFFFull;
+                }
                 if (S.e0 + ne > A.max_entries || S.i0 + ni > A.max_ids) atomicOr(A.status, ST_TABLE_FULL);
             }
             bar_lds(A);

@@ -320,6 +320,8 @@ struct BinArgs {
     uint32_t ldsbar;           // 1: barriers that order LDS only skip the global-store drain (KB_BIN_LDSBAR)
     uint32_t corrupt;          // diagnostic (KB_DIAG_CORRUPT=1): block 0 adds one to a count, so the
                                // finalize's invariant (sum of pre-prune counts == k-mers) must fail
+    uint32_t diag_alloc;       // diagnostic builds (KB_BIN_ABL): a second returning atomic in series with
+                               // the prune's allocation (KB_DIAG_ALLOC; prices its round trip)
     uint32_t skew;             // diagnostic builds (KB_BIN_ABL): wave skew - 1 arrives late at every
                                // partition-loop top (KB_DIAG_SKEW; a barrier-ordering stress test)
     // Ranked bins (long lists, C3's coverage): a light bin first ranks its
