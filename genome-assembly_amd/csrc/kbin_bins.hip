@@ -26,6 +26,7 @@
 
 #include <hip/hip_ext.h>
 
+#define KB_BINS_TU  // (kbin_internal.h: BinArgs pointers are global in this file's device code)
 #include "kbin_internal.h"
 #include "kbin_device.h"
 
@@ -2600,8 +2601,11 @@ DEV void bin_body(const BinArgs& A) {
 // The bin kernels read their arguments from device memory (bin_args_kernel
 // puts them there, stream-ordered, right before): a by-value BinArgs is
 // loaded into SGPRs at entry and stays live through the whole persistent loop
-// (297 SGPRs and 25 VGPRs spilled, 104 B of scratch per lane in bin_kernel<1>);
-// through a pointer the fields are loaded nearer their uses
+// (297 SGPRs and 25 VGPRs spilled, 104 B of scratch per lane in bin_kernel<1>;
+// the ranked variant 456 / 73 / 280 B); through a pointer the fields are
+// loaded nearer their uses (109 / 13 / 40 B; ranked 194 / 45 / 168 B) -- with
+// the pointer fields global-typed (kbin_internal.h KB_G), else every access
+// through them is a FLAT instruction
 __global__ __launch_bounds__(64) void bin_args_kernel(BinArgs a, BinArgs* __restrict__ dst) {
     static_assert(sizeof(BinArgs) % 8 == 0, "copied in 8-B words");
     constexpr uint32_t NW = sizeof(BinArgs) / 8;
@@ -2616,12 +2620,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_kernel(const BinArgs* __restr
 }
 
 // phase 0 with ranked bins (the long-list regime)
-// (the ranked variant keeps its arguments by value: through the pointer its
-// deep loops -- the windows' stage pass, the bitmap emission -- spilled more
-// VGPRs to scratch, C3 39.0 -> 44.9 ms per pass, gpurun_out r5g3)
 template <int KW>
-__global__ __launch_bounds__(BIN_THREADS) void bin_kernel_ranked(BinArgs A) {
-    bin_body<KW, 0, true>(A);
+__global__ __launch_bounds__(BIN_THREADS) void bin_kernel_ranked(const BinArgs* __restrict__ A) {
+    bin_body<KW, 0, true>(*A);
 }
 
 // phase 1: the heavy bins' partitions, any block any partition
@@ -4557,14 +4558,10 @@ static hipError_t launch_bins_kw(const BinArgs& a, uint64_t max_bins, hipStream_
     hipLaunchKernelGGL(bin_args_kernel, dim3(1), dim3(64), 0, s, a2, d_args);
     // timing: the kernel's own start and stop (hipExtLaunchKernelGGL) -- an
     // event recorded on the stream before and after it idled the GPU ~6 us each
-    if (a.rank_mode)
-        hipExtLaunchKernelGGL(bin_kernel_ranked<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)),
-                              dim3(BIN_THREADS), (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr,
-                              ev_bin ? ev_bin[1] : nullptr, 0u, a2);
-    else
-        hipExtLaunchKernelGGL(bin_kernel<KW>, dim3((unsigned)std::min<uint64_t>(max_bins, blocks)),
-                              dim3(BIN_THREADS), (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr,
-                              ev_bin ? ev_bin[1] : nullptr, 0u, (const BinArgs*)d_args);
+    hipExtLaunchKernelGGL(a.rank_mode ? bin_kernel_ranked<KW> : bin_kernel<KW>,
+                          dim3((unsigned)std::min<uint64_t>(max_bins, blocks)), dim3(BIN_THREADS),
+                          (std::uint32_t)lds, s, ev_bin ? ev_bin[0] : nullptr, ev_bin ? ev_bin[1] : nullptr, 0u,
+                          (const BinArgs*)d_args);
     e = hipGetLastError();
     if (e != hipSuccess || !heavy) return e;
     return launch_heavy_kw<KW>(a, s, d_args);

@@ -213,43 +213,56 @@ __device__ __forceinline__ uint32_t sub_ctx(int so, int K, int M, uint32_t b, ui
 
 constexpr uint32_t KB_FLAT_MAX = 16384;  // partitions of one heavy bin's flat lists (kbin_bins.hip FLAT_MAX)
 
+// The bin kernels read BinArgs through a pointer (launch_bins): pointers loaded
+// from device memory are generic to the compiler, so every access through them
+// became a FLAT instruction -- counted in lgkmcnt as well, so each LDS wait
+// (every barrier) also waited for the global stores in flight.  In device code
+// the fields are global-address-space pointers (the layout is the host's) --
+// in kbin_bins.hip's device pass, where the bin kernels live (KB_BINS_TU): the
+// other files' host code assigns the fields from generic pointers, which the
+// device pass of those files also type-checks.
+#if defined(__HIP_DEVICE_COMPILE__) && defined(KB_BINS_TU)
+#define KB_G __attribute__((address_space(1)))
+#else
+#define KB_G
+#endif
 struct BinArgs {
-    const uint64_t* hdr;       // [2R] bin-ordered (header, span bases 0..31) pairs (header: SkScanArgs::pay)
-    const uint64_t* w1;        // [R] span bases 32..63, or [2R] (32..63, 64..95) pairs (K > 31)
-    const uint64_t* w3;        // [R] span bases 96..127 (K > 31: two-word k-mers)
-    const uint32_t* bstart;    // [nbins] first record of bin
-    const uint32_t* bcount;    // [nbins] records of bin
-    const uint32_t* bmmer;     // [nbins] canonical mmer of bin
-    const uint32_t* bocc;      // [nbins] its k-mer occurrences (0 or null: count them)
+    KB_G const uint64_t* hdr;       // [2R] bin-ordered (header, span bases 0..31) pairs (header: SkScanArgs::pay)
+    KB_G const uint64_t* w1;        // [R] span bases 32..63, or [2R] (32..63, 64..95) pairs (K > 31)
+    KB_G const uint64_t* w3;        // [R] span bases 96..127 (K > 31: two-word k-mers)
+    KB_G const uint32_t* bstart;    // [nbins] first record of bin
+    KB_G const uint32_t* bcount;    // [nbins] records of bin
+    KB_G const uint32_t* bmmer;     // [nbins] canonical mmer of bin
+    KB_G const uint32_t* bocc;      // [nbins] its k-mer occurrences (0 or null: count them)
     uint64_t max_bins;         // capacity of the descriptors (nbins never exceeds it)
-    unsigned long long* stage_ctr;  // stage allocation (zeroed): each bin takes its occurrences
-    const uint32_t* order;     // [nbins] processing order (largest bins first)
-    const uint4* bdesc;        // [2 nbins] or null: per processing slot {bin, start, count, mmer},
+    KB_G unsigned long long* stage_ctr;  // stage allocation (zeroed): each bin takes its occurrences
+    KB_G const uint32_t* order;     // [nbins] processing order (largest bins first)
+    KB_G const uint4* bdesc;        // [2 nbins] or null: per processing slot {bin, start, count, mmer},
                                // {occurrences, stage base lo, hi, 0} (bins_desc_kernel)
-    unsigned long long* work;  // work counter (zeroed)
-    uint64_t* stage;           // [N] (LDS slot << 48 | position << 32 | ordinal) per occurrence
+    KB_G unsigned long long* work;  // work counter (zeroed)
+    KB_G uint64_t* stage;           // [N] (LDS slot << 48 | position << 32 | ordinal) per occurrence
     // light bins of the first phase without first-occurrence tracking: the
     // stage as two arrays, 6 B per occurrence (null: the 8-B stage everywhere)
-    uint32_t* stage_ord;       // [N] ordinal
-    uint16_t* stage_slot;      // [N] LDS slot + 1 (0: not in the table)
-    uint64_t* kstage;          // [KW N] heavy bins: the k-mer's table key per occurrence, parallel to stage
+    KB_G uint32_t* stage_ord;       // [N] ordinal
+    KB_G uint16_t* stage_slot;      // [N] LDS slot + 1 (0: not in the table)
+    KB_G uint64_t* kstage;          // [KW N] heavy bins: the k-mer's table key per occurrence, parallel to stage
     uint32_t flat_l;           // heavy bin: initial partition depth >= flat_l (0 = never)
     // heavy bins, two launches: phase 0 bins every light bin and turns each heavy
     // bin into flat per-partition lists (published below); phase 1 sweeps the
     // published partitions, any block any partition
-    uint32_t* flat_list;            // [max_bins] published heavy bins
-    unsigned long long* flat_n;     // (zeroed) [0] published bins [1] pool [2] build items,
+    KB_G uint32_t* flat_list;            // [max_bins] published heavy bins
+    KB_G unsigned long long* flat_n;     // (zeroed) [0] published bins [1] pool [2] build items,
                                     // claims: [3] count [4] scatter [5] phase 1
-    uint32_t* flat_next;            // [max_bins] next partition to claim
-    uint32_t* flat_l0;              // [max_bins] partition depth
-    unsigned long long* flat_sbase; // [max_bins] stage base
-    unsigned long long* flat_obase; // [max_bins] the bin's range of flat_off
-    uint32_t* flat_off;             // pool of list offsets, np + 1 per heavy (or split) bin
-    uint32_t* flat_cur;             // the same layout: scatter cursors (flat bins)
-    uint32_t* flat_chunk;           // [max_bins] first build item (record chunk) of the bin
-    uint32_t* pool_bin;             // [flat_off] bin of an offset-pool entry (phase 1 items)
-    uint32_t* chunk_bin;            // [R / 1024 + max_bins] bin of a build item
-    unsigned long long* flat_octr;  // (zeroed) pool allocation
+    KB_G uint32_t* flat_next;            // [max_bins] next partition to claim
+    KB_G uint32_t* flat_l0;              // [max_bins] partition depth
+    KB_G unsigned long long* flat_sbase; // [max_bins] stage base
+    KB_G unsigned long long* flat_obase; // [max_bins] the bin's range of flat_off
+    KB_G uint32_t* flat_off;             // pool of list offsets, np + 1 per heavy (or split) bin
+    KB_G uint32_t* flat_cur;             // the same layout: scatter cursors (flat bins)
+    KB_G uint32_t* flat_chunk;           // [max_bins] first build item (record chunk) of the bin
+    KB_G uint32_t* pool_bin;             // [flat_off] bin of an offset-pool entry (phase 1 items)
+    KB_G uint32_t* chunk_bin;            // [R / 1024 + max_bins] bin of a build item
+    KB_G unsigned long long* flat_octr;  // (zeroed) pool allocation
     // split bins (light bins above a fair share of one block): published like
     // heavy bins (flat_l0 | SPLIT_BIT), their partitions binned from the records
     uint64_t n_occ;                 // occurrences of this finalize
@@ -257,12 +270,12 @@ struct BinArgs {
     uint64_t split_occ;             // (set at launch)
     uint32_t big_div;               // flat lists for a multi-table bin above n_occ / (blocks x big_div)
     uint64_t big_occ;               // (set at launch; 0 = by depth only)
-    const uint64_t* totals;    // totals[2] = nbins
+    KB_G const uint64_t* totals;    // totals[2] = nbins
     int K, M;
     uint32_t keep_gt;
     uint32_t ts_log2;
     float rho;                 // expected distinct keys per occurrence
-    const float* rho_dev;      // cold pass: rho estimated on the device (hll_finish_kernel); else null
+    KB_G const float* rho_dev;      // cold pass: rho estimated on the device (hll_finish_kernel); else null
     float fill;                // target table load when choosing the partition depth
     uint32_t ringfree;         // unpartitioned bins expand without the per-wave ring (KB_BIN_RINGFREE)
     // offset partitions: a light bin of initial depth 1 <= l <= opart is split by
@@ -278,25 +291,25 @@ struct BinArgs {
     uint64_t heavy_hint;       // heavy / split bins the last finalize published (0: small grids for their kernels)
     int ablate;                // diagnostic builds (KB_BIN_PROF / KB_BIN_ABL) only: 1 expansion only,
                                // 2 no staging, 3 no id windows, 4 windows without sorts
-    unsigned long long* gcount;  // [0] entries << 32 | ids  [2] distinct keys before prune
-    uint32_t* status;
-    uint32_t* e_mmer;
-    uint64_t* e_hi;
-    uint64_t* e_lo;
-    uint32_t* e_cnt;
-    uint64_t* e_off;
-    uint64_t* e_first;         // KB_TRACK_FIRST: (ordinal << 16 | position) of each key's first occurrence
-    uint32_t* ids_ord;
-    int32_t* ids_out;
-    const int32_t* read_ids;
+    KB_G unsigned long long* gcount;  // [0] entries << 32 | ids  [2] distinct keys before prune
+    KB_G uint32_t* status;
+    KB_G uint32_t* e_mmer;
+    KB_G uint64_t* e_hi;
+    KB_G uint64_t* e_lo;
+    KB_G uint32_t* e_cnt;
+    KB_G uint64_t* e_off;
+    KB_G uint64_t* e_first;         // KB_TRACK_FIRST: (ordinal << 16 | position) of each key's first occurrence
+    KB_G uint32_t* ids_ord;
+    KB_G int32_t* ids_out;
+    KB_G const int32_t* read_ids;
     uint32_t id_off;
     uint64_t max_entries, max_ids;
     // list items for lists_kernel: (first entry << 16 | entries <= 256) of every
     // partition whose ids took the global path (and one-entry items for lists
     // > 256 of the LDS path); the LDS path leaves its lists final in ids_out.
     // null: the global path for every partition, lists_kernel over all entries
-    uint64_t* lq_items;
-    unsigned long long* lq_n;  // (zeroed) items
+    KB_G uint64_t* lq_items;
+    KB_G unsigned long long* lq_n;  // (zeroed) items
     uint64_t lq_cap;
     // singleton pre-filter of heavy (flat) bins: a partition's k-mers first
     // go through a 2-bit "seen twice" sketch in LDS; keys seen once are
@@ -308,14 +321,14 @@ struct BinArgs {
                                // depth stays light, its singles screened by a per-bin LDS sketch
     uint32_t fs_lds;           // 1: heavy bins with 9..2048 partitions write their lists LDS-staged
     float rho_tab;             // expected table keys per occurrence under the pre-filter
-    unsigned long long* tab_keys;  // (zeroed) keys that entered a table
+    KB_G unsigned long long* tab_keys;  // (zeroed) keys that entered a table
     // (zeroed) path counters for kb_timing, one atomic per bin or partition:
     // [0] heavy bins published as flat lists [1] split bins published
     // [2] partitions swept to their prune [3] partitions redone split (overflow)
     // [4] deepest partition depth (max) [5] keys kept out by the pre-filter
     // [6] offset-range partitions [7] partitions swept from flat lists
     // [8] light pre-filtered bins [9] ranked bins [10] partitions emitted from rank bitmaps
-    unsigned long long* pstat;
+    KB_G unsigned long long* pstat;
     uint32_t ts_adapt;         // 1: one-table light bins take the smallest table for their keys (KB_BIN_TS_ADAPT)
     uint32_t ldsbar;           // 1: barriers that order LDS only skip the global-store drain (KB_BIN_LDSBAR)
     uint32_t corrupt;          // diagnostic (KB_DIAG_CORRUPT=1): block 0 adds one to a count, so the
@@ -333,8 +346,8 @@ struct BinArgs {
     // call order (binning.c:1061-1068) with no sort and no list kernels
     uint32_t rank_mode;        // 1: rank bins of 512 .. rank_max records (KB_BIN_RANK)
     uint32_t rank_merge;       // ranked bins: long lists' bitmaps set in the id windows' stage pass (KB_BIN_RANK_MERGE)
-    uint32_t* rrank;           // [R] record -> rank in its bin
-    uint32_t* rord;            // [R] (bin start + rank) -> ordinal
+    KB_G uint32_t* rrank;           // [R] record -> rank in its bin
+    KB_G uint32_t* rord;            // [R] (bin start + rank) -> ordinal
 };
 constexpr int KB_PSTAT = 11;
 // light pre-filtered bins (kbin_bins.hip): the per-bin sketch's cells and the
