@@ -721,7 +721,8 @@ hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint6
 // ---------------------------------------------------------------------------
 #ifdef KB_BIN_PROF
 // per-phase cycle accounting (tid 0, between barriers): a diagnostic build only
-__device__ unsigned long long g_bin_prof[26];
+constexpr int PROF_N = 34;
+__device__ unsigned long long g_bin_prof[PROF_N];
 #define PROF_MARK(ph)                                              \
     do {                                                           \
         if (tid == 0) {                                            \
@@ -1339,7 +1340,8 @@ template <int R>
 DEV void wave_sort_desc(uint32_t* p, uint32_t n, int lane);
 
 // (so, ss: the split stage of a light bin -- ordinals and slots -- or null:
-// the 8-B stage entries)
+// the 8-B stage entries; RK with so and no ss: a ranked bin's packed 4-B
+// stage, slot + 1 << 16 | rank)
 // (RK, rord_bin: a ranked bin's stage holds ranks; its ordinal is
 // rord_bin[rank]; only the kept short lists' occurrences are mapped.  bmw:
 // the long lists' bitmaps (bmW words each, past win_cap) -- their slots hold
@@ -1393,21 +1395,16 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
         }
         // ---- this window's occurrences into LDS at their list positions
         // (the claim words and rings are dead); WL stage loads in flight
+        PROF_CNT(26, ns);
+        PROF_CNT(29, 1);
         constexpr int WL = KB_WIN_LOADS;
+        // (a ranked bin's packed stage has a copy of the pass of its own: the
+        // layout test inside the unrolled loads cost C3 20 % of this phase)
+        auto place = [&](auto&& ld) {
         for (uint32_t i0s = tid; i0s < ns; i0s += (uint32_t)WL * BIN_THREADS) {
             uint32_t vo[WL], vs[WL];  // ordinal, slot + 1 (0: a pre-filtered single, or nothing)
 #pragma unroll
-            for (int u = 0; u < WL; u++) {
-                const uint32_t i = i0s + (uint32_t)u * BIN_THREADS;
-                if (so) {
-                    vo[u] = i < ns ? so[i] : 0u;
-                    vs[u] = i < ns ? (uint32_t)ss[i] : 0u;
-                } else {
-                    const uint64_t x = i < ns ? stage[i] : 0ull;
-                    vo[u] = (uint32_t)x;
-                    vs[u] = (uint32_t)(x >> 48);
-                }
-            }
+            for (int u = 0; u < WL; u++) ld(i0s + (uint32_t)u * BIN_THREADS, vo[u], vs[u]);
             if constexpr (RK) {
                 if (rord_bin) {
                     // only kept short lists of this window gather their ordinal;
@@ -1440,6 +1437,28 @@ DEV void lds_lists(const BinArgs& A, BinShared& S, uint32_t* cnt, uint32_t TS, u
                 const uint32_t pos = atomicAdd(&cnt[ls], 1u);
                 if (pos < PRUNED) wv[pos - wlo] = vo[u] + 1u;  // ordinal + 1 (0 pads the sorts)
             }
+        }
+        };
+        auto ld_any = [&](uint32_t i, uint32_t& o, uint32_t& sl) {
+            if (so) {
+                o = i < ns ? so[i] : 0u;
+                sl = i < ns ? (uint32_t)ss[i] : 0u;
+            } else {
+                const uint64_t x = i < ns ? stage[i] : 0ull;
+                o = (uint32_t)x;
+                sl = (uint32_t)(x >> 48);
+            }
+        };
+        if (RK && so && !ss) {  // a ranked bin's packed stage: slot + 1 << 16 | rank
+            place([&](uint32_t i, uint32_t& o, uint32_t& sl) {
+                const uint32_t x = i < ns ? so[i] : 0u;
+                o = x & 0xFFFFu;
+                sl = x >> 16;
+            });
+        } else {
+            // (the unranked kernel keeps the layout test inside the loads:
+            // separate copies measured C2 bin_kernel 1.233 -> 1.328 ms)
+            place(ld_any);
         }
         bar_lds(A);
         PROF_MARK(4);
@@ -1701,13 +1720,16 @@ DEV bool bitmap_lists(const uint64_t* __restrict__ e_off, const uint32_t* __rest
         // with non-returning atomics -- a bit set twice shows as a bitmap
         // holding fewer bits than its key's count, bm_check)
         constexpr int BL = 4;
+        PROF_CNT(27, ns);
+        PROF_CNT(33, 1);
         for (uint32_t j0 = tid; j0 < ns; j0 += (uint32_t)BL * BIN_THREADS) {
             uint32_t vs[BL], vr[BL];
 #pragma unroll
             for (int u = 0; u < BL; u++) {
                 const uint32_t i = j0 + (uint32_t)u * BIN_THREADS;
-                vs[u] = i < ns ? (uint32_t)ss[i] : 0u;
-                vr[u] = i < ns ? so[i] : 0u;
+                const uint32_t x = i < ns ? so[i] : 0u;  // (packed: slot + 1 << 16 | rank)
+                vs[u] = x >> 16;
+                vr[u] = x & 0xFFFFu;
             }
 #pragma unroll
             for (int u = 0; u < BL; u++) {
@@ -1762,7 +1784,7 @@ DEV void bin_body(const BinArgs& A) {
     const uint64_t nbins = min(A.totals[2], A.max_bins);
     const uint32_t tid = threadIdx.x;
 #ifdef KB_BIN_PROF
-    unsigned long long pacc[26] = {};
+    unsigned long long pacc[PROF_N] = {};
     unsigned long long pt = clock64();
 #endif
     if (tid < 64) S.dummy[tid] = 0;  // (the first loop barrier publishes it)
@@ -2025,6 +2047,7 @@ DEV void bin_body(const BinArgs& A) {
                 bar_lds(A);
                 PROF_MARK(7);
                 bin_ranks(A.hdr, A.rrank, A.rord, S, lo, hi, nl, cnt PROF_ARGS);
+                PROF_CNT(30, R);
                 if (tid == 0 && A.pstat) atomicAdd(&A.pstat[9], 1ull);
             }
         }
@@ -2055,6 +2078,12 @@ DEV void bin_body(const BinArgs& A) {
         uint32_t* const sp_ord = A.stage_ord && !A.e_first ? A.stage_ord + S.stage_base + fa : nullptr;
         uint16_t* const sp_slot = sp_ord ? A.stage_slot + S.stage_base + fa : nullptr;
         const bool sp_ord_w = !(PHASE == 1 && flat);
+        // a ranked bin stages 4 B per occurrence, slot + 1 << 16 | rank (its
+        // ranks and slots are 16-bit): one store in sweep 1 and one load per
+        // occurrence in each later stage pass, instead of 4 + 2 B in two arrays
+        // (C3: 3 G occurrences per pass written once and read 1.3 times)
+        const bool pk = RANKED && rmode && sp_ord;
+        const uint16_t* const sp_slot_rd = pk ? nullptr : sp_slot;
         while (true) {
             const uint32_t ts = S.ts, bmask = ts / 4 - 1, limit = ts - ts / 4;  // (uniform)
             // (the stack is stable here: every write to it is followed by a
@@ -2178,7 +2207,9 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_ABL
                         if (A.ablate != 2)
 #endif
-                        if (sp_ord) {
+                        if (pk) {
+                            sp_ord[s0] = ((uint32_t)(l0 + 1) << 16) | o0;
+                        } else if (sp_ord) {
                             if (sp_ord_w) sp_ord[s0] = o0;
                             sp_slot[s0] = (uint16_t)(l0 + 1);
                         } else {
@@ -2194,7 +2225,9 @@ DEV void bin_body(const BinArgs& A) {
 #ifdef KB_BIN_ABL
                         if (A.ablate != 2)
 #endif
-                        if (sp_ord) {
+                        if (pk) {
+                            sp_ord[s1] = ((uint32_t)(l1 + 1) << 16) | o1;
+                        } else if (sp_ord) {
                             if (sp_ord_w) sp_ord[s1] = o1;
                             sp_slot[s1] = (uint16_t)(l1 + 1);
                         } else {
@@ -2436,6 +2469,7 @@ DEV void bin_body(const BinArgs& A) {
             // no kept ids -- must not read them after tid 0 reset them for the
             // next partition)
             const uint32_t n_stage = S.n_stage, maxc = S.maxc;
+            PROF_CNT(31, n_stage);
             const uint32_t n_ent_all = (uint32_t)tot;
             const uint32_t n_ent = (uint32_t)tot_s, n_ids = (uint32_t)(tot_s >> 32);  // the short lists
             // a ranked partition's long lists: from bitmaps over the ranks when
@@ -2456,6 +2490,7 @@ DEV void bin_body(const BinArgs& A) {
                                     n_ids <= 64u * n_ent && A.rank_merge;
                 bool bm_ok;
                 if (merged) {
+                    PROF_CNT(28, 1);
                     uint32_t* offs = win + (win_cap - tail);
                     uint32_t* tile = offs + ((n_long + 3u) & ~3u);
                     uint32_t* bm = tile + RANK_TILE_WORDS;
@@ -2464,7 +2499,7 @@ DEV void bin_body(const BinArgs& A) {
                     if (tid == 0) S.dup = 0;
                     __syncthreads();
                     lds_lists<KW, RANKED>(A, S, cnt, ts, win, win_cap - tail, n_stage, e0, i0, n_ent, n_ids, stage,
-                                          sp_ord, sp_slot, (uint32_t)ex, A.rord + lo, bm, W PROF_ARGS);
+                                          sp_ord, sp_slot_rd, (uint32_t)ex, A.rord + lo, bm, W PROF_ARGS);
                     __syncthreads();
                     PROF_MARK(18);
                     bm_ok = bm_check(A.e_off, A.e_cnt, S, cnt, per, e0, i0, n_ent, (uint32_t)ex_l, 0u, n_long, bm, W);
@@ -2475,7 +2510,7 @@ DEV void bin_body(const BinArgs& A) {
                     const uint32_t G = fixed + W <= win_cap ? (win_cap - fixed) / W : 0u;
                     bm_ok = G && (n_long + G - 1u) / G <= RANK_GROUPS &&
                             bitmap_lists<KW>(A.e_off, A.e_cnt, A.ids_out, A.read_ids, A.id_off, S, cnt, ts, win, win_cap,
-                                             n_stage, e0, i0, n_long, n_ent, (uint32_t)ex_l, sp_ord, sp_slot,
+                                             n_stage, e0, i0, n_long, n_ent, (uint32_t)ex_l, sp_ord, sp_slot_rd,
                                              R, A.rord + lo PROF_ARGS);
                 }
                 if (bm_ok) {
@@ -2485,11 +2520,12 @@ DEV void bin_body(const BinArgs& A) {
                     // to ordinals in one coalesced pass (no gather inside the
                     // atomics' dependent chain)
                     const uint32_t ns = n_stage;
+                    PROF_CNT(32, ns);
                     for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
-                        const uint32_t sl = sp_slot[i];
+                        const uint32_t x = sp_ord[i], sl = pk ? x >> 16 : sp_slot[i];
                         if (!sl || (cnt[sl - 1u] & (LONGB | PRUNED)) != LONGB) continue;
                         const uint32_t pos = atomicAdd(&cnt[sl - 1u], 1u) & ~LONGB;
-                        A.ids_ord[i0 + pos] = sp_ord[i];
+                        A.ids_ord[i0 + pos] = pk ? x & 0xFFFFu : x;
                     }
                     __syncthreads();
                     const uint32_t l0i = (uint32_t)(tot_s >> 32), l1i = (uint32_t)(tot >> 32);
@@ -2520,7 +2556,7 @@ DEV void bin_body(const BinArgs& A) {
             // and two-word keys (C5: 624 -> 641 ms) keep the global path
             if (win_phase && lds_ok && maxc <= win_cap - 3u && n_ids <= 64u * n_ent) {
                 lds_lists<KW, RANKED>(A, S, cnt, ts, win, win_cap, n_stage, e0, i0, n_ent, n_ids, stage, sp_ord,
-                                      sp_slot, (uint32_t)ex, rmode ? A.rord + lo : nullptr, nullptr, 0u PROF_ARGS);
+                                      sp_slot_rd, (uint32_t)ex, rmode ? A.rord + lo : nullptr, nullptr, 0u PROF_ARGS);
                 PROF_MARK(4);
                 continue;
             }
@@ -2535,7 +2571,13 @@ DEV void bin_body(const BinArgs& A) {
                 const uint32_t pmask = (1u << Lv) - 1u;
                 for (uint32_t i = tid; i < ns; i += BIN_THREADS) {
                     if (filt && (kst_load<KW>(kst, fa + i).part() & pmask) != P) continue;
-                    const uint64_t v = sp_ord ? ((uint64_t)sp_slot[i] << 48) | sp_ord[i] : stage[i];
+                    uint64_t v;
+                    if (pk) {
+                        const uint32_t x = sp_ord[i];
+                        v = ((uint64_t)(x >> 16) << 48) | (x & 0xFFFFu);
+                    } else {
+                        v = sp_ord ? ((uint64_t)sp_slot[i] << 48) | sp_ord[i] : stage[i];
+                    }
                     if (PHASE == 1 && !(v >> 48)) continue;  // a pre-filtered single (flat partitions only)
                     const uint32_t ls = (uint32_t)(v >> 48) - 1u;
                     // one returning atomic: a pruned key's cursor starts at PRUNED and
@@ -2587,7 +2629,7 @@ DEV void bin_body(const BinArgs& A) {
     }
 #ifdef KB_BIN_PROF
     if (tid == 0)
-        for (int i = 0; i < 26; i++) {
+        for (int i = 0; i < PROF_N; i++) {
             if (i == 12) continue;
             if (i == 13) {  // max over blocks (and that bin's occurrences)
                 if (atomicMax(&g_bin_prof[13], pacc[13]) < pacc[13]) g_bin_prof[12] = pacc[12];
@@ -3016,7 +3058,7 @@ __global__ __launch_bounds__(FSL_THREADS) void flat_scatter_lds_kernel(BinArgs A
 
 #ifdef KB_BIN_PROF
 void bins_prof_report(hipStream_t s) {
-    unsigned long long h[26];
+    unsigned long long h[PROF_N];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bin_prof), sizeof(h));
     {
@@ -3026,14 +3068,16 @@ void bins_prof_report(hipStream_t s) {
         unsigned long long z8[8] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sk_prof), z8, sizeof(z8));
     }
-    static const char* nm[26] = {"bin records", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
+    static const char* nm[PROF_N] = {"bin records", "zero", "sweep1", "prune/entries", "sweep2/win place", "win sort", "win ids out", "flat",
                                  "partitions", "overflows", "omode-ovf(1e6*n+1e3*width+Lv)", "bins", "slowest-bin-occ", "slowest-bin-cycles",
-                                 "occ", "records expanded", "rank", "long bitmaps", "bitmap set", "bitmap emit", "bin claim", "bin desc", "rank loads", "rank hist", "rank scatter", "rank stores"};
+                                 "occ", "records expanded", "rank", "long bitmaps", "bitmap set", "bitmap emit", "bin claim", "bin desc", "rank loads", "rank hist", "rank scatter", "rank stores",
+                                 "win stage reads", "bm stage reads", "merged parts", "windows", "ranked records", "stage writes",
+                                 "rank-fallback stage reads", "bm groups"};
     fprintf(stderr, "[bin_prof]");
-    for (int i = 0; i < 26; i++)
+    for (int i = 0; i < PROF_N; i++)
         if (h[i]) fprintf(stderr, " %s=%llu", nm[i], h[i]);
     fprintf(stderr, "\n");
-    unsigned long long z[26] = {};
+    unsigned long long z[PROF_N] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bin_prof), z, sizeof(z));
 }
 #endif
