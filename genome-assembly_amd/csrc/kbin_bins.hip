@@ -721,7 +721,7 @@ hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint6
 // ---------------------------------------------------------------------------
 #ifdef KB_BIN_PROF
 // per-phase cycle accounting (tid 0, between barriers): a diagnostic build only
-constexpr int PROF_N = 34;
+constexpr int PROF_N = 37;
 __device__ unsigned long long g_bin_prof[PROF_N];
 #define PROF_MARK(ph)                                              \
     do {                                                           \
@@ -1798,11 +1798,16 @@ DEV void bin_body(const BinArgs& A) {
         // first.  Phase 1: the partitions of the heavy bins phase 0 turned into
         // flat lists, any block any partition (a giant bin is no longer one
         // workgroup's serial loop)
+        PROF_MARK(34);  // (the bin's tail)
         bar_lds(A);
+        PROF_MARK(35);  // (the loop-top barrier)
         if (tid == 0) {
             if (PHASE == 0) {
                 S.item = (uint32_t)min(next_item, 0xFFFFFFFFull);
                 if (next_item < nbins) next_item = atomicAdd(A.work, 1ull);
+#ifdef KB_BIN_PROF
+                if (next_item == 0xFFFFFFFFFFFFull) S.dup = 1;  // (the claim's wait, measured here)
+#endif
             } else {
                 // items are offset-pool indices: entry e0 + p of a published
                 // bin is its partition p (the bin's last entry is no item)
@@ -1819,6 +1824,7 @@ DEV void bin_body(const BinArgs& A) {
                 }
             }
         }
+        PROF_MARK(36);  // (tid 0's claim)
         bar_lds(A);
         PROF_MARK(20);
         if (PHASE == 0 ? S.item >= nbins : S.item == 0xFFFFFFFFu) break;  // uniform
@@ -3072,7 +3078,7 @@ void bins_prof_report(hipStream_t s) {
                                  "partitions", "overflows", "omode-ovf(1e6*n+1e3*width+Lv)", "bins", "slowest-bin-occ", "slowest-bin-cycles",
                                  "occ", "records expanded", "rank", "long bitmaps", "bitmap set", "bitmap emit", "bin claim", "bin desc", "rank loads", "rank hist", "rank scatter", "rank stores",
                                  "win stage reads", "bm stage reads", "merged parts", "windows", "ranked records", "stage writes",
-                                 "rank-fallback stage reads", "bm groups"};
+                                 "rank-fallback stage reads", "bm groups", "bin tail", "loop-top barrier", "claim wait"};
     fprintf(stderr, "[bin_prof]");
     for (int i = 0; i < PROF_N; i++)
         if (h[i]) fprintf(stderr, " %s=%llu", nm[i], h[i]);
