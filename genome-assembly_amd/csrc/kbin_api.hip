@@ -433,9 +433,10 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     // (the zeroing goes up as a host-to-device copy: the context's first such
     // copy sets up the copy path, here rather than inside a first finalize)
     memset(c->h_totals, 0, 32 * sizeof(uint64_t));
-    if (c->misc.ensure_exact(16) != hipSuccess || c->totals.ensure_exact(16) != hipSuccess ||
+    if (c->misc.ensure_exact(16) != hipSuccess || c->totals.ensure_exact(KB_TOTALS) != hipSuccess ||
         hipMemsetAsync(c->misc.p, 0, 16 * sizeof(uint32_t), c->s) != hipSuccess ||
-        hipMemcpyAsync(c->totals.p, c->h_totals, 16 * sizeof(uint64_t), hipMemcpyHostToDevice, c->s) != hipSuccess ||
+        hipMemcpyAsync(c->totals.p, c->h_totals, KB_TOTALS * sizeof(uint64_t), hipMemcpyHostToDevice, c->s) !=
+            hipSuccess ||
         hipStreamSynchronize(c->s) != hipSuccess) {
         kb_destroy(c);
         return fail(KB_ENOMEM, "device alloc");
@@ -792,7 +793,7 @@ static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered
 // destination = owner(mmer); counts now, a stable sort by destination and
 // the pack in kb_route_pack (same record format and order as route_kernel)
 static int route_plan_binned(kb_ctx* c, uint32_t G, uint64_t* h_counts) {
-    HIPCHK(c->totals.ensure(16));
+    HIPCHK(c->totals.ensure(KB_TOTALS));
     uint64_t R = 0, N = 0;
     int rc = binned_read_records(c, R, N, true);  // routed records keep read order
     if (rc) return rc;
@@ -1536,8 +1537,10 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
     // capacity (stride), rerun bigger on overflow.
     const bool exact = bmap == nullptr;
     HIPCHK(c->bfill.ensure(NB));
+    // (every batch's per-block k-mer sums side by side: one sum at the end,
+    // inside bucket_stats_kernel, where each batch launched a kernel for it)
     uint64_t kp = 1;
-    for (auto& b : c->batches) kp = std::max(kp, sk_blocks(b.n_reads, b.RW));
+    for (auto& b : c->batches) kp += b.routed || b.superkmers ? 0 : sk_blocks(b.n_reads, b.RW);
     HIPCHK(c->kpart.ensure(kp));
     if (exact) HIPCHK(c->rbase.ensure(NB + 1));
     HIPCHK(c->regions.ensure(1));  // (non-null: the record kernel's region mode keys on it)
@@ -1554,6 +1557,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
             HIPCHK(launch_clear(cl, c->s));
         }
         if (!counting && !use_base) HIPCHK(c->regions.ensure(NB * cap * RWD));
+        uint64_t koff = 0;  // (kpart entries written by this attempt's record passes)
         for (auto& b : c->batches) {
             if (b.routed || !b.n_reads) continue;
             if (received) {
@@ -1585,14 +1589,15 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
                 a.sub_map = bsub;
                 a.sub_stamp = bm && bm->split ? 1 : 0;
                 a.binned_fmt = 1;
-                a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p);
+                a.n_kmers = reinterpret_cast<unsigned long long*>(c->kpart.p) + koff;
                 HIPCHK(launch_sk(a, true, c->s));
-                HIPCHK(launch_sk_kmers_total(reinterpret_cast<unsigned long long*>(c->kpart.p),
-                                             sk_blocks(b.n_reads, b.RW),
-                                             reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
+                koff += sk_blocks(b.n_reads, b.RW);
             }
             c->tm.scan_insert_launches++;
         }
+        if (counting && koff)
+            HIPCHK(launch_sk_kmers_total(reinterpret_cast<unsigned long long*>(c->kpart.p), koff,
+                                         reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
         std::vector<unsigned long long> fill(counting ? NB : 0);
         uint64_t mx = 0;
         if (counting) {  // the exact layout needs every bucket's count
@@ -1603,7 +1608,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
         } else {  // R, the largest bucket and the status word folded next to N: one copy
             HIPCHK(c->bbase.ensure(NB + 1));
             HIPCHK(launch_bucket_stats(c->bfill.p, NB, c->misc.p, c->totals.p, cap, use_base ? c->rbase.p : nullptr,
-                                       c->bbase.p, c->s));
+                                       c->bbase.p, reinterpret_cast<unsigned long long*>(c->kpart.p), koff, c->s));
             HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         }
         HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync (two without a map): R and N size the rest
@@ -2123,8 +2128,10 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
 #ifdef KB_BIN_PROF
         bins_prof_report(c->s);
 #endif
+        // (deferred tail: nothing runs after bins_final, so it gathers the
+        // finalize's stats next to the totals for one copy instead of three)
         HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries, flat_l ? c->flat_n.p : nullptr,
-                                 a.lq_n, c->s));
+                                 a.lq_n, defer ? c->pstat.p : nullptr, defer ? c->misc.p : nullptr, c->s));
         REC(4);
         ListArgs la{};
         la.totals = c->totals.p;
@@ -2150,8 +2157,13 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         lists_prof_report(c->s);
 #endif
         REC(5);
-        HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 14 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
-        HIPCHK(hipMemcpyAsync(c->h_totals + 16, c->pstat.p, KB_PSTAT * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        if (defer) {
+            HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 31 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+        } else {
+            HIPCHK(hipMemcpyAsync(c->h_totals, c->totals.p, 14 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
+            HIPCHK(hipMemcpyAsync(c->h_totals + 16, c->pstat.p, KB_PSTAT * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                  c->s));
+        }
         if (learn) {  // the bins' descriptors for the map (bmap_apply), in the same copy batch
             HIPCHK(c->h_bins.ensure(3 * max_bins));
             HIPCHK(hipMemcpyAsync(c->h_bins.p, c->bmmer.p, max_bins * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
@@ -2160,11 +2172,16 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             HIPCHK(hipMemcpyAsync(c->h_bins.p + 2 * max_bins, c->bocc.p, max_bins * sizeof(uint32_t),
                                   hipMemcpyDeviceToHost, c->s));
         }
-        HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
+        if (!defer) HIPCHK(hipMemcpyAsync(c->h_misc, c->misc.p, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         if (R && !bucketed)
             HIPCHK(hipMemcpyAsync(c->h_misc + 8, c->os_aux.p + 1028, sizeof(uint32_t), hipMemcpyDeviceToHost, c->s));
         else c->h_misc[8] = 0;
         HIPCHK(hipStreamSynchronize(c->s));
+        if (defer)
+            for (int k = 0; k < 3; k++) {
+                c->h_misc[2 * k] = (uint32_t)c->h_totals[28 + k];
+                c->h_misc[2 * k + 1] = (uint32_t)(c->h_totals[28 + k] >> 32);
+            }
         if (defer && (c->h_totals[12] || c->h_totals[13])) {
             // the tail after all (a heavy bin published, or lists queued):
             // full grids, then the totals again
@@ -2172,7 +2189,7 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
             a.heavy_hint = ~0ull;
             HIPCHK(launch_bins_heavy(a, KW, c->s, c->bargs.p));
             HIPCHK(launch_bins_final(a.gcount, c->e_off.p, c->totals.p, a.max_entries,
-                                     flat_l ? c->flat_n.p : nullptr, a.lq_n, c->s));
+                                     flat_l ? c->flat_n.p : nullptr, a.lq_n, nullptr, nullptr, c->s));
             la.lq_hint = ~0ull;
             la.long_hint[0] = la.long_hint[1] = ~0ull;
             HIPCHK(launch_lists(la, c->n_occ_entries_hint ? c->n_occ_entries_hint : ecap, c->s));

@@ -4630,7 +4630,12 @@ hipError_t launch_bins_heavy(const BinArgs& a, int KW, hipStream_t s, const BinA
 
 __global__ void bins_final_kernel(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                                   uint64_t max_entries, const unsigned long long* flat_n,
-                                  const unsigned long long* lq_n) {
+                                  const unsigned long long* lq_n, const unsigned long long* pstat,
+                                  const uint32_t* misc) {
+    if (pstat)  // (the finalize's stats next to the totals: one copy, kbin_internal.h)
+        for (int k = 0; k < KB_PSTAT; k++) totals[16 + k] = pstat[k];
+    if (misc)
+        for (int k = 0; k < 3; k++) totals[28 + k] = (uint64_t)misc[2 * k] | ((uint64_t)misc[2 * k + 1] << 32);
     // (the next finalize's grid hints: published heavy / split bins, queued list items)
     totals[12] = flat_n ? flat_n[0] : 0ull;
     totals[13] = lq_n ? *lq_n : 0ull;
@@ -4656,11 +4661,15 @@ __global__ __launch_bounds__(1024) void clear_kernel(ClearList l) {
 __global__ __launch_bounds__(1024) void bucket_stats_kernel(const unsigned long long* __restrict__ bfill, uint32_t NB,
                                                             const uint32_t* misc, uint64_t* totals, uint64_t cap,
                                                             const uint64_t* __restrict__ rbase,
-                                                            uint64_t* __restrict__ bbase) {
+                                                            uint64_t* __restrict__ bbase,
+                                                            const unsigned long long* __restrict__ kpart, uint64_t nk) {
     __shared__ uint64_t red[16];
     __shared__ uint32_t mxw[16];
     const uint32_t t = threadIdx.x;
     const int lane = (int)(t & 63u), wid = (int)(t >> 6);
+    // (the record pass's per-block k-mer sums: N, where a kernel of its own did it)
+    uint64_t ks = 0;
+    for (uint64_t i = t; i < nk; i += 1024) ks += kpart[i];
     const uint64_t f = t < NB ? bfill[t] : 0ull;  // (NB <= 1024)
     const uint64_t v = t < NB ? min<uint64_t>(f, region_room(rbase, cap, t)) : 0ull;
     const uint64_t inc = wave_incl_scan(v, lane);
@@ -4668,24 +4677,32 @@ __global__ __launch_bounds__(1024) void bucket_stats_kernel(const unsigned long 
     const uint32_t m = wave_max_u32((uint32_t)min<uint64_t>(f, 0xFFFFFFFFull));
     uint64_t fs = f;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) fs += (uint64_t)__shfl_xor((long long)fs, off, 64);
+    for (int off = 32; off > 0; off >>= 1) {
+        fs += (uint64_t)__shfl_xor((long long)fs, off, 64);
+        ks += (uint64_t)__shfl_xor((long long)ks, off, 64);
+    }
     if (lane == 63) red[wid] = inc;
     if (lane == 0) mxw[wid] = m;
-    __shared__ uint64_t fsum[16];
-    if (lane == 0) fsum[wid] = fs;
+    __shared__ uint64_t fsum[16], ksum[16];
+    if (lane == 0) {
+        fsum[wid] = fs;
+        ksum[wid] = ks;
+    }
     __syncthreads();
-    uint64_t wp = 0, tot = 0, sum = 0;
+    uint64_t wp = 0, tot = 0, sum = 0, kt = 0;
     uint32_t mx = 0;
 #pragma unroll
     for (int w = 0; w < 16; w++) {
         if (w < wid) wp += red[w];
         tot += red[w];
         sum += fsum[w];
+        kt += ksum[w];
         mx = max(mx, mxw[w]);
     }
     if (t < NB) bbase[t] = wp + inc - v;
     if (t == 0) {
         bbase[NB] = tot;
+        totals[8] += kt;
         totals[12] = sum;
         totals[13] = mx;
         totals[14] = misc[0];
@@ -4693,9 +4710,11 @@ __global__ __launch_bounds__(1024) void bucket_stats_kernel(const unsigned long 
 }
 
 hipError_t launch_bucket_stats(const unsigned long long* bfill, uint32_t NB, const uint32_t* misc, uint64_t* totals,
-                               uint64_t cap, const uint64_t* rbase, uint64_t* bbase, hipStream_t s) {
+                               uint64_t cap, const uint64_t* rbase, uint64_t* bbase, const unsigned long long* kpart,
+                               uint64_t nk, hipStream_t s) {
     if (NB > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(bucket_stats_kernel, dim3(1), dim3(1024), 0, s, bfill, NB, misc, totals, cap, rbase, bbase);
+    hipLaunchKernelGGL(bucket_stats_kernel, dim3(1), dim3(1024), 0, s, bfill, NB, misc, totals, cap, rbase, bbase,
+                       kpart, nk);
     return hipGetLastError();
 }
 
@@ -4707,8 +4726,9 @@ hipError_t launch_clear(const ClearList& l, hipStream_t s) {
 
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                              uint64_t max_entries, const unsigned long long* flat_n, const unsigned long long* lq_n,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(bins_final_kernel, dim3(1), dim3(1), 0, s, gcount, e_off, totals, max_entries, flat_n, lq_n);
+                             const unsigned long long* pstat, const uint32_t* report_misc, hipStream_t s) {
+    hipLaunchKernelGGL(bins_final_kernel, dim3(1), dim3(1), 0, s, gcount, e_off, totals, max_entries, flat_n, lq_n,
+                       pstat, report_misc);
     return hipGetLastError();
 }
 

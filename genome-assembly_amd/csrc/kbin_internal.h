@@ -455,12 +455,17 @@ struct ClearList {
 };
 hipError_t launch_clear(const ClearList& l, hipStream_t s);
 // totals[12] = sum of the NB bucket fills (records), totals[13] = the largest,
-// totals[14] = status word misc[0]: the record pass's results in one copy
+// totals[14] = status word misc[0]: the record pass's results in one copy;
+// totals[8] += the nk per-block k-mer sums kpart (the record pass's N)
 hipError_t launch_bucket_stats(const unsigned long long* bfill, uint32_t NB, const uint32_t* misc, uint64_t* totals,
-                               uint64_t cap, const uint64_t* rbase, uint64_t* bbase, hipStream_t s);
+                               uint64_t cap, const uint64_t* rbase, uint64_t* bbase, const unsigned long long* kpart,
+                               uint64_t nk, hipStream_t s);
+// report (non-null): the finalize's stats in one copy -- totals[16 ..
+// 16 + KB_PSTAT) = pstat, totals[28 .. 31) = misc[0 .. 6) in pairs
 hipError_t launch_bins_final(const unsigned long long* gcount, uint64_t* e_off, uint64_t* totals,
                              uint64_t max_entries, const unsigned long long* flat_n, const unsigned long long* lq_n,
-                             hipStream_t s);
+                             const unsigned long long* pstat, const uint32_t* report_misc, hipStream_t s);
+constexpr int KB_TOTALS = 32;  // device totals words (the report layout above)
 
 // launch helpers implemented in kbin_kernels.hip (all asynchronous on `s`)
 hipError_t launch_pack(const uint8_t* d_bases, const uint64_t* d_off, uint64_t n_reads,
