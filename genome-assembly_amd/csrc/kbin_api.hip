@@ -2044,6 +2044,11 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         // ~2300 ids measured 342 -> 351 ms with them)
         a.win_heavy = (uint32_t)(env_int("KB_BIN_WIN_HEAVY", 1) != 0 &&
                                  (c->hint_entries == 0 || c->hint_ids <= 128 * c->hint_entries));
+        // (bit 1: two-word keys too -- KB_BIN_WIN_HEAVY2; C5 share 510 -> 482 ms
+        // per step: its short lists no longer wait for the list kernels, emit
+        // 32 -> 0.04 ms, the bin phase +4.5 ms; round 2 had measured 624 -> 641
+        // before the pre-filter, r5g29)
+        if (a.win_heavy && env_int("KB_BIN_WIN_HEAVY2", 1)) a.win_heavy |= 2u;
         a.gcount = reinterpret_cast<unsigned long long*>(c->totals.p + 4);
         a.status = c->misc.p + 2;  // the bin kernel's own status word
         a.e_mmer = c->e_mmer.p;

@@ -2482,7 +2482,8 @@ DEV void bin_body(const BinArgs& A) {
             // they fit the window area in at most RANK_GROUPS groups, else (or on
             // a key seen twice in one record) ordinals at their cursors and the
             // list kernels; then their slots leave the short lists' way
-            const bool win_phase = PHASE == 0 || (KW == 1 && A.win_heavy && !(flat && Lv > l0));
+            const bool win_phase =
+                PHASE == 0 || ((KW == 1 || (A.win_heavy & 2u)) && (A.win_heavy & 1u) && !(flat && Lv > l0));
             if (RANKED && n_ent_all > n_ent) {
                 PROF_MARK(3);
                 const uint32_t n_long = n_ent_all - n_ent;

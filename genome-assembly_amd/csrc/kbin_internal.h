@@ -287,7 +287,7 @@ struct BinArgs {
     uint32_t osplit;           // big light bins split by offset range across blocks (KB_BIN_OSPLIT; experimental)
     uint8_t ocut[5][17];
     uint32_t fsl_run;          // LDS-staged flat lists below this many entries per partition per chunk
-    uint32_t win_heavy;        // LDS id windows in the heavy bins' partitions too (KB_BIN_WIN_HEAVY)
+    uint32_t win_heavy;        // LDS id windows in the heavy bins' partitions too (KB_BIN_WIN_HEAVY; bit 1: two-word keys)
     uint64_t heavy_hint;       // heavy / split bins the last finalize published (0: small grids for their kernels)
     int ablate;                // diagnostic builds (KB_BIN_PROF / KB_BIN_ABL) only: 1 expansion only,
                                // 2 no staging, 3 no id windows, 4 windows without sorts
