@@ -329,6 +329,10 @@ struct kb_ctx {
     PinBuf<uint8_t> map_stage;  // bucket map uploads (bmap_build)
     hipEvent_t map_done = nullptr;
     bool map_stage_used = false;
+    // the bucket ordering launched before the mid-finalize wait (spec_bucket_phase)
+    hipEvent_t ev_mid = nullptr;
+    bool spec = false;
+    uint64_t spec_rlay = 0, spec_bins = 0, prev_R = 0;
     bool exported = false;
 
     // timing
@@ -399,6 +403,8 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
         if (e != hipSuccess) { kb_destroy(c); return fail(KB_EDEVICE, "hipEventCreate"); }
     }
     e = hipEventCreateWithFlags(&c->map_done, hipEventDisableTiming);
+    if (e != hipSuccess) { kb_destroy(c); return fail(KB_EDEVICE, "hipEventCreate"); }
+    e = hipEventCreateWithFlags(&c->ev_mid, hipEventDisableTiming);
     if (e != hipSuccess) { kb_destroy(c); return fail(KB_EDEVICE, "hipEventCreate"); }
     {
         {
@@ -472,6 +478,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->h_mmer.release(); c->h_cnt.release(); c->h_hi.release(); c->h_lo.release(); c->h_off.release();
     c->h_first.release(); c->h_ids.release(); c->h_bins.release(); c->map_stage.release();
     if (c->map_done) (void)hipEventDestroy(c->map_done);
+    if (c->ev_mid) (void)hipEventDestroy(c->ev_mid);
     if (c->h_alpha) (void)hipHostFree(c->h_alpha);
     c->table.release(); c->occ_a.release();
     c->seg.release(); c->pay.release(); c->srec.release(); c->stage.release(); c->stage_ord.release(); c->stage_slot.release(); c->kstage.release(); c->rrank.release(); c->rord.release(); c->bargs.release(); c->long_q.release(); c->border.release(); c->bdesc.release(); c->bcount.release(); c->bmmer.release(); c->bocc.release();
@@ -1509,8 +1516,66 @@ static int bmap_prior(kb_ctx* c, uint32_t NB) {
     return KB_OK;
 }
 
+// The bucket ordering and the bin plan of a bucketed pass: records in rlay
+// slots (hdr pairs, then w1 / w3 at 2 rlay / 4 rlay), descriptors for
+// max_bins bins.  rcap (speculative launches): records past it are not
+// placed -- the layout was sized from the last pass, and the caller reruns.
+static int bucket_phase(kb_ctx* c, uint32_t NB, uint64_t rlay, uint64_t max_bins, uint64_t cap, bool rexact,
+                        uint64_t rcap, bool plan = true) {
+    const int KW = c->KW;
+    const uint64_t RWD = 1 + 2 * (uint64_t)KW;
+    HIPCHK(c->starts.ensure(max_bins + 1));
+    HIPCHK(c->bcount.ensure(max_bins));
+    HIPCHK(c->bmmer.ensure(max_bins));
+    HIPCHK(c->bocc.ensure(max_bins));
+    HIPCHK(c->srec.ensure(RWD * rlay));
+    BucketArgs ba{};
+    ba.regions = c->regions.p;
+    ba.cap = cap;
+    ba.rbase = rexact ? c->rbase.p : nullptr;
+    ba.bfill = c->bfill.p;
+    ba.M = c->p.M;
+    ba.hdr = c->srec.p;  // ((header, word 0) pairs, then word 1 / (word 1, word 2) pairs + word 3)
+    ba.w1 = c->srec.p + 2 * rlay;
+    ba.w3 = KW == 2 ? c->srec.p + 4 * rlay : nullptr;
+    ba.spw = 2 * KW;
+    HIPCHK(c->bbase.ensure(NB + 1));
+    ba.bbase = c->bbase.p;
+    ba.bases_ready = 1;  // (bucket_stats_kernel, after the record pass that made these regions)
+    {
+        // records written by a map-routed pass carry their sub-bin (zero
+        // for an unsplit mmer); a hash-routed pass writes spans untouched
+        kb_ctx::BucketMap* bm = bmap_find(c, NB);  // (the map the record pass used)
+        ba.sub = bm && bm->split ? 1 : 0;
+    }
+    ba.bin_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 2);
+    ba.bstart = c->starts.p;
+    ba.bcount = c->bcount.p;
+    ba.bmmer = c->bmmer.p;
+    ba.bocc = c->bocc.p;
+    ba.max_bins = max_bins;
+#ifdef KB_BIN_ABL
+    {   // (diagnostic: from a context's third finalize on, so the records
+        // the bin kernel reads are the last pass's -- replay input only)
+        static int abl_calls = 0;
+        ba.ablate = abl_calls++ >= 2 ? env_int("KB_BK_ABLATE", 0) : 0;
+    }
+#endif
+    ba.status = c->misc.p;
+    ba.rcap = rcap;
+    HIPCHK(launch_bucket_sort(ba, NB, c->s));
+    c->tm.sort_passes = 0;
+    if (!plan) return KB_OK;  // (KB_BIN_DESC=0: the caller orders the bins by count)
+    HIPCHK(c->border.ensure(max_bins));
+    HIPCHK(c->bdesc.ensure(2 * max_bins));
+    HIPCHK(launch_bins_plan(c->starts.p, c->bcount.p, c->bmmer.p, c->bocc.p, c->totals.p, max_bins, c->border.p,
+                            c->bdesc.p, reinterpret_cast<unsigned long long*>(c->totals.p + 10), c->s));
+    return KB_OK;
+}
+
 static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, uint64_t& R, uint64_t& N) {
     const int M = c->p.M;
+    c->spec = false;
     kb_ctx::BucketMap* bm = bmap_find(c, NB);
     if (bm && bm->pending) {  // the last pass of this key left its bins: rebuild the map from them
         const double t0 = now_ms();
@@ -1549,13 +1614,16 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
         const bool counting = exact && attempt == 0;
         const bool use_base = exact && attempt > 0;
         const uint64_t cap = exact ? 0 : bm->cap;
+        if (c->spec) HIPCHK(hipStreamSynchronize(c->s));  // (a rerun: nothing in flight reads what is regrown)
         if (attempt > 0 || !zeroed) {  // (the finalize's first clear zeroed them for attempt 0)
             ClearList cl{};
             cl.add(c->bfill.p, NB * sizeof(unsigned long long));
             cl.add(c->totals.p + 8, sizeof(uint64_t));
             cl.add(c->misc.p, sizeof(uint32_t));
+            if (c->spec) cl.add(c->totals.p + 2, sizeof(uint64_t));  // (the speculative ordering's bins)
             HIPCHK(launch_clear(cl, c->s));
         }
+        c->spec = false;
         if (!counting && !use_base) HIPCHK(c->regions.ensure(NB * cap * RWD));
         uint64_t koff = 0;  // (kpart entries written by this attempt's record passes)
         for (auto& b : c->batches) {
@@ -1611,7 +1679,26 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
                                        c->bbase.p, reinterpret_cast<unsigned long long*>(c->kpart.p), koff, c->s));
             HIPCHK(hipMemcpyAsync(c->h_totals + 8, c->totals.p + 8, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
         }
-        HIPCHK(hipStreamSynchronize(c->s));  // the one mid-finalize sync (two without a map): R and N size the rest
+        HIPCHK(hipEventRecord(c->ev_mid, c->s));
+        // Speculation: the bucket ordering and the bin plan go out before the
+        // host waits for R -- sized from the last pass's R with a quarter of
+        // headroom -- so the GPU orders buckets while the host wakes, checks
+        // and queues the bin kernel (the wait left it idle ~20 us per C2
+        // step).  finalize_binned keeps the result when R fits the layout and
+        // the bin count is the budget's, else reruns the phase exactly
+        if (!counting && attempt == 0 && c->prev_R && c->rho > 0.f && env_int("KB_BIN_SPEC", 1) &&
+            env_int("KB_BIN_DESC", 1)) {
+            const uint64_t bk = bin_budget(c, NB);
+            if (c->prev_R >= 2 * bk) {
+                const uint64_t rl = c->prev_R + c->prev_R / 4 + 65536;
+                const int rc = bucket_phase(c, NB, rl, bk, cap, use_base, rl);
+                if (rc) return rc;
+                c->spec = true;
+                c->spec_rlay = rl;
+                c->spec_bins = bk;
+            }
+        }
+        HIPCHK(hipEventSynchronize(c->ev_mid));  // the one mid-finalize wait (two without a map): R and N size the rest
         KB_DBG("record pass attempt %d: %s cap %llu, %.3f ms since finalize (allocations %.3f ms)\n", attempt,
                counting ? "counting" : use_base ? "exact" : "stride", (unsigned long long)cap, now_ms() - c->t_fin,
                g_alloc_ms);
@@ -1811,11 +1898,25 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     // budget: the buffers sized by it keep their size as maps change)
     const uint64_t bin_keys = bucketed ? bin_budget(c, NB) : 1ull << (2 * M - 1);
     const uint64_t max_bins = std::max<uint64_t>(1, std::min<uint64_t>(R, bin_keys));
+    const bool use_desc = bucketed && env_int("KB_BIN_DESC", 1);
+    // the speculative bucket ordering (binned_buckets) stands when R fitted
+    // its layout and the bin count is the budget's; otherwise it is rerun
+    // exactly, after its counter is zeroed
+    const bool spec_ok = use_desc && c->spec && R <= c->spec_rlay && max_bins == c->spec_bins;
+    if (c->spec && !spec_ok) {
+        HIPCHK(hipStreamSynchronize(c->s));  // (nothing in flight reads what is regrown)
+        HIPCHK(hipMemsetAsync(c->totals.p + 2, 0, sizeof(uint64_t), c->s));
+    }
+    c->spec = false;
+    KB_DBG("bucket ordering: %s (R %llu, layout %llu)\n", spec_ok ? "speculative, kept" : "exact",
+           (unsigned long long)R, (unsigned long long)(spec_ok ? c->spec_rlay : R));
+    const uint64_t rlay = spec_ok ? c->spec_rlay : R;  // (the records' layout: hdr, w1 at 2 rlay, w3 at 4 rlay)
+    c->prev_R = R;
     HIPCHK(c->starts.ensure(max_bins + 1));
     HIPCHK(c->bcount.ensure(max_bins));
     HIPCHK(c->bmmer.ensure(max_bins));
     if (bucketed) HIPCHK(c->bocc.ensure(max_bins));
-    HIPCHK(c->srec.ensure(RWD * R));
+    HIPCHK(c->srec.ensure(RWD * rlay));
     HIPCHK(c->occ_b.ensure(std::max<uint64_t>(R, N / 2 + 4)));  // ids by ordinal (+ radix ping-pong)
     // the stage: 4-B ordinals + 2-B slots (KB_BIN_STAGE6, default), or 8-B
     // entries -- also with first-occurrence tracking, whose entries carry the
@@ -1845,41 +1946,10 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", few_bins ? 4 : (KW == 1 && opart >= 4) ? 5 : 3));
     if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(KW * N, 1)));
     if (bucketed) {
-        BucketArgs ba{};
-        ba.regions = c->regions.p;
-        ba.cap = c->bucket_cap_used;
-        ba.rbase = c->rexact ? c->rbase.p : nullptr;
-        ba.bfill = c->bfill.p;
-        ba.M = M;
-        ba.hdr = c->srec.p;  // ((header, word 0) pairs, then word 1 / (word 1, word 2) pairs + word 3)
-        ba.w1 = c->srec.p + 2 * R;
-        ba.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
-        ba.spw = 2 * KW;
-        HIPCHK(c->bbase.ensure(NB + 1));
-        ba.bbase = c->bbase.p;
-        ba.bases_ready = 1;  // (bucket_stats_kernel, after the record pass that made these regions)
-        {
-            // records written by a map-routed pass carry their sub-bin (zero
-            // for an unsplit mmer); a hash-routed pass writes spans untouched
-            kb_ctx::BucketMap* bm = bmap_find(c, NB);  // (the map the record pass used)
-            ba.sub = bm && bm->split ? 1 : 0;
+        if (!spec_ok) {
+            const int rc2 = bucket_phase(c, NB, R, max_bins, c->bucket_cap_used, c->rexact, 0, use_desc);
+            if (rc2) return rc2;
         }
-        ba.bin_ctr = reinterpret_cast<unsigned long long*>(c->totals.p + 2);
-        ba.bstart = c->starts.p;
-        ba.bcount = c->bcount.p;
-        ba.bmmer = c->bmmer.p;
-        ba.bocc = c->bocc.p;
-        ba.max_bins = max_bins;
-#ifdef KB_BIN_ABL
-        {   // (diagnostic: from a context's third finalize on, so the records
-            // the bin kernel reads are the last pass's -- replay input only)
-            static int abl_calls = 0;
-            ba.ablate = abl_calls++ >= 2 ? env_int("KB_BK_ABLATE", 0) : 0;
-        }
-#endif
-        ba.status = c->misc.p;
-        HIPCHK(launch_bucket_sort(ba, NB, c->s));
-        c->tm.sort_passes = 0;
     } else {
         // ---- stable sort of the records by (mmer, 63 - n), bin boundaries
         const int key_bits = 2 * M + 6;
@@ -1902,22 +1972,16 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         HIPCHK(launch_sk_gather(c->sorted, c->pay.p, R, c->srec.p, c->s));
     }
     HIPCHK(c->border.ensure(max_bins));
-    const bool use_desc = bucketed && env_int("KB_BIN_DESC", 1);
-    if (use_desc) {  // (bocc: the bucket ordering counted every bin's occurrences)
-        HIPCHK(c->bdesc.ensure(2 * max_bins));
-        HIPCHK(launch_bins_plan(c->starts.p, c->bcount.p, c->bmmer.p, c->bocc.p, c->totals.p, max_bins, c->border.p,
-                                c->bdesc.p, reinterpret_cast<unsigned long long*>(c->totals.p + 10), c->s));
-    } else {
+    if (!use_desc)  // (bucketed: bucket_phase planned the bins from their descriptors; bocc counted by it)
         HIPCHK(launch_bins_order(c->bcount.p, c->totals.p, c->border.p, max_bins, c->s));
-    }
     float* rho_dev = nullptr;
     if (c->rho <= 0.f && N && env_int("KB_BIN_HLL", 1)) {
         // the context's first finalize: distinct keys per occurrence from one
         // HyperLogLog over the records (no learned density yet)
         BinArgs h{};
         h.hdr = c->srec.p;  // ((header, word 0) pairs, then word 1 / (word 1, word 2) pairs + word 3)
-        h.w1 = c->srec.p + 2 * R;
-        h.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
+        h.w1 = c->srec.p + 2 * rlay;
+        h.w3 = KW == 2 ? c->srec.p + 4 * rlay : nullptr;
         h.K = c->p.K;
         h.M = M;
         // large passes estimate from the bins of 1/8 of the mmers (whole bins:
@@ -1972,8 +2036,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
         }
         a = BinArgs{};
         a.hdr = c->srec.p;  // ((header, word 0) pairs, then word 1 / (word 1, word 2) pairs + word 3)
-        a.w1 = c->srec.p + 2 * R;
-        a.w3 = KW == 2 ? c->srec.p + 4 * R : nullptr;
+        a.w1 = c->srec.p + 2 * rlay;
+        a.w3 = KW == 2 ? c->srec.p + 4 * rlay : nullptr;
         a.bstart = c->starts.p;
         a.bcount = c->bcount.p;
         a.bmmer = c->bmmer.p;

@@ -4286,6 +4286,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
             bk_decode<ROWS>(h[u], a[u], b[u], SPW == 2 ? b[u] : d[u], A, bkey, row);
             const int sl = bk_slot(keys, bkey, false);
             const uint64_t pos = base + atomicAdd(&hist[sl * ROWS + row], 1u);
+            if (A.rcap && pos >= A.rcap) continue;  // (a speculative launch's layout is too small: rerun)
 #ifdef KB_BIN_ABL
             if (A.ablate == 1) {
                 if (pos == ~0ull) A.hdr[0] = h[u] ^ a[u] ^ b[u];  // (keeps the loads alive)

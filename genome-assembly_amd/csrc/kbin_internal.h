@@ -145,6 +145,7 @@ struct BucketArgs {
     int ablate;                // KB_BIN_ABL builds: KB_BK_ABLATE (1: no placement stores, 2: no
                                // placement pass) -- results wrong by design
     uint32_t* status;          // ST_BUCKET_FULL: a bucket holds too many bins
+    uint64_t rcap;             // records the hdr / w1 / w3 layout holds (0: every one; a speculative launch)
 };
 
 // region d of a record region set: fixed stride cap, or exact bases
