@@ -4055,12 +4055,23 @@ __global__ __launch_bounds__(1024) void bins_plan_kernel(const uint32_t* __restr
     __threadfence_block();
     __syncthreads();
     uint64_t carry = 0;
+    // (each round's four descriptor gathers are issued a round ahead: the
+    // rounds' scans no longer wait for their loads one after another)
+    auto gather = [&](uint32_t i, uint32_t& occ, uint4& d0) {
+        const bool v = i < nbins;
+        const uint32_t b = v ? (in_lds ? ordl[i] : order[i]) : 0u;
+        occ = v ? bocc[b] : 0u;
+        d0 = v ? make_uint4(b, bstart[b], bcount[b], bmmer[b]) : make_uint4(0u, 0u, 0u, 0u);
+    };
+    uint32_t occ_n = 0;
+    uint4 d0_n = make_uint4(0u, 0u, 0u, 0u);
+    gather(t, occ_n, d0_n);
     for (uint32_t base = 0; base < nbins; base += 1024) {
         const uint32_t i = base + t;
         const bool v = i < nbins;
-        const uint32_t b = v ? (in_lds ? ordl[i] : order[i]) : 0u;
-        const uint32_t occ = v ? bocc[b] : 0u;
-        const uint4 d0 = v ? make_uint4(b, bstart[b], bcount[b], bmmer[b]) : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t occ = occ_n;
+        const uint4 d0 = d0_n;
+        if (base + 1024 < nbins) gather(base + 1024 + t, occ_n, d0_n);
         const uint64_t inc = wave_incl_scan((uint64_t)occ, lane);
         if (lane == 63) red[wid] = inc;
         __syncthreads();
@@ -4165,7 +4176,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     __shared__ uint32_t hist[BK_SLOTS * ROWS];  // (slot, ROWS - n) counts, then cursors
     __shared__ uint64_t red[BK_THREADS / 64];
     __shared__ unsigned long long s_base, s_bin;
-    __shared__ uint32_t s_nb, s_full;
+    __shared__ uint32_t s_full;
     __shared__ uint32_t socc[BK_SLOTS];  // occurrences (k-mers) per slot
     const uint32_t tid = threadIdx.x, bk = blockIdx.x;
     const uint64_t cnt = min<uint64_t>(A.bfill[bk], region_room(A.rbase, A.cap, bk));
@@ -4173,10 +4184,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     const uint64_t* src = A.regions + region_off(A.rbase, A.cap, bk) * RWD;
     for (uint32_t i = tid; i < BK_SLOTS; i += BK_THREADS) keys[i] = 0;
     for (uint32_t i = tid; i < BK_SLOTS * ROWS; i += BK_THREADS) hist[i] = 0;
-    if (tid == 0) {
-        s_nb = 0;
-        s_full = 0;
-    }
+    if (tid == 0) s_full = 0;
     __syncthreads();
     constexpr int U = SPW == 2 ? 4 : 2;  // records in flight per thread
     for (uint64_t i0 = tid; i0 < cnt; i0 += U * BK_THREADS) {
@@ -4238,15 +4246,23 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     __syncthreads();
     // count non-empty slots, reserve bin descriptors (one per bin key: an
     // mmer, or one context sub-bin of a split mmer)
+    // (the dense index of a slot among the non-empty ones, from the waves'
+    // ballots -- a thread counting the set slots below it walked up to 255
+    // LDS words in series)
     const bool has = tid < BK_SLOTS && keys[tid] != 0;
-    if (has) atomicAdd(&s_nb, 1u);
+    const uint64_t hb = __ballot(has);
+    __shared__ uint32_t wset[BK_SLOTS / 64];
+    if (tid < BK_SLOTS && lane == 0) wset[wid] = (uint32_t)__popcll(hb);
     __syncthreads();
-    if (tid == 0) s_bin = s_nb ? atomicAdd(A.bin_ctr, (unsigned long long)s_nb) : 0ull;
+    uint32_t nb = 0, below = (uint32_t)__popcll(hb & ((1ull << lane) - 1ull));
+#pragma unroll
+    for (int w = 0; w < (int)(BK_SLOTS / 64); w++) {
+        if (w < wid) below += wset[w];
+        nb += wset[w];
+    }
+    if (tid == 0) s_bin = nb ? atomicAdd(A.bin_ctr, (unsigned long long)nb) : 0ull;
     __syncthreads();
     if (has) {
-        // dense index of this slot among non-empty ones: count set slots below
-        uint32_t below = 0;
-        for (uint32_t j = 0; j < tid; j++) below += keys[j] != 0;
         const uint64_t bi = s_bin + below;
         const uint32_t first = hist[tid * ROWS];
         const uint32_t last = tid + 1 < BK_SLOTS ? hist[(tid + 1) * ROWS] : (uint32_t)cnt;
