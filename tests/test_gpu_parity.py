@@ -902,3 +902,29 @@ def test_edge_inputs_and_context_reuse(engine):
             eng.submit(bases=bases, lens=lens, first_id=0)
             eng.finalize(prune=True)
             assert_same(eng.export(), oracle.bin_reads(bases, lens, K, M, 1, True))
+
+
+def test_speculative_bucket_layout():
+    """The bucket ordering goes out before the finalize's mid-way wait, in a
+    layout sized from the last pass's records (kbin_api.hip bucket_phase).
+    One context: a pass, then one with 3x the records (the layout is too
+    small: the ordering reruns exactly), then the same again (the speculative
+    ordering stands) -- each bit-exact against the oracle."""
+    rng = np.random.default_rng(77)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=400_000)
+
+    def reads(n, seed):
+        r = np.random.default_rng(seed)
+        starts = r.integers(0, len(genome) - 150, n)
+        out = np.stack([genome[s:s + 150] for s in starts])
+        flip = r.random(out.shape) < 0.001
+        out[flip] = r.choice(np.frombuffer(b"ACGT", np.uint8), size=int(flip.sum()))
+        return out.reshape(-1).tobytes(), np.full(n, 150, dtype=np.uint32)
+
+    with kbin.Engine(31, 7, cutoff=1, max_read_len=150) as eng:
+        for n, seed in ((20_000, 1), (60_000, 2), (60_000, 3)):
+            bases, lens = reads(n, seed)
+            eng.reset()
+            eng.submit(bases=bases, lens=lens, first_id=0)
+            eng.finalize(prune=True)
+            assert_same(eng.export(), oracle.bin_reads(bases, lens, 31, 7, 1, True))
