@@ -368,10 +368,9 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     const kb_params& p = *params;
     if (p.M < 1 || p.M > 8)
         return fail(KB_EINVAL, "M=%d outside [1,8] (power_val, binning.c:17)", p.M);
-    if (p.K < 2 * p.M)
-        return fail(KB_EINVAL,
-                    "K=%d < 2M=%d: the reference's incremental branch (binning.c:992-1021) is live; "
-                    "unsupported", p.K, 2 * p.M);
+    // (K < 2M: the reference's incremental branch, binning.c:992-1021, is
+    // live -- the binned engine's record pass walks it, reads of <= 512 bp,
+    // one GPU; kb_finalize and the routing calls check the rest)
     if (p.K > 63) return fail(KB_EINVAL, "K=%d > 63 unsupported", p.K);
     if (p.cutoff < 0) return fail(KB_EINVAL, "cutoff < 0");
     if (p.max_read_len < 1 || p.max_read_len > 65535)
@@ -863,6 +862,8 @@ extern "C" int kb_record_words(kb_ctx* c, uint32_t* out) {
 
 extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
     if (!c || !h_counts) return fail(KB_EINVAL, "null argument");
+    if (c->p.K < 2 * c->p.M)  // (routed records carry no complement flag: the receiver rederives it)
+        return fail(KB_EINVAL, "K=%d < 2M=%d: one GPU only (no routing)", c->p.K, 2 * c->p.M);
     if (n_dest < 1 || n_dest > 64) return fail(KB_EINVAL, "n_dest=%u outside [1,64]", n_dest);
     if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
     int rc = set_device(c);
@@ -938,6 +939,8 @@ extern "C" int kb_split_passes(kb_ctx* c, uint32_t n_parts, uint64_t* d_regions,
 static int scatter_regions(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions, uint64_t region_cap,
                            uint64_t* h_counts, uint64_t salt, bool by_pass) {
     if (!c || !h_counts) return fail(KB_EINVAL, "null argument");
+    if (c->p.K < 2 * c->p.M)  // (routed records carry no complement flag: the receiver rederives it)
+        return fail(KB_EINVAL, "K=%d < 2M=%d: one GPU only (no routing, no split passes)", c->p.K, 2 * c->p.M);
     if (n_dest < 1 || n_dest > 64) return fail(KB_EINVAL, "n_dest=%u outside [1,64]", n_dest);
     if (by_pass && c->part_n > 1) return fail(KB_ESTATE, "kb_split_passes on a partitioned context");
     if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
@@ -1240,6 +1243,7 @@ static kb_ctx::BucketMap* bmap_find(kb_ctx* c, uint32_t NB) {
 static uint32_t sub_depth(const kb_ctx* c, double w, double keys, double mean) {
     int bmax = std::min<int>((int)SUB_MAX_B, std::max(0, env_int("KB_BIN_SUB", (int)SUB_MAX_B)));
     if (!sub_room(c->p.K, c->p.M, 2 * c->KW)) bmax = 0;  // (no spare span bits for the stamp)
+    if (c->p.K < 2 * c->p.M) bmax = 0;  // (K < 2M: a signature is no function of its key's k-mer)
     const double ts = c->KW == 1 ? 8192.0 : 4096.0;
     // (the long-list regime: sub-bins at 40 % of a table, so that they stay under
     // the ranking's LDS limit and their long lists take the bitmaps -- C3 261 ->
@@ -1437,6 +1441,7 @@ static int bmap_build(kb_ctx* c, uint32_t NB, double rho, bool prior = false) {
 static bool bmap_wants(kb_ctx* c, uint32_t NB, uint64_t R) {
     if (!env_int("KB_BIN_BALANCE", 1) || R < (uint64_t)std::max(0, env_int("KB_BIN_BALANCE_MIN", 1 << 18)))
         return false;
+    if (c->p.K < 2 * c->p.M) return false;  // (K < 2M: no map, see binned_buckets)
     const kb_ctx::BucketMap* m = bmap_find(c, NB);
     return !m || m->stale;
 }
@@ -1576,7 +1581,11 @@ static int bucket_phase(kb_ctx* c, uint32_t NB, uint64_t rlay, uint64_t max_bins
 static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, uint64_t& R, uint64_t& N) {
     const int M = c->p.M;
     c->spec = false;
-    kb_ctx::BucketMap* bm = bmap_find(c, NB);
+    // K < 2M: a record's mmer code is the reference's complemented-or-not
+    // signature, not the canonical (larger) one the bucket map is indexed by
+    // (bucket_map[canon - 2^(2M-1)]): no map -- hash routing, exact regions
+    const bool nomap = c->p.K < 2 * M;
+    kb_ctx::BucketMap* bm = nomap ? nullptr : bmap_find(c, NB);
     if (bm && bm->pending) {  // the last pass of this key left its bins: rebuild the map from them
         const double t0 = now_ms();
         const int rc = bmap_apply(c, NB, bm->p_mm.data(), bm->p_cnt.data(), bm->p_occ.data(), bm->p_mm.size(),
@@ -1585,7 +1594,7 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
         bm = bmap_find(c, NB);
         KB_DBG("map rebuilt part %u/%u: %.3f ms, %u split\n", c->part, c->part_n, now_ms() - t0, bm->split);
     }
-    if (!bm && !c->prior_off && env_int("KB_BIN_PRIOR", 1) && env_int("KB_BIN_BALANCE", 1)) {
+    if (!bm && !nomap && !c->prior_off && env_int("KB_BIN_PRIOR", 1) && env_int("KB_BIN_BALANCE", 1)) {
         const double t0 = now_ms();
         const int rc = bmap_prior(c, NB);
         if (rc) return rc;
@@ -1941,7 +1950,8 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     // flat lists for one-word keys
     // (one-word keys only: two-word bins expand through the ring, which
     // would still walk every k-mer of the bin per range)
-    const int opart = KW == 1 ? std::min(4, std::max(0, env_int("KB_BIN_OPART", 4))) : 0;
+    // (K < 2M: no offset partitions -- their exactness needs the leftmost-argmax signature)
+    const int opart = KW == 1 && c->p.K >= 2 * M ? std::min(4, std::max(0, env_int("KB_BIN_OPART", 4))) : 0;
     const uint32_t flat_l =
         (uint32_t)std::max(0, env_int("KB_BIN_FLAT_L", few_bins ? 4 : (KW == 1 && opart >= 4) ? 5 : 3));
     if (flat_l) HIPCHK(c->kstage.ensure(std::max<uint64_t>(KW * N, 1)));
@@ -2415,6 +2425,16 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     }
     if (any_reads && any_sk)
         return fail(KB_ESTATE, "a context bins either its own reads or received super-k-mers");
+    if (c->p.K < 2 * c->p.M) {  // (the record pass's K < 2M walk: thread-per-read kernel, binned engine)
+        if (!binned_applies(c))
+            return fail(KB_EINVAL, "K=%d < 2M=%d needs the binned engine", c->p.K, 2 * c->p.M);
+        for (auto& b : c->batches)
+            if (!b.routed && !b.superkmers && b.RW > 16)
+                return fail(KB_EINVAL, "K=%d < 2M=%d: reads of at most 512 bp", c->p.K, 2 * c->p.M);
+        if (any_sk)
+            return fail(KB_EINVAL, "K=%d < 2M=%d: received super-k-mers carry no complement flag", c->p.K,
+                        2 * c->p.M);
+    }
     memset(&c->tm, 0, sizeof(c->tm));
     const int SW = c->KW == 1 ? 2 : 4;
     const bool track_first = (c->p.flags & KB_TRACK_FIRST) != 0;

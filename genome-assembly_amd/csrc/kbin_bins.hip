@@ -291,7 +291,13 @@ __device__ unsigned long long g_sk_prof[8];
 #else
 #define SKPROF(ph) do {} while (0)
 #endif
-template <bool WRITE>
+// QK (K < 2M): the reference's incremental branch is live (binning.c:992-1021:
+// j runs K-M .. M-1, appending bases to a score it never trims, in int
+// arithmetic that wraps).  Each lane then walks its read k-mer by k-mer with
+// the reference's own state (score, rev_score, max_score, is_rev, signature),
+// and a record is a run of k-mers with one signature position -- its so, rev
+// and mmer are whatever that state says, not the window's leftmost argmax
+template <bool WRITE, bool QK = false>
 __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const int RW = A.RW, K = A.K, M = A.M;
@@ -340,12 +346,72 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
         const uint64_t rbase = WRITE && !alloc && tid < nrows ? A.rec_base[r] : 0;
         uint32_t nseg = 0;
         int lo = 0;
+        // (QK) the reference's walk state after k-mer q_i, and the record it
+        // closed (kept across a stage-full round: the walk does not repeat)
+        int32_t q_s = 0, q_r = 0, q_m = 0;
+        bool q_rev = false;
+        int q_sig = -1, q_i = -1, q_lo = -1, q_e = 0, q_rsig = 0;
+        bool q_rrev = false;
+        auto q_code = [&](int p) { return (uint32_t)(window64(sw, p) >> sh) & maskM; };
+        auto q_step = [&](int i) {  // binning.c:922-1021 for the k-mer at i
+            if (i > q_sig) {  // a fresh window (binning.c:922-989)
+                uint32_t sm = q_code(i);
+                int32_t sc = (int32_t)sm, rv = (int32_t)(maskM - sm);
+                q_m = sc > rv ? sc : rv;
+                q_rev = !(sc > rv);
+                q_sig = i;
+                for (int p = i + 1; p <= i + K - M; p++) {
+                    sm = q_code(p);
+                    sc = (int32_t)sm;
+                    rv = (int32_t)(maskM - sm);
+                    if ((sc > rv ? sc : rv) > q_m) {
+                        q_m = sc > rv ? sc : rv;
+                        q_rev = !(sc > rv);
+                        q_sig = p;
+                    }
+                }
+                q_s = sc;
+                q_r = rv;
+            } else {  // the incremental branch (binning.c:992-1021), live for K < 2M
+                for (int j = K - M; j < M; j++) {
+                    const uint32_t v = (uint32_t)(window64(sw, i + j) >> 62);
+                    q_s = (int32_t)((uint32_t)q_s * 4u + v);
+                    q_r = (int32_t)((uint32_t)q_r * 4u + 3u - v);
+                }
+                if ((q_s > q_r ? q_s : q_r) > q_m) {
+                    q_m = q_s > q_r ? q_s : q_r;
+                    q_rev = !(q_s > q_r);
+                    q_sig = i + K - M;
+                }
+            }
+            q_i = i;
+        };
         for (;;) {
             while (lo < nK) {
                 // leftmost strict argmax of the canonical score over the window
                 int best = -1, sig = lo;
                 uint32_t bsm = 0;
-                if (one_word) {
+                int nlo = 0;  // the next record's first k-mer
+                if (QK) {
+                    if (q_lo != lo) {  // (a stage-full round keeps the record it closed)
+                        if (q_i < lo) q_step(lo);
+                        q_rsig = q_sig;
+                        q_rrev = q_rev;
+                        int e = lo + 1;
+                        while (e < nK) {
+                            q_step(e);
+                            if (q_sig != q_rsig) break;
+                            e++;
+                        }
+                        q_lo = lo;
+                        q_e = e;
+                    }
+                    sig = q_rsig;
+                    const uint32_t sm = q_code(sig);
+                    best = (int)(q_rrev ? maskM - sm : sm);  // the bin's mmer code
+                    bsm = q_rrev ? 0u : halfM;               // (rev below: bsm < halfM)
+                    nlo = q_e;
+                } else if (one_word) {
                     // K <= 31: the window's W mmers all lie in the 64-bit word at
                     // lo, so each score is one shift of it (no shifting chain),
                     // and the argmax is a max over (score << 8 | 255 - offset):
@@ -376,9 +442,10 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                         y <<= 2;
                     }
                 }
-                const uint64_t n = (uint64_t)(min(sig, nK - 1) - lo + 1);
+                if (!QK) nlo = sig + 1;
+                const uint64_t n = QK ? (uint64_t)(nlo - lo) : (uint64_t)(min(sig, nK - 1) - lo + 1);
                 if (!in_part((uint32_t)best, A.part, A.part_n)) {  // another pass's super-k-mer
-                    lo = sig + 1;
+                    lo = nlo;
                     continue;
                 }
                 if (WRITE) {
@@ -429,7 +496,7 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 }
                 kmers += n;
                 nseg++;
-                lo = sig + 1;
+                lo = nlo;
             }
             if (!WRITE && tid < nrows) A.seg_count[r] = nseg;
             if (WRITE && !alloc && nseg)
@@ -581,12 +648,19 @@ hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s) {
     if (a.RW <= SK_THREAD_RW) {
         const size_t lds = (size_t)SKT * sk_row_words(a.RW, a.rw) * sizeof(uint64_t) +
                            (write ? SK_STAGE * sizeof(uint64_t) : 0);
-        if (write)
+        if (a.K < 2 * a.M) {  // (QK: the reference's incremental branch is live)
+            if (write)
+                hipLaunchKernelGGL((sk_thread_kernel<true, true>), dim3((unsigned)blocks), dim3(SKT), lds, s, a);
+            else
+                hipLaunchKernelGGL((sk_thread_kernel<false, true>), dim3((unsigned)blocks), dim3(SKT), lds, s, a);
+        } else if (write) {
             hipLaunchKernelGGL(sk_thread_kernel<true>, dim3((unsigned)blocks), dim3(SKT), lds, s, a);
-        else
+        } else {
             hipLaunchKernelGGL(sk_thread_kernel<false>, dim3((unsigned)blocks), dim3(SKT), lds, s, a);
+        }
         return hipGetLastError();
     }
+    if (a.K < 2 * a.M) return hipErrorInvalidValue;  // (K < 2M: reads of <= 512 bp only; the API checks)
     const size_t lds = (size_t)4 * (a.RW + 2) * sizeof(uint64_t);
     if (write)
         hipLaunchKernelGGL(sk_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);

@@ -928,3 +928,32 @@ def test_speculative_bucket_layout():
             eng.submit(bases=bases, lens=lens, first_id=0)
             eng.finalize(prune=True)
             assert_same(eng.export(), oracle.bin_reads(bases, lens, 31, 7, 1, True))
+
+
+@pytest.mark.parametrize("K,M", [(10, 6), (5, 4), (5, 3), (7, 4), (3, 2), (13, 7), (15, 8), (1, 1)])
+def test_k_below_2m_vs_oracle(K, M, engine):
+    """K < 2M: the reference's incremental branch (binning.c:992-1021) is live
+    -- the record pass walks the reference's own score state k-mer by k-mer
+    (sk_thread_kernel QK); bit-exact against the oracle, which
+    test_oracle_vs_reference_binary pins to the compiled reference at (10, 6)
+    and (5, 4).  The table engine refuses these configurations."""
+    rng = np.random.default_rng(K * 1000 + M)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=3000)
+    reads = []
+    for _ in range(1500):
+        L = int(rng.integers(0, 260))
+        s = int(rng.integers(0, 3000 - L))
+        r = genome[s:s + L].copy()
+        m = rng.random(L) < 0.01
+        r[m] = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=int(m.sum()))
+        reads.append(r.tobytes())
+    bases, lens = kbin.pack_reads(reads)
+    if engine != "binned":
+        with pytest.raises(kbin.KbError):
+            gpu_result(bases, lens, K, M, 1, True)
+        return
+    for prune in (False, True):
+        ora = oracle.bin_reads(bases, lens, K, M, 1, prune)
+        res = gpu_result(bases, lens, K, M, 1, prune, batches=3)
+        assert res.n_kmers == ora.n_kmers
+        assert_same(res, ora)
