@@ -107,6 +107,13 @@ int kbh_configure(int K, int M, int cutoff, int device)
     return 0;
 }
 
+void kbh_get_config(int *K, int *M, int *cutoff)
+{
+    if (K) *K = g_K;
+    if (M) *M = g_M;
+    if (cutoff) *cutoff = g_cutoff;
+}
+
 int kbh_configure_gpus(int n_gpus, const int *devices)
 {
     if (n_gpus < 1 || n_gpus > KBH_MAX_GPUS) return KB_EINVAL;

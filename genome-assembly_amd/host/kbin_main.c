@@ -4,7 +4,12 @@
  * chunking, process_read per chunk, prune_data, then the canonical dump of the
  * materialised two-level table (instead of the reference's unitig steps).
  *
- *   kbin_main <reads-file> <K> <M> <READ_LENGTH> <cutoff> <prune 0|1> [device] [--gpus N|d0,d1,..]
+ *   kbin_main <reads-file> <K> <M> <READ_LENGTH> <cutoff> <prune 0|1> [device] [--gpus N|d0,d1,..] [--unitigs]
+ *
+ * --unitigs: instead of the dump, the rest of the reference's main
+ * (binning.c:1171-1180): expand_read_id_list, find_kmer_extensions forward
+ * and backward (the exact replay, unitig.c), print_kmers -- the reference
+ * program's own stdout.
  *
  * --gpus: bin on several GPUs through one multi-GPU group (mmer-sharded,
  * records exchanged over RCCL; kbh_configure_gpus); the dump is identical.
@@ -23,9 +28,12 @@
 int main(int argc, char **argv)
 {
     /* (--gpus anywhere after the positional arguments) */
-    int gpus[64], ng = 0, pos = argc;
+    int gpus[64], ng = 0, pos = argc, unitigs = 0;
     for (int i = 1; i < argc; i++)
-        if (!strcmp(argv[i], "--gpus")) {
+        if (!strcmp(argv[i], "--unitigs")) {
+            unitigs = 1;
+            if (pos == argc) pos = i;
+        } else if (!strcmp(argv[i], "--gpus")) {
             if (i + 1 >= argc) return 2;
             const char *q = argv[i + 1];
             if (!strchr(q, ',')) {
@@ -86,6 +94,28 @@ int main(int argc, char **argv)
                 read_id, kmers, loop, t.finalize_ms, t.export_ms, t.materialise_ms, t.prune_ms, loop + t.total_ms,
                 (unsigned long long)t.entries, (unsigned long long)t.ids, (unsigned long long)t.nodes, t.order_ms,
                 t.group_ms, t.fill_ms, t.release_ms);
+    }
+    if (unitigs) { /* binning.c:1171-1180 */
+        struct timespec u0, u1, u2;
+        clock_gettime(CLOCK_MONOTONIC, &u0);
+        expand_read_id_list(hash_table);
+        clock_gettime(CLOCK_MONOTONIC, &u1);
+        find_kmer_extensions(hash_table, true);
+        find_kmer_extensions(hash_table, false);
+        clock_gettime(CLOCK_MONOTONIC, &u2);
+        if (tenv && *tenv == '1') {
+            kbh_unitig_stats us;
+            kbh_unitig_stats_get(&us);
+            fprintf(stderr,
+                    "{\"expand_ms\": %.3f, \"unitig_ms\": %.3f, \"unitig_index_ms\": %.3f, \"unitigs\": %llu, "
+                    "\"merges\": %llu, \"u1_events\": %llu}\n",
+                    (u1.tv_sec - u0.tv_sec) * 1e3 + (u1.tv_nsec - u0.tv_nsec) * 1e-6,
+                    (u2.tv_sec - u1.tv_sec) * 1e3 + (u2.tv_nsec - u1.tv_nsec) * 1e-6, us.index_ms,
+                    (unsigned long long)us.unitigs, (unsigned long long)us.merges,
+                    (unsigned long long)us.u1_events);
+        }
+        if (!(denv && *denv == '1')) kbh_print_kmers(hash_table, stdout);
+        return 0;
     }
     if (!(denv && *denv == '1')) kbh_dump_table(hash_table, stdout);
     return 0;

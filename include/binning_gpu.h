@@ -118,6 +118,30 @@ int kbh_read_fgets(const char *path, int read_length, char **bases, uint32_t **l
                    uint64_t *n_reads);
 void kbh_free_reads(char *bases, uint32_t *lens);
 
+/* the configuration in effect (kbh_configure, else the compile-time defaults) */
+void kbh_get_config(int *K, int *M, int *cutoff);
+
+/* binning.c:659-783: the reference's unitig extension, exact (same merges, same
+ * keys, same per-base read-id lists, same table and iterator state after it),
+ * without its all-pairs candidate scan (genome-assembly_amd/host/unitig.c).
+ * A strong definition: a drop-in that links the reference's binning.o weakens
+ * the reference's copy (oracle/build_ref.sh dropin).  Works on
+ * any level-1 table laid out as zhash.h (ours or the reference's own), after
+ * expand_read_id_list as in the reference's main (binning.c:1171-1177). */
+void find_kmer_extensions(struct ZHashTable *hash_table, bool forward);
+typedef struct {
+    uint64_t calls, queries, unitigs, merges, multiple, resumes, candidates;
+    uint64_t deleted, inserted, set_existing;
+    uint64_t u1_events; /* binning.c:721-731 with the extension the kmer's chain
+                           successor: a use-after-free in the reference (unitig.c) */
+    double index_ms, walk_ms;
+} kbh_unitig_stats;
+int kbh_unitig_stats_get(kbh_unitig_stats *out);
+/* print_kmers (binning.c:827-843), including the first level-2 table's resume
+ * from the iterator cursor find_kmer_extensions may leave (binning.c:403-427) */
+int kbh_print_kmers(struct ZHashTable *hash_table, FILE *out);
+void kbh_unitig_reset(void);
+
 /* canonical dump of a materialised two-level table:
  * "mmer\tkmer\tcount\tid1,id2,...\n", lines sorted bytewise */
 int kbh_dump_table(struct ZHashTable *hash_table, FILE *out);

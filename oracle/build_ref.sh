@@ -22,11 +22,22 @@
 #                                 weakened and the GPU shim's strong definitions
 #                                 (genome-assembly_amd/host/binning_gpu.c over
 #                                 libkbin.so) win at link time -- the drop-in
-#                                 integration described in INTEGRATION.md
+#                                 integration described in INTEGRATION.md;
+#                                 find_kmer_extensions is replaced as well
+#                                 (genome-assembly_amd/host/unitig.c)
+#   build_ref.sh dropinw K M [C]  dropinw_k<K>_m<M>_c<C>: the drop-in with the
+#                                 reference's OWN find_kmer_extensions kept
+#                                 (the unitig walk's timing baseline)
+#   build_ref.sh unitig K M [C]   unitig_k<K>_m<M>_c<C>: the reference program
+#                                 as shipped (its own process_read, prune,
+#                                 expansion, print_kmers) with ONLY
+#                                 find_kmer_extensions replaced by unitig.c --
+#                                 CPU only: the unitig replay's parity test on
+#                                 the reference's own tables
 # No-op when /root/reference is absent (e.g. on the GPU box).
 set -euo pipefail
 MODE=harness
-case "${1:-}" in full|dropin|g) MODE=$1; shift ;; esac
+case "${1:-}" in full|dropin|dropinw|unitig|g) MODE=$1; shift ;; esac
 K=${1:?K}; M=${2:?M}; C=${3:-1}
 REF=${KB_REFERENCE_DIR:-/root/reference}
 HERE="$(cd "$(dirname "$0")" && pwd)"
@@ -38,6 +49,8 @@ case $MODE in
   g)       BIN="$OUT/refg_k${K}_m${M}_c${C}$RL" ;;
   full)    BIN="$OUT/full_k${K}_m${M}_c${C}$RL" ;;
   dropin)  BIN="$OUT/dropin_k${K}_m${M}_c${C}$RL" ;;
+  dropinw) BIN="$OUT/dropinw_k${K}_m${M}_c${C}$RL" ;;
+  unitig)  BIN="$OUT/unitig_k${K}_m${M}_c${C}$RL" ;;
 esac
 if [ ! -f "$REF/binning.c" ]; then
   echo "reference not present at $REF; skipping" >&2
@@ -47,8 +60,9 @@ mkdir -p "$OUT"
 # (a drop-in binary links the shim: rebuilt whenever the shim or the engine
 # library is newer than it)
 if [ -x "$BIN" ]; then
-  if [ "$MODE" != dropin ]; then exit 0; fi
+  if [ "$MODE" != dropin ] && [ "$MODE" != dropinw ] && [ "$MODE" != unitig ]; then exit 0; fi
   if [ ! "$REPO/genome-assembly_amd/host/binning_gpu.c" -nt "$BIN" ] && \
+     [ ! "$REPO/genome-assembly_amd/host/unitig.c" -nt "$BIN" ] && \
      [ ! "$REPO/genome-assembly_amd/lib/libkbin.so" -nt "$BIN" ]; then exit 0; fi
 fi
 TMP="$(mktemp -d)"
@@ -77,7 +91,15 @@ case $MODE in
     gcc -O2 -w -I"$REF" $DEFS -c "$HERE/ref_harness.c" -o "$TMP/harness.o"
     gcc "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/harness.o" -o "$BIN"
     ;;
-  full|dropin)
+  unitig)
+    gcc -g -O0 -fno-inline -w -I"$REF" $DEFS -c "$TMP/binning_guarded.c" -o "$TMP/binning.o"
+    gcc -g -O0 -w -I"$REF" -c "$REF/zhash.c" -o "$TMP/zhash.o"
+    gcc -g -O0 -w -I"$REF" -c "$REF/llist.c" -o "$TMP/llist.o"
+    objcopy --weaken-symbol=find_kmer_extensions "$TMP/binning.o"
+    gcc -O2 -w $DEFS -c "$REPO/genome-assembly_amd/host/unitig.c" -o "$TMP/unitig.o"
+    gcc "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/unitig.o" -o "$BIN"
+    ;;
+  full|dropin|dropinw)
     # makefile:2-5 flags (-g, no -O): calls stay relocations against the
     # global symbols, so a strong definition elsewhere can replace them
     gcc -g -O0 -fno-inline -w -I"$REF" $DEFS -c "$TMP/binning_guarded.c" -o "$TMP/binning.o"
@@ -92,7 +114,13 @@ case $MODE in
       # the shim includes our kb_zhash.h (same layout as zhash.h/llist.h); its
       # container calls resolve to the reference's zhash.o / llist.o
       gcc -O2 -w -pthread $DEFS -c "$REPO/genome-assembly_amd/host/binning_gpu.c" -o "$TMP/shim.o"
-      gcc -pthread "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" "$TMP/shim.o" -L"$LIB" -lkbin \
+      OBJS="$TMP/shim.o"
+      if [ "$MODE" = dropin ]; then
+        objcopy --weaken-symbol=find_kmer_extensions "$TMP/binning.o"
+        gcc -O2 -w $DEFS -c "$REPO/genome-assembly_amd/host/unitig.c" -o "$TMP/unitig.o"
+        OBJS="$OBJS $TMP/unitig.o"
+      fi
+      gcc -pthread "$TMP/binning.o" "$TMP/zhash.o" "$TMP/llist.o" $OBJS -L"$LIB" -lkbin \
           -Wl,-rpath,"\$ORIGIN/../../genome-assembly_amd/lib" -o "$BIN"
     fi
     ;;

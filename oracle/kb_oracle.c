@@ -66,7 +66,8 @@ static int o_getval(char c)
 
 typedef struct {
     uint64_t hi, lo;   /* k-mer code, first base most significant */
-    uint32_t mmer;     /* mmer code */
+    uint16_t mmer;     /* mmer code (M <= 8) */
+    uint16_t pos;      /* k-mer position in the read (reads < 64 K bases) */
     uint32_t ord;      /* call ordinal of the read */
 } rec_t;
 
@@ -185,7 +186,8 @@ static int scan_read(const char *read, int read_len, int K, int M, uint32_t ord,
         rec_t r;
         uint64_t mh, ml;
         pack_code(signature_cpy, M, &mh, &ml);
-        r.mmer = (uint32_t)ml;
+        r.mmer = (uint16_t)ml;
+        r.pos = (uint16_t)i;
         (*n_kmers)++;
         if (!mmer_mask || mmer_mask[r.mmer]) { /* test-side partition filter */
             memcpy(kmer_key, kmer, (size_t)K);
@@ -259,7 +261,8 @@ int kbo_bin_masked(const char *bases, const uint64_t *read_off, uint64_t n_reads
     out->count = malloc((n_ent ? n_ent : 1) * sizeof(uint32_t));
     out->offset = malloc((n_ent + 1) * sizeof(uint64_t));
     out->ids = malloc((n_ids ? n_ids : 1) * sizeof(int32_t));
-    if (!out->mmer || !out->kmer_hi || !out->kmer_lo || !out->count || !out->offset || !out->ids) {
+    out->first = malloc((n_ent ? n_ent : 1) * sizeof(uint64_t));
+    if (!out->mmer || !out->kmer_hi || !out->kmer_lo || !out->count || !out->offset || !out->ids || !out->first) {
         free(v.r);
         kbo_free(out);
         return KBO_ENOMEM;
@@ -277,8 +280,13 @@ int kbo_bin_masked(const char *bases, const uint64_t *read_off, uint64_t n_reads
             out->kmer_hi[e] = v.r[a].hi;
             out->kmer_lo[e] = v.r[a].lo;
             out->count[e] = (uint32_t)c;
-            for (uint64_t k = a; k < b; k++)
+            uint64_t first = UINT64_MAX; /* the key's first occurrence: the reference's insertion order */
+            for (uint64_t k = a; k < b; k++) {
                 out->ids[p++] = read_ids ? read_ids[v.r[k].ord] : (int32_t)v.r[k].ord;
+                const uint64_t st = (uint64_t)v.r[k].ord << 16 | v.r[k].pos;
+                if (st < first) first = st;
+            }
+            out->first[e] = first;
             e++;
             out->offset[e] = p;
         }
@@ -292,7 +300,7 @@ void kbo_free(kbo_result *r)
 {
     if (!r) return;
     free(r->mmer); free(r->kmer_hi); free(r->kmer_lo);
-    free(r->count); free(r->offset); free(r->ids);
+    free(r->count); free(r->offset); free(r->ids); free(r->first);
     memset(r, 0, sizeof(*r));
 }
 

@@ -18,6 +18,8 @@ typedef struct {
     int32_t *ids;       /* read ids per entry, reverse call order */
     uint64_t n_kmers;   /* k-mer occurrences scanned */
     int alphabet_ok;    /* 0 if any byte outside ACGT was seen */
+    uint64_t *first;    /* per entry: first occurrence, call ordinal << 16 | k-mer
+                           position (kbin.h KB_TRACK_FIRST's stamp) */
 } kbo_result;
 
 int kbo_bin(const char *bases, const uint64_t *read_off, uint64_t n_reads,

@@ -20,7 +20,8 @@ class kbo_result(C.Structure):
     _fields_ = [("n_entries", C.c_uint64), ("mmer", C.POINTER(C.c_uint32)),
                 ("kmer_hi", C.POINTER(C.c_uint64)), ("kmer_lo", C.POINTER(C.c_uint64)),
                 ("count", C.POINTER(C.c_uint32)), ("offset", C.POINTER(C.c_uint64)),
-                ("ids", C.POINTER(C.c_int32)), ("n_kmers", C.c_uint64), ("alphabet_ok", C.c_int)]
+                ("ids", C.POINTER(C.c_int32)), ("n_kmers", C.c_uint64), ("alphabet_ok", C.c_int),
+                ("first", C.POINTER(C.c_uint64))]
 
 
 _lib = None
@@ -67,10 +68,11 @@ def lib() -> C.CDLL:
 class OracleResult:
     """Same field names as kbin.Result, already in canonical order."""
 
-    def __init__(self, mmer, kmer_hi, kmer_lo, count, offset, ids, n_kmers, alphabet_ok):
+    def __init__(self, mmer, kmer_hi, kmer_lo, count, offset, ids, n_kmers, alphabet_ok, first=None):
         self.mmer, self.kmer_hi, self.kmer_lo = mmer, kmer_hi, kmer_lo
         self.count, self.offset, self.ids = count, offset, ids
         self.n_kmers, self.alphabet_ok = n_kmers, alphabet_ok
+        self.first = first  # per entry: call ordinal << 16 | k-mer position of its first occurrence
 
     @property
     def n_entries(self):
@@ -109,7 +111,7 @@ def bin_reads(bases: bytes, lens, K: int, M: int, cutoff: int = 1, prune: bool =
         out = OracleResult(arr(r.mmer, n, np.uint32), arr(r.kmer_hi, n, np.uint64),
                            arr(r.kmer_lo, n, np.uint64), arr(r.count, n, np.uint32), off_a,
                            arr(r.ids, int(off_a[-1]) if n else 0, np.int32), int(r.n_kmers),
-                           bool(r.alphabet_ok))
+                           bool(r.alphabet_ok), arr(r.first, n, np.uint64))
     finally:
         l.kbo_free(C.byref(r))
     return out

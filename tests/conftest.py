@@ -41,3 +41,26 @@ def engine(request, monkeypatch):
     runs either way"""
     monkeypatch.setenv("KB_ENGINE", request.param)
     return request.param
+
+
+def golden_input_path(row, tmp_dir) -> pathlib.Path:
+    """the input file of a tests/golden/unitigs.json row: a bundled file, or
+    "c2:<n>" -- the C2 generator's first n reads, one 150-bp read per line
+    (tools/unitig_golden.py)"""
+    src = row["input"]
+    if not src.startswith("c2:"):
+        return GOLDEN / src
+    import oracle
+    n = int(src.split(":")[1])
+    raw = oracle.gen_reads(n, 150, 5_000_000, 1000, 2)
+    p = pathlib.Path(tmp_dir) / f"c2_{n}.txt"
+    with open(p, "wb") as f:
+        for i in range(n):
+            f.write(raw[i * 150:(i + 1) * 150] + b"\n")
+    return p
+
+
+def ref_exe_name(prefix: str, row) -> str:
+    """oracle/build_ref.sh's binary name for a unitigs.json row"""
+    rl = row.get("read_length", 101)
+    return f"{prefix}_k{row['K']}_m{row['M']}_c{row['cutoff']}" + (f"_rl{rl}" if rl != 101 else "")

@@ -3,6 +3,7 @@
   (2) the CPU oracle (oracle/, clean-room restatement) on the same inputs,
 bit-exact on every (mmer, kmer) key, count and read-id list."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -785,22 +786,46 @@ def test_host_cli_process_read_prune_data(digests, golden_dir):
         assert hashlib.sha256(out).hexdigest() == row["sha256"], row
 
 
-def test_dropin_reference_program(golden_dir):
-    """DROP-IN: the reference program itself (binning.c main + its unitig
-    extension + print_kmers, compiled from /root/reference into oracle/_ref in
-    the build container) with ONLY process_read/prune_data replaced by the GPU
-    shim at link time.  Its stdout must equal the reference program's stdout
-    byte for byte -- which requires the materialised ZHashTable layout (bucket
-    chains, sizes, rehash history) to match the reference's exactly."""
+def test_kbin_main_unitigs(golden_dir, tmp_path):
+    """kbin_main --unitigs: the rest of the reference's main (binning.c:1171-
+    1180) after the GPU binning -- expand_read_id_list, the exact unitig
+    replay forward and backward (host/unitig.c), print_kmers -- gives the
+    reference program's stdout (sha256) on every unitigs.json row, without the
+    reference linked: the replay's own print (kbh_print_kmers) reproduces
+    print_kmers' resume from the iterator cursor the walk leaves."""
     import json
     import subprocess
+    from conftest import golden_input_path
+    exe = kbin.LIB_DIR / "kbin_main"
+    for row in json.loads((golden_dir / "unitigs.json").read_text()):
+        r = subprocess.run([str(exe), str(golden_input_path(row, tmp_path)), str(row["K"]), str(row["M"]),
+                            str(row.get("read_length", 101)), str(row["cutoff"]), "1", "--unitigs"],
+                           capture_output=True, timeout=300, env=dict(os.environ, KBH_TIMING="1"))
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert r.stdout.count(b"\n") == row["lines"], row
+        assert hashlib.sha256(r.stdout).hexdigest() == row["sha256"], row
+
+
+def test_dropin_reference_program(golden_dir, tmp_path):
+    """DROP-IN: the reference program itself (binning.c main + print_kmers,
+    compiled from /root/reference into oracle/_ref in the build container)
+    with process_read/prune_data/expand_read_id_list replaced by the GPU shim
+    and find_kmer_extensions by the exact unitig replay (host/unitig.c) at
+    link time.  Its stdout must equal the reference program's stdout byte for
+    byte -- which requires the materialised ZHashTable layout (bucket chains,
+    sizes, rehash history) to match the reference's exactly, and the replay to
+    merge exactly the reference's pairs (reads.txt K31 M4 and K6 M3, the C2
+    generator's first 20 K reads at M4: the extension is live)."""
+    import json
+    import subprocess
+    from conftest import golden_input_path, ref_exe_name
     rows = json.loads((golden_dir / "unitigs.json").read_text())
     ran = 0
     for row in rows:
-        exe = kbin.REPO_ROOT / "oracle" / "_ref" / f"dropin_k{row['K']}_m{row['M']}_c1"
+        exe = kbin.REPO_ROOT / "oracle" / "_ref" / ref_exe_name("dropin", row)
         if not exe.exists():
             continue
-        out = subprocess.run([str(exe), str(golden_dir / row["input"])], check=True,
+        out = subprocess.run([str(exe), str(golden_input_path(row, tmp_path))], check=True,
                              capture_output=True, timeout=300).stdout
         assert hashlib.sha256(out).hexdigest() == row["sha256"], row
         ran += 1
@@ -823,7 +848,7 @@ def test_host_cli_multi_gpu(digests, golden_dir):
         assert hashlib.sha256(out).hexdigest() == row["sha256"], row
 
 
-def test_dropin_reference_program_multi_gpu(golden_dir):
+def test_dropin_reference_program_multi_gpu(golden_dir, tmp_path):
     """the unchanged reference program on several GPUs (KBH_GPUS): its stdout
     (unitig extension and print_kmers over the materialised tables) stays
     byte-identical to the reference program's -- the merged multi-GPU result
@@ -831,14 +856,15 @@ def test_dropin_reference_program_multi_gpu(golden_dir):
     import json
     import os
     import subprocess
+    from conftest import golden_input_path, ref_exe_name
     rows = json.loads((golden_dir / "unitigs.json").read_text())
     ran = 0
     for row in rows:
-        exe = kbin.REPO_ROOT / "oracle" / "_ref" / f"dropin_k{row['K']}_m{row['M']}_c1"
+        exe = kbin.REPO_ROOT / "oracle" / "_ref" / ref_exe_name("dropin", row)
         if not exe.exists():
             continue
         for gpus in ("0,0", "0,0,0,0"):
-            out = subprocess.run([str(exe), str(golden_dir / row["input"])], check=True, capture_output=True,
+            out = subprocess.run([str(exe), str(golden_input_path(row, tmp_path))], check=True, capture_output=True,
                                  timeout=300, env=dict(os.environ, KBH_GPUS=gpus)).stdout
             assert hashlib.sha256(out).hexdigest() == row["sha256"], (row, gpus)
         ran += 1
