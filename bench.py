@@ -448,7 +448,7 @@ def capacity_leg(local, steps=2, warmup=1):
     log = []
     for _ in range(steps):
         step()
-        log.extend((d, kbin.timing_dict(t)) for d, t, _ in pass_log)
+        log.extend((d, kbin.timing_dict(t)) for d, t, *_ in pass_log)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     kmers = n * (L - K + 1)
@@ -467,6 +467,134 @@ def capacity_leg(local, steps=2, warmup=1):
            "digest": list(dig), "digest_expected": list(C3_DIGEST), "digest_ok": dig == C3_DIGEST}
     if not out["digest_ok"]:
         print(f"capacity leg: C3 digest {dig} != committed {C3_DIGEST}", file=sys.stderr)
+    return out
+
+
+def routed_runner(K, M, L, cutoff, n, wpr, P, local, rank, reads, pass_log, pipeline=True, cur=None):
+    """one rank of the mmer-sharded job (kbin.dist over the C-ABI group: C
+    routing, RCCL exchange from C under an nccl process group; torch
+    collectives under gloo): rank r bins reads(off) = its n reads (ids r n ..)
+    together with every other rank's, P mmer-partitioned passes a step.
+    Returns (runner, engine, step, drain)."""
+    from kbin import dist as kdist
+    runner = kdist.ShardedBinner(K, M, cutoff, L, device=local, group=None)
+    eng = runner.engine
+    pending = []  # pipelined: the next unit, already scattered, its records in flight
+
+    def send(p, off=0):
+        w, ln = reads(off)
+        return runner.send(w, ln, n, wpr, first_id=rank * n, part=p, n_parts=P)
+
+    def step(digest=False):
+        pass_log.clear()
+        dig = [0, 0, 0, 0]
+        for p in range(P):
+            if pipeline:
+                # unit (step, pass p): its records were sent with the last
+                # unit (or now, at the start); the next unit's -- the next
+                # pass, or the next step's first -- go out before it is binned
+                unit = pending.pop() if pending else send(p)
+                pending.append(send((p + 1) % P, 1 if p + 1 == P else 0))
+                runner.receive(unit)
+            else:
+                w, ln = reads()
+                runner.step(w, ln, n, wpr, first_id=rank * n, part=p, n_parts=P)
+            pass_log.append((eng.export_device() if P > 1 else None, eng.timing_raw(), runner.last_times,
+                             runner.last_counts))
+            if digest:
+                dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
+        if cur is not None:
+            cur[0] += 1
+        return dig
+
+    def drain():
+        # no unit crosses into the timed region: the timed steps send their
+        # own first unit (and one last prefetch goes unused -- counted in)
+        while pending:
+            runner.discard(pending.pop())
+
+    return runner, eng, step, drain
+
+
+def multi_capacity_leg(name, rank, world, local, dist, backend, steps=2, warmup=1, scale=1):
+    """N > 1: one of BASELINE's multi-GPU configurations AS SPECIFIED (SURVEY
+    8(d)): C4 -- 125 M x 150 bp reads per rank (1 B over 8 GPUs) of ONE
+    3.1-Gbp genome, K31 M7, P = 5 passes; C5 -- 62.5 M x 250 bp per rank, 1 %
+    errors, K63 M7, P = 4 -- routed by owner(mmer) over the C group (RCCL
+    all-to-all from C) and binned by the owners.  ms per step (max over
+    ranks), whole-job k-mers/s, the bin phase's roofline, and the exchange:
+    the records this rank sent to its peers per step and their rate per peer
+    link (xGMI is point-to-point: one link per peer).  scale > 1 divides the
+    reads (a rehearsal of the plumbing, e.g. gloo ranks sharing one GPU)."""
+    wl = WORKLOADS[name]
+    n, L, K, M, P = wl["reads"] // scale, wl["read_len"], wl["K"], wl["M"], wl["parts"]
+    wpr = (L + 31) // 32
+    w = torch.empty(n * wpr, dtype=torch.int64, device="cuda")
+    ln = torch.empty(n, dtype=torch.int32, device="cuda")
+    kbin.generate_reads_device(w.data_ptr(), ln.data_ptr(), n, L, wl["genome"], wl["err_ppm"],
+                               gen_seed(wl["seed"]), device=local, read_base=rank * n)
+    torch.cuda.synchronize()
+    pass_log = []
+    runner, eng, step, drain = routed_runner(K, M, L, 1, n, wpr, P, local, rank, lambda off=0: (w, ln), pass_log)
+    eng.set_timing(True)
+
+    def barrier():
+        dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        tt = torch.tensor([x], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    barrier()
+    tc = time.perf_counter()
+    step()
+    barrier()
+    cold_ms = max_over_ranks((time.perf_counter() - tc) * 1e3)
+    for _ in range(warmup):
+        step()
+    drain()
+    barrier()
+    t0 = time.perf_counter()
+    log, sent = [], []
+    for _ in range(steps):
+        step()
+        log.extend((d if d is not None else eng.export_device(), kbin.timing_dict(t)) for d, t, _, _ in pass_log)
+        # records this rank sent to each peer this step (its row of every pass's counts)
+        row = np.zeros(world, dtype=np.float64)
+        for _, _, _, c in pass_log:
+            if c is not None:
+                row += np.asarray(c[0], dtype=np.float64)
+        sent.append(row)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    drain()
+    dt = elapsed / steps
+    kmers = n * (L - K + 1) * world
+    rec_bytes = runner.rec_words * 8
+    row = np.mean(sent, axis=0)
+    off_rank = float(row.sum() - row[rank]) * rec_bytes
+    phases = {k: round(float(sum(t[k] for _, t in log)) / steps, 3)
+              for k in ("scan_insert_ms", "sort_ms", "runs_ms", "emit_ms", "total_ms")}
+    route = pass_log[-1][2] if pass_log else {}
+    out = {"workload": f"{wl['name'].split(' ')[0]} as specified: {n * world} x {L}bp reads over {world} GPUs "
+                       f"({n} per GPU), genome {wl['genome']} bp, {wl['err_ppm'] / 1e4:.2f}% substitutions, "
+                       f"seed {wl['seed']}, K={K} M={M}, prune cutoff 1, {P} mmer-partitioned passes, "
+                       f"mmer-sharded (owner(mmer)), records routed over the group",
+           "value": round(kmers / dt, 1), "unit": "k-mers/s", "ms_per_step": round(dt * 1e3, 3), "steps": steps,
+           "cold_first_step_ms": round(cold_ms, 1),
+           "roofline": roofline(log, L, K, world, kmers / dt, f"n{n}_L{L}_K{K}_M{M}_P{P}"),
+           "phases_ms_rank0": phases,
+           "exchange": {"bytes_sent_off_rank_per_step": int(off_rank), "record_bytes": rec_bytes,
+                        "peer_links": world - 1,
+                        "per_link_GBps_over_step": round(off_rank / max(1, world - 1) / dt / 1e9, 3),
+                        "route_ms_last_pass": {k: round(float(v), 3) for k, v in route.items()}
+                        if isinstance(route, dict) else route}}
+    if scale > 1:
+        out["rehearsal_scale"] = scale
+    del runner, eng, step, w, ln
+    torch.cuda.empty_cache()
     return out
 
 
@@ -601,41 +729,8 @@ def main():
     P = args.parts
     pass_log = []  # (export_device, timing[, route times]) of every pass of the last step
     if world > 1 or args.routed:
-        from kbin import dist as kdist
-        runner = kdist.ShardedBinner(K, M, args.cutoff, L, device=local, group=None)
-        eng = runner.engine
-        pipeline = not args.no_pipeline
-        pending = []  # pipelined: the next unit, already scattered, its records in flight
-
-        def send(p, off=0):
-            w, ln = reads(off)
-            return runner.send(w, ln, n, wpr, first_id=rank * n, part=p, n_parts=P)
-
-        def step(digest=False):
-            pass_log.clear()
-            dig = [0, 0, 0, 0]
-            for p in range(P):
-                if pipeline:
-                    # unit (step, pass p): its records were sent with the last
-                    # unit (or now, at the start); the next unit's -- the next
-                    # pass, or the next step's first -- go out before it is binned
-                    unit = pending.pop() if pending else send(p)
-                    pending.append(send((p + 1) % P, 1 if p + 1 == P else 0))
-                    runner.receive(unit)
-                else:
-                    w, ln = reads()
-                    runner.step(w, ln, n, wpr, first_id=rank * n, part=p, n_parts=P)
-                pass_log.append((eng.export_device() if P > 1 else None, eng.timing_raw(), runner.last_times))
-                if digest:
-                    dig = [(a + b) % (1 << 64) for a, b in zip(dig, eng.digest())]
-            cur[0] += 1
-            return dig
-
-        def drain():
-            # no unit crosses into the timed region: the timed steps send their
-            # own first unit (and one last prefetch goes unused -- counted in)
-            while pending:
-                runner.discard(pending.pop())
+        runner, eng, step, drain = routed_runner(K, M, L, args.cutoff, n, wpr, P, local, rank, reads, pass_log,
+                                                 not args.no_pipeline, cur)
     else:
         eng, step = single_gpu_runner(K, M, L, args.cutoff, n, wpr, P, local, reads, pass_log,
                                       scan_once=not args.no_scan_once)
@@ -673,7 +768,7 @@ def main():
     # timed steps record only its two events (the roofline's kernel time) and
     # the phases come from one more step after them; heavy-bin workloads keep
     # every event (their roofline kernel is the whole bin phase)
-    phase_log = [(d, kbin.timing_dict(t)) for d, t, _ in pass_log] if args.warmup else []
+    phase_log = [(d, kbin.timing_dict(t)) for d, t, *_ in pass_log] if args.warmup else []
     light = bool(phase_log) and not args.timing_all and all(int(t["engine"]) == kbin.KB_ENG_BINNED and t["bin_kernel_ms"] > 0
                                     and t["bin_kernel_ms"] >= 0.5 * t["runs_ms"] for _, t in phase_log)
     if dist is not None:  # (every rank takes the same branch: the phase step runs collectives)
@@ -689,9 +784,9 @@ def main():
     route_t = []
     for _ in range(args.steps):
         step()
-        steps_log.append([(d, t) for d, t, _ in pass_log])  # (converted after the timed steps)
+        steps_log.append([(d, t) for d, t, *_ in pass_log])  # (converted after the timed steps)
         if world > 1 or args.routed:
-            rts = [r for _, _, r in pass_log]
+            rts = [r for _, _, r, *_ in pass_log]
             route_t.append({k: sum(r[k] for r in rts) for k in rts[0]})
     barrier()
     elapsed = time.perf_counter() - t0
@@ -709,7 +804,7 @@ def main():
         eng.set_timing(True)
         step()
         drain()
-        phase_log = [(d, kbin.timing_dict(t)) for d, t, _ in pass_log]
+        phase_log = [(d, kbin.timing_dict(t)) for d, t, *_ in pass_log]
         eng.set_timing("kernel")
     steps_log = [[(d if d is not None else ex_last, kbin.timing_dict(t)) for d, t in st] for st in steps_log]
     last = steps_log[-1]  # the passes of the last step, added up
@@ -785,6 +880,18 @@ def main():
                    "engine": {1: "table", 2: "binned"}.get(int(tim[-1]["engine"]), "?"),
                    "bins": int(tim[-1]["n_bins"]), "superkmers": int(tim[-1]["n_superkmers"])},
     }
+    if world > 1 and args.capacity and args.workload == "c2":
+        # BASELINE's multi-GPU configurations as specified (the headline stays
+        # C2 weak scaling: the same per-GPU work at every N); the main leg's
+        # contexts and read sets go first
+        del runner, eng, step, sets
+        torch.cuda.empty_cache()
+        scale = max(1, int(os.environ.get("KB_CAPACITY_SCALE", "1")))
+        out["capacity"] = {}
+        for name in ("c4", "c5"):
+            out["capacity"][name] = multi_capacity_leg(name, rank, world, local, dist, backend, scale=scale)
+            if rank == 0:
+                print(json.dumps({name: out["capacity"][name]}), file=sys.stderr, flush=True)
     if world == 1 and args.host_input and P == 1:
         out["host_input"] = host_input_leg(sets[0][0], sets[0][1], n, wpr, L, K, M, args.cutoff, local)
     if world == 1 and args.capacity and args.workload == "c2" and not args.routed:

@@ -372,6 +372,9 @@ extern "C" int kb_create(const kb_params* params, kb_ctx** out) {
     // live -- the binned engine's record pass walks it, reads of <= 512 bp,
     // one GPU; kb_finalize and the routing calls check the rest)
     if (p.K > 63) return fail(KB_EINVAL, "K=%d > 63 unsupported", p.K);
+    // (a k-mer holds its signature mmer: K >= M, binning.c:931-936 reads M bases
+    // of every k-mer; the incremental walk starts at K - M >= 0)
+    if (p.K < 1 || p.K < p.M) return fail(KB_EINVAL, "K=%d outside [M=%d, 63]", p.K, p.M);
     if (p.cutoff < 0) return fail(KB_EINVAL, "cutoff < 0");
     if (p.max_read_len < 1 || p.max_read_len > 65535)
         return fail(KB_EINVAL, "max_read_len=%d outside [1,65535]", p.max_read_len);
@@ -1905,7 +1908,9 @@ static int finalize_binned(kb_ctx* c, int prune, bool affine, int64_t id_c, bool
     REC(2);
     // bins: canonical mmers, or context sub-bins of the split ones (a fixed
     // budget: the buffers sized by it keep their size as maps change)
-    const uint64_t bin_keys = bucketed ? bin_budget(c, NB) : 1ull << (2 * M - 1);
+    // (the radix path's bins are mmer codes: canonical ones, 2^(2M-1) of them,
+    // except for K < 2M signatures, which take any of the 4^M codes -- ADVICE r05)
+    const uint64_t bin_keys = bucketed ? bin_budget(c, NB) : 1ull << (2 * M - (c->p.K < 2 * M ? 0 : 1));
     const uint64_t max_bins = std::max<uint64_t>(1, std::min<uint64_t>(R, bin_keys));
     const bool use_desc = bucketed && env_int("KB_BIN_DESC", 1);
     // the speculative bucket ordering (binned_buckets) stands when R fitted

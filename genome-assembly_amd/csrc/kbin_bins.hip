@@ -69,6 +69,15 @@ uint32_t sk_hash_dest(uint32_t mmer, uint32_t G, uint64_t salt) {
     x ^= x >> 31;
     return (uint32_t)((x >> 32) % G);
 }
+
+// CPU-callable check of the guard above (tests/test_abi.py): the first
+// destination of a depth-0 record of code `canon` on a bucketed pass with map
+// `map` over NB buckets -- the map's bucket for a canonical code, the hash
+// route for any other (never map[canon - half] with canon < half)
+extern "C" uint32_t kb_internal_map_dest(const uint32_t* map, uint32_t canon, int M, uint32_t NB) {
+    if (!map || !bm_has_entry(canon, M)) return sk_hash_dest(canon, NB, BUCKET_SALT);
+    return map[canon - (1u << (2 * M - 1))] & 1023u;
+}
 DEV uint32_t owner_of_mmer(uint32_t mmer, uint32_t G) { return dest_of(mmer, G, OWNER_SALT); }
 // a pass keeps the super-k-mers of its own mmer partition
 DEV bool in_part(uint32_t mmer, uint32_t part, uint32_t part_n) {
@@ -167,7 +176,7 @@ DEV uint32_t record_pieces(const SkScanArgs& A, uint32_t canon, int lo, int n, i
                            const uint64_t* row, uint32_t (&d)[2], uint32_t (&sub)[2], int& ne) {
     ne = 0;
     sub[0] = sub[1] = 0;
-    if (!A.bucket_map) {
+    if (!A.bucket_map || !bm_has_entry(canon, A.M)) {
         d[0] = dest_of(canon, A.G, A.dest_salt);
         return 1;
     }
@@ -204,7 +213,7 @@ DEV uint64_t record_plan(const SkScanArgs& A, uint64_t e, uint32_t me, const uin
     const bool rev = ((e >> 28) & 1u) != 0;
     uint32_t d0 = 0, d1 = 0, b = 0, two = 0;
     int ne = 0;
-    if (!A.bucket_map) {
+    if (!A.bucket_map || !bm_has_entry(canon, A.M)) {  // (me: not loaded for such a code)
         d0 = dest_of(canon, A.G, A.dest_salt);
     } else if (!(b = bm_depth(me))) {
         d0 = me & 1023u;
@@ -517,9 +526,10 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                     const bool v1 = i1 < span;
                     const uint64_t e0 = stg[i0], e1 = v1 ? stg[i1] : e0;
                     uint32_t me0 = 0, me1 = 0;
-                    if (A.bucket_map) {
-                        me0 = A.bucket_map[(uint32_t)(e0 >> 38) - half];
-                        me1 = A.bucket_map[(uint32_t)(e1 >> 38) - half];
+                    if (A.bucket_map) {  // (codes below half: no entry, record_plan hashes them)
+                        const uint32_t c0 = (uint32_t)(e0 >> 38), c1 = (uint32_t)(e1 >> 38);
+                        me0 = c0 >= half ? A.bucket_map[c0 - half] : 0u;
+                        me1 = c1 >= half ? A.bucket_map[c1 - half] : 0u;
                     }
                     const uint64_t p0 = record_plan(A, e0, me0, smem + ((e0 >> 29) & 0x1FFu) * RS);
                     const uint64_t p1 = record_plan(A, e1, me1, smem + ((e1 >> 29) & 0x1FFu) * RS);
@@ -4473,7 +4483,9 @@ DEV void convert_plan(const uint64_t* __restrict__ recs, uint64_t n_rec, int rw,
     if (bucket_map) {
 #pragma unroll
         for (int j = 0; j < PERT; j++)
-            if (dst[j] != 0xFFFFFFFFu) me[j] = bucket_map[canon[j] - halfM];
+            // (canon >= halfM by construction -- the larger of a code and its
+            // complement -- so the guard never hashes here; it bounds the index)
+            if (dst[j] != 0xFFFFFFFFu) me[j] = canon[j] >= halfM ? bucket_map[canon[j] - halfM] : 0u;
 #pragma unroll
         for (int j = 0; j < PERT; j++) {
             if (dst[j] == 0xFFFFFFFFu) continue;

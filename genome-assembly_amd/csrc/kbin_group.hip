@@ -634,9 +634,22 @@ extern "C" void kb_group_destroy(kb_group* g) {
     {
         std::lock_guard<std::mutex> lk(g->mu);
         g->stop = true;
+        // units sent but never received or discarded (kbin.h: a program error):
+        // the queued ones never start their collectives -- a peer that has
+        // already gone would leave them blocked in the counts all-gather
+        // (ADVICE r05); a stage already running is waited for
+        if (g->inflight)
+            fprintf(stderr, "kbin: kb_group_destroy with %d unit(s) in flight (receive or discard them first)\n",
+                    g->inflight);
+        for (const int s : g->jobs) {
+            g->u[s].rc = KB_ESTATE;
+            g->u[s].err = "group destroyed before the unit was sent";
+            g->u[s].done = true;
+        }
+        g->jobs.clear();
     }
     g->cv.notify_all();
-    if (g->th.joinable()) g->th.join();  // (after the queued units' send stages)
+    if (g->th.joinable()) g->th.join();
     for (auto& rk : g->r) rank_free(rk);
     delete g;
 }
@@ -772,12 +785,17 @@ extern "C" int kb_group_discard(kb_group* g) {
     if (!g) return gfail(KB_EINVAL, "null group");
     if (!g->inflight) return gfail(KB_ESTATE, "kb_group_discard: nothing sent");
     const int s = g->tail;
+    Unit& un = g->u[s];
     const int src = wait_unit(g, s);
-    if (!src)
-        for (auto& rk : g->r) {
-            GHIP(hipSetDevice(rk.dev));
-            GHIP(hipEventSynchronize(rk.landed[s]));
-        }
+    if (src) { // (kbin.h: _discard returns the unit's failure, as _receive does)
+        const std::string e = un.err;
+        retire(g, s);
+        return gfail(src, "%s", e.c_str());
+    }
+    for (auto& rk : g->r) {
+        GHIP(hipSetDevice(rk.dev));
+        GHIP(hipEventSynchronize(rk.landed[s]));
+    }
     retire(g, s);
     return KB_OK;
 }

@@ -185,6 +185,13 @@ __host__ __device__ inline uint32_t sub_count(uint32_t b) { return b ? (1u << (2
 //                 b = (entry >> 28) & 7 in 1..SUB_MAX_B; sub-bin s lives in
 //                 bucket sub_map[(entry & 0x0FFFFFFF) + s]
 constexpr uint32_t BM_SPLIT = 0x80000000u;
+// The bucket map covers the canonical mmer codes [2^(2M-1), 4^M) only
+// (bucket_map[canon - 2^(2M-1)]).  A record whose code is below that -- a
+// K < 2M signature (binning.c:992-1021: the host turns the map off for those
+// passes) or a malformed received record -- has no entry and takes the hash
+// route every map-less pass takes; no kernel indexes below the map
+// (the r5g38 fault's class).
+__host__ __device__ __forceinline__ bool bm_has_entry(uint32_t canon, int M) { return canon >= (1u << (2 * M - 1)); }
 __device__ __forceinline__ uint32_t bm_depth(uint32_t e) { return (e & BM_SPLIT) ? (e >> 28) & 7u : 0u; }
 __device__ __forceinline__ uint32_t bm_bucket(uint32_t e, const uint16_t* sub_map, uint32_t sub) {
     return (e & BM_SPLIT) ? (uint32_t)sub_map[(e & 0x0FFFFFFFu) + sub] : (e & 1023u);

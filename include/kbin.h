@@ -69,8 +69,9 @@ extern "C" {
 typedef struct kb_ctx kb_ctx;
 
 typedef struct {
-    int32_t K;              /* KMER_SIZE       (binning.c:11); 2 <= K <= 63      */
-    int32_t M;              /* MMER_SIZE       (binning.c:10); 1 <= M <= 8, K >= 2M */
+    int32_t K;              /* KMER_SIZE       (binning.c:11); M <= K <= 63      */
+    int32_t M;              /* MMER_SIZE       (binning.c:10); 1 <= M <= 8 (K < 2M:
+                               the live incremental branch, one GPU, binned engine) */
     int32_t cutoff;         /* ABUNDANCE_CUTOFF (binning.c:12); >= 0            */
     int32_t max_read_len;   /* longest read accepted (READ_LENGTH-2 for fgets)  */
     int32_t device;         /* HIP device ordinal                               */
@@ -353,6 +354,10 @@ int kb_group_create_rank(const kb_params *params, int rank, int n_ranks, const v
                          kb_group **out);
 int kb_group_create_rank_host(const kb_params *params, int rank, int n_ranks, const kb_group_host_transport *t,
                               kb_group **out);
+/* destroy: receive or discard every sent unit first (all ranks).  Units still
+ * queued are dropped unsent (their collectives never start, so a peer that
+ * has gone cannot block the teardown); a unit whose send stage is already in
+ * its collectives is waited for; a warning goes to stderr either way. */
 void kb_group_destroy(kb_group *grp);
 int kb_group_info(kb_group *grp, int *n_ranks, int *n_local, int *rank0, int *transport);
 int kb_group_submit_ids(kb_group *grp, int local, const char *bases, const uint32_t *lens, uint64_t n_reads,

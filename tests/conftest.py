@@ -52,7 +52,7 @@ def golden_input_path(row, tmp_dir) -> pathlib.Path:
         return GOLDEN / src
     import oracle
     n = int(src.split(":")[1])
-    raw = oracle.gen_reads(n, 150, 5_000_000, 1000, 2)
+    raw = oracle.gen_reads(n, 150, 5_000_000, 1000, 2 * 1000003)
     p = pathlib.Path(tmp_dir) / f"c2_{n}.txt"
     with open(p, "wb") as f:
         for i in range(n):

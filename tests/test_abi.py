@@ -6,6 +6,7 @@ import pathlib
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 import kbin
@@ -78,7 +79,8 @@ def test_struct_layouts_match_header(tmp_path):
 
 # (K < 2M is accepted since round 5: the binned engine walks the reference's
 # incremental branch, test_gpu_parity.py::test_k_below_2m_vs_oracle)
-@pytest.mark.parametrize("K,M,code", [(64, 7, kbin.KB_EINVAL), (31, 9, kbin.KB_EINVAL), (31, 0, kbin.KB_EINVAL)])
+@pytest.mark.parametrize("K,M,code", [(64, 7, kbin.KB_EINVAL), (31, 9, kbin.KB_EINVAL), (31, 0, kbin.KB_EINVAL),
+                                      (5, 7, kbin.KB_EINVAL), (0, 3, kbin.KB_EINVAL), (-1, 1, kbin.KB_EINVAL)])
 def test_param_validation(K, M, code):
     with pytest.raises(kbin.KbError) as ei:
         kbin.Engine(K, M)
@@ -96,3 +98,24 @@ def test_no_silent_cpu_fallback():
 def test_missing_library_raises(tmp_path):
     with pytest.raises(FileNotFoundError):
         kbin.load_library(tmp_path / "nope.so")
+
+
+@pytest.mark.parametrize("M", range(1, 9))
+def test_bucket_map_guard(M):
+    """a record whose mmer code is below 2^(2M-1) (no entry
+    in the bucket map, which covers canonical codes only) takes the hash
+    route; the map is indexed only for canonical codes.  The kernels and this
+    CPU hook share the predicate (kbin_internal.h bm_has_entry)."""
+    lib = kbin.load_library()
+    f = lib.kb_internal_map_dest
+    f.restype = C.c_uint32
+    f.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.c_int, C.c_uint32]
+    half, NB = 1 << (2 * M - 1), 97
+    poison = np.full(half, 0xFFFFFFFF, dtype=np.uint32)
+    mp = np.arange(half, dtype=np.uint32) % NB
+    nomap = [f(None, c, M, NB) for c in range(half)]
+    for c in range(0, half, max(1, half // 512)):
+        assert f(poison.ctypes.data_as(C.POINTER(C.c_uint32)), c, M, NB) == nomap[c]  # hash route, map untouched
+        assert nomap[c] < NB
+    for c in range(half, 2 * half, max(1, half // 512)):
+        assert f(mp.ctypes.data_as(C.POINTER(C.c_uint32)), c, M, NB) == (c - half) % NB

@@ -439,6 +439,36 @@ def test_group_pipelined_partitions(engine):
     assert union == skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, 31, 7, 1, True))
 
 
+def test_group_discard_reports_failed_unit(engine):
+    """kb_group_discard returns the unit's failure, as kb_group_receive does
+    (ADVICE r05): a unit whose routing fails (a read byte outside ACGT on one
+    rank: kb_route_plan's ingest check) is discarded with KB_EALPHABET, not
+    silently dropped with zero counts; after kb_group_reset the group bins
+    the next unit bit-exact"""
+    if engine != "binned":
+        pytest.skip("routing is engine-independent")
+    good = _reads(300)
+    bad = list(good[:100])
+    bad[7] = bad[7][:20] + b"N" + bad[7][21:]
+    K, M = 31, 7
+    with kbin.Group(K, M, cutoff=1, max_read_len=300, devices=[0, 0]) as grp:
+        grp.submit(0, bad, first_id=0)
+        grp.submit(1, good[100:], first_id=100)
+        grp.send_async()
+        with pytest.raises(kbin.KbError) as ei:
+            grp.discard()
+        assert ei.value.code == kbin.KB_EALPHABET
+        grp.reset()
+        grp.submit(0, good[:100], first_id=0)
+        grp.submit(1, good[100:], first_id=100)
+        grp.finalize(True)
+        union = {}
+        for g in range(2):
+            union.update(_result_dict(grp.ctx(g).export()))
+    bases, lens = kbin.pack_reads(good)
+    assert union == skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, True))
+
+
 def test_group_track_first(engine):
     """first occurrences through a group (the drop-in's multi-GPU mode): the
     sender switches to plan/pack (read order), receivers keep (id << 16 |
@@ -469,3 +499,37 @@ def test_group_track_first(engine):
                 seen += 1
             union.update(_result_dict(r))
     assert seen == ref.n_entries and union == want
+
+
+def test_bench_multi_gpu_capacity_rehearsal(tmp_path, engine):
+    """bench.py at N = 2 (gloo rehearsal: two ranks on one GPU) runs the
+    headline C2 weak-scaling leg and then BASELINE's multi-GPU configurations
+    as specified -- C4 (K31, 150 bp, one 3.1-Gbp genome, P = 5) and C5 (K63,
+    250 bp, 1 % errors, P = 4) -- routed between the ranks; here at 1/400 of
+    their reads (KB_CAPACITY_SCALE) to test the legs' plumbing: the one JSON
+    line carries both legs with their timings, rooflines and exchange bytes"""
+    if engine != "binned":
+        pytest.skip("bench picks its engine itself")
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, KB_DIST_BACKEND="gloo", KB_CAPACITY_SCALE="400")
+    env.pop("KB_ENGINE", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(kbin.REPO_ROOT / "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--reads", "100000"],
+                       capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    for name, K in (("c4", 31), ("c5", 63)):
+        leg = line["capacity"][name]
+        assert leg["value"] > 0 and leg["ms_per_step"] > 0, leg
+        assert f"K={K}" in leg["workload"] and leg["rehearsal_scale"] == 400
+        assert leg["exchange"]["bytes_sent_off_rank_per_step"] > 0
+        assert 0 < leg["roofline"]["frac"] < 1

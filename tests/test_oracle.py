@@ -79,8 +79,10 @@ def _ref_or_skip(K, M, c=1):
     return exe
 
 
+# (13, 7), (15, 8), (3, 2), (1, 1): K < 2M pairs whose incremental branch
+# (binning.c:992-1021) overflows the reference's int differently
 @pytest.mark.parametrize("K,M,rl", [(31, 7, 152), (6, 3, 101), (10, 6, 80), (5, 4, 60), (40, 8, 130),
-                                    (63, 7, 260)])
+                                    (63, 7, 260), (13, 7, 90), (15, 8, 100), (3, 2, 50), (1, 1, 30)])
 def test_oracle_vs_reference_binary(tmp_path, K, M, rl):
     exe = _ref_or_skip(K, M)
     rng = np.random.default_rng(K * 31 + M)

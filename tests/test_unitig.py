@@ -102,7 +102,7 @@ def golden_input(case):
     rl = case.get("read_length", 101)
     if src.startswith("c2:"):  # the C2 generator's first n reads, one per line (tools/unitig_golden.py)
         n = int(src.split(":")[1])
-        raw = oracle.gen_reads(n, 150, 5_000_000, 1000, 2)
+        raw = oracle.gen_reads(n, 150, 5_000_000, 1000, 2 * 1000003)
         d = tempfile.mkdtemp()
         p = os.path.join(d, "reads.txt")
         with open(p, "wb") as f:

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Adds whole-program goldens of the reference AS SHIPPED (its main: bin,
 prune, expand, unitig extension, print_kmers) on the C2 generator's first n
-reads, one 150-bp read per line, READ_LENGTH 152, at the reference's own
-MMER_SIZE 4 (binning.c:10) -- where its unitig extension is live and
+reads (bench.py C2: seed 2, generator stream gen_seed(2) = 2000006), one
+150-bp read per line, READ_LENGTH 152, at the reference's own MMER_SIZE 4
+(binning.c:10) -- where its unitig extension is live and
 quadratic (20 000 reads: ~13 min on one core here).  Runs only where
 /root/reference is (oracle/build_ref.sh full); writes tests/golden/unitigs.json
 entries {"input": "c2:<n>", "read_length": 152, ...}.
@@ -32,7 +33,7 @@ def main():
     subprocess.run(["bash", str(REPO / "oracle" / "build_ref.sh"), "full", str(K), str(M), "1"], env=env,
                    check=True, capture_output=True)
     exe = REPO / "oracle" / "_ref" / f"full_k{K}_m{M}_c1_rl152"
-    raw = oracle.gen_reads(n, 150, 5_000_000, 1000, 2)
+    raw = oracle.gen_reads(n, 150, 5_000_000, 1000, 2 * 1000003)
     with tempfile.TemporaryDirectory() as d:
         p = pathlib.Path(d) / "reads.txt"
         with open(p, "wb") as f:

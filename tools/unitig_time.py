@@ -58,6 +58,8 @@ def run(exe, path, timeout, env=None):
             out["prune_data"] = json.loads(ln)
         elif ln.startswith("{\"expand_ms\""):  # the shim's expand_read_id_list (binning.c:857-888)
             out["expand"] = json.loads(ln)
+        elif ln.startswith("{\"find_kmer_extensions_ms\""):  # the exact replay (host/unitig.c)
+            out.setdefault("find_kmer_extensions", []).append(json.loads(ln))
         elif ln.startswith("{\"t_exit_s\""):  # exit() started: the reference's main has returned
             out["t_exit_s"] = json.loads(ln)["t_exit_s"]
     if "expand" in out and "t_exit_s" in out:
@@ -74,6 +76,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--reads", type=int, nargs="+", default=[100_000, 1_000_000])
 ap.add_argument("--full-max", type=int, default=1_000_000, help="run the reference as shipped up to this many reads")
 ap.add_argument("--timeout", type=int, default=500)
+ap.add_argument("--M", type=int, default=7, help="MMER_SIZE of the binaries (4: the reference as shipped, "
+                                                 "where the unitig extension is live)")
+ap.add_argument("--walk-ref", action="store_true",
+                help="also run dropinw (the drop-in with the reference's own find_kmer_extensions)")
 a = ap.parse_args()
 wl = bench.WORKLOADS["c2"]
 L = wl["read_len"]
@@ -91,9 +97,13 @@ for n in a.reads:
         f.write(np.concatenate([raw[:n], np.full((n, 1), 10, np.uint8)], axis=1).tobytes())
         f.flush()
         row = {"reads": n, "read_len": L}
-        row["dropin"] = run(ref / "dropin_k31_m7_c1_rl152", f.name, a.timeout, dict(os.environ, KBH_TRACE="1"))
+        row["M"] = a.M
+        row["dropin"] = run(ref / f"dropin_k31_m{a.M}_c1_rl152", f.name, a.timeout, dict(os.environ, KBH_TRACE="1"))
+        if a.walk_ref:
+            row["dropin_refwalk"] = run(ref / f"dropinw_k31_m{a.M}_c1_rl152", f.name, a.timeout,
+                                        dict(os.environ, KBH_TRACE="1"))
         if n <= a.full_max:
-            row["reference"] = run(ref / "full_k31_m7_c1_rl152", f.name, a.timeout)
+            row["reference"] = run(ref / f"full_k31_m{a.M}_c1_rl152", f.name, a.timeout)
             if "sha256" in row["reference"] and "sha256" in row["dropin"]:
                 row["identical"] = row["reference"]["sha256"] == row["dropin"]["sha256"]
         print(json.dumps(row), flush=True)
