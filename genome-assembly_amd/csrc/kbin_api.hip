@@ -865,8 +865,10 @@ extern "C" int kb_record_words(kb_ctx* c, uint32_t* out) {
 
 extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
     if (!c || !h_counts) return fail(KB_EINVAL, "null argument");
-    if (c->p.K < 2 * c->p.M)  // (routed records carry no complement flag: the receiver rederives it)
-        return fail(KB_EINVAL, "K=%d < 2M=%d: one GPU only (no routing)", c->p.K, 2 * c->p.M);
+    // (K < 2M: routed records carry the complement flag, ROUTED_REV_BIT; the
+    // binned engine's record pass walks the live incremental branch)
+    if (c->p.K < 2 * c->p.M && !(binned_applies(c) && c->KW == 1))
+        return fail(KB_EINVAL, "K=%d < 2M=%d routes through the binned engine only", c->p.K, 2 * c->p.M);
     if (n_dest < 1 || n_dest > 64) return fail(KB_EINVAL, "n_dest=%u outside [1,64]", n_dest);
     if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
     int rc = set_device(c);
@@ -942,8 +944,6 @@ extern "C" int kb_split_passes(kb_ctx* c, uint32_t n_parts, uint64_t* d_regions,
 static int scatter_regions(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions, uint64_t region_cap,
                            uint64_t* h_counts, uint64_t salt, bool by_pass) {
     if (!c || !h_counts) return fail(KB_EINVAL, "null argument");
-    if (c->p.K < 2 * c->p.M)  // (routed records carry no complement flag: the receiver rederives it)
-        return fail(KB_EINVAL, "K=%d < 2M=%d: one GPU only (no routing, no split passes)", c->p.K, 2 * c->p.M);
     if (n_dest < 1 || n_dest > 64) return fail(KB_EINVAL, "n_dest=%u outside [1,64]", n_dest);
     if (by_pass && c->part_n > 1) return fail(KB_ESTATE, "kb_split_passes on a partitioned context");
     if (c->finalized) return fail(KB_ESTATE, "route after finalize (call kb_reset)");
@@ -1780,7 +1780,7 @@ static int binned_sk_records(kb_ctx* c, uint64_t& R, uint64_t& N) {
     uint64_t off = 0;
     for (auto& b : c->batches) {
         if (!b.superkmers) continue;
-        HIPCHK(launch_sk_convert(b.recs, b.n_reads, rec_words(c), off, c->p.M, c->pay.p, c->occ_a.p,
+        HIPCHK(launch_sk_convert(b.recs, b.n_reads, rec_words(c), off, c->p.M, c->p.K, c->pay.p, c->occ_a.p,
                                  c->misc.p, reinterpret_cast<unsigned long long*>(c->totals.p + 8), c->s));
         off += b.n_reads;
         c->tm.scan_insert_launches++;
@@ -2436,9 +2436,6 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
         for (auto& b : c->batches)
             if (!b.routed && !b.superkmers && b.RW > 16)
                 return fail(KB_EINVAL, "K=%d < 2M=%d: reads of at most 512 bp", c->p.K, 2 * c->p.M);
-        if (any_sk)
-            return fail(KB_EINVAL, "K=%d < 2M=%d: received super-k-mers carry no complement flag", c->p.K,
-                        2 * c->p.M);
     }
     memset(&c->tm, 0, sizeof(c->tm));
     const int SW = c->KW == 1 ? 2 : 4;

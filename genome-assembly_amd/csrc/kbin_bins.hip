@@ -158,7 +158,7 @@ DEV void put_record(const SkScanArgs& A, uint64_t* o, uint32_t ord, uint64_t lo,
         o[0] = (uint64_t)ord | (n << 32) | (so << 38) | (rev << 44) | (lo << 45);
     } else {
         const uint32_t id = (uint32_t)id_of(ord, A.read_ids, A.id_off);
-        o[0] = (uint64_t)id | (lo << 32) | (n << 48) | (so << 54);
+        o[0] = (uint64_t)id | (lo << 32) | (n << 48) | (so << 54) | (rev << ROUTED_REV_BIT);
     }
     for (int w = 1; w < A.rw; w++) {
         uint64_t x = window64(sw, (int)lo + 32 * (w - 1));
@@ -703,7 +703,8 @@ hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t 
 // ---------------------------------------------------------------------------
 // routing (one process per GPU): the sender's records go to
 // owner(mmer) in the routed record format of route_kernel (kbin_kernels.hip)
-// -- header {id | i0 << 32 | n << 48 | sig_off << 54}, then the span words --
+// -- header {id | i0 << 32 | n << 48 | sig_off << 54 | rev << 60}, then the
+// span words (rev: kbin_internal.h ROUTED_REV_BIT) --
 // destination-major, read order within a destination; the receiver turns
 // them back into binned records.
 // ---------------------------------------------------------------------------
@@ -741,9 +742,9 @@ __global__ __launch_bounds__(256) void route_pack_binned_kernel(const uint64_t* 
         const uint64_t t = (uint32_t)sorted[k];
         const uint64_t hd = pay[3 * t];
         const uint32_t id = (uint32_t)id_of((uint32_t)hd, read_ids, id_off);
-        const uint64_t n = (hd >> 32) & 63u, so = (hd >> 38) & 63u, lo = (hd >> 45) & 0xFFFFu;
+        const uint64_t n = (hd >> 32) & 63u, so = (hd >> 38) & 63u, lo = (hd >> 45) & 0xFFFFu, rev = (hd >> 44) & 1u;
         uint64_t* o = out + k * (uint64_t)rw;
-        o[0] = (uint64_t)id | (lo << 32) | (n << 48) | (so << 54);
+        o[0] = (uint64_t)id | (lo << 32) | (n << 48) | (so << 54) | (rev << ROUTED_REV_BIT);
         o[1] = pay[3 * t + 1];
         if (rw >= 3) o[2] = pay[3 * t + 2];
         for (int w = 3; w < rw; w++) o[w] = 0;  // (K <= 31 spans fit two words)
@@ -761,7 +762,7 @@ hipError_t launch_route_pack_binned(const uint64_t* sorted, const uint64_t* pay,
 }
 
 __global__ __launch_bounds__(256) void sk_convert_kernel(const uint64_t* __restrict__ recs, uint64_t n_rec,
-                                                         int rw, uint64_t off, int M, uint64_t* __restrict__ pay,
+                                                         int rw, uint64_t off, int M, int K, uint64_t* __restrict__ pay,
                                                          uint64_t* __restrict__ keys, uint32_t* status,
                                                          unsigned long long* n_kmers) {
     const uint32_t maskM = (1u << (2 * M)) - 1u, halfM = 1u << (2 * M - 1);
@@ -774,7 +775,7 @@ __global__ __launch_bounds__(256) void sk_convert_kernel(const uint64_t* __restr
         const uint32_t id = (uint32_t)h;
         const uint64_t lo = (h >> 32) & 0xFFFFu, n = (h >> 48) & 63u, so = (h >> 54) & 63u;
         const uint32_t sm = (uint32_t)(span_window(w0, w1, 0ull, 0ull, (int)so) >> (64 - 2 * M));
-        const bool rev = sm < halfM;  // complement wins (binning.c:1029-1040)
+        const bool rev = routed_rev(h, sm, K, M);  // complement wins (binning.c:1029-1040)
         const uint32_t canon = rev ? maskM - sm : sm;
         neg |= (int32_t)id < 0;
         const uint64_t t = off + k;
@@ -790,12 +791,12 @@ __global__ __launch_bounds__(256) void sk_convert_kernel(const uint64_t* __restr
     if (threadIdx.x == 0 && kmers) atomicAdd(n_kmers, (unsigned long long)kmers);
 }
 
-hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint64_t off, int M,
+hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint64_t off, int M, int K,
                              uint64_t* pay, uint64_t* keys, uint32_t* status, unsigned long long* n_kmers,
                              hipStream_t s) {
     if (!n_rec) return hipSuccess;
     const uint64_t blocks = std::min<uint64_t>((n_rec + 255) / 256, 8192);
-    hipLaunchKernelGGL(sk_convert_kernel, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, off, M, pay,
+    hipLaunchKernelGGL(sk_convert_kernel, dim3((unsigned)blocks), dim3(256), 0, s, recs, n_rec, rw, off, M, K, pay,
                        keys, status, n_kmers);
     return hipGetLastError();
 }
@@ -4473,7 +4474,7 @@ DEV void convert_plan(const uint64_t* __restrict__ recs, uint64_t n_rec, int rw,
         const uint64_t lo = (h >> 32) & 0xFFFFu, n = (h >> 48) & 63u, so = (h >> 54) & 63u;
         // the signature (so <= 56) ends inside the first two span words
         const uint32_t sm = (uint32_t)(span_window(ps[j][0], ps[j][1], 0ull, 0ull, (int)so) >> (64 - 2 * M));
-        const bool rev = sm < halfM;  // complement wins (binning.c:1029-1040)
+        const bool rev = routed_rev(h, sm, K, M);  // complement wins (binning.c:1029-1040)
         canon[j] = rev ? maskM - sm : sm;
         neg |= (int32_t)id < 0;
         kmers += n;
@@ -4483,8 +4484,9 @@ DEV void convert_plan(const uint64_t* __restrict__ recs, uint64_t n_rec, int rw,
     if (bucket_map) {
 #pragma unroll
         for (int j = 0; j < PERT; j++)
-            // (canon >= halfM by construction -- the larger of a code and its
-            // complement -- so the guard never hashes here; it bounds the index)
+            // (K >= 2M: canon >= halfM by construction, the larger of a code and
+            // its complement; K < 2M passes run without a map.  The guard bounds
+            // the index whatever a received record says)
             if (dst[j] != 0xFFFFFFFFu) me[j] = canon[j] >= halfM ? bucket_map[canon[j] - halfM] : 0u;
 #pragma unroll
         for (int j = 0; j < PERT; j++) {

@@ -298,9 +298,13 @@ int rank_route_body(kb_group* g, int i, int s) {
             GHIP(rk.regions[s].ensure((uint64_t)G * rk.cap * W));
             const int rc = kb_route_scatter(rk.send, (uint32_t)G, rk.regions[s].p, rk.cap, cnt);
             if (rc == KB_OK) {
+                // (the layout this call wrote: destination d at d * cap -- the
+                // headroom raised below is the NEXT unit's; raising it first
+                // pointed the exchange at the wrong records whenever a
+                // destination came within 10 % + 1024 of the old cap)
+                for (int d = 0; d < G; d++) off[d] = (uint64_t)d * rk.cap;
                 const uint64_t mx = *std::max_element(cnt, cnt + G);
                 rk.cap = std::max(rk.cap, mx + mx / 10 + 1024);
-                for (int d = 0; d < G; d++) off[d] = (uint64_t)d * rk.cap;
                 return KB_OK;
             }
             if (rc == KB_EINVAL) break;  // (the one-pass sender does not apply: plan/pack)

@@ -192,6 +192,17 @@ constexpr uint32_t BM_SPLIT = 0x80000000u;
 // route every map-less pass takes; no kernel indexes below the map
 // (the r5g38 fault's class).
 __host__ __device__ __forceinline__ bool bm_has_entry(uint32_t canon, int M) { return canon >= (1u << (2 * M - 1)); }
+
+// Routed super-k-mer record header: id | i0 << 32 | n << 48 | sig_off << 54 |
+// rev << 60.  rev is the complement flag (binning.c:1029-1040's is_rev).  For
+// K >= 2M it is a function of the span -- the signature's code is below half
+// exactly when the complement won -- and receivers rederive it; for K < 2M the
+// incremental branch (binning.c:992-1021) sets is_rev from scores polluted by
+// appended bases, so the sender's flag is the only source
+constexpr int ROUTED_REV_BIT = 60;
+__host__ __device__ __forceinline__ bool routed_rev(uint64_t h, uint32_t sm, int K, int M) {
+    return K < 2 * M ? ((h >> ROUTED_REV_BIT) & 1u) != 0 : sm < (1u << (2 * M - 1));
+}
 __device__ __forceinline__ uint32_t bm_depth(uint32_t e) { return (e & BM_SPLIT) ? (e >> 28) & 7u : 0u; }
 __device__ __forceinline__ uint32_t bm_bucket(uint32_t e, const uint16_t* sub_map, uint32_t sub) {
     return (e & BM_SPLIT) ? (uint32_t)sub_map[(e & 0x0FFFFFFFu) + sub] : (e & 1023u);
@@ -385,9 +396,9 @@ struct ListArgs {
 
 hipError_t launch_lists(const ListArgs& a, uint64_t max_entries, hipStream_t s);
 hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s);
-// received routed records (rw words: {id | i0 << 32 | n << 48 | sig_off << 54}, span words)
+// received routed records (rw words: {id | i0 << 32 | n << 48 | sig_off << 54 | rev << 60}, span words)
 // -> binned records at t = off + k; ids < 0 set ST_NEG_ID in *status
-hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint64_t off, int M,
+hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint64_t off, int M, int K,
                              uint64_t* pay, uint64_t* keys, uint32_t* status, unsigned long long* n_kmers,
                              hipStream_t s);
 // sender: destination of every record (owner of its mmer) -> dkeys = dest << 32 | t, counts[dest]

@@ -519,9 +519,12 @@ __global__ __launch_bounds__(256) void route_kernel(RouteArgs A) {
                 if (PACK && mine) {
                     const uint64_t pos = (uint64_t)(uint32_t)__shfl((int)run, (int)dest, 64);
                     uint64_t* rec = A.out + pos * (uint64_t)A.rec_words;
-                    if (lane == 0)
+                    if (lane == 0) {
+                        // (the complement flag, kbin_internal.h ROUTED_REV_BIT)
+                        const uint64_t rev = (uint32_t)(window64(sw, sig) >> (64 - 2 * M)) < halfM ? 1ull : 0ull;
                         rec[0] = (uint64_t)ordv | ((uint64_t)seg_lo << 32) | ((uint64_t)n << 48) |
-                                 ((uint64_t)(sig - seg_lo) << 54);
+                                 ((uint64_t)(sig - seg_lo) << 54) | (rev << ROUTED_REV_BIT);
+                    }
                     else if (lane < A.rec_words) {
                         const int p = seg_lo + 32 * (lane - 1);
                         rec[lane] = p < L ? window64(sw, p) : 0ull;

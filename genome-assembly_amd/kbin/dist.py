@@ -183,6 +183,7 @@ class ShardedBinner:
         self.last_times = {}
         self._regions = torch.empty(0, dtype=torch.int64, device=self.device)
         self._cap = 0
+        self._wcap = 0  # the region capacity of the last scatter (its layout)
         self.scatter = True  # one-pass sender while the engine accepts it
         # pipelined steps (send / receive): a sender context of its own and
         # two region buffers, so one unit's records can be in flight while
@@ -217,6 +218,9 @@ class ShardedBinner:
                 self.scatter = False
                 return None
             if ok:
+                # the layout this call wrote (destination d at d * cap) is the
+                # exchange's; the raised headroom is the next unit's
+                self._wcap = self._cap
                 self._cap = max(self._cap, int(int(counts.max()) * 1.1) + 1024)
                 return counts
             self._cap = int(int(counts.max()) * 1.2) + 1024  # retry once with room for all
@@ -245,7 +249,7 @@ class ShardedBinner:
         if counts is not None:  # one pass: records straight into destination regions
             t.append(time.perf_counter())
             t.append(t[-1])
-            recvs, rc = exchange_regions(self._regions, counts.tolist(), self._cap, self.rec_words,
+            recvs, rc = exchange_regions(self._regions, counts.tolist(), self._wcap, self.rec_words,
                                          self.group)
         else:  # plan / pack: destination-major, read order (any engine)
             counts = eng.route_plan(self.world)  # synchronises the engine stream
@@ -291,7 +295,7 @@ class ShardedBinner:
         counts = self._scatter(n_reads, engine=eng, slot=slot) if self.scatter else None
         if counts is not None:  # one pass: records straight into destination regions
             t1 = time.perf_counter()
-            recvs, rc, work = exchange_regions_async(self._pregions[slot], counts.tolist(), self._cap,
+            recvs, rc, work = exchange_regions_async(self._pregions[slot], counts.tolist(), self._wcap,
                                                      self.rec_words, self.group)
         else:  # plan / pack (table engine): destination-major, read order
             counts = eng.route_plan(self.world)

@@ -63,7 +63,11 @@ def encode(reads, ids, K: int, M: int, G: int):
     for read, rid in zip(reads, ids):
         v = [V[b] for b in read]
         for i0, n, so, cm in superkmers(read, K, M):
-            rec = [int(rid) | (i0 << 32) | (n << 48) | (so << 54)]
+            sm = 0
+            for b in v[i0 + so:i0 + so + M]:
+                sm = sm * 4 + b
+            rev = 1 if sm < (1 << (2 * M - 1)) else 0  # the complement flag (kbin_internal.h ROUTED_REV_BIT)
+            rec = [int(rid) | (i0 << 32) | (n << 48) | (so << 54) | (rev << 60)]
             for w in range(rw - 1):
                 p = i0 + 32 * w
                 rec.append(_word(v, p) if p < len(v) else 0)
