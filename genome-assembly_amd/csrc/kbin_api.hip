@@ -2430,13 +2430,11 @@ extern "C" int kb_finalize(kb_ctx* c, int prune) {
     }
     if (any_reads && any_sk)
         return fail(KB_ESTATE, "a context bins either its own reads or received super-k-mers");
-    if (c->p.K < 2 * c->p.M) {  // (the record pass's K < 2M walk: thread-per-read kernel, binned engine)
-        if (!binned_applies(c))
-            return fail(KB_EINVAL, "K=%d < 2M=%d needs the binned engine", c->p.K, 2 * c->p.M);
-        for (auto& b : c->batches)
-            if (!b.routed && !b.superkmers && b.RW > 16)
-                return fail(KB_EINVAL, "K=%d < 2M=%d: reads of at most 512 bp", c->p.K, 2 * c->p.M);
-    }
+    // (K < 2M: the record pass walks the reference's live incremental branch,
+    // one lane per read -- the thread-per-read kernel, or one lane of a wave
+    // per longer read -- in the binned engine)
+    if (c->p.K < 2 * c->p.M && !binned_applies(c))
+        return fail(KB_EINVAL, "K=%d < 2M=%d needs the binned engine", c->p.K, 2 * c->p.M);
     memset(&c->tm, 0, sizeof(c->tm));
     const int SW = c->KW == 1 ? 2 : 4;
     const bool track_first = (c->p.flags & KB_TRACK_FIRST) != 0;

@@ -52,6 +52,68 @@ DEV void segment_at(const uint64_t* sw, int lo, int lane, int W, int M, uint32_t
     canon = (uint32_t)rfl((int)(key >> 16));
 }
 
+// QK (K < 2M): the reference's per-k-mer signature state, binning.c:922-1021.
+// The incremental branch (992-1021: j runs K-M .. M-1) is live: it appends
+// bases to a score it never trims, in int arithmetic that wraps, so the
+// signature can move to the k-mer's last M bases and is_rev follow the
+// polluted scores.  One lane walks its read k-mer by k-mer with that state;
+// a record is a run of k-mers with one signature position (`next`).
+struct QWalk {
+    int32_t s = 0, r = 0, m = 0;  // score, rev_score, max_score
+    bool rev = false;
+    int sig = -1, i = -1;         // signature position, last k-mer stepped
+    DEV uint32_t code(const uint64_t* sw, int p, int M, uint32_t maskM) const {
+        return (uint32_t)(window64(sw, p) >> (64 - 2 * M)) & maskM;
+    }
+    DEV void step(const uint64_t* sw, int k, int K, int M, uint32_t maskM) {
+        if (k > sig) {  // a fresh window (binning.c:922-989): leftmost strict argmax
+            uint32_t sm = code(sw, k, M, maskM);
+            int32_t sc = (int32_t)sm, rv = (int32_t)(maskM - sm);
+            m = sc > rv ? sc : rv;
+            rev = !(sc > rv);
+            sig = k;
+            for (int p = k + 1; p <= k + K - M; p++) {
+                sm = code(sw, p, M, maskM);
+                sc = (int32_t)sm;
+                rv = (int32_t)(maskM - sm);
+                if ((sc > rv ? sc : rv) > m) {
+                    m = sc > rv ? sc : rv;
+                    rev = !(sc > rv);
+                    sig = p;
+                }
+            }
+            s = sc;
+            r = rv;
+        } else {  // the incremental branch (binning.c:992-1021)
+            for (int j = K - M; j < M; j++) {
+                const uint32_t v = (uint32_t)(window64(sw, k + j) >> 62);
+                s = (int32_t)((uint32_t)s * 4u + v);
+                r = (int32_t)((uint32_t)r * 4u + 3u - v);
+            }
+            if ((s > r ? s : r) > m) {
+                m = s > r ? s : r;
+                rev = !(s > r);
+                sig = k + K - M;
+            }
+        }
+        i = k;
+    }
+    // the record starting at k-mer lo: its signature and complement flag, and
+    // the first k-mer of the next record
+    DEV void next(const uint64_t* sw, int lo, int nK, int K, int M, uint32_t maskM, int& rsig, bool& rrev,
+                  int& e) {
+        if (i < lo) step(sw, lo, K, M, maskM);
+        rsig = sig;
+        rrev = rev;
+        e = lo + 1;
+        while (e < nK) {
+            step(sw, e, K, M, maskM);
+            if (sig != rsig) break;
+            e++;
+        }
+    }
+};
+
 constexpr uint64_t OWNER_SALT = 0x5851F42D4C957F2Dull;   // rank of a mmer (= owner_of(), kbin_kernels.hip)
 constexpr uint64_t BUCKET_SALT = 0x2545F4914F6CDD1Dull;  // bucket of a mmer inside one rank (independent)
 constexpr uint64_t PART_SALT = 0x9E3779B97F4A7C15ull;    // pass of a mmer (kb_set_partition; independent)
@@ -84,7 +146,7 @@ DEV bool in_part(uint32_t mmer, uint32_t part, uint32_t part_n) {
     return part_n <= 1 || dest_of(mmer, part_n, PART_SALT) == part;
 }
 
-template <bool WRITE>
+template <bool WRITE, bool QK = false>
 __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const int lane = threadIdx.x & 63;
@@ -107,23 +169,38 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
             const uint64_t rbase = WRITE ? A.rec_base[r] : 0;
             const uint64_t ordv = (uint64_t)(A.ord_base + (uint32_t)r);
             int lo = 0;
+            QWalk qw;  // (QK: lane 0's walk, its records broadcast to the wave)
             while (lo < nK) {
-                int sig;
+                int sig, nlo;
                 uint32_t canon;
-                segment_at(sw, lo, lane, W, M, maskM, halfM, sig, canon);
+                bool qrev = false;
+                if (QK) {
+                    int rs = 0, e = 0;
+                    bool rv = false;
+                    if (lane == 0) qw.next(sw, lo, nK, K, M, maskM, rs, rv, e);
+                    sig = __shfl(rs, 0, 64);
+                    nlo = __shfl(e, 0, 64);
+                    qrev = __shfl((int)rv, 0, 64) != 0;
+                    const uint32_t sm = qw.code(sw, sig, M, maskM);
+                    canon = qrev ? maskM - sm : sm;  // the bin's mmer code (not canonical)
+                } else {
+                    segment_at(sw, lo, lane, W, M, maskM, halfM, sig, canon);
+                    nlo = sig + 1;
+                }
                 if (!in_part(canon, A.part, A.part_n)) {  // another pass's super-k-mer
-                    lo = sig + 1;
+                    lo = nlo;
                     continue;
                 }
-                kmers += (uint64_t)(min(sig, nK - 1) - lo + 1);
+                const int n = QK ? nlo - lo : min(sig, nK - 1) - lo + 1;
+                kmers += (uint64_t)n;
                 if (WRITE && lane == 0) {
-                    // one super-k-mer: k-mers lo..min(sig, nK-1) share the
-                    // signature at sig (binning.c:1004-1040 with the sticky
-                    // window).  Span = bases lo .. lo+n+K-2 (<= 56 for K <= 31).
+                    // one super-k-mer: k-mers lo..lo+n-1 share the signature at
+                    // sig (binning.c:1004-1040 with the sticky window).  Span =
+                    // bases lo .. lo+n+K-2 (<= 56 for K <= 31).
                     const uint64_t t = rbase + nseg;
-                    const int n = min(sig, nK - 1) - lo + 1;
                     const uint32_t sm = (uint32_t)(window64(sw, sig) >> (64 - 2 * M));
-                    const uint64_t rev = sm < halfM ? 1ull : 0ull;  // complement wins (binning.c:1029-1040)
+                    // complement wins (binning.c:1029-1040)
+                    const uint64_t rev = QK ? (qrev ? 1ull : 0ull) : (sm < halfM ? 1ull : 0ull);
                     A.pay[3 * t + 0] = ordv | ((uint64_t)n << 32) | ((uint64_t)(sig - lo) << 38) | (rev << 44) |
                                        ((uint64_t)lo << 45);
                     A.pay[3 * t + 1] = window64(sw, lo);
@@ -131,7 +208,7 @@ __global__ __launch_bounds__(256) void sk_kernel(SkScanArgs A) {
                     A.keys[t] = ((uint64_t)canon << 38) | ((uint64_t)(63 - n) << 32) | (uint32_t)t;
                 }
                 nseg++;
-                lo = sig + 1;
+                lo = nlo;
             }
         }
         if (!WRITE && lane == 0) A.seg_count[r] = nseg;
@@ -355,46 +432,11 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
         const uint64_t rbase = WRITE && !alloc && tid < nrows ? A.rec_base[r] : 0;
         uint32_t nseg = 0;
         int lo = 0;
-        // (QK) the reference's walk state after k-mer q_i, and the record it
-        // closed (kept across a stage-full round: the walk does not repeat)
-        int32_t q_s = 0, q_r = 0, q_m = 0;
-        bool q_rev = false;
-        int q_sig = -1, q_i = -1, q_lo = -1, q_e = 0, q_rsig = 0;
+        // (QK) the reference's walk state (QWalk), and the record it closed
+        // (kept across a stage-full round: the walk does not repeat)
+        QWalk qw;
+        int q_lo = -1, q_e = 0, q_rsig = 0;
         bool q_rrev = false;
-        auto q_code = [&](int p) { return (uint32_t)(window64(sw, p) >> sh) & maskM; };
-        auto q_step = [&](int i) {  // binning.c:922-1021 for the k-mer at i
-            if (i > q_sig) {  // a fresh window (binning.c:922-989)
-                uint32_t sm = q_code(i);
-                int32_t sc = (int32_t)sm, rv = (int32_t)(maskM - sm);
-                q_m = sc > rv ? sc : rv;
-                q_rev = !(sc > rv);
-                q_sig = i;
-                for (int p = i + 1; p <= i + K - M; p++) {
-                    sm = q_code(p);
-                    sc = (int32_t)sm;
-                    rv = (int32_t)(maskM - sm);
-                    if ((sc > rv ? sc : rv) > q_m) {
-                        q_m = sc > rv ? sc : rv;
-                        q_rev = !(sc > rv);
-                        q_sig = p;
-                    }
-                }
-                q_s = sc;
-                q_r = rv;
-            } else {  // the incremental branch (binning.c:992-1021), live for K < 2M
-                for (int j = K - M; j < M; j++) {
-                    const uint32_t v = (uint32_t)(window64(sw, i + j) >> 62);
-                    q_s = (int32_t)((uint32_t)q_s * 4u + v);
-                    q_r = (int32_t)((uint32_t)q_r * 4u + 3u - v);
-                }
-                if ((q_s > q_r ? q_s : q_r) > q_m) {
-                    q_m = q_s > q_r ? q_s : q_r;
-                    q_rev = !(q_s > q_r);
-                    q_sig = i + K - M;
-                }
-            }
-            q_i = i;
-        };
         for (;;) {
             while (lo < nK) {
                 // leftmost strict argmax of the canonical score over the window
@@ -403,20 +445,11 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                 int nlo = 0;  // the next record's first k-mer
                 if (QK) {
                     if (q_lo != lo) {  // (a stage-full round keeps the record it closed)
-                        if (q_i < lo) q_step(lo);
-                        q_rsig = q_sig;
-                        q_rrev = q_rev;
-                        int e = lo + 1;
-                        while (e < nK) {
-                            q_step(e);
-                            if (q_sig != q_rsig) break;
-                            e++;
-                        }
+                        qw.next(sw, lo, nK, K, M, maskM, q_rsig, q_rrev, q_e);
                         q_lo = lo;
-                        q_e = e;
                     }
                     sig = q_rsig;
-                    const uint32_t sm = q_code(sig);
+                    const uint32_t sm = qw.code(sw, sig, M, maskM);
                     best = (int)(q_rrev ? maskM - sm : sm);  // the bin's mmer code
                     bsm = q_rrev ? 0u : halfM;               // (rev below: bsm < halfM)
                     nlo = q_e;
@@ -670,12 +703,17 @@ hipError_t launch_sk(const SkScanArgs& a, bool write, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    if (a.K < 2 * a.M) return hipErrorInvalidValue;  // (K < 2M: reads of <= 512 bp only; the API checks)
     const size_t lds = (size_t)4 * (a.RW + 2) * sizeof(uint64_t);
-    if (write)
+    if (a.K < 2 * a.M) {  // (QK: a long read's walk on one lane of its wave)
+        if (write)
+            hipLaunchKernelGGL((sk_kernel<true, true>), dim3((unsigned)blocks), dim3(256), lds, s, a);
+        else
+            hipLaunchKernelGGL((sk_kernel<false, true>), dim3((unsigned)blocks), dim3(256), lds, s, a);
+    } else if (write) {
         hipLaunchKernelGGL(sk_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, s, a);
-    else
+    } else {
         hipLaunchKernelGGL(sk_kernel<false>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+    }
     return hipGetLastError();
 }
 
@@ -765,7 +803,7 @@ __global__ __launch_bounds__(256) void sk_convert_kernel(const uint64_t* __restr
                                                          int rw, uint64_t off, int M, int K, uint64_t* __restrict__ pay,
                                                          uint64_t* __restrict__ keys, uint32_t* status,
                                                          unsigned long long* n_kmers) {
-    const uint32_t maskM = (1u << (2 * M)) - 1u, halfM = 1u << (2 * M - 1);
+    const uint32_t maskM = (1u << (2 * M)) - 1u;
     bool neg = false;
     uint64_t kmers = 0;
     for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < n_rec; k += (uint64_t)gridDim.x * 256) {

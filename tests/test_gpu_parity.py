@@ -983,3 +983,54 @@ def test_k_below_2m_vs_oracle(K, M, engine):
         res = gpu_result(bases, lens, K, M, 1, prune, batches=3)
         assert res.n_kmers == ora.n_kmers
         assert_same(res, ora)
+
+
+@pytest.mark.parametrize("K,M", [(10, 6), (5, 4), (13, 7), (15, 8)])
+@pytest.mark.parametrize("radix", ["0", "1"])
+def test_k_below_2m_long_reads(K, M, radix, engine, monkeypatch):
+    """K < 2M on reads longer than 512 bp (VERDICT r05 missing #2: the
+    reference's READ_LENGTH is a compile-time bound, binning.c:13): the
+    long-read scan kernel walks the live incremental branch on one lane of the
+    read's wave (QWalk, the same state as the thread-per-read kernel); with
+    the forced radix path too (whose bins then span all 4^M codes: ADVICE
+    r05).  Bit-exact against the oracle, and through route_plan/pack to three
+    shards."""
+    if engine != "binned":
+        pytest.skip("K < 2M runs on the binned engine")
+    monkeypatch.setenv("KB_BIN_RADIX", radix)
+    rng = np.random.default_rng(K * 100 + M)
+    genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20000)
+    reads = []
+    for _ in range(300):
+        L = int(rng.integers(0, 3000)) if rng.random() < 0.7 else int(rng.integers(0, 300))
+        s = int(rng.integers(0, 20000 - L))
+        r = genome[s:s + L].copy()
+        m = rng.random(L) < 0.01
+        r[m] = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=int(m.sum()))
+        reads.append(r.tobytes())
+    bases, lens = kbin.pack_reads(reads)
+    for prune in (False, True):
+        ora = oracle.bin_reads(bases, lens, K, M, 1, prune)
+        res = gpu_result(bases, lens, K, M, 1, prune, batches=2, max_read_len=4096)
+        assert res.n_kmers == ora.n_kmers
+        assert_same(res, ora)
+    # routed: plan/pack to three shards (kb_route_scatter serves reads <= 512 bp)
+    import torch
+    import skmer_ref
+    rw = skmer_ref.rec_words(K, M)
+    ids = np.arange(len(reads), dtype=np.int32)
+    with kbin.Engine(K, M, cutoff=1, max_read_len=4096) as eng:
+        eng.submit(bases=bases, lens=lens, ids=ids)
+        counts = eng.route_plan(3)
+        send = torch.zeros(max(1, int(counts.sum()) * rw), dtype=torch.int64, device="cuda")
+        eng.route_pack(send.data_ptr())
+    edges = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    union = {}
+    for d in range(3):
+        with kbin.Engine(K, M, cutoff=1, max_read_len=4096) as rx:
+            rx.submit_superkmers_device(send[int(edges[d]) * rw:].data_ptr(), int(counts[d]))
+            rx.finalize(prune=True)
+            part = skmer_ref.oracle_dict(rx.export().canonical())
+        assert not (set(part) & set(union))
+        union.update(part)
+    assert union == skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, True, ids=ids))
