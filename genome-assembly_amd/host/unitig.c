@@ -56,11 +56,13 @@
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE
 #endif
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "../../include/binning_gpu.h"
 
@@ -328,6 +330,181 @@ static void ut_reset(void)
     memset(&U, 0, sizeof U);
 }
 
+/* ---- the initial index, built by worker threads (the tables are read-only
+ * here): entries per table counted, then filled at their offsets (codes,
+ * positions), then the pointer map and the two candidate maps filled
+ * lock-free (compare-and-swap on a slot; every key distinct) ---- */
+
+typedef struct {
+    uint32_t *cnt;   /* [ntab] entries per table, then offsets */
+    uint32_t n_work, next;
+    int phase;       /* 0 count, 1 fill, 2 pointer map, 3 candidate maps */
+    uint64_t used_pre, used_suf;
+    int general;
+} ut_job;
+
+static long ut_threads(void)
+{
+    long nt = sysconf(_SC_NPROCESSORS_ONLN);
+    const char *env = getenv("KBH_THREADS");
+    if (env && atol(env) > 0) nt = atol(env);
+    if (nt < 1) nt = 1;
+    return nt > 16 ? 16 : nt;
+}
+
+/* push entry i onto map's chain of its (table, code), lock-free */
+static int ut_cmap_push(uint32_t *map, int pre, uint32_t i)
+{
+    ut_ent *x = &U.ent[i];
+    const u128 code = pre ? x->pre : x->suf;
+    uint64_t s = ut_chash(x->tab, code) & (U.ccap - 1);
+    for (;;) {
+        uint32_t h = __atomic_load_n(&map[s], __ATOMIC_ACQUIRE);
+        if (h == NONE) {
+            if (pre) x->npre = NONE; else x->nsuf = NONE;
+            if (__atomic_compare_exchange_n(&map[s], &h, i, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) return 1;
+            continue; /* (someone took the slot: look again) */
+        }
+        const ut_ent *y = &U.ent[h];
+        if (y->tab == x->tab && (pre ? y->pre : y->suf) == code) {
+            if (pre) x->npre = h; else x->nsuf = h;
+            if (__atomic_compare_exchange_n(&map[s], &h, i, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) return 0;
+            continue;
+        }
+        s = (s + 1) & (U.ccap - 1);
+    }
+}
+
+static void *ut_index_worker(void *arg)
+{
+    ut_job *j = arg;
+    uint64_t up = 0, us = 0;
+    int general = 0;
+    const int o = U.K - 1;
+    const uint32_t CH = 4096; /* (entries per work item in phases 2-3) */
+    for (;;) {
+        const uint32_t w = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+        if (w >= j->n_work) break;
+        if (j->phase <= 1) {
+            struct ZHashTable *T = U.tabs[w];
+            if (!T) continue;
+            const size_t m2 = UT_LADDER[T->size_index];
+            uint32_t k = j->phase ? j->cnt[w] : 0;
+            for (size_t b = 0; b < m2; b++) {
+                int64_t p = 0;
+                for (struct ZHashEntry *ke = T->entries[b]; ke; ke = ke->next, p++, k++) {
+                    if (!j->phase) continue;
+                    ut_ent *x = &U.ent[k];
+                    memset(x, 0, sizeof *x);
+                    x->e = ke;
+                    x->tab = w;
+                    x->bucket = (uint32_t)b;
+                    x->seq = p;
+                    x->live = 1;
+                    x->npre = x->nsuf = NONE;
+                    const char *key = ke->key;
+                    const size_t len = strlen(key);
+                    x->klen = (uint32_t)len;
+                    for (size_t c = 0; c < len && !general; c++) general |= !ut_acgt(key[c]);
+                    if (len >= (size_t)o) {
+                        x->pre = ut_code(key, o);
+                        x->suf = ut_code(key + len - o, o);
+                        x->indexed = 1;
+                    }
+                }
+            }
+            if (!j->phase) j->cnt[w] = k;
+        } else {
+            const uint32_t a = w * CH, e = a + CH < U.n ? a + CH : U.n;
+            for (uint32_t i = a; i < e; i++) {
+                if (j->phase == 2) {
+                    const uintptr_t key = (uintptr_t)U.ent[i].e;
+                    uint64_t s = ut_mix(key) & (U.pcap - 1);
+                    for (;;) {
+                        uintptr_t cur = 0;
+                        if (__atomic_compare_exchange_n(&U.pk[s], &cur, key, 0, __ATOMIC_ACQ_REL,
+                                                        __ATOMIC_ACQUIRE)) {
+                            U.pv[s] = i;
+                            break;
+                        }
+                        s = (s + 1) & (U.pcap - 1);
+                    }
+                } else if (U.ent[i].indexed) {
+                    up += (uint64_t)ut_cmap_push(U.cpre, 1, i);
+                    us += (uint64_t)ut_cmap_push(U.csuf, 0, i);
+                }
+            }
+        }
+    }
+    __atomic_fetch_add(&j->used_pre, up, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&j->used_suf, us, __ATOMIC_RELAXED);
+    if (general) __atomic_store_n(&j->general, 1, __ATOMIC_RELAXED);
+    return NULL;
+}
+
+static void ut_run(ut_job *j, int phase, uint32_t n_work)
+{
+    j->phase = phase;
+    j->next = 0;
+    j->n_work = n_work;
+    long nt = ut_threads();
+    if ((uint64_t)nt > n_work) nt = n_work ? (long)n_work : 1;
+    pthread_t th[16];
+    int started[16] = {0};
+    for (long t = 1; t < nt; t++) started[t] = pthread_create(&th[t], NULL, ut_index_worker, j) == 0;
+    ut_index_worker(j);
+    for (long t = 1; t < nt; t++)
+        if (started[t]) pthread_join(th[t], NULL);
+}
+
+static void ut_index_tables(void)
+{
+    ut_job j;
+    memset(&j, 0, sizeof j);
+    j.cnt = ut_alloc(((size_t)U.ntab + 1) * sizeof(uint32_t));
+    ut_run(&j, 0, U.ntab);
+    uint64_t tot = 0;
+    for (uint32_t t = 0; t < U.ntab; t++) {
+        const uint32_t c = j.cnt[t];
+        j.cnt[t] = (uint32_t)tot;
+        tot += c;
+    }
+    if (tot >= NONE) ut_fail("more than 2^32 entries");
+    if (tot + 4096 > U.cap) {
+        U.cap = (uint32_t)(tot + tot / 4 + 4096);
+        U.ent = realloc(U.ent, (size_t)U.cap * sizeof(ut_ent));
+        if (!U.ent) exit(EXIT_FAILURE);
+    }
+    ut_run(&j, 1, U.ntab);
+    U.n = (uint32_t)tot;
+    if (j.general) U.general = 1;
+    /* pointer map and candidate maps at <= 1/2 load (new entries grow them) */
+    uint64_t pc = 1024;
+    while (pc < 2 * ((uint64_t)U.n + U.n / 4 + 1)) pc *= 2;
+    if (pc > U.pcap) {
+        free(U.pk);
+        free(U.pv);
+        U.pcap = pc;
+        U.pk = calloc(U.pcap, sizeof *U.pk);
+        U.pv = ut_alloc(U.pcap * sizeof *U.pv);
+        if (!U.pk) exit(EXIT_FAILURE);
+    }
+    U.pused = U.n;
+    const uint32_t chunks = (U.n + 4095) / 4096;
+    ut_run(&j, 2, chunks);
+    U.ccap = pc;
+    free(U.cpre);
+    free(U.csuf);
+    U.cpre = ut_alloc(U.ccap * sizeof(uint32_t));
+    U.csuf = ut_alloc(U.ccap * sizeof(uint32_t));
+    memset(U.cpre, 0xff, U.ccap * sizeof(uint32_t));
+    memset(U.csuf, 0xff, U.ccap * sizeof(uint32_t));
+    ut_run(&j, 3, chunks);
+    U.cused_pre = j.used_pre;
+    U.cused_suf = j.used_suf;
+    free(j.cnt);
+}
+
 /* index every level-2 entry of level1 (the first call on a table set) */
 static void ut_build(struct ZHashTable *level1, int K, int M)
 {
@@ -368,18 +545,7 @@ static void ut_build(struct ZHashTable *level1, int K, int M)
             U.tab_val[U.ntab] = v;
             U.ntab++;
         }
-    for (uint32_t t = 0; t < U.ntab; t++) {
-        struct ZHashTable *T = U.tabs[t];
-        if (!T) continue;
-        const size_t m2 = UT_LADDER[T->size_index];
-        for (size_t b = 0; b < m2; b++) {
-            int64_t p = 0;
-            for (struct ZHashEntry *ke = T->entries[b]; ke; ke = ke->next) ut_add(ke, t, (uint32_t)b, p++);
-        }
-    }
-    uint64_t cap = 1024;
-    while (cap < 2 * ((uint64_t)U.n + U.n / 4 + 1)) cap *= 2;
-    ut_cmap_rebuild(cap);
+    ut_index_tables();
 }
 
 /* the table of mmer string s (zhash_get(hash_table, compare_mmer), :514) */
