@@ -377,6 +377,12 @@ __device__ unsigned long long g_sk_prof[8];
 #else
 #define SKPROF(ph) do {} while (0)
 #endif
+// a value the compiler must keep in a VGPR and cannot see through
+DEV uint32_t vreg(uint32_t v) {
+    asm("" : "+v"(v));
+    return v;
+}
+
 // QK (K < 2M): the reference's incremental branch is live (binning.c:992-1021:
 // j runs K-M .. M-1, appending bases to a score it never trims, in int
 // arithmetic that wraps).  Each lane then walks its read k-mer by k-mer with
@@ -457,15 +463,41 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
                     // K <= 31: the window's W mmers all lie in the 64-bit word at
                     // lo, so each score is one shift of it (no shifting chain),
                     // and the argmax is a max over (score << 8 | 255 - offset):
-                    // larger score first, then the leftmost position
+                    // larger score first, then the leftmost position.  In
+                    // 32-bit halves: position i's mmer sits at bit sh - 2i,
+                    // inside the high half for i < 17 - M, across both for
+                    // i < 16, in the low half after -- one bit-field extract
+                    // (two across), and both orientations' keys in one max3
+                    // (the complement's key is the forward key ^ maskM << 8)
                     const uint64_t x = window64(sw, lo);
+                    const uint32_t xh = (uint32_t)(x >> 32), xl = (uint32_t)x;
+                    // (loop constants held in VGPRs: a VOP3 reads one SGPR on gfx9)
+                    const uint32_t xc = vreg(maskM << 8), w2 = vreg(2u * (uint32_t)M);
+                    const int e1 = min(W, 17 - M), e2 = min(W, 16);
                     uint32_t bk = 0;
-#pragma unroll 5
-                    for (int i = 0; i < W; i++) {
-                        const uint32_t sm = (uint32_t)(x >> (sh - 2 * i)) & maskM;
-                        const uint32_t c = max(sm, sm ^ maskM);  // (maskM - sm = sm ^ maskM)
-                        bk = max(bk, (c << 8) | (uint32_t)(255 - i));
-                    }
+                    const auto hi_at = [&](int p) {
+                        const uint32_t k =
+                            vreg((__builtin_amdgcn_ubfe(xh, (uint32_t)(sh - 32 - 2 * p), w2) << 8) | (uint32_t)(255 - p));
+                        bk = max(max(bk, k), k ^ xc);
+                    };
+                    const auto mid_at = [&](int p) {
+                        const uint32_t k = vreg(((__builtin_amdgcn_alignbit(xh, xl, (uint32_t)(sh - 2 * p)) & maskM) << 8) |
+                                                (uint32_t)(255 - p));
+                        bk = max(max(bk, k), k ^ xc);
+                    };
+                    const auto lo_at = [&](int p) {
+                        const uint32_t k =
+                            vreg((__builtin_amdgcn_ubfe(xl, (uint32_t)(sh - 2 * p), w2) << 8) | (uint32_t)(255 - p));
+                        bk = max(max(bk, k), k ^ xc);
+                    };
+                    // (unrolled by hand: the loop bounds are uniform but not constant)
+                    int p = 0;
+                    for (; p + 2 <= e1; p += 2) hi_at(p), hi_at(p + 1);
+                    if (p < e1) hi_at(p++);
+                    for (; p + 2 <= e2; p += 2) mid_at(p), mid_at(p + 1);
+                    if (p < e2) mid_at(p++);
+                    for (; p + 3 <= W; p += 3) lo_at(p), lo_at(p + 1), lo_at(p + 2);
+                    for (; p < W; p++) lo_at(p);
                     const int i = 255 - (int)(bk & 255u);
                     sig = lo + i;
                     best = (int)(bk >> 8);
