@@ -477,7 +477,11 @@ def routed_runner(K, M, L, cutoff, n, wpr, P, local, rank, reads, pass_log, pipe
     together with every other rank's, P mmer-partitioned passes a step.
     Returns (runner, engine, step, drain)."""
     from kbin import dist as kdist
-    runner = kdist.ShardedBinner(K, M, cutoff, L, device=local, group=None)
+    # (KB_ROUTED_TRANSPORT=c|torch: the exchange's transport; default the C
+    # group under nccl, torch collectives under gloo -- a gloo rehearsal of
+    # the C group's plumbing sets c)
+    runner = kdist.ShardedBinner(K, M, cutoff, L, device=local, group=None,
+                                 transport=os.environ.get("KB_ROUTED_TRANSPORT") or None)
     eng = runner.engine
     pending = []  # pipelined: the next unit, already scattered, its records in flight
 
@@ -641,6 +645,9 @@ def main():
     ap.add_argument("--no-capacity", dest="capacity", action="store_false",
                     help="N=1: skip the C3 capacity leg (100M x 150 bp in 4 passes, digest-checked; on by "
                          "default)")
+    ap.add_argument("--multi-legs", action="store_true",
+                    help="N=1 with --routed: run the N > 1 run's C4 and C5 legs through the one-rank group "
+                         "(a full-size rehearsal of their memory and time)")
     ap.add_argument("--dropin", action="store_true",
                     help="N=1: also time the reference surface (kbin_main: fgets + process_read loop, "
                          "prune_data with materialised zhash tables) on the workload's reads")
@@ -880,7 +887,8 @@ def main():
                    "engine": {1: "table", 2: "binned"}.get(int(tim[-1]["engine"]), "?"),
                    "bins": int(tim[-1]["n_bins"]), "superkmers": int(tim[-1]["n_superkmers"])},
     }
-    if world > 1 and args.capacity and args.workload == "c2":
+    legs = (world > 1 or (args.routed and args.multi_legs)) and args.capacity and args.workload == "c2"
+    if legs:
         # BASELINE's multi-GPU configurations as specified (the headline stays
         # C2 weak scaling: the same per-GPU work at every N); the main leg's
         # contexts and read sets go first
@@ -892,13 +900,13 @@ def main():
             out["capacity"][name] = multi_capacity_leg(name, rank, world, local, dist, backend, scale=scale)
             if rank == 0:
                 print(json.dumps({name: out["capacity"][name]}), file=sys.stderr, flush=True)
-    if world == 1 and args.host_input and P == 1:
+    if world == 1 and args.host_input and P == 1 and not legs:
         out["host_input"] = host_input_leg(sets[0][0], sets[0][1], n, wpr, L, K, M, args.cutoff, local)
     if world == 1 and args.capacity and args.workload == "c2" and not args.routed:
         out["capacity"] = capacity_leg(local)
-    if rank == 0 and world == 1 and args.dropin and P == 1:
+    if rank == 0 and world == 1 and args.dropin and P == 1 and not legs:
         out["dropin"] = dropin_leg(sets[0][0], sets[0][1], n, wpr, L, K, M, args.cutoff, local)
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and not legs:
         out["cpu_baseline"] = cpu_baseline(sets[0][0], sets[0][1], n, min(args.cpu_sample, n), wpr, L, K, M,
                                            args.cutoff, args.ref_sample)
     if rank == 0:

@@ -1740,8 +1740,9 @@ static int binned_buckets(kb_ctx* c, uint32_t NB, bool received, bool zeroed, ui
         // expected, scaled to this pass's records): relearn it after this pass
         if (bm && R && bm->want_tot &&
             (double)mx > 1.5 * (double)bm->want_max * (double)R / (double)bm->want_tot + 64.0) {
-            KB_DBG("map stale: bucket %llu vs expected %.0f\n", (unsigned long long)mx,
-                   (double)bm->want_max * (double)R / (double)bm->want_tot);
+            KB_DBG("map stale: bucket %llu vs expected %.0f (records %llu, k-mers %llu)\n", (unsigned long long)mx,
+                   (double)bm->want_max * (double)R / (double)bm->want_tot, (unsigned long long)R,
+                   (unsigned long long)N);
             bm->stale = true;
         }
         if (use_base || mx <= cap) {

@@ -384,6 +384,11 @@ int exchange_counts(kb_group* g, Unit& un) {
     return KB_OK;
 }
 
+static uint64_t genv_u64(const char* k, uint64_t d) {
+    const char* v = getenv(k);
+    return v && *v ? strtoull(v, nullptr, 0) : d;
+}
+
 // the records: rank s's region for d -> rank d's receive slot, sources in
 // rank order (received records concatenated by source rank)
 int exchange_records(kb_group* g, Unit& un, int s) {
@@ -449,16 +454,52 @@ int exchange_records(kb_group* g, Unit& un, int s) {
         // (the staging is reused by the next unit: the copy completes first)
         GHIP(hipStreamSynchronize(rk.xs));
     } else {
+        // A rank's own records are a device copy.  Peer messages go in pieces
+        // of at most XCHUNK words, matched in order on both sides: a one-rank
+        // RCCL group's self send/recv of C4's pass (6 GB at 125 M reads)
+        // delivered only about half of its records, the rest of the receive
+        // slot left as it was -- every such record then read as a zero-length
+        // TTTTTTT super-k-mer (one bucket of 129 M records, KB_ENOMEM)
+        const uint64_t XCHUNK = genv_u64("KB_GROUP_CHUNK", 1ull << 25);  // 256 MB of records (words per piece)
+        const bool self_rccl = genv_u64("KB_GROUP_SELF_RCCL", 0) != 0;  // (tests: the self copy by RCCL)
+        const auto pieces = [&](uint64_t n, const auto& f) -> int {
+            for (uint64_t o = 0; o < n;) {
+                const uint64_t c = XCHUNK ? std::min<uint64_t>(n - o, XCHUNK) : n - o;
+                if (const int rc = f(o, c)) return rc;
+                o += c;
+            }
+            return KB_OK;
+        };
+        for (auto& rk : g->r) {
+            const uint64_t n = un.C[(size_t)rk.grank * G + rk.grank];
+            uint64_t off = 0;
+            for (int src = 0; src < rk.grank; src++) off += un.C[(size_t)src * G + rk.grank];
+            if (n && !self_rccl) {
+                GHIP(hipSetDevice(rk.dev));
+                GHIP(hipMemcpyAsync(rk.rbuf[s].p + off * W, rk.regions[s].p + rk.soff[s][rk.grank] * W,
+                                    n * W * sizeof(uint64_t), hipMemcpyDeviceToDevice, rk.xs));
+            }
+        }
         Rccl& R = rccl();
         GNCCL(R.GroupStart());
         for (auto& rk : g->r) {
             uint64_t off = 0;
             for (int peer = 0; peer < G; peer++) {
                 const uint64_t ns = un.C[(size_t)rk.grank * G + peer], nr = un.C[(size_t)peer * G + rk.grank];
-                if (ns)
-                    GNCCL(R.Send(rk.regions[s].p + rk.soff[s][peer] * W, (size_t)(ns * W), ncclUint64, peer,
-                                 rk.comm, rk.xs));
-                if (nr) GNCCL(R.Recv(rk.rbuf[s].p + off * W, (size_t)(nr * W), ncclUint64, peer, rk.comm, rk.xs));
+                if (peer != rk.grank || self_rccl) {
+                    const uint64_t* sp = rk.regions[s].p + rk.soff[s][peer] * W;
+                    uint64_t* rp = rk.rbuf[s].p + off * W;
+                    const int rc = pieces(ns * W, [&](uint64_t o, uint64_t c) -> int {
+                        GNCCL(R.Send(sp + o, (size_t)c, ncclUint64, peer, rk.comm, rk.xs));
+                        return KB_OK;
+                    });
+                    if (rc) return rc;
+                    const int rc2 = pieces(nr * W, [&](uint64_t o, uint64_t c) -> int {
+                        GNCCL(R.Recv(rp + o, (size_t)c, ncclUint64, peer, rk.comm, rk.xs));
+                        return KB_OK;
+                    });
+                    if (rc2) return rc2;
+                }
                 off += nr;
             }
         }
@@ -777,6 +818,9 @@ extern "C" int kb_group_receive(kb_group* g, int prune) {
         GHIP(hipStreamWaitEvent((hipStream_t)kb_stream(rk.recv), rk.landed[s], 0));
         uint64_t tot = 0;
         for (int src = 0; src < G; src++) tot += un.C[(size_t)src * G + rk.grank];
+        if (getenv("KB_DEBUG") && atoi(getenv("KB_DEBUG")))
+            fprintf(stderr, "[kb] group receive: rank %d, part %u/%u, %llu records\n", rk.grank, un.part, un.n_parts,
+                    (unsigned long long)tot);
         if (tot) GKB(kb_submit_superkmers_device(rk.recv, rk.rbuf[s].p, tot));
         GKB(kb_finalize(rk.recv, prune));
         return KB_OK;

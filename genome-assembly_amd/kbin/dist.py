@@ -407,6 +407,7 @@ class GroupBinner(ShardedBinner):
             self.grp = Group(K, M, cutoff=cutoff, max_read_len=max_read_len, rank=self.rank, n_ranks=self.world,
                              device=device, flags=flags, host=(self._host.allgather, self._host.alltoallv))
         self.engine = self.grp.ctx(0)
+        self.rec_words = self.engine.record_words()  # (the routed record's int64 words: exchange accounting)
         self.last_counts = None
         self.last_times = {}
         self._prune = True

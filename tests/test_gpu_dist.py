@@ -372,15 +372,21 @@ def _c2_prefix(n):
     return w, ln, wpr, L, bases, lens
 
 
-@pytest.mark.parametrize("api", ["create", "create_rank"])
-def test_group_rccl_c2_prefix(api, engine):
+@pytest.mark.parametrize("api", ["create", "create_rank", "self_rccl_pieces"])
+def test_group_rccl_c2_prefix(api, engine, monkeypatch):
     """G = 1 through RCCL itself (ncclCommInitAll / ncclCommInitRank with a
-    unique id; counts all-gathered, records by ncclSend/ncclRecv to self),
-    bit-exact against the oracle on the C2 generator's first 40 K reads"""
+    unique id; counts all-gathered), bit-exact against the oracle on the C2
+    generator's first 40 K reads.  A rank's own records are a device copy;
+    self_rccl_pieces sends them through RCCL in 32-KB pieces instead -- the
+    piecewise exchange every peer message takes (a single multi-GB RCCL
+    message delivered about half of its records, round 6)"""
+    if api == "self_rccl_pieces":
+        monkeypatch.setenv("KB_GROUP_SELF_RCCL", "1")
+        monkeypatch.setenv("KB_GROUP_CHUNK", "4096")
     n = 40_000
     w, ln, wpr, L, bases, lens = _c2_prefix(n)
     kw = dict(cutoff=1, max_read_len=L)
-    if api == "create":
+    if api != "create_rank":
         grp = kbin.Group(31, 7, devices=[0], **kw)
     else:
         grp = kbin.Group(31, 7, rank=0, n_ranks=1, unique_id=kbin.group_unique_id(), device=0, **kw)
@@ -501,13 +507,16 @@ def test_group_track_first(engine):
     assert seen == ref.n_entries and union == want
 
 
-def test_bench_multi_gpu_capacity_rehearsal(tmp_path, engine):
+@pytest.mark.parametrize("transport", ["torch", "c"])
+def test_bench_multi_gpu_capacity_rehearsal(tmp_path, engine, transport):
     """bench.py at N = 2 (gloo rehearsal: two ranks on one GPU) runs the
     headline C2 weak-scaling leg and then BASELINE's multi-GPU configurations
     as specified -- C4 (K31, 150 bp, one 3.1-Gbp genome, P = 5) and C5 (K63,
     250 bp, 1 % errors, P = 4) -- routed between the ranks; here at 1/400 of
     their reads (KB_CAPACITY_SCALE) to test the legs' plumbing: the one JSON
-    line carries both legs with their timings, rooflines and exchange bytes"""
+    line carries both legs with their timings, rooflines and exchange bytes.
+    transport c: the legs through the C group (kb_group_create_rank_host over
+    gloo), the object the driver's RCCL run uses (GroupBinner)"""
     if engine != "binned":
         pytest.skip("bench picks its engine itself")
     import json
@@ -518,7 +527,7 @@ def test_bench_multi_gpu_capacity_rehearsal(tmp_path, engine):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    env = dict(os.environ, KB_DIST_BACKEND="gloo", KB_CAPACITY_SCALE="400")
+    env = dict(os.environ, KB_DIST_BACKEND="gloo", KB_CAPACITY_SCALE="400", KB_ROUTED_TRANSPORT=transport)
     env.pop("KB_ENGINE", None)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), str(kbin.REPO_ROOT / "bench.py"),
