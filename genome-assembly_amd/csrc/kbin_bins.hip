@@ -903,9 +903,11 @@ __device__ unsigned long long g_bin_prof[PROF_N];
 #define KB_BIN_THREADS 1024
 #endif
 constexpr int BIN_THREADS = KB_BIN_THREADS;
+static_assert((BIN_THREADS & (BIN_THREADS - 1)) == 0 && BIN_THREADS >= 256 && BIN_THREADS <= 1024,
+              "bin_kernel's LDS carve and strides assume a power-of-two workgroup (768 faulted, r06)");
 #ifndef KB_WIN_LOADS
 #define KB_WIN_LOADS 4  // stage loads in flight per thread in the id windows (8: more spills, measured slower)
-#endif  // (A/B builds: -DKB_BIN_THREADS=512 with KB_BIN_TS_LOG2=12)
+#endif  // (A/B builds: -DKB_BIN_THREADS=512 with KB_BIN_TS_LOG2=12; powers of two only -- 768 faults)
 constexpr int BIN_STACK = 32;
 
 DEV uint64_t lds_load_u64(const uint64_t* p) {
