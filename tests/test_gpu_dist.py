@@ -544,6 +544,34 @@ def test_bench_multi_gpu_capacity_rehearsal(tmp_path, engine, transport):
         assert 0 < leg["roofline"]["frac"] < 1
 
 
+def test_bench_multi_legs_one_rank_rccl(engine):
+    """bench.py --routed --multi-legs: the N > 1 run's C4 and C5 legs through
+    a one-rank RCCL group (GroupBinner: the object the driver's multi-GPU run
+    uses), here at 1/400 of their reads -- the full-size run of the same
+    command is the legs' memory and time rehearsal"""
+    if engine != "binned":
+        pytest.skip("bench picks its engine itself")
+    import json
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, KB_CAPACITY_SCALE="400")
+    env.pop("KB_ENGINE", None)
+    env.pop("KB_DIST_BACKEND", None)
+    r = subprocess.run([sys.executable, str(kbin.REPO_ROOT / "bench.py"), "--routed", "--multi-legs", "--steps", "2",
+                        "--warmup", "1", "--reads", "100000", "--cpu-sample", "0", "--no-host-input"],
+                       capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0
+    for name, K in (("c4", 31), ("c5", 63)):
+        leg = line["capacity"][name]
+        assert leg["value"] > 0 and leg["ms_per_step"] > 0, leg
+        assert f"K={K}" in leg["workload"] and leg["rehearsal_scale"] == 400
+        assert leg["exchange"]["record_bytes"] == (24 if K == 31 else 40)
+        assert 0 < leg["roofline"]["frac"] < 1
+
+
 def _k_below_2m_reads(K, M):
     rng = np.random.default_rng(K * 1000 + M + 7)
     genome = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=3000)
