@@ -30,7 +30,7 @@ OUT = REPO / "tests" / "golden" / "oracle_digests.json"
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("workload", choices=["c2", "c3"])
+    ap.add_argument("workload", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--cap-log2", type=int, default=27)
     ap.add_argument("--reads", type=int, default=0, help="a prefix of the workload's reads (0: all)")
