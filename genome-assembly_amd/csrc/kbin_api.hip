@@ -228,6 +228,9 @@ struct kb_ctx {
     bool route_affine = false;
     int64_t route_id_c = 0;
     DevBuf<unsigned long long> rcount;  // records per destination
+    DevBuf<uint8_t> owner_dev;          // owner ranks of the canonical mmers (owner_map_dev)
+    uint64_t owner_key = ~0ull;         // (n_dest, part, part_n) the device table holds
+    std::vector<uint8_t> owner_h;
 
     // host ingest (kb_submit): double-buffered pinned staging, pooled batches
     IngestSlot ring[2];
@@ -798,6 +801,64 @@ static int read_id_map(kb_ctx* c, bool& affine, int64_t& id_c) {
 
 static int binned_read_records(kb_ctx* c, uint64_t& R, uint64_t& N, bool ordered);
 
+// Owner ranks.  The owner of a canonical mmer had been a hash
+// of it modulo the ranks; the minimizer rule skews the mmers' loads (bmap_prior),
+// so at 8 ranks the busiest rank bound 1.19x the mean k-mers on C2's reads,
+// and 1.4-1.7x inside one pass of C4's and C5's partitioned legs (the pass
+// keeps a hashed fifth or quarter of the mmers).  Instead every pass packs
+// its own canonical mmers onto the ranks, heaviest expected load first, each
+// onto the least-loaded rank (ties: the lower rank) -- LPT over bmap_prior's
+// weight shape ((i + 1) / half)^(K - M), the expected signature frequency on
+// uniform sequence: C2 at 8 ranks 1.019x.  A function of (K, M, ranks, part,
+// part_n) only, so every rank and process computes the same table; mmers of
+// other passes keep the hash (never routed in this pass).  K < 2M codes are
+// not canonical (binning.c:992-1021): the hash, as before.
+static void owner_table_host(int K, int M, uint32_t n_dest, uint32_t part, uint32_t part_n, uint8_t* out) {
+    const uint32_t half = 1u << (2 * M - 1);
+    std::vector<double> load(n_dest, 0.0);
+    for (uint32_t i = half; i-- > 0;) {  // the weight grows with i: heaviest first
+        const uint32_t mm = half + i;
+        if (part_n > 1 && sk_hash_dest(mm, part_n, 0x9E3779B97F4A7C15ull) != part) {
+            out[i] = (uint8_t)sk_hash_dest(mm, n_dest, 0x5851F42D4C957F2Dull);
+            continue;
+        }
+        uint32_t r = 0;
+        for (uint32_t d = 1; d < n_dest; d++)
+            if (load[d] < load[r]) r = d;
+        out[i] = (uint8_t)r;
+        load[r] += std::pow((double)(i + 1) / half, K - M);
+    }
+}
+
+extern "C" int kb_owner_table(int K, int M, uint32_t n_dest, uint32_t part, uint32_t n_parts, uint8_t* out) {
+    if (!out) return fail(KB_EINVAL, "null argument");
+    if (M < 1 || M > 8 || K < M || K > 63) return fail(KB_EINVAL, "K=%d, M=%d outside 1 <= M <= 8, M <= K <= 63", K, M);
+    if (n_dest < 1 || n_dest > 64) return fail(KB_EINVAL, "n_dest=%u outside [1,64]", n_dest);
+    if (n_parts < 1 || part >= n_parts) return fail(KB_EINVAL, "part %u of %u", part, n_parts);
+    owner_table_host(K, M, n_dest, part, n_parts, out);
+    return KB_OK;
+}
+
+// the context's owner table for n_dest ranks in its current pass, on the
+// device (null for K < 2M: the hash)
+static int owner_map_dev(kb_ctx* c, uint32_t n_dest, const uint8_t** out) {
+    *out = nullptr;
+    if (c->p.K < 2 * c->p.M) return KB_OK;
+    const uint32_t pn = std::max(1u, c->part_n), pt = pn > 1 ? c->part : 0u;
+    const uint64_t key = (uint64_t)n_dest | ((uint64_t)pt << 8) | ((uint64_t)pn << 36);
+    const uint32_t half = 1u << (2 * c->p.M - 1);
+    if (c->owner_key != key || !c->owner_dev.p) {
+        c->owner_h.resize(half);
+        owner_table_host(c->p.K, c->p.M, n_dest, pt, pn, c->owner_h.data());
+        HIPCHK(c->owner_dev.ensure_exact(half));
+        HIPCHK(hipMemcpyAsync(c->owner_dev.p, c->owner_h.data(), half, hipMemcpyHostToDevice, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));  // (owner_h is the next table's)
+        c->owner_key = key;
+    }
+    *out = c->owner_dev.p;
+    return KB_OK;
+}
+
 // routing through the binned engine's record pass: records in read order,
 // destination = owner(mmer); counts now, a stable sort by destination and
 // the pack in kb_route_pack (same record format and order as route_kernel)
@@ -810,7 +871,10 @@ static int route_plan_binned(kb_ctx* c, uint32_t G, uint64_t* h_counts) {
     if (rc) return rc;
     HIPCHK(c->rcount.ensure(64));
     HIPCHK(hipMemsetAsync(c->rcount.p, 0, 64 * sizeof(unsigned long long), c->s));
-    HIPCHK(launch_route_dest(c->occ_a.p, R, G, c->occ_b.p, c->rcount.p, c->s));
+    const uint8_t* om = nullptr;
+    rc = owner_map_dev(c, G, &om);
+    if (rc) return rc;
+    HIPCHK(launch_route_dest(c->occ_a.p, R, G, om, c->p.M, c->occ_b.p, c->rcount.p, c->s));
     std::vector<unsigned long long> cnt(G);
     HIPCHK(hipMemcpyAsync(cnt.data(), c->rcount.p, G * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
@@ -901,6 +965,8 @@ extern "C" int kb_route_plan(kb_ctx* c, uint32_t n_dest, uint64_t* h_counts) {
         a.RW = b.RW;
         a.K = c->p.K;
         a.M = c->p.M;
+        rc = owner_map_dev(c, n_dest, &a.owner_map);
+        if (rc) return rc;
         HIPCHK(launch_route(a, false, c->s));
         // dest-major exclusive scan -> every (dest, read) slot in a dest-major buffer
         HIPCHK(c->scratch.ensure(std::max(scan_u32_scratch_elems(cells), c->scratch.cap)));
@@ -983,6 +1049,10 @@ static int scatter_regions(kb_ctx* c, uint32_t n_dest, uint64_t* d_regions, uint
         a.id_off = (uint32_t)(affine ? id_c : 0);
         a.G = n_dest;
         a.dest_salt = salt;  // owner_of (kbin_kernels.hip), or in_part's PART_SALT (kbin_bins.hip)
+        if (!by_pass) {  // ranks: the pass's owner table (passes: the partition hash)
+            const int orc = owner_map_dev(c, n_dest, &a.owner_map);
+            if (orc) return orc;
+        }
         a.rw = rec_words(c);
         HIPCHK(launch_sk(a, true, c->s));
     }
@@ -1050,6 +1120,10 @@ extern "C" int kb_route_pack(kb_ctx* c, uint64_t* d_send) {
         a.RW = b.RW;
         a.K = c->p.K;
         a.M = c->p.M;
+        {
+            const int orc = owner_map_dev(c, G, &a.owner_map);  // (the plan's table)
+            if (orc) return orc;
+        }
         HIPCHK(launch_route(a, true, c->s));
         HIPCHK(hipStreamSynchronize(c->s));  // h_adj / adj reuse
         b.routed = true;

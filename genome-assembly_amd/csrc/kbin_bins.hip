@@ -254,7 +254,8 @@ DEV uint32_t record_pieces(const SkScanArgs& A, uint32_t canon, int lo, int n, i
     ne = 0;
     sub[0] = sub[1] = 0;
     if (!A.bucket_map || !bm_has_entry(canon, A.M)) {
-        d[0] = dest_of(canon, A.G, A.dest_salt);
+        d[0] = A.owner_map && bm_has_entry(canon, A.M) ? (uint32_t)A.owner_map[canon - (1u << (2 * A.M - 1))]
+                                                       : dest_of(canon, A.G, A.dest_salt);
         return 1;
     }
     const uint32_t me = A.bucket_map[canon - (1u << (2 * A.M - 1))];
@@ -291,7 +292,8 @@ DEV uint64_t record_plan(const SkScanArgs& A, uint64_t e, uint32_t me, const uin
     uint32_t d0 = 0, d1 = 0, b = 0, two = 0;
     int ne = 0;
     if (!A.bucket_map || !bm_has_entry(canon, A.M)) {  // (me: not loaded for such a code)
-        d0 = dest_of(canon, A.G, A.dest_salt);
+        d0 = A.owner_map && bm_has_entry(canon, A.M) ? (uint32_t)A.owner_map[canon - (1u << (2 * A.M - 1))]
+                                                     : dest_of(canon, A.G, A.dest_salt);
     } else if (!(b = bm_depth(me))) {
         d0 = me & 1023u;
     } else {
@@ -781,13 +783,16 @@ hipError_t launch_sk_gather(const uint64_t* keys, const uint64_t* pay, uint64_t 
 
 
 __global__ __launch_bounds__(256) void route_dest_kernel(const uint64_t* __restrict__ keys, uint64_t R,
-                                                         uint32_t G, uint64_t* __restrict__ dkeys,
+                                                         uint32_t G, const uint8_t* __restrict__ owner_map, int M,
+                                                         uint64_t* __restrict__ dkeys,
                                                          unsigned long long* __restrict__ counts) {
     __shared__ uint32_t hist[64];
     if (threadIdx.x < 64) hist[threadIdx.x] = 0;
     __syncthreads();
     for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < R; t += (uint64_t)gridDim.x * 256) {
-        const uint32_t d = owner_of_mmer((uint32_t)(keys[t] >> 38), G);
+        const uint32_t mm = (uint32_t)(keys[t] >> 38);
+        const uint32_t d = owner_map && bm_has_entry(mm, M) ? (uint32_t)owner_map[mm - (1u << (2 * M - 1))]
+                                                            : owner_of_mmer(mm, G);
         dkeys[t] = ((uint64_t)d << 32) | (uint32_t)t;
         atomicAdd(&hist[d], 1u);
     }
@@ -795,12 +800,13 @@ __global__ __launch_bounds__(256) void route_dest_kernel(const uint64_t* __restr
     if (threadIdx.x < G && hist[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)hist[threadIdx.x]);
 }
 
-hipError_t launch_route_dest(const uint64_t* keys, uint64_t R, uint32_t G, uint64_t* dkeys,
+hipError_t launch_route_dest(const uint64_t* keys, uint64_t R, uint32_t G, const uint8_t* owner_map, int M,
+                             uint64_t* dkeys,
                              unsigned long long* counts, hipStream_t s) {
     if (!R) return hipSuccess;
     if (G < 1 || G > 64) return hipErrorInvalidValue;
     const uint64_t blocks = std::min<uint64_t>((R + 255) / 256, 2048);
-    hipLaunchKernelGGL(route_dest_kernel, dim3((unsigned)blocks), dim3(256), 0, s, keys, R, G, dkeys, counts);
+    hipLaunchKernelGGL(route_dest_kernel, dim3((unsigned)blocks), dim3(256), 0, s, keys, R, G, owner_map, M, dkeys, counts);
     return hipGetLastError();
 }
 

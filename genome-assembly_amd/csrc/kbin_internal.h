@@ -55,6 +55,7 @@ struct RouteArgs {
     uint32_t part, part_n;     // kb_set_partition: route only this mmer partition's records
     int rec_words;
     int RW, K, M;
+    const uint8_t* owner_map;  // canonical mmer - 2^(2M-1) -> owner rank (kb_owner_table; null: the hash)
 };
 
 struct SkArgs {
@@ -116,6 +117,9 @@ struct SkScanArgs {
     const uint32_t* bucket_map;
     const uint16_t* sub_map;
     int sub_stamp;             // the map splits mmers: bucket records carry their sub-bin (sub_room)
+    // routing to ranks only: canonical mmer - 2^(2M-1) -> owner rank
+    // (kb_owner_table; null: the owner hash, and always for K < 2M codes)
+    const uint8_t* owner_map;
     // partitioned passes (kb_set_partition): only super-k-mers whose mmer is in
     // partition part of part_n are emitted and counted (part_n <= 1: all)
     uint32_t part, part_n;
@@ -402,8 +406,8 @@ hipError_t launch_sk_convert(const uint64_t* recs, uint64_t n_rec, int rw, uint6
                              uint64_t* pay, uint64_t* keys, uint32_t* status, unsigned long long* n_kmers,
                              hipStream_t s);
 // sender: destination of every record (owner of its mmer) -> dkeys = dest << 32 | t, counts[dest]
-hipError_t launch_route_dest(const uint64_t* keys, uint64_t R, uint32_t G, uint64_t* dkeys,
-                             unsigned long long* counts, hipStream_t s);
+hipError_t launch_route_dest(const uint64_t* keys, uint64_t R, uint32_t G, const uint8_t* owner_map, int M,
+                             uint64_t* dkeys, unsigned long long* counts, hipStream_t s);
 // sender: records in destination-sorted order -> routed record format
 hipError_t launch_route_pack_binned(const uint64_t* sorted, const uint64_t* pay, uint64_t R, int rw,
                                     const int32_t* read_ids, uint32_t id_off, uint64_t* out,

@@ -513,7 +513,7 @@ __global__ __launch_bounds__(256) void route_kernel(RouteArgs A) {
                 const int sig = rfl((int)(0xFFFFu - (key & 0xFFFFu)));
                 const uint32_t c = key >> 16;
                 const int n = min(sig, nK - 1) - seg_lo + 1;
-                const uint32_t dest = owner_of(c, A.G);
+                const uint32_t dest = A.owner_map ? (uint32_t)A.owner_map[c - halfM] : owner_of(c, A.G);
                 // another pass's super-k-mer: neither counted nor written
                 const bool mine = route_in_part(c, A.part, A.part_n);
                 if (PACK && mine) {

@@ -39,7 +39,7 @@ EXPORTED = [
     "kb_group_unique_id", "kb_group_create", "kb_group_create_rank", "kb_group_destroy", "kb_group_info",
     "kb_group_submit_ids", "kb_group_submit_packed_device", "kb_group_set_partition", "kb_group_send",
     "kb_group_receive", "kb_group_finalize", "kb_group_discard", "kb_group_reset", "kb_group_ctx",
-    "kb_group_send_async", "kb_group_unit_counts", "kb_group_create_rank_host",
+    "kb_group_send_async", "kb_group_unit_counts", "kb_group_create_rank_host", "kb_owner_table",
 ]
 KB_TRANSPORT_RCCL, KB_TRANSPORT_LOCAL = 1, 2
 
@@ -124,6 +124,7 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     lib.kb_generate_reads_device_at.argtypes = [C.c_int, vp, vp, u64, u32, u64, u32, u64, u64]
     lib.kb_unpack_reads_to_host.argtypes = [C.c_int, vp, vp, u64, u32, C.c_char_p, C.POINTER(u32)]
     lib.kb_record_words.argtypes = [vp, C.POINTER(u32)]
+    lib.kb_owner_table.argtypes = [C.c_int, C.c_int, u32, u32, u32, C.POINTER(C.c_uint8)]
     lib.kb_route_plan.argtypes = [vp, u32, C.POINTER(u64)]
     lib.kb_route_pack.argtypes = [vp, vp]
     lib.kb_submit_superkmers_device.argtypes = [vp, vp, u64]
@@ -582,6 +583,15 @@ class Group:
 
 def timing_dict(t: "kb_timing") -> dict:
     return {f: getattr(t, f) for f, _ in kb_timing._fields_ if f != "reserved"}
+
+
+def owner_table(K: int, M: int, n_dest: int, part: int = 0, n_parts: int = 1) -> np.ndarray:
+    """kb_owner_table: the owner rank of every canonical mmer 2^(2M-1) + i
+    (index i) for n_dest ranks in pass (part, n_parts) -- host only"""
+    lib = load_library()
+    out = np.zeros(1 << (2 * M - 1), dtype=np.uint8)
+    _check(lib, lib.kb_owner_table(K, M, n_dest, part, n_parts, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return out
 
 
 def generate_reads_device(words_ptr: int, lens_ptr: int, n_reads: int, read_len: int,

@@ -60,10 +60,23 @@ def _mix64(x: int) -> int:
     return x
 
 
-def owner_of(mmer_code: int, n_dest: int) -> int:
-    """Owning rank of a canonical mmer (same function as owner_of() in
-    csrc/kbin_kernels.hip)."""
-    return (_mix64(mmer_code + _MIX_SALT) >> 32) % n_dest
+_OWNER_TABLES = {}
+
+
+def owner_of(mmer_code: int, n_dest: int, K: int = 31, M: int = 7, part: int = 0, n_parts: int = 1) -> int:
+    """Owning rank of a mmer among n_dest ranks in pass (part, n_parts): the
+    routing kernels' owner -- kb_owner_table (include/kbin.h) for a canonical
+    code at K >= 2M, the owner hash (owner_of() in csrc/kbin_kernels.hip)
+    for any other code"""
+    half = 1 << (2 * M - 1)
+    if K < 2 * M or not half <= mmer_code < 2 * half:
+        return (_mix64(mmer_code + _MIX_SALT) >> 32) % n_dest
+    key = (K, M, n_dest, part if n_parts > 1 else 0, max(1, n_parts))
+    t = _OWNER_TABLES.get(key)
+    if t is None:
+        from . import owner_table
+        t = _OWNER_TABLES[key] = owner_table(K, M, n_dest, key[3], key[4])
+    return int(t[mmer_code - half])
 
 
 def exchange_records(send: torch.Tensor, counts, rec_words: int, group=None):

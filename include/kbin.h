@@ -232,7 +232,8 @@ int kb_unpack_reads_to_host(int device, const uint64_t *d_words,
 
 /* ---- multi-GPU routing ------------------------------
  * The canonical-mmer space shards: a super-k-mer (a run of consecutive k-mers
- * of one read sharing a signature) is owned by GPU owner(mmer) of n_dest.
+ * of one read sharing a signature) is owned by GPU owner(mmer) of n_dest
+ * (kb_owner_table).
  * Sender: kb_route_plan counts the records per destination for every read
  * batch submitted so far; kb_route_pack writes them, destination-major and in
  * read order, into d_send (sum(counts) * kb_record_words u64 words) and marks
@@ -242,6 +243,15 @@ int kb_unpack_reads_to_host(int device, const uint64_t *d_words,
  * the senders' read ids: across all ranks they must increase with call order
  * (rank r's ids below rank r+1's) and be >= 0; they are the list order key. */
 int kb_record_words(kb_ctx *ctx, uint32_t *out);
+/* owner(mmer) for n_dest ranks in pass (part, n_parts) of kb_set_partition
+ * (n_parts 1: one pass): out[i] is the rank of canonical mmer 2^(2M-1) + i,
+ * for i < 2^(2M-1).  Each pass's canonical mmers are packed onto the ranks,
+ * heaviest expected load first (the signature frequency on uniform sequence,
+ * ((i + 1) / 2^(2M-1))^(K-M)), each onto the least-loaded rank -- so every
+ * rank and process derives the same table from (K, M, n_dest, part,
+ * n_parts) alone.  K < 2M codes (not canonical) go to a hash of the code
+ * instead.  Host only (no device needed). */
+int kb_owner_table(int K, int M, uint32_t n_dest, uint32_t part, uint32_t n_parts, uint8_t *out);
 int kb_route_plan(kb_ctx *ctx, uint32_t n_dest, uint64_t *h_counts);
 int kb_route_pack(kb_ctx *ctx, uint64_t *d_send);
 int kb_submit_superkmers_device(kb_ctx *ctx, const uint64_t *d_records, uint64_t n_records);

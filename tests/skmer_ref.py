@@ -56,8 +56,15 @@ def _word(v, p):
     return w
 
 
-def encode(reads, ids, K: int, M: int, G: int):
-    """dest-major record buffer (uint64) + per-destination counts, in read order"""
+def _in_part(mmer: int, part: int, n_parts: int) -> bool:
+    """kb_set_partition membership (route_in_part, csrc/kbin_kernels.hip)"""
+    from kbin.dist import _mix64
+    return n_parts <= 1 or (_mix64(mmer + 0x9E3779B97F4A7C15) >> 32) % n_parts == part
+
+
+def encode(reads, ids, K: int, M: int, G: int, part: int = 0, n_parts: int = 1):
+    """dest-major record buffer (uint64) + per-destination counts, in read
+    order; n_parts > 1: only pass `part`'s records, to that pass's owners"""
     rw = rec_words(K, M)
     per = [[] for _ in range(G)]
     for read, rid in zip(reads, ids):
@@ -71,7 +78,9 @@ def encode(reads, ids, K: int, M: int, G: int):
             for w in range(rw - 1):
                 p = i0 + 32 * w
                 rec.append(_word(v, p) if p < len(v) else 0)
-            per[owner_of(cm, G)].append(rec)
+            if not _in_part(cm, part, n_parts):
+                continue
+            per[owner_of(cm, G, K, M, part, n_parts)].append(rec)
     counts = [len(x) for x in per]
     flat = [w for d in per for rec in d for w in rec]
     return np.array(flat, dtype=np.uint64).reshape(-1), counts

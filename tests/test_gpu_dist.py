@@ -64,7 +64,7 @@ def test_virtual_shards(K, M, G):
             shard.submit_superkmers_device(seg.data_ptr(), int(counts[d]))
             shard.finalize(prune=True)
             part = _result_dict(shard.export())
-        assert all(kbin.dist.owner_of(mm, G) == d for mm, _ in part)
+        assert all(kbin.dist.owner_of(mm, G, K, M) == d for mm, _ in part)
         assert not (set(part) & set(union))
         union.update(part)
     assert union == ora
@@ -211,7 +211,9 @@ def test_partitioned_routing(P, K, M, engine):
     bases, lens = kbin.pack_reads(reads)
     ids = np.arange(len(reads), dtype=np.int32) * 2 + 5
     rw = skmer_ref.rec_words(K, M)
-    _, wcounts = skmer_ref.encode(reads, ids.tolist(), K, M, G)
+    # (each pass routes to its own owner table: kb_owner_table)
+    pcounts = [skmer_ref.encode(reads, ids.tolist(), K, M, G, p, P)[1] for p in range(P)]
+    wcounts = np.sum(pcounts, axis=0).tolist()
     ora = skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, True, ids=ids))
     union = {}
     tot = np.zeros(G, dtype=np.int64)
@@ -226,12 +228,13 @@ def test_partitioned_routing(P, K, M, engine):
                 edges = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
                 segs = [(send, int(edges[d]) * rw) for d in range(G)]
             else:
-                cap = int(max(wcounts)) + 16
+                cap = int(max(pcounts[p])) + 16
                 regions = torch.zeros(G * cap * rw, dtype=torch.int64, device="cuda")
                 ok, counts = eng.route_scatter(G, regions.data_ptr(), cap)
                 assert ok
                 segs = [(regions, d * cap * rw) for d in range(G)]
             torch.cuda.synchronize()
+            assert counts.tolist() == list(pcounts[p])
             tot += counts.astype(np.int64)
             for d in range(G):
                 buf, o = segs[d]
@@ -240,6 +243,7 @@ def test_partitioned_routing(P, K, M, engine):
                         shard.submit_superkmers_device(buf[o:].data_ptr(), int(counts[d]))
                     shard.finalize(prune=True)
                     part = _result_dict(shard.export())
+                assert all(kbin.dist.owner_of(mm, G, K, M, p, P) == d for mm, _ in part)
                 assert not (set(part) & set(union))
                 union.update(part)
     assert tot.tolist() == list(wcounts)
@@ -325,11 +329,11 @@ def test_ranks_rehearsal(tmp_path, transport):
 # ---- multi-GPU groups through the C-ABI (kb_group_*: routing, exchange over
 # RCCL or device copies, receivers -- all in C; kbin.h "multi-GPU groups")
 
-def _group_union(grp, G_local):
+def _group_union(grp, G_local, K=31, M=7, p=0, P=1):
     union = {}
     for g in range(G_local):
         part = _result_dict(grp.ctx(g).export())
-        assert all(kbin.dist.owner_of(mm, grp.n_ranks) == grp.rank0 + g for mm, _ in part)
+        assert all(kbin.dist.owner_of(mm, grp.n_ranks, K, M, p, P) == grp.rank0 + g for mm, _ in part)
         assert not (set(part) & set(union))
         union.update(part)
     return union
@@ -355,7 +359,7 @@ def test_group_virtual_shards(K, M, G, engine):
                 grp.submit(g, bases=bases[off[a]:off[b]], lens=lens[a:b], ids=ids[a:b])
             grp.finalize(prune)
             want = skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, K, M, 1, prune, ids=ids))
-            assert _group_union(grp, G) == want
+            assert _group_union(grp, G, K, M) == want
 
 
 def _c2_prefix(n):
@@ -439,7 +443,7 @@ def test_group_pipelined_partitions(engine):
                 grp.set_partition(p + 1, P)
                 grp.send()
             grp.receive(True)
-            part = _group_union(grp, G)
+            part = _group_union(grp, G, p=p, P=P)
             assert not (set(part) & set(union))
             union.update(part)
     assert union == skmer_ref.oracle_dict(oracle.bin_reads(bases, lens, 31, 7, 1, True))
