@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <map>
 #include <queue>
 #include <string>
 #include <unordered_map>
@@ -228,9 +229,9 @@ struct kb_ctx {
     bool route_affine = false;
     int64_t route_id_c = 0;
     DevBuf<unsigned long long> rcount;  // records per destination
-    DevBuf<uint8_t> owner_dev;          // owner ranks of the canonical mmers (owner_map_dev)
-    uint64_t owner_key = ~0ull;         // (n_dest, part, part_n) the device table holds
-    std::vector<uint8_t> owner_h;
+    // owner ranks of the canonical mmers per (n_dest, part, part_n) (owner_map_dev):
+    // host copy (the upload's source stays alive) and device table
+    std::map<uint64_t, std::pair<std::vector<uint8_t>, DevBuf<uint8_t>>> owners;
 
     // host ingest (kb_submit): double-buffered pinned staging, pooled batches
     IngestSlot ring[2];
@@ -493,6 +494,7 @@ extern "C" void kb_destroy(kb_ctx* c) {
     c->e_lo.release(); c->e_off.release(); c->ids_out.release(); c->scratch.release();
     c->misc.release(); c->totals.release(); c->first.release(); c->e_first.release();
     for (auto& m : c->bmaps) { m.map.release(); m.sub.release(); }
+    for (auto& o : c->owners) o.second.second.release();
     c->flat_list.release(); c->flat_next.release(); c->flat_l0.release(); c->flat_off.release();
     c->flat_cur.release(); c->flat_chunk.release(); c->pool_bin.release(); c->chunk_bin.release();
     c->flat_sbase.release(); c->flat_obase.release(); c->flat_n.release(); c->hll.release();
@@ -847,15 +849,14 @@ static int owner_map_dev(kb_ctx* c, uint32_t n_dest, const uint8_t** out) {
     const uint32_t pn = std::max(1u, c->part_n), pt = pn > 1 ? c->part : 0u;
     const uint64_t key = (uint64_t)n_dest | ((uint64_t)pt << 8) | ((uint64_t)pn << 36);
     const uint32_t half = 1u << (2 * c->p.M - 1);
-    if (c->owner_key != key || !c->owner_dev.p) {
-        c->owner_h.resize(half);
-        owner_table_host(c->p.K, c->p.M, n_dest, pt, pn, c->owner_h.data());
-        HIPCHK(c->owner_dev.ensure_exact(half));
-        HIPCHK(hipMemcpyAsync(c->owner_dev.p, c->owner_h.data(), half, hipMemcpyHostToDevice, c->s));
-        HIPCHK(hipStreamSynchronize(c->s));  // (owner_h is the next table's)
-        c->owner_key = key;
+    auto& t = c->owners[key];  // (a partitioned job's passes each keep theirs)
+    if (!t.second.p) {
+        t.first.resize(half);
+        owner_table_host(c->p.K, c->p.M, n_dest, pt, pn, t.first.data());
+        HIPCHK(t.second.ensure_exact(half));
+        HIPCHK(hipMemcpyAsync(t.second.p, t.first.data(), half, hipMemcpyHostToDevice, c->s));
     }
-    *out = c->owner_dev.p;
+    *out = t.second.p;
     return KB_OK;
 }
 
