@@ -302,8 +302,9 @@ void *kb_stream(kb_ctx *ctx);
  * owner(mmer) (kb_route_scatter), the records move in ONE exchange -- the
  * per-destination counts (ncclAllGather), then grouped ncclSend/ncclRecv,
  * over RCCL / xGMI, called from C, each peer message in pieces of at most
- * KB_GROUP_CHUNK words (default 2^25 = 256 MB; a rank's own records by a
- * device copy) -- and every rank bins what it received
+ * KB_GROUP_CHUNK words (default 2^25 = 256 MB; the same on every rank: the
+ * pieces are matched in order; a rank's own records by a device copy) -- and
+ * every rank bins what it received
  * (kb_submit_superkmers_device + kb_finalize).  The ranks' results are
  * disjoint; their union is the single-GPU result, entry for entry and list
  * for list, provided read ids increase with the global call order (rank r's
