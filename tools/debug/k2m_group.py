@@ -30,6 +30,6 @@ for K, M, G in [(15, 8, 4), (13, 7, 4), (15, 8, 2), (15, 8, 3)]:
     dup = {k: v for k, v in seen.items() if len(v) > 1}
     print(K, M, G, "keys", len(seen), "oracle", len(ora), "dup", len(dup), flush=True)
     for k, v in list(dup.items())[:5]:
-        print("  key", k, "ranks", v, "owner", kbin.dist.owner_of(k[0], G), [parts[g][k] for g in v], "ora", ora.get(k))
-    wrong = sum(1 for g, p in enumerate(parts) for k in p if kbin.dist.owner_of(k[0], G) != g)
+        print("  key", k, "ranks", v, "owner", kbin.dist.owner_of(k[0], G, K, M), [parts[g][k] for g in v], "ora", ora.get(k))
+    wrong = sum(1 for g, p in enumerate(parts) for k in p if kbin.dist.owner_of(k[0], G, K, M) != g)
     print("  keys at a non-owner rank:", wrong)
