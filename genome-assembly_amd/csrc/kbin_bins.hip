@@ -417,9 +417,24 @@ __global__ __launch_bounds__(SKT) void sk_thread_kernel(SkScanArgs A) {
     for (uint64_t r0 = (uint64_t)blockIdx.x * SKT; r0 < A.n_reads; r0 += (uint64_t)gridDim.x * SKT) {
         const uint32_t nrows = (uint32_t)min<uint64_t>(SKT, A.n_reads - r0);
         __syncthreads();
-        for (uint32_t i = tid; i < nrows * (uint32_t)RW; i += SKT) {
-            const uint32_t row = i / (uint32_t)RW, col = i - row * (uint32_t)RW;
-            smem[row * RS + col] = A.words[r0 * RW + i];
+        {
+            // (the block's reads into LDS rows, eight loads in flight per lane)
+            const uint32_t nw = nrows * (uint32_t)RW;
+            for (uint32_t i0 = tid; i0 < nw; i0 += 8u * SKT) {
+                uint64_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint32_t i = i0 + (uint32_t)u * SKT;
+                    v[u] = i < nw ? A.words[r0 * RW + i] : 0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint32_t i = i0 + (uint32_t)u * SKT;
+                    if (i >= nw) break;
+                    const uint32_t row = i / (uint32_t)RW, col = i - row * (uint32_t)RW;
+                    smem[row * RS + col] = v[u];
+                }
+            }
         }
         if (tid < nrows)
             for (int w = RW; w < RS; w++) smem[tid * RS + w] = 0;
@@ -4352,7 +4367,10 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
 #ifndef KB_BK_U
 #define KB_BK_U 8  // (8 records in flight: C2 1.809 -> 1.796 ms, profiles/r06/ab_bku/)
 #endif
-    constexpr int U = SPW == 2 ? KB_BK_U : 2;  // records in flight per thread (A/B builds: -DKB_BK_U)
+#ifndef KB_BK_U4
+#define KB_BK_U4 4  // (C5 share 491.6 -> 489.2 ms, profiles/r06/ab_rows/)
+#endif
+    constexpr int U = SPW == 2 ? KB_BK_U : KB_BK_U4;  // records in flight per thread (A/B builds: -DKB_BK_U, -DKB_BK_U4)
     for (uint64_t i0 = tid; i0 < cnt; i0 += U * BK_THREADS) {
         uint64_t h[U], a[U], b[U], z[U];
 #pragma unroll
