@@ -4309,7 +4309,10 @@ hipError_t launch_bins_describe(const uint64_t* keys, const uint32_t* starts, co
 // descriptors.  Replaces a global radix sort + gather: no random reads, one
 // bucket per workgroup.
 // ---------------------------------------------------------------------------
-constexpr int BK_THREADS = 512;
+#ifndef KB_BK_THREADS
+#define KB_BK_THREADS 1024  // (C2 1.784 -> 1.752 ms, profiles/r06/ab_bkt/)
+#endif
+constexpr int BK_THREADS = KB_BK_THREADS;  // (A/B builds: -DKB_BK_THREADS)
 constexpr uint32_t BK_SLOTS = 256;  // mmers per bucket (a bucket with more is reported)
 
 // a bucket's bins: key (mmer << SUB_BITS | context sub-bin) + 1 in an LDS table
