@@ -4368,7 +4368,7 @@ __global__ __launch_bounds__(BK_THREADS) void bucket_kernel(BucketArgs A) {
     if (tid == 0) s_full = 0;
     __syncthreads();
 #ifndef KB_BK_U
-#define KB_BK_U 8  // (8 records in flight: C2 1.809 -> 1.796 ms, profiles/r06/ab_bku/)
+#define KB_BK_U 12  // (records in flight: 4 -> 8 C2 1.809 -> 1.796 ms at 512 threads, profiles/r06/ab_bku/; 12 at 1024 threads, ab_bku3/)
 #endif
 #ifndef KB_BK_U4
 #define KB_BK_U4 4  // (C5 share 491.6 -> 489.2 ms, profiles/r06/ab_rows/)
