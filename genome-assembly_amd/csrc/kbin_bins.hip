@@ -953,6 +953,12 @@ struct alignas(16) BinShared {
     uint32_t stack_p[BIN_STACK], stack_l[BIN_STACK];
     uint64_t red[BIN_THREADS / 64];
     unsigned long long dummy[64];  // zero: the claim target of lanes with nothing to claim
+#ifdef KB_BIN_PROF
+    // (diagnostic builds) the phase accumulators and the last stamp, in LDS:
+    // kept in private memory (scratch) each stamp's update waited out the
+    // wave's outstanding global stores, charging their drain to the phase
+    unsigned long long prof[PROF_N + 1];
+#endif
 };
 static_assert(sizeof(BinShared) % 16 == 0, "LDS carve must stay 16-B aligned (guide G17)");
 
@@ -1962,8 +1968,12 @@ DEV void bin_body(const BinArgs& A) {
     const uint64_t nbins = min(A.totals[2], A.max_bins);
     const uint32_t tid = threadIdx.x;
 #ifdef KB_BIN_PROF
-    unsigned long long pacc[PROF_N] = {};
-    unsigned long long pt = clock64();
+    unsigned long long* const pacc = S.prof;
+    unsigned long long& pt = S.prof[PROF_N];
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < PROF_N; i++) pacc[i] = 0;
+        pt = clock64();
+    }
 #endif
     if (tid < 64) S.dummy[tid] = 0;  // (the first loop barrier publishes it)
     // phase 0: block thread 0 claims the next bin one bin ahead, so the
